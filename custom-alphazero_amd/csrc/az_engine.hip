@@ -1,0 +1,623 @@
+// az_engine.hip -- host side of libaz: the C ABI (include/az.h), device
+// buffers, BatchNorm folding, and the lockstep self-play driver.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/az.h"
+#include "az_nn.h"
+#include "az_tree.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define AZ_HIP(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t err__ = (expr);                                                          \
+    if (err__ != hipSuccess)                                                            \
+      return fail(AZ_E_HIP, std::string(#expr) + ": " + hipGetErrorString(err__));      \
+  } while (0)
+
+// libm pow through a volatile pointer: Python's `int ** 0.5` (mcts.py:50) is
+// float_pow -> pow(n, 0.5), which is NOT sqrt for 1,638 n <= 2e6.
+double (*volatile g_pow)(double, double) = pow;
+
+}  // namespace
+
+struct az_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  az_config cfg{};
+  az::GameCfg g{};
+  az::TreeDev t{};
+  az::SampleDev smp{};
+  az::NetDev net{};
+  az::ConvTimer timer;
+  float* x = nullptr;
+  float* act[3] = {nullptr, nullptr, nullptr};
+  float* probs = nullptr;
+  float* values = nullptr;
+  double* uniforms = nullptr;
+  int32_t* dev_i32 = nullptr;  // scratch for az_tree_reset
+  az::Board* dev_boards = nullptr;
+  std::vector<void*> owned;
+  std::vector<void*> sample_bufs;
+  int64_t sp_first = 0, sp_n = 0;
+
+  template <typename T>
+  int alloc(T** p, size_t count) {
+    void* q = nullptr;
+    AZ_HIP(hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)));
+    owned.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+  }
+};
+
+namespace {
+
+int check_device_errors(az_engine* e) {
+  unsigned long long err = 0;
+  AZ_HIP(hipMemcpy(&err, e->t.stats + az::kStatErrors, sizeof(err), hipMemcpyDeviceToHost));
+  if (err) {
+    std::string m = "device error flags:";
+    if (err & az::kErrArena) m += " arena-overflow(raise az_config.arena_edges)";
+    if (err & az::kErrPow) m += " visit-table-overflow(raise az_config.max_tree_visits)";
+    if (err & az::kErrPath) m += " path-overflow";
+    if (err & az::kErrIllegal) m += " illegal-move";
+    if (err & az::kErrNoRoot) m += " play-before-search";
+    return fail(AZ_E_DEVICE, m);
+  }
+  return 0;
+}
+
+az::Board board_from_cells(const int8_t* cells, int HW) {
+  az::Board b;
+  b.own[0] = b.own[1] = b.opp[0] = b.opp[1] = 0;
+  for (int c = 0; c < HW; ++c) {
+    if (cells[c] == 1) az::set_bit(b.own, c);
+    else if (cells[c] == -1) az::set_bit(b.opp, c);
+  }
+  return b;
+}
+
+void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
+  for (int c = 0; c < HW; ++c)
+    cells[c] = az::bit(b.own, c) ? 1 : (az::bit(b.opp, c) ? -1 : 0);
+}
+
+// one simulation for every active slot (MCTS.search body, mcts.py:171-180)
+int simulate(az_engine* e) {
+  hipStream_t s = e->stream;
+  AZ_HIP(hipMemsetAsync(e->t.eval_count, 0, sizeof(int32_t), s));
+  az::launch_select(e->g, e->t, s);
+  if (e->cfg.evaluator == AZ_EVAL_NETWORK) {
+    az::launch_encode(e->t.eval_board, e->t.eval_count, e->g.slots, e->g.HW, e->x, s);
+    az::launch_forward(e->net, e->x, e->t.eval_count, e->g.slots, e->g.H, e->g.W, e->g.A,
+                       e->act[0], e->act[1], e->act[2], e->probs, e->values, s,
+                       e->timer.enabled ? &e->timer : nullptr);
+  } else {
+    az::launch_synth_eval(e->g, e->t, e->probs, e->values, s);
+  }
+  az::launch_expand(e->g, e->t, e->probs, e->values, s);
+  AZ_HIP(hipGetLastError());
+  return 0;
+}
+
+int ready_to_search(az_engine* e) {
+  if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
+    return fail(AZ_E_STATE, "network evaluator selected but az_engine_set_weights was not called");
+  return 0;
+}
+
+// ------------------------------------------------------------ weight folding
+int fetch(const std::map<std::string, const az_tensor*>& m, const std::string& name,
+          int64_t numel, std::vector<double>& out) {
+  auto it = m.find(name);
+  if (it == m.end()) return fail(AZ_E_INVALID, "missing weight tensor '" + name + "'");
+  const az_tensor* t = it->second;
+  if (t->numel != numel)
+    return fail(AZ_E_INVALID, "weight '" + name + "' has " + std::to_string(t->numel) +
+                                  " elements, expected " + std::to_string(numel));
+  std::vector<float> tmp(numel);
+  if (t->on_device) {
+    AZ_HIP(hipMemcpy(tmp.data(), t->data, numel * sizeof(float), hipMemcpyDeviceToHost));
+  } else {
+    memcpy(tmp.data(), t->data, numel * sizeof(float));
+  }
+  out.assign(tmp.begin(), tmp.end());
+  return 0;
+}
+
+// InnerConvBlock (base_layers.py:20-66): conv kernel [kh][kw][cin][cout] +
+// bias, BatchNorm(gamma, beta, moving mean/var).  Returns the folded kernel in
+// Keras layout (double) and folded bias.
+int fold_unit(const std::map<std::string, const az_tensor*>& m, const std::string& u, int kk,
+              int cin, int cout, double eps, std::vector<double>& w, std::vector<double>& b) {
+  std::vector<double> gamma, beta, mean, var;
+  int rc;
+  if ((rc = fetch(m, u + ".kernel", (int64_t)kk * kk * cin * cout, w))) return rc;
+  if ((rc = fetch(m, u + ".bias", cout, b))) return rc;
+  if ((rc = fetch(m, u + ".gamma", cout, gamma))) return rc;
+  if ((rc = fetch(m, u + ".beta", cout, beta))) return rc;
+  if ((rc = fetch(m, u + ".mean", cout, mean))) return rc;
+  if ((rc = fetch(m, u + ".var", cout, var))) return rc;
+  for (int n = 0; n < cout; ++n) {
+    const double sc = gamma[n] / sqrt(var[n] + eps);
+    for (int i = 0; i < kk * kk * cin; ++i) w[(size_t)i * cout + n] *= sc;
+    b[n] = (b[n] - mean[n]) * sc + beta[n];
+  }
+  return 0;
+}
+
+int upload(az_engine* e, float** dst, const std::vector<float>& src) {
+  int rc;
+  if (!*dst && (rc = e->alloc(dst, src.size()))) return rc;
+  AZ_HIP(hipMemcpy(*dst, src.data(), src.size() * sizeof(float), hipMemcpyHostToDevice));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int az_abi_version(void) { return AZ_ABI_VERSION; }
+const char* az_last_error(void) { return g_last_error.c_str(); }
+
+int az_engine_create(int device, const az_config* cfg, az_engine** out) {
+  if (!cfg || !out) return fail(AZ_E_INVALID, "null argument");
+  const az_config& c = *cfg;
+  if (c.board_height < 2 || c.board_width < 2 || c.board_height * c.board_width > az::kMaxCells)
+    return fail(AZ_E_INVALID, "board must have 4..128 cells");
+  if (c.n < 2 || c.n > std::min(c.board_height, c.board_width))
+    return fail(AZ_E_INVALID, "need 2 <= n <= min(width, height) (connect_n/board.py:14-18)");
+  const int A = c.gravity ? c.board_width : c.board_width * c.board_height;
+  if (A > az::kMaxActions) return fail(AZ_E_INVALID, "action space too large");
+  if (c.slots < 1 || c.mcts_iterations < 1) return fail(AZ_E_INVALID, "slots and mcts_iterations must be >= 1");
+  if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC)
+    return fail(AZ_E_INVALID, "unknown evaluator");
+  if (c.evaluator == AZ_EVAL_NETWORK && c.filters != 128)
+    return fail(AZ_E_INVALID, "network evaluator supports filters == 128 (ConfigModel.filters)");
+  int dev_count = 0;
+  if (hipGetDeviceCount(&dev_count) != hipSuccess || dev_count == 0)
+    return fail(AZ_E_HIP, "no HIP device visible: libaz has no CPU fallback");
+  if (device < 0 || device >= dev_count) return fail(AZ_E_INVALID, "bad device index");
+  AZ_HIP(hipSetDevice(device));
+
+  az_engine* e = new az_engine();
+  e->device = device;
+  e->cfg = c;
+  az::GameCfg& g = e->g;
+  g.H = c.board_height;
+  g.W = c.board_width;
+  g.HW = g.H * g.W;
+  g.n = c.n;
+  g.gravity = c.gravity ? 1 : 0;
+  g.A = A;
+  g.sims = c.mcts_iterations;
+  g.greedy_ply = c.index_move_greedy;
+  g.c_puct = c.exploration_constant;
+  g.slots = c.slots;
+  g.max_depth = g.HW + 1;
+  const int64_t visits = c.max_tree_visits > 0 ? c.max_tree_visits : (int64_t)c.mcts_iterations * g.HW + 2;
+  const int64_t arena = c.arena_edges > 0 ? c.arena_edges : (int64_t)c.mcts_iterations * g.HW * A + A;
+  if (visits > (1 << 30) || arena > (1 << 30)) {
+    delete e;
+    return fail(AZ_E_INVALID, "tree bounds too large");
+  }
+  g.pow_len = (int)visits;
+  g.arena_cap = (int)arena;
+
+  auto cleanup = [&](int rc) {
+    az_engine_destroy(e);
+    return rc;
+  };
+  int rc;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(AZ_E_HIP, "hipStreamCreate failed"));
+  const size_t S = (size_t)g.slots;
+  az::TreeDev& t = e->t;
+  if ((rc = e->alloc(&t.edges, S * g.arena_cap)) || (rc = e->alloc(&t.root_board, S)) ||
+      (rc = e->alloc(&t.root_first, S)) || (rc = e->alloc(&t.root_n, S)) ||
+      (rc = e->alloc(&t.root_value, S)) || (rc = e->alloc(&t.arena_top, S)) ||
+      (rc = e->alloc(&t.ply, S)) || (rc = e->alloc(&t.game_id, S)) ||
+      (rc = e->alloc(&t.path, S * g.max_depth)) || (rc = e->alloc(&t.path_len, S)) ||
+      (rc = e->alloc(&t.slot_expansions, S)) || (rc = e->alloc(&t.mt, S * (az::kMtN + 1))) ||
+      (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_board, S)) ||
+      (rc = e->alloc(&t.eval_count, 1)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
+      (rc = e->alloc(&t.last_move, S)) || (rc = e->alloc(&t.last_status, S)) ||
+      (rc = e->alloc(&t.last_policy, S * A)))
+    return cleanup(rc);
+  double* powtab = nullptr;
+  if ((rc = e->alloc(&powtab, g.pow_len))) return cleanup(rc);
+  {
+    std::vector<double> h(g.pow_len);
+    for (int k = 0; k < g.pow_len; ++k) h[k] = k == 0 ? 0.0 : g_pow((double)k, 0.5);
+    if (hipMemcpy(powtab, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail(AZ_E_HIP, "pow table upload failed"));
+  }
+  t.powtab = powtab;
+  if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
+    return cleanup(fail(AZ_E_HIP, "memset failed"));
+  // evaluator buffers (batch = slots)
+  if ((rc = e->alloc(&e->probs, S * A)) || (rc = e->alloc(&e->values, S)) ||
+      (rc = e->alloc(&e->uniforms, S)) || (rc = e->alloc(&e->dev_i32, S)) ||
+      (rc = e->alloc(&e->dev_boards, S)))
+    return cleanup(rc);
+  if ((rc = e->alloc(&e->x, S * g.HW * 4))) return cleanup(rc);
+  if (c.evaluator == AZ_EVAL_NETWORK) {
+    const size_t act = S * g.HW * 128;
+    for (int i = 0; i < 3; ++i)
+      if ((rc = e->alloc(&e->act[i], act))) return cleanup(rc);
+  }
+  e->net.depth = c.depth;
+  e->net.hidden = c.value_hidden;
+  *out = e;
+  return 0;
+}
+
+int az_engine_destroy(az_engine* eng) {
+  if (!eng) return 0;
+  (void)hipSetDevice(eng->device);
+  if (eng->stream) (void)hipStreamSynchronize(eng->stream);
+  for (void* p : eng->sample_bufs) (void)hipFree(p);
+  for (void* p : eng->owned) (void)hipFree(p);
+  if (eng->stream) (void)hipStreamDestroy(eng->stream);
+  delete eng;
+  return 0;
+}
+
+int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
+  if (!e || (!tensors && n)) return fail(AZ_E_INVALID, "null argument");
+  AZ_HIP(hipSetDevice(e->device));
+  std::map<std::string, const az_tensor*> m;
+  for (int i = 0; i < n; ++i) {
+    if (!tensors[i].name || !tensors[i].data) return fail(AZ_E_INVALID, "tensor without name/data");
+    m[tensors[i].name] = &tensors[i];
+  }
+  const int F = 128, HW = e->g.HW, A = e->g.A, hidden = e->net.hidden;
+  const double eps = e->cfg.bn_epsilon;
+  az::NetDev& net = e->net;
+  std::vector<double> w, b, wr, br;
+  int rc;
+  // stem: [3][3][4][F] -> [tap*4 + c][F]
+  if ((rc = fold_unit(m, "stem", 3, 4, F, eps, w, b))) return rc;
+  {
+    std::vector<float> ws(36 * F), bs(F);
+    for (int i = 0; i < 36 * F; ++i) ws[i] = (float)w[i];  // Keras order == (tap, c, n)
+    for (int i = 0; i < F; ++i) bs[i] = (float)b[i];
+    if ((rc = upload(e, &net.stem_w, ws)) || (rc = upload(e, &net.stem_b, bs))) return rc;
+  }
+  net.c1_w.resize(net.depth, nullptr);
+  net.c1_b.resize(net.depth, nullptr);
+  net.c2_w.resize(net.depth, nullptr);
+  net.c2_b.resize(net.depth, nullptr);
+  for (int d = 0; d < net.depth; ++d) {
+    const std::string p = "block" + std::to_string(d);
+    if ((rc = fold_unit(m, p + ".conv1", 3, F, F, eps, w, b))) return rc;
+    std::vector<float> wt((size_t)F * 9 * F), bt(F);
+    for (int n2 = 0; n2 < F; ++n2)
+      for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
+    for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
+    if ((rc = upload(e, &net.c1_w[d], wt)) || (rc = upload(e, &net.c1_b[d], bt))) return rc;
+    if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
+    if ((rc = fold_unit(m, p + ".res", 1, F, F, eps, wr, br))) return rc;
+    std::vector<float> wt2((size_t)F * 10 * F), bt2(F);
+    for (int n2 = 0; n2 < F; ++n2) {
+      for (int k = 0; k < 9 * F; ++k) wt2[(size_t)n2 * 10 * F + k] = (float)w[(size_t)k * F + n2];
+      for (int c = 0; c < F; ++c) wt2[(size_t)n2 * 10 * F + 9 * F + c] = (float)wr[(size_t)c * F + n2];
+    }
+    for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
+    if ((rc = upload(e, &net.c2_w[d], wt2)) || (rc = upload(e, &net.c2_b[d], bt2))) return rc;
+  }
+  // heads
+  if ((rc = fold_unit(m, "policy.conv", 1, F, 2, eps, w, b))) return rc;
+  {
+    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    if ((rc = upload(e, &net.pc_w, a)) || (rc = upload(e, &net.pc_b, c))) return rc;
+  }
+  if ((rc = fold_unit(m, "value.conv", 1, F, 1, eps, w, b))) return rc;
+  {
+    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    if ((rc = upload(e, &net.vc_w, a)) || (rc = upload(e, &net.vc_b, c))) return rc;
+  }
+  struct DenseSpec {
+    const char* name;
+    int in, out;
+    float** w;
+    float** b;
+  } dense[] = {{"policy.dense", 2 * HW, A, &net.pd_w, &net.pd_b},
+               {"value.dense1", HW, hidden, &net.v1_w, &net.v1_b},
+               {"value.dense2", hidden, 1, &net.v2_w, &net.v2_b}};
+  for (auto& ds : dense) {
+    if ((rc = fetch(m, std::string(ds.name) + ".kernel", (int64_t)ds.in * ds.out, w))) return rc;
+    if ((rc = fetch(m, std::string(ds.name) + ".bias", ds.out, b))) return rc;
+    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    if ((rc = upload(e, ds.w, a)) || (rc = upload(e, ds.b, c))) return rc;
+  }
+  net.ready = true;
+  return 0;
+}
+
+int az_encode(az_engine* e, const int8_t* boards, int n, float* state, uint8_t* mask) {
+  if (!e || n < 0 || (n && !boards)) return fail(AZ_E_INVALID, "bad arguments");
+  AZ_HIP(hipSetDevice(e->device));
+  const int HW = e->g.HW, A = e->g.A;
+  const int chunk = e->g.slots;
+  std::vector<az::Board> hb(std::min(n, chunk));
+  uint8_t* dmask = reinterpret_cast<uint8_t*>(e->probs);  // slots*A floats >= slots*A bytes
+  for (int off = 0; off < n; off += chunk) {
+    const int m = std::min(chunk, n - off);
+    for (int i = 0; i < m; ++i) hb[i] = board_from_cells(boards + (size_t)(off + i) * HW, HW);
+    AZ_HIP(hipMemcpyAsync(e->dev_boards, hb.data(), m * sizeof(az::Board), hipMemcpyHostToDevice, e->stream));
+    if (state) {
+      az::launch_encode(e->dev_boards, nullptr, m, HW, e->x, e->stream);
+      AZ_HIP(hipMemcpyAsync(state + (size_t)off * HW * 4, e->x, (size_t)m * HW * 4 * sizeof(float),
+                            hipMemcpyDeviceToHost, e->stream));
+    }
+    if (mask) {
+      az::launch_legal_mask(e->dev_boards, m, e->g, dmask, e->stream);
+      AZ_HIP(hipMemcpyAsync(mask + (size_t)off * A, dmask, (size_t)m * A, hipMemcpyDeviceToHost, e->stream));
+    }
+    AZ_HIP(hipStreamSynchronize(e->stream));
+  }
+  return 0;
+}
+
+int az_forward(az_engine* e, const float* x, int n, float* probs, float* values) {
+  if (!e || n < 0 || (n && (!x || !probs || !values))) return fail(AZ_E_INVALID, "bad arguments");
+  if (!e->net.ready) return fail(AZ_E_STATE, "az_engine_set_weights was not called");
+  AZ_HIP(hipSetDevice(e->device));
+  const int HW = e->g.HW, A = e->g.A, chunk = e->g.slots;
+  for (int off = 0; off < n; off += chunk) {
+    const int m = std::min(chunk, n - off);
+    AZ_HIP(hipMemcpyAsync(e->x, x + (size_t)off * HW * 4, (size_t)m * HW * 4 * sizeof(float),
+                          hipMemcpyHostToDevice, e->stream));
+    az::launch_forward(e->net, e->x, nullptr, m, e->g.H, e->g.W, A, e->act[0], e->act[1], e->act[2],
+                       e->probs, e->values, e->stream, nullptr);
+    AZ_HIP(hipGetLastError());
+    AZ_HIP(hipMemcpyAsync(probs + (size_t)off * A, e->probs, (size_t)m * A * sizeof(float),
+                          hipMemcpyDeviceToHost, e->stream));
+    AZ_HIP(hipMemcpyAsync(values + off, e->values, (size_t)m * sizeof(float), hipMemcpyDeviceToHost,
+                          e->stream));
+    AZ_HIP(hipStreamSynchronize(e->stream));
+  }
+  return 0;
+}
+
+int az_stats_get(az_engine* e, az_stats* st) {
+  if (!e || !st) return fail(AZ_E_INVALID, "null argument");
+  AZ_HIP(hipSetDevice(e->device));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  unsigned long long h[az::kStatCount];
+  AZ_HIP(hipMemcpy(h, e->t.stats, sizeof(h), hipMemcpyDeviceToHost));
+  std::vector<int64_t> gid(e->g.slots);
+  AZ_HIP(hipMemcpy(gid.data(), e->t.game_id, gid.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+  memset(st, 0, sizeof(*st));
+  st->expansions = (int64_t)h[az::kStatExpansions];
+  st->terminal_visits = (int64_t)h[az::kStatTerminal];
+  st->games_done = (int64_t)h[az::kStatGamesDone];
+  st->simulations = (int64_t)h[az::kStatSims];
+  st->plies = (int64_t)h[az::kStatPlies];
+  st->errors = (int64_t)h[az::kStatErrors];
+  st->active_slots = std::count_if(gid.begin(), gid.end(), [](int64_t v) { return v >= 0; });
+  e->timer.flush();
+  st->conv_ms = e->timer.total_ms;
+  st->conv_launches = e->timer.launches;
+  return 0;
+}
+
+int az_timer_enable(az_engine* e, int on) {
+  if (!e) return fail(AZ_E_INVALID, "null engine");
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  e->timer.flush();
+  e->timer.reset();
+  e->timer.enabled = on != 0;
+  return 0;
+}
+
+int az_pow_table(az_engine* e, double* out, int64_t n) {
+  if (!e || !out || n < 0 || n > e->g.pow_len) return fail(AZ_E_INVALID, "bad arguments");
+  AZ_HIP(hipMemcpy(out, e->t.powtab, n * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ------------------------------------------------------------------ self-play
+int az_selfplay_begin(az_engine* e, int64_t first_game, int64_t n_games, uint32_t base_seed) {
+  if (!e || n_games < 0 || first_game < 0) return fail(AZ_E_INVALID, "bad arguments");
+  int rc;
+  if ((rc = ready_to_search(e))) return rc;
+  AZ_HIP(hipSetDevice(e->device));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  for (void* p : e->sample_bufs) (void)hipFree(p);
+  e->sample_bufs.clear();
+  az::SampleDev& smp = e->smp;
+  smp = az::SampleDev{};
+  smp.first_game = first_game;
+  smp.n_games = n_games;
+  smp.base_seed = base_seed;
+  const size_t G = (size_t)std::max<int64_t>(n_games, 1), P = (size_t)e->g.HW, A = (size_t)e->g.A;
+  auto get = [&](void** p, size_t bytes) -> int {
+    AZ_HIP(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    e->sample_bufs.push_back(*p);
+    AZ_HIP(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 16), e->stream));
+    return 0;
+  };
+  if ((rc = get((void**)&smp.boards, G * P * sizeof(az::Board))) ||
+      (rc = get((void**)&smp.policy, G * P * A * sizeof(double))) ||
+      (rc = get((void**)&smp.moves, G * P * sizeof(int16_t))) ||
+      (rc = get((void**)&smp.length, G * sizeof(int32_t))) ||
+      (rc = get((void**)&smp.result, G * sizeof(int32_t))) ||
+      (rc = get((void**)&smp.expansions, G * sizeof(int32_t))))
+    return rc;
+  unsigned long long st[az::kStatCount] = {0};
+  const int64_t first_wave = std::min<int64_t>(n_games, e->g.slots);
+  st[az::kStatNextGame] = (unsigned long long)(first_game + first_wave);
+  AZ_HIP(hipMemcpyAsync(e->t.stats, st, sizeof(st), hipMemcpyHostToDevice, e->stream));
+  az::launch_slot_init(e->g, e->t, smp, first_wave, e->stream);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  e->sp_first = first_game;
+  e->sp_n = n_games;
+  return 0;
+}
+
+int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
+  if (!e || n_moves < 0) return fail(AZ_E_INVALID, "bad arguments");
+  int rc;
+  if ((rc = ready_to_search(e))) return rc;
+  AZ_HIP(hipSetDevice(e->device));
+  for (int mv = 0; mv < n_moves; ++mv) {
+    for (int s = 0; s < e->g.sims; ++s)
+      if ((rc = simulate(e))) return rc;
+    az::launch_play(e->g, e->t, e->smp, nullptr, -1, 0, 1, e->stream);
+    AZ_HIP(hipGetLastError());
+  }
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  if ((rc = check_device_errors(e))) return rc;
+  if (st) return az_stats_get(e, st);
+  return 0;
+}
+
+int az_selfplay_run(az_engine* e, int64_t first_game, int64_t n_games, uint32_t base_seed,
+                    az_stats* st) {
+  int rc;
+  if ((rc = az_selfplay_begin(e, first_game, n_games, base_seed))) return rc;
+  az_stats tmp;
+  for (;;) {
+    if ((rc = az_selfplay_step(e, 1, &tmp))) return rc;
+    if (tmp.active_slots == 0) break;
+  }
+  if (st) *st = tmp;
+  return 0;
+}
+
+int az_selfplay_results(az_engine* e, int32_t* lengths, int32_t* results, int32_t* expansions,
+                        int8_t* boards, double* policies, int32_t* moves) {
+  if (!e) return fail(AZ_E_INVALID, "null engine");
+  AZ_HIP(hipSetDevice(e->device));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  const size_t G = (size_t)e->sp_n, P = (size_t)e->g.HW, A = (size_t)e->g.A, HW = (size_t)e->g.HW;
+  if (G == 0) return 0;
+  const az::SampleDev& smp = e->smp;
+  if (lengths) AZ_HIP(hipMemcpy(lengths, smp.length, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (results) AZ_HIP(hipMemcpy(results, smp.result, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (expansions) AZ_HIP(hipMemcpy(expansions, smp.expansions, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (policies) AZ_HIP(hipMemcpy(policies, smp.policy, G * P * A * sizeof(double), hipMemcpyDeviceToHost));
+  if (boards) {
+    std::vector<az::Board> hb(G * P);
+    AZ_HIP(hipMemcpy(hb.data(), smp.boards, hb.size() * sizeof(az::Board), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < hb.size(); ++i) cells_from_board(hb[i], (int)HW, boards + i * HW);
+  }
+  if (moves) {
+    std::vector<int16_t> hm(G * P);
+    AZ_HIP(hipMemcpy(hm.data(), smp.moves, hm.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < hm.size(); ++i) moves[i] = hm[i];
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ tree API
+int az_tree_reset(az_engine* e, int n, const int32_t* slots, const int8_t* boards) {
+  if (!e || n < 0 || n > e->g.slots || (n && (!slots || !boards))) return fail(AZ_E_INVALID, "bad arguments");
+  AZ_HIP(hipSetDevice(e->device));
+  std::vector<az::Board> hb(n);
+  for (int i = 0; i < n; ++i) {
+    if (slots[i] < 0 || slots[i] >= e->g.slots) return fail(AZ_E_INVALID, "slot out of range");
+    hb[i] = board_from_cells(boards + (size_t)i * e->g.HW, e->g.HW);
+  }
+  e->smp = az::SampleDev{};
+  AZ_HIP(hipMemcpyAsync(e->dev_i32, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+  AZ_HIP(hipMemcpyAsync(e->dev_boards, hb.data(), n * sizeof(az::Board), hipMemcpyHostToDevice, e->stream));
+  az::launch_slot_set_root(e->g, e->t, e->dev_i32, e->dev_boards, n, e->stream);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int az_tree_search(az_engine* e, int n_sims) {
+  if (!e || n_sims < 0) return fail(AZ_E_INVALID, "bad arguments");
+  int rc;
+  if ((rc = ready_to_search(e))) return rc;
+  AZ_HIP(hipSetDevice(e->device));
+  for (int s = 0; s < n_sims; ++s)
+    if ((rc = simulate(e))) return rc;
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  return check_device_errors(e);
+}
+
+int az_tree_play(az_engine* e, const double* uniforms, int greedy, int deterministic,
+                 int32_t* moves, int32_t* status, double* policy) {
+  if (!e || (!deterministic && !uniforms)) return fail(AZ_E_INVALID, "bad arguments");
+  AZ_HIP(hipSetDevice(e->device));
+  const size_t S = (size_t)e->g.slots;
+  if (!deterministic)
+    AZ_HIP(hipMemcpyAsync(e->uniforms, uniforms, S * sizeof(double), hipMemcpyHostToDevice, e->stream));
+  AZ_HIP(hipMemsetAsync(e->t.last_move, 0xff, S * sizeof(int32_t), e->stream));
+  az::SampleDev none{};
+  az::launch_play(e->g, e->t, none, deterministic ? nullptr : e->uniforms, greedy ? 1 : 0,
+                  deterministic, 0, e->stream);
+  AZ_HIP(hipGetLastError());
+  if (moves) AZ_HIP(hipMemcpyAsync(moves, e->t.last_move, S * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  if (status) AZ_HIP(hipMemcpyAsync(status, e->t.last_status, S * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  if (policy)
+    AZ_HIP(hipMemcpyAsync(policy, e->t.last_policy, S * e->g.A * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  return check_device_errors(e);
+}
+
+int az_tree_info(az_engine* e, int slot, int64_t* info, float* root_value) {
+  if (!e || !info || slot < 0 || slot >= e->g.slots) return fail(AZ_E_INVALID, "bad arguments");
+  AZ_HIP(hipSetDevice(e->device));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  int32_t top, first, cnt, ply;
+  int64_t gid;
+  AZ_HIP(hipMemcpy(&top, e->t.arena_top + slot, 4, hipMemcpyDeviceToHost));
+  AZ_HIP(hipMemcpy(&first, e->t.root_first + slot, 4, hipMemcpyDeviceToHost));
+  AZ_HIP(hipMemcpy(&cnt, e->t.root_n + slot, 4, hipMemcpyDeviceToHost));
+  AZ_HIP(hipMemcpy(&ply, e->t.ply + slot, 4, hipMemcpyDeviceToHost));
+  AZ_HIP(hipMemcpy(&gid, e->t.game_id + slot, 8, hipMemcpyDeviceToHost));
+  if (root_value) AZ_HIP(hipMemcpy(root_value, e->t.root_value + slot, 4, hipMemcpyDeviceToHost));
+  info[0] = top;
+  info[1] = first;
+  info[2] = cnt;
+  info[3] = ply;
+  info[4] = gid >= 0;
+  return 0;
+}
+
+int az_tree_export(az_engine* e, int slot, double* prior, double* w, int32_t* n, int32_t* child,
+                   int32_t* child_n, int32_t* action, float* child_value) {
+  if (!e || slot < 0 || slot >= e->g.slots) return fail(AZ_E_INVALID, "bad arguments");
+  AZ_HIP(hipSetDevice(e->device));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  int32_t top;
+  AZ_HIP(hipMemcpy(&top, e->t.arena_top + slot, 4, hipMemcpyDeviceToHost));
+  std::vector<az::Edge> h(top);
+  if (top)
+    AZ_HIP(hipMemcpy(h.data(), e->t.edges + (size_t)slot * e->g.arena_cap, top * sizeof(az::Edge),
+                     hipMemcpyDeviceToHost));
+  for (int i = 0; i < top; ++i) {
+    if (prior) prior[i] = h[i].prior;
+    if (w) w[i] = h[i].W;
+    if (n) n[i] = h[i].N;
+    if (child) child[i] = h[i].child;
+    if (child_n) child_n[i] = h[i].child_n;
+    if (action) action[i] = h[i].action;
+    if (child_value) child_value[i] = h[i].child_value;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+// az_nn.h -- device-side network weights and the forward launchers.
+#pragma once
+#include <vector>
+
+#include "az_device.h"
+
+namespace az {
+
+// Folded (BatchNorm-in) fp32 weights resident in HBM.  Layouts are chosen for
+// the kernels, not copied from Keras: conv weights are [Cout][K] with K
+// contiguous (K = tap*Cin + c), so a 32-wide K chunk of 128 output channels is
+// a [128][32] tile loaded with 16-byte reads.
+struct NetDev {
+  int filters = 128, depth = 0, hidden = 256;
+  float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c)
+  float* stem_b = nullptr;  // [F]
+  std::vector<float*> c1_w, c1_b;  // [F][9F], [F]
+  std::vector<float*> c2_w, c2_b;  // [F][10F] (conv2 taps, then 1x1 residual), [F]
+  float *pc_w = nullptr, *pc_b = nullptr;  // policy conv [F][2], [2]
+  float *vc_w = nullptr, *vc_b = nullptr;  // value conv [F], [1]
+  float *pd_w = nullptr, *pd_b = nullptr;  // policy dense [2HW][A], [A]
+  float *v1_w = nullptr, *v1_b = nullptr;  // value dense1 [HW][hidden], [hidden]
+  float *v2_w = nullptr, *v2_b = nullptr;  // value dense2 [hidden], [1]
+  bool ready = false;
+};
+
+// hipEvent pairs around the conv launches of every forward while enabled, so
+// bench.py can price the dominant kernel live (roofline.achieved).
+struct ConvTimer {
+  bool enabled = false;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  double total_ms = 0.0;
+  long long launches = 0;
+  void begin(hipStream_t s) {
+    if (!enabled) return;
+    if (used + 2 > pool.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        pool.push_back(e);
+      }
+    }
+    (void)hipEventRecord(pool[used++], s);
+  }
+  void end(hipStream_t s, int n_launches) {
+    if (!enabled) return;
+    (void)hipEventRecord(pool[used++], s);
+    launches += n_launches;
+  }
+  // call after a stream synchronize: folds recorded pairs into total_ms
+  void flush() {
+    for (size_t i = 0; i + 1 < used; i += 2) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, pool[i], pool[i + 1]);
+      total_ms += ms;
+    }
+    used = 0;
+  }
+  void reset() {
+    used = 0;
+    total_ms = 0.0;
+    launches = 0;
+  }
+  ~ConvTimer() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+void launch_encode(const Board* boards, const int* count, int n_max, int HW, float* x,
+                   hipStream_t s);
+void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* mask,
+                       hipStream_t s);
+// x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
+void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
+                    int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
+                    hipStream_t s, ConvTimer* timer);
+
+}  // namespace az

@@ -1,0 +1,88 @@
+// az_tree.h -- device-resident MCTS forest: one tree per game slot.
+#pragma once
+#include "az_device.h"
+
+namespace az {
+
+// One tree edge (reference UCTEdge, mcts/mcts.py:22-33) = 32 bytes.  A node
+// is implicit: the contiguous run of edges its expansion allocated.  Child
+// boards are not stored; select() replays the path's moves from the root
+// board (board rules are cheap, HBM bytes are not).
+struct Edge {
+  double W;           // total_action_value (float64, += in path order)
+  double prior;       // float32 prior widened exactly, or the float64 1/n uniform
+  int32_t N;          // visit_count
+  int32_t child;      // first edge of the child's expansion, kNoChild if leaf
+  int16_t child_n;    // child's edge count (0 = unexpanded or terminal)
+  int16_t action;     // index into all_possible_moves
+  float child_value;  // child's evaluated_value (tree export only)
+};
+static_assert(sizeof(Edge) == 32, "Edge must stay 32 bytes");
+
+// Counters/stat words (unsigned long long, device).
+enum : int {
+  kStatExpansions = 0,   // evaluate_and_expand calls
+  kStatTerminal = 1,     // terminal leaf visits
+  kStatGamesDone = 2,
+  kStatErrors = 3,       // bit flags below
+  kStatSims = 4,         // per-slot simulations
+  kStatPlies = 5,
+  kStatNextGame = 6,     // next game id to hand to a free slot
+  kStatCount = 8
+};
+enum : unsigned long long {
+  kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16
+};
+
+// All device state of a forest (struct of arrays over slots).
+struct TreeDev {
+  Edge* edges;                 // [slots][arena_cap]
+  Board* root_board;           // [slots]
+  int32_t* root_first;         // [slots]
+  int32_t* root_n;             // [slots]
+  float* root_value;           // [slots]
+  int32_t* arena_top;          // [slots]
+  int32_t* ply;                // [slots] (Board.fullmove_number)
+  int64_t* game_id;            // [slots], -1 = idle
+  int32_t* path;               // [slots][max_depth]
+  int32_t* path_len;           // [slots]
+  int32_t* slot_expansions;    // [slots], this game's expansions so far
+  uint32_t* mt;                // [625][slots], word-major MT19937 state (+ index)
+  int32_t* eval_slot;          // [slots] compacted eval queue
+  Board* eval_board;           // [slots]
+  int32_t* eval_count;         // [1]
+  unsigned long long* stats;   // [kStatCount]
+  const double* powtab;        // [pow_len]: libm pow(n, 0.5), host-built
+  // per-move outputs (MCTS API play())
+  int32_t* last_move;          // [slots] action played (-1 none)
+  int32_t* last_status;        // [slots] 0 ongoing / 1 win / 2 draw
+  double* last_policy;         // [slots][A]
+};
+
+// Self-play sample sink, indexed by game id - first_game.
+struct SampleDev {
+  int64_t first_game = 0, n_games = 0;
+  uint32_t base_seed = 0;
+  Board* boards = nullptr;     // [n_games][max_plies]: root board before each move
+  double* policy = nullptr;    // [n_games][max_plies][A]
+  int16_t* moves = nullptr;    // [n_games][max_plies]
+  int32_t* length = nullptr;   // [n_games]
+  int32_t* result = nullptr;   // [n_games]: get_result(keep_same_player=True)
+  int32_t* expansions = nullptr;  // [n_games]
+};
+
+void launch_select(const GameCfg& g, const TreeDev& t, hipStream_t s);
+void launch_synth_eval(const GameCfg& g, const TreeDev& t, float* probs, float* values,
+                       hipStream_t s);
+void launch_expand(const GameCfg& g, const TreeDev& t, const float* probs, const float* values,
+                   hipStream_t s);
+// uniforms: device [slots] draws for play (MCTS API), or null -> per-slot MT19937;
+// greedy_mode -1 = by ply (self-play), 0/1 = caller's flag
+void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const double* uniforms,
+                 int greedy_mode, int deterministic, int refill, hipStream_t s);
+void launch_slot_init(const GameCfg& g, const TreeDev& t, const SampleDev& smp, int64_t n_first,
+                      hipStream_t s);
+void launch_slot_set_root(const GameCfg& g, const TreeDev& t, const int32_t* slots,
+                          const Board* boards, int n, hipStream_t s);
+
+}  // namespace az

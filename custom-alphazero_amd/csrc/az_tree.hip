@@ -1,0 +1,373 @@
+// az_tree.hip -- lockstep PUCT search over a forest of game trees on gfx950.
+//
+// One lane = one game slot.  Per simulation the engine launches
+//   select  (PUCT descent, terminal backups, eval-queue compaction)
+//   -> evaluator (network forward or synthetic) on the compacted queue
+//   -> expand  (mask + normalise priors, allocate edges, backup).
+// After `sims` simulations, `play` commits one move per slot.
+//
+// Arithmetic contract (bit-exact with the reference under numpy<2 legacy
+// promotion):
+//   UCB   = Q + U, Q = W/N or 0.0, U = ((1.5*prior)*pow(sumN,0.5))/(1+N), all
+//           IEEE f64, no contraction (this file builds with -ffp-contract=off);
+//           pow(sumN, 0.5) comes from a host-built libm table (mcts.py:50 is
+//           Python `** 0.5`, i.e. libm pow, which differs from sqrt at 2921...)
+//   best  = first maximum (np.argmax, mcts.py:64-68)
+//   prior = float32 pairwise sum + float32 divide, or float64 1/n uniform
+//   W    += v in path order leaf->root with v negated per level (mcts.py:163-168)
+//   move  = cumsum / last / searchsorted-right on one legacy random_sample
+#include "az_tree.h"
+
+namespace az {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ void stat_add(const TreeDev& t, int which, unsigned long long v) {
+  atomicAdd(t.stats + which, v);
+}
+__device__ __forceinline__ void flag_error(const TreeDev& t, unsigned long long f) {
+  atomicOr(t.stats + kStatErrors, f);
+}
+
+__device__ __forceinline__ void backup(Edge* E, const int32_t* path, int depth, double v) {
+  for (int d = depth - 1; d >= 0; --d) {
+    Edge& e = E[path[d]];
+    e.N += 1;
+    e.W += v;
+    v = -v;
+  }
+}
+
+// MT19937, state word-major: word w of slot g at mt[w * slots + g].
+__device__ void mt_seed(const TreeDev& t, int slots, int g, uint32_t seed) {
+  uint32_t prev = seed;
+  t.mt[g] = seed;
+  for (int i = 1; i < kMtN; ++i) {
+    prev = 1812433253u * (prev ^ (prev >> 30)) + (uint32_t)i;
+    t.mt[(size_t)i * slots + g] = prev;
+  }
+  t.mt[(size_t)kMtN * slots + g] = kMtN;  // force a twist on first use
+}
+
+__device__ uint32_t mt_next(const TreeDev& t, int slots, int g) {
+  uint32_t* m = t.mt;
+  uint32_t pos = m[(size_t)kMtN * slots + g];
+  if (pos >= (uint32_t)kMtN) {
+    for (int i = 0; i < kMtN; ++i) {
+      const uint32_t y = (m[(size_t)i * slots + g] & 0x80000000u) |
+                         (m[(size_t)((i + 1) % kMtN) * slots + g] & 0x7fffffffu);
+      m[(size_t)i * slots + g] =
+          m[(size_t)((i + 397) % kMtN) * slots + g] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    pos = 0;
+  }
+  const uint32_t y = m[(size_t)pos * slots + g];
+  m[(size_t)kMtN * slots + g] = pos + 1;
+  return mt_temper(y);
+}
+
+// legacy random_sample: ((a >> 5) * 2^26 + (b >> 6)) / 2^53
+__device__ double mt_uniform(const TreeDev& t, int slots, int g) {
+  const uint32_t a = mt_next(t, slots, g) >> 5;
+  const uint32_t b = mt_next(t, slots, g) >> 6;
+  return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+
+__device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gid,
+                           uint32_t seed) {
+  Board b;
+  b.own[0] = b.own[1] = b.opp[0] = b.opp[1] = 0;
+  t.root_board[s] = b;
+  t.root_first[s] = 0;
+  t.root_n[s] = 0;
+  t.root_value[s] = 0.f;
+  t.arena_top[s] = 0;
+  t.ply[s] = 0;
+  t.path_len[s] = 0;
+  t.slot_expansions[s] = 0;
+  t.game_id[s] = gid;
+  t.last_move[s] = -1;
+  t.last_status[s] = kOngoing;
+  mt_seed(t, g.slots, s, seed);
+}
+
+// ------------------------------------------------------------------- select
+// MCTS.select (mcts.py:111-120) + the terminal branch of MCTS.search
+// (mcts.py:176-180).  Non-terminal leaves are appended to the eval queue.
+__global__ __launch_bounds__(256) void select_kernel(GameCfg g, TreeDev t) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.slots || t.game_id[s] < 0) return;
+  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  int32_t* path = t.path + (size_t)s * g.max_depth;
+  Board b = t.root_board[s];
+  int first = t.root_first[s], cnt = t.root_n[s];
+  int depth = 0, status = kOngoing;
+  while (cnt > 0) {
+    int sum = 0;
+    for (int i = 0; i < cnt; ++i) sum += E[first + i].N;
+    if (sum >= g.pow_len) {
+      flag_error(t, kErrPow);
+      return;
+    }
+    const double sq = t.powtab[sum];
+    int best = 0;
+    double best_v = 0.0;
+    for (int i = 0; i < cnt; ++i) {
+      const Edge e = E[first + i];
+      const double q = e.N ? e.W / (double)e.N : 0.0;
+      const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
+      const double ucb = q + u;
+      if (i == 0 || ucb > best_v) {
+        best = i;
+        best_v = ucb;
+      }
+    }
+    if (depth >= g.max_depth) {
+      flag_error(t, kErrPath);
+      return;
+    }
+    const Edge& e = E[first + best];
+    path[depth++] = first + best;
+    status = play(g, b, e.action);
+    if (status < 0) {
+      flag_error(t, kErrIllegal);
+      return;
+    }
+    first = e.child;
+    cnt = e.child_n;
+  }
+  stat_add(t, kStatSims, 1);
+  if (depth > 0 && status != kOngoing) {
+    // get_result(keep_same_player=True): 1 for the player who just moved, 0 draw
+    backup(E, path, depth, status == kWin ? 1.0 : 0.0);
+    stat_add(t, kStatTerminal, 1);
+    return;
+  }
+  const int q = atomicAdd(t.eval_count, 1);
+  t.eval_slot[q] = s;
+  t.eval_board[q] = b;
+  t.path_len[s] = depth;
+}
+
+// ------------------------------------------------------ synthetic evaluator
+__global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, TreeDev t,
+                                                         float* __restrict__ probs,
+                                                         float* __restrict__ values) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *t.eval_count) return;
+  synth_eval(t.eval_board[i], g.A, probs + (size_t)i * g.A, values + i);
+}
+
+// ------------------------------------------------------------------- expand
+// MCTS.evaluate_and_expand (mcts.py:145-161) with normalize_probabilities
+// (mcts/utils.py:4-16), then backup(-value) (mcts.py:175, 163-168).
+template <int MAXA>
+__global__ __launch_bounds__(256) void expand_kernel(GameCfg g, TreeDev t,
+                                                     const float* __restrict__ probs,
+                                                     const float* __restrict__ values) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *t.eval_count) return;
+  const int s = t.eval_slot[i];
+  const Board b = t.eval_board[i];
+  const float* p = probs + (size_t)i * g.A;
+  const float v = values[i];
+  float masked[MAXA];
+  int nl = 0;
+  for (int a = 0; a < g.A; ++a)
+    if (action_cell(g, b, a) >= 0) masked[nl++] = p[a];
+  int moves[MAXA];
+  const int nm = moves_order(g, b, moves);
+  const float sum = pairwise_sum_f32(masked, nl);
+  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  const int first = t.arena_top[s];
+  if (first + nm > g.arena_cap) {
+    flag_error(t, kErrArena);
+    return;
+  }
+  for (int k = 0; k < nm; ++k) {
+    Edge e;
+    e.W = 0.0;
+    // zip(probabilities, board.moves) pairs priors (action order) with moves
+    // (moves order) by position -- mcts.py:151; identical orders with gravity
+    e.prior = sum == 0.0f ? 1.0 / (double)nl : (double)(masked[k] / sum);
+    e.N = 0;
+    e.child = kNoChild;
+    e.child_n = 0;
+    e.action = (int16_t)moves[k];
+    e.child_value = 0.f;
+    E[first + k] = e;
+  }
+  t.arena_top[s] = first + nm;
+  const int depth = t.path_len[s];
+  const int32_t* path = t.path + (size_t)s * g.max_depth;
+  if (depth == 0) {
+    t.root_first[s] = first;
+    t.root_n[s] = nm;
+    t.root_value[s] = v;
+  } else {
+    Edge& pe = E[path[depth - 1]];
+    pe.child = first;
+    pe.child_n = (int16_t)nm;
+    pe.child_value = v;
+  }
+  backup(E, path, depth, -(double)v);
+  t.slot_expansions[s] += 1;
+  stat_add(t, kStatExpansions, 1);
+}
+
+// --------------------------------------------------------------------- play
+// MCTS.play (mcts.py:182-222) and the self_play.play_game move loop
+// (self_play.py:59-67): greedy one-hot from fullmove_number >= index_move_greedy,
+// else normalised visit counts; one uniform per move even when greedy.
+template <int MAXA>
+__global__ __launch_bounds__(256) void play_kernel(GameCfg g, TreeDev t, SampleDev smp,
+                                                   const double* __restrict__ uniforms,
+                                                   int greedy_mode, int deterministic, int refill) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.slots || t.game_id[s] < 0) return;
+  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  const int first = t.root_first[s], cnt = t.root_n[s];
+  if (cnt <= 0) {
+    flag_error(t, kErrNoRoot);
+    return;
+  }
+  const int ply = t.ply[s];
+  // greedy_mode < 0: self_play's rule fullmove_number >= index_move_greedy
+  // (self_play.py:62); 0/1: the caller's MCTS.play(greedy=...) argument
+  const bool greedy = greedy_mode < 0 ? ply >= g.greedy_ply : greedy_mode != 0;
+  double pr[MAXA];
+  if (greedy) {
+    int best = 0;
+    for (int i = 1; i < cnt; ++i)
+      if (E[first + i].N > E[first + best].N) best = i;
+    for (int i = 0; i < cnt; ++i) pr[i] = i == best ? 1.0 : 0.0;
+  } else {
+    double c[MAXA];
+    for (int i = 0; i < cnt; ++i) c[i] = (double)E[first + i].N;
+    const double sum = pairwise_sum_f64(c, cnt);
+    for (int i = 0; i < cnt; ++i) pr[i] = sum == 0.0 ? 1.0 / (double)cnt : c[i] / sum;
+  }
+  int k;
+  if (deterministic) {
+    k = 0;
+    for (int i = 1; i < cnt; ++i)
+      if (pr[i] > pr[k]) k = i;
+  } else {
+    const double u = uniforms ? uniforms[s] : mt_uniform(t, g.slots, s);
+    double cdf[MAXA];
+    double acc = 0.0;
+    for (int i = 0; i < cnt; ++i) {
+      acc += pr[i];
+      cdf[i] = acc;
+    }
+    const double last = cdf[cnt - 1];
+    k = 0;
+    for (int i = 0; i < cnt; ++i)
+      if (cdf[i] / last <= u) k = i + 1;
+  }
+  const Edge chosen = E[first + k];
+  double* lp = t.last_policy + (size_t)s * g.A;
+  for (int a = 0; a < g.A; ++a) lp[a] = 0.0;
+  for (int i = 0; i < cnt; ++i) lp[E[first + i].action] = pr[i];
+  const int64_t gid = t.game_id[s];
+  const bool record = smp.n_games > 0 && gid >= smp.first_game && gid < smp.first_game + smp.n_games;
+  if (record) {
+    const size_t gi = (size_t)(gid - smp.first_game);
+    const size_t si = gi * g.HW + ply;
+    smp.boards[si] = t.root_board[s];
+    smp.moves[si] = (int16_t)chosen.action;
+    double* pol = smp.policy + si * g.A;
+    for (int a = 0; a < g.A; ++a) pol[a] = lp[a];
+  }
+  Board b = t.root_board[s];
+  const int status = play(g, b, chosen.action);
+  t.root_board[s] = b;
+  t.root_first[s] = chosen.child;
+  t.root_n[s] = chosen.child_n;
+  t.root_value[s] = chosen.child_value;
+  t.ply[s] = ply + 1;
+  t.last_move[s] = chosen.action;
+  t.last_status[s] = status;
+  stat_add(t, kStatPlies, 1);
+  if (status == kOngoing) return;
+  if (record) {
+    const size_t gi = (size_t)(gid - smp.first_game);
+    smp.length[gi] = ply + 1;
+    smp.result[gi] = status == kWin ? 1 : 0;
+    smp.expansions[gi] = t.slot_expansions[s];
+  }
+  stat_add(t, kStatGamesDone, 1);
+  if (!refill) {
+    t.game_id[s] = -1;
+    return;
+  }
+  const unsigned long long nid = atomicAdd(t.stats + kStatNextGame, 1ull);
+  if ((int64_t)nid < smp.first_game + smp.n_games)
+    slot_reset(g, t, s, (int64_t)nid, (uint32_t)(smp.base_seed + (uint64_t)nid));
+  else
+    t.game_id[s] = -1;
+}
+
+// First n_first slots get games first_game .. first_game+n_first-1; the rest idle.
+__global__ void slot_init_kernel(GameCfg g, TreeDev t, SampleDev smp, int64_t n_first) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.slots) return;
+  if (s < n_first) {
+    const int64_t gid = smp.first_game + s;
+    slot_reset(g, t, s, gid, (uint32_t)(smp.base_seed + (uint64_t)gid));
+  } else {
+    t.game_id[s] = -1;
+  }
+}
+
+// MCTS API: fresh tree on a given root board (the MCTS constructor,
+// mcts.py:89-106), game id = slot index, no sample recording.
+__global__ void slot_set_root_kernel(GameCfg g, TreeDev t, const int32_t* slots,
+                                     const Board* boards, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = slots[i];
+  slot_reset(g, t, s, s, 0u);
+  t.root_board[s] = boards[i];
+}
+
+// ---------------------------------------------------------------- launchers
+static inline int blocks_for(int n) { return (n + 255) / 256; }
+
+void launch_select(const GameCfg& g, const TreeDev& t, hipStream_t s) {
+  select_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t);
+}
+
+void launch_synth_eval(const GameCfg& g, const TreeDev& t, float* probs, float* values,
+                       hipStream_t s) {
+  synth_eval_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, probs, values);
+}
+
+void launch_expand(const GameCfg& g, const TreeDev& t, const float* probs, const float* values,
+                   hipStream_t s) {
+  if (g.A <= 16)
+    expand_kernel<16><<<blocks_for(g.slots), 256, 0, s>>>(g, t, probs, values);
+  else
+    expand_kernel<kMaxActions><<<blocks_for(g.slots), 256, 0, s>>>(g, t, probs, values);
+}
+
+void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const double* uniforms,
+                 int greedy_mode, int deterministic, int refill, hipStream_t s) {
+  if (g.A <= 16)
+    play_kernel<16><<<blocks_for(g.slots), 256, 0, s>>>(g, t, smp, uniforms, greedy_mode,
+                                                        deterministic, refill);
+  else
+    play_kernel<kMaxActions><<<blocks_for(g.slots), 256, 0, s>>>(g, t, smp, uniforms, greedy_mode,
+                                                                 deterministic, refill);
+}
+
+void launch_slot_init(const GameCfg& g, const TreeDev& t, const SampleDev& smp, int64_t n_first,
+                      hipStream_t s) {
+  slot_init_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, smp, n_first);
+}
+
+void launch_slot_set_root(const GameCfg& g, const TreeDev& t, const int32_t* slots,
+                          const Board* boards, int n, hipStream_t s) {
+  if (n > 0) slot_set_root_kernel<<<blocks_for(n), 256, 0, s>>>(g, t, slots, boards, n);
+}
+
+}  // namespace az

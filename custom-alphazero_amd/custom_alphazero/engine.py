@@ -1,0 +1,266 @@
+"""ctypes binding of libaz (include/az.h): the only way this package computes.
+
+There is deliberately no CPU fallback: if ``_lib/libaz.so`` is missing or no
+HIP device is visible, every entry point raises.  The reference's evaluator,
+tree and worker seams all land here.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libaz.so")
+
+EVAL_NETWORK = 0
+EVAL_SYNTHETIC = 1
+
+
+class AzError(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("board_height", ctypes.c_int32), ("board_width", ctypes.c_int32),
+        ("n", ctypes.c_int32), ("gravity", ctypes.c_int32),
+        ("mcts_iterations", ctypes.c_int32), ("index_move_greedy", ctypes.c_int32),
+        ("exploration_constant", ctypes.c_double), ("slots", ctypes.c_int32),
+        ("evaluator", ctypes.c_int32), ("filters", ctypes.c_int32), ("depth", ctypes.c_int32),
+        ("value_hidden", ctypes.c_int32), ("bn_epsilon", ctypes.c_double),
+        ("arena_edges", ctypes.c_int64), ("max_tree_visits", ctypes.c_int64),
+        ("reserved", ctypes.c_int32 * 8),
+    ]
+
+
+class Tensor(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64),
+                ("on_device", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("expansions", ctypes.c_int64), ("terminal_visits", ctypes.c_int64),
+        ("games_done", ctypes.c_int64), ("simulations", ctypes.c_int64),
+        ("plies", ctypes.c_int64), ("active_slots", ctypes.c_int64), ("errors", ctypes.c_int64),
+        ("conv_launches", ctypes.c_int64), ("conv_ms", ctypes.c_double),
+        ("reserved", ctypes.c_int64 * 7),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+EXPORTED = (
+    "az_abi_version", "az_last_error", "az_engine_create", "az_engine_destroy",
+    "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
+    "az_selfplay_run", "az_selfplay_results", "az_tree_reset", "az_tree_search", "az_tree_play",
+    "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
+)
+
+_lib = None
+
+
+def load_library():
+    """Load libaz.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AzError(f"libaz.so not built at {LIB_PATH}; run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        "az_abi_version": (ctypes.c_int, []),
+        "az_last_error": (ctypes.c_char_p, []),
+        "az_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(Config), ctypes.POINTER(P)]),
+        "az_engine_destroy": (ctypes.c_int, [P]),
+        "az_engine_set_weights": (ctypes.c_int, [P, ctypes.POINTER(Tensor), ctypes.c_int]),
+        "az_encode": (ctypes.c_int, [P, P, ctypes.c_int, P, P]),
+        "az_forward": (ctypes.c_int, [P, P, ctypes.c_int, P, P]),
+        "az_selfplay_begin": (ctypes.c_int, [P, I64, I64, ctypes.c_uint32]),
+        "az_selfplay_step": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(Stats)]),
+        "az_selfplay_run": (ctypes.c_int, [P, I64, I64, ctypes.c_uint32, ctypes.POINTER(Stats)]),
+        "az_selfplay_results": (ctypes.c_int, [P, P, P, P, P, P, P]),
+        "az_tree_reset": (ctypes.c_int, [P, ctypes.c_int, P, P]),
+        "az_tree_search": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_tree_play": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, P, P, P]),
+        "az_tree_info": (ctypes.c_int, [P, ctypes.c_int, P, P]),
+        "az_tree_export": (ctypes.c_int, [P, ctypes.c_int, P, P, P, P, P, P, P]),
+        "az_stats_get": (ctypes.c_int, [P, ctypes.POINTER(Stats)]),
+        "az_timer_enable": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_pow_table": (ctypes.c_int, [P, P, I64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _ = I32
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        msg = load_library().az_last_error().decode("utf-8", "replace")
+        raise AzError(f"libaz error {rc}: {msg}")
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Engine:
+    """One libaz engine: one device, one HIP stream, `slots` concurrent trees."""
+
+    def __init__(self, height=6, width=7, n=4, gravity=True, mcts_iterations=100, slots=1,
+                 evaluator=EVAL_NETWORK, index_move_greedy=8, exploration_constant=1.5,
+                 filters=128, depth=4, value_hidden=256, bn_epsilon=1e-3, arena_edges=0,
+                 max_tree_visits=0, device=0):
+        L = load_library()
+        self.height, self.width, self.n, self.gravity = height, width, n, bool(gravity)
+        self.action_space = width if gravity else width * height
+        self.slots = slots
+        self.mcts_iterations = mcts_iterations
+        cfg = Config(board_height=height, board_width=width, n=n, gravity=int(bool(gravity)),
+                     mcts_iterations=mcts_iterations, index_move_greedy=index_move_greedy,
+                     exploration_constant=exploration_constant, slots=slots, evaluator=evaluator,
+                     filters=filters, depth=depth, value_hidden=value_hidden,
+                     bn_epsilon=bn_epsilon, arena_edges=arena_edges,
+                     max_tree_visits=max_tree_visits)
+        handle = ctypes.c_void_p()
+        _check(L.az_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
+        self._h = handle
+        self._L = L
+        self._n_games = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.az_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter teardown
+            pass
+
+    # ------------------------------------------------------------- weights
+    def set_weights(self, named):
+        """named: iterable of (name, array-like or torch tensor)."""
+        keep, items = [], []
+        for name, t in named:
+            on_dev = 0
+            if hasattr(t, "is_cuda"):
+                t = t.detach().float().contiguous()
+                on_dev = int(t.is_cuda)
+                if not on_dev:
+                    t = t.numpy()
+            if on_dev:
+                ptr, numel = t.data_ptr(), t.numel()
+            else:
+                t = np.ascontiguousarray(t, np.float32)
+                ptr, numel = t.ctypes.data, t.size
+            keep.append(t)
+            items.append(Tensor(name.encode(), ptr, numel, on_dev, 0))
+        arr = (Tensor * len(items))(*items)
+        if any(i.on_device for i in items):
+            import torch
+            torch.cuda.synchronize()
+        _check(self._L.az_engine_set_weights(self._h, arr, len(items)))
+
+    # ------------------------------------------------------------- eval
+    def encode(self, boards):
+        b = np.ascontiguousarray(boards, np.int8).reshape(-1, self.height, self.width)
+        state = np.zeros(b.shape + (4,), np.float32)
+        mask = np.zeros((len(b), self.action_space), np.uint8)
+        _check(self._L.az_encode(self._h, _ptr(b), len(b), _ptr(state), _ptr(mask)))
+        return state, mask.astype(bool)
+
+    def forward(self, x):
+        x = np.ascontiguousarray(x, np.float32).reshape(-1, self.height, self.width, 4)
+        probs = np.zeros((len(x), self.action_space), np.float32)
+        values = np.zeros(len(x), np.float32)
+        _check(self._L.az_forward(self._h, _ptr(x), len(x), _ptr(probs), _ptr(values)))
+        return probs, values
+
+    # ------------------------------------------------------------- self-play
+    def selfplay_begin(self, first_game, n_games, base_seed):
+        _check(self._L.az_selfplay_begin(self._h, int(first_game), int(n_games),
+                                         int(base_seed) & 0xFFFFFFFF))
+        self._n_games = int(n_games)
+
+    def selfplay_step(self, n_moves=1):
+        st = Stats()
+        _check(self._L.az_selfplay_step(self._h, int(n_moves), ctypes.byref(st)))
+        return st.as_dict()
+
+    def selfplay_run(self, first_game, n_games, base_seed):
+        st = Stats()
+        _check(self._L.az_selfplay_run(self._h, int(first_game), int(n_games),
+                                       int(base_seed) & 0xFFFFFFFF, ctypes.byref(st)))
+        self._n_games = int(n_games)
+        return st.as_dict()
+
+    def selfplay_results(self):
+        G, P, A = self._n_games, self.height * self.width, self.action_space
+        lengths = np.zeros(G, np.int32)
+        results = np.zeros(G, np.int32)
+        expansions = np.zeros(G, np.int32)
+        boards = np.zeros((G, P, self.height, self.width), np.int8)
+        policies = np.zeros((G, P, A), np.float64)
+        moves = np.zeros((G, P), np.int32)
+        _check(self._L.az_selfplay_results(self._h, _ptr(lengths), _ptr(results), _ptr(expansions),
+                                           _ptr(boards), _ptr(policies), _ptr(moves)))
+        return dict(lengths=lengths, results=results, expansions=expansions, boards=boards,
+                    policies=policies, moves=moves)
+
+    # ------------------------------------------------------------- tree API
+    def tree_reset(self, slots, boards):
+        slots = np.ascontiguousarray(slots, np.int32)
+        b = np.ascontiguousarray(boards, np.int8).reshape(len(slots), self.height, self.width)
+        _check(self._L.az_tree_reset(self._h, len(slots), _ptr(slots), _ptr(b)))
+
+    def tree_search(self, n_sims):
+        _check(self._L.az_tree_search(self._h, int(n_sims)))
+
+    def tree_play(self, uniforms=None, greedy=False, deterministic=False):
+        S, A = self.slots, self.action_space
+        u = None if deterministic else np.ascontiguousarray(uniforms, np.float64).reshape(S)
+        moves = np.zeros(S, np.int32)
+        status = np.zeros(S, np.int32)
+        policy = np.zeros((S, A), np.float64)
+        _check(self._L.az_tree_play(self._h, _ptr(u), int(bool(greedy)), int(bool(deterministic)),
+                                    _ptr(moves), _ptr(status), _ptr(policy)))
+        return moves, status, policy
+
+    def tree_export(self, slot):
+        info = np.zeros(5, np.int64)
+        rv = np.zeros(1, np.float32)
+        _check(self._L.az_tree_info(self._h, int(slot), _ptr(info), _ptr(rv)))
+        n = int(info[0])
+        out = {
+            "prior": np.zeros(n, np.float64), "w": np.zeros(n, np.float64),
+            "n": np.zeros(n, np.int32), "child": np.zeros(n, np.int32),
+            "child_n": np.zeros(n, np.int32), "action": np.zeros(n, np.int32),
+            "child_value": np.zeros(n, np.float32),
+        }
+        _check(self._L.az_tree_export(self._h, int(slot), _ptr(out["prior"]), _ptr(out["w"]),
+                                      _ptr(out["n"]), _ptr(out["child"]), _ptr(out["child_n"]),
+                                      _ptr(out["action"]), _ptr(out["child_value"])))
+        out.update(arena_top=n, root_first=int(info[1]), root_n=int(info[2]), ply=int(info[3]),
+                   active=bool(info[4]), root_value=float(rv[0]))
+        return out
+
+    # ------------------------------------------------------------- misc
+    def stats(self):
+        st = Stats()
+        _check(self._L.az_stats_get(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def timer(self, on):
+        _check(self._L.az_timer_enable(self._h, int(bool(on))))
+
+    def pow_table(self, n):
+        out = np.zeros(int(n), np.float64)
+        _check(self._L.az_pow_table(self._h, _ptr(out), int(n)))
+        return out

@@ -1,0 +1,143 @@
+/*
+ * az.h -- C ABI of libaz, the MI355X (gfx950) self-play engine.
+ *
+ * The reference (neuronest/custom-alphazero) is Python: its plug-in seams are
+ * duck-typed calls, not an FFI.  Each entry point below replaces one of those
+ * seams; the Python drop-in package (custom-alphazero_amd/custom_alphazero)
+ * binds them with ctypes (INTEGRATION.md shows the binding).  Paths are
+ * relative to the reference root.
+ *
+ * Conventions: every function returns 0 on success or a negative AZ_E* code;
+ * az_last_error() then holds a thread-local message.  Host buffers are owned
+ * by the caller; the engine owns all device memory.  One engine = one device
+ * = one HIP stream; calls are synchronous (results are in the caller's
+ * buffers on return).  No exception or abort crosses the ABI.
+ */
+#ifndef AZ_H_
+#define AZ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AZ_ABI_VERSION 1
+
+#define AZ_OK 0
+#define AZ_E_INVALID -1  /* bad argument / config */
+#define AZ_E_HIP -2      /* HIP runtime error */
+#define AZ_E_STATE -3    /* call out of order (e.g. no weights) */
+#define AZ_E_DEVICE -4   /* a kernel flagged an error (arena/pow/path overflow) */
+
+#define AZ_EVAL_NETWORK 0    /* the policy/value network (model/tensorflow/model.py) */
+#define AZ_EVAL_SYNTHETIC 1  /* oracle/synth.py's exact evaluator (parity runs) */
+
+typedef struct az_engine az_engine;
+
+/* Engine configuration: the reference's Config* class constants
+ * (custom_alphazero/config.py:7-71) plus device sizing. */
+typedef struct az_config {
+    int32_t board_height;          /* ConfigConnectN.board_height (config.py:40) */
+    int32_t board_width;           /* ConfigConnectN.board_width (config.py:39) */
+    int32_t n;                     /* ConfigConnectN.n (config.py:41) */
+    int32_t gravity;               /* ConfigConnectN.gravity (config.py:42) */
+    int32_t mcts_iterations;       /* sims per move: ConfigSelfPlay.mcts_iterations (config.py:21) */
+    int32_t index_move_greedy;     /* ConfigMCTS.index_move_greedy (config.py:55) */
+    double exploration_constant;   /* ConfigMCTS.exploration_constant (config.py:51) */
+    int32_t slots;                 /* concurrent games (trees) on this device */
+    int32_t evaluator;             /* AZ_EVAL_* */
+    int32_t filters;               /* ConfigModel.filters (config.py:71); 128 supported */
+    int32_t depth;                 /* ConfigModel.depth (config.py:63) */
+    int32_t value_hidden;          /* ValueHead hidden_dim (model/tensorflow/model.py:110) */
+    double bn_epsilon;             /* Keras BatchNormalization epsilon (1e-3) */
+    int64_t arena_edges;           /* tree edges per slot; 0 = mcts_iterations*H*W*A */
+    int64_t max_tree_visits;       /* bound on visits through one node; 0 = mcts_iterations*H*W */
+    int32_t reserved[8];
+} az_config;
+
+/* One named weight tensor in Keras layout ("Weights"). */
+typedef struct az_tensor {
+    const char* name;   /* e.g. "block0.conv1.kernel" */
+    const float* data;  /* host pointer, or device pointer when on_device = 1 */
+    int64_t numel;
+    int32_t on_device;
+    int32_t reserved;
+} az_tensor;
+
+typedef struct az_stats {
+    int64_t expansions;       /* evaluate_and_expand calls (mcts/mcts.py:145) */
+    int64_t terminal_visits;  /* leaves that were game-over (mcts.py:176-179) */
+    int64_t games_done;
+    int64_t simulations;      /* per-tree simulations executed */
+    int64_t plies;            /* moves committed */
+    int64_t active_slots;     /* slots still holding a game */
+    int64_t errors;           /* device error flags (0 = none) */
+    int64_t conv_launches;    /* timed conv kernels (az_timer_enable) */
+    double conv_ms;           /* their summed device time */
+    int64_t reserved[7];
+} az_stats;
+
+int az_abi_version(void);
+const char* az_last_error(void);
+
+/* Replaces constructing PolicyValueModel + MCTS per game
+ * (self_play.py:46-57, utils.py:42-48). */
+int az_engine_create(int device, const az_config* cfg, az_engine** out);
+int az_engine_destroy(az_engine* eng);
+
+/* Replaces PolicyValueModel.load_with_meta / set_weights
+ * (model/tensorflow/model.py:190-201): the engine copies and folds them. */
+int az_engine_set_weights(az_engine* eng, const az_tensor* tensors, int n);
+
+/* Board.full_state + Board.legal_moves_mask for a batch of canonical int8
+ * boards [n][H][W] (connect_n/board.py:91-98, :154-155) -> state
+ * [n][H][W][4] f32, mask [n][A] u8.  Either output may be NULL. */
+int az_encode(az_engine* eng, const int8_t* boards, int n, float* state, uint8_t* mask);
+
+/* PolicyValueModel.__call__ (model/tensorflow/model.py:182-188): x [n][H][W][4]
+ * f32 -> probs [n][A] f32, values [n] f32.  Host buffers. */
+int az_forward(az_engine* eng, const float* x, int n, float* probs, float* values);
+
+/* Batched self_play.play / play_game (self_play.py:37-119): games
+ * first_game .. first_game+n_games-1, game g seeded with MT19937(base_seed+g)
+ * (the reference seeds np.random per game, self_play.py:45), slots refilled
+ * as games end.  begin+step lets a caller time a window of moves; run does
+ * begin + steps until every game is done. */
+int az_selfplay_begin(az_engine* eng, int64_t first_game, int64_t n_games, uint32_t base_seed);
+int az_selfplay_step(az_engine* eng, int n_moves, az_stats* st);
+int az_selfplay_run(az_engine* eng, int64_t first_game, int64_t n_games, uint32_t base_seed,
+                    az_stats* st);
+/* Per game g (index from first_game): lengths[g] plies; results[g] =
+ * get_result(keep_same_player=True) of the final board (1 win, 0 draw);
+ * expansions[g]; boards [g][H*W][H][W] int8 canonical root before each move;
+ * policies [g][H*W][A] f64 (MCTS.play return_details policy); moves [g][H*W]. */
+int az_selfplay_results(az_engine* eng, int32_t* lengths, int32_t* results, int32_t* expansions,
+                        int8_t* boards, double* policies, int32_t* moves);
+
+/* MCTS tree API (mcts/mcts.py:88-222) over the engine's slots. */
+int az_tree_reset(az_engine* eng, int n, const int32_t* slots, const int8_t* boards);
+int az_tree_search(az_engine* eng, int n_sims);
+/* MCTS.play(greedy, deterministic) (mcts.py:182-222) on every active slot:
+ * uniforms [slots] are the np.random.random_sample draws np.random.choice
+ * would consume (ignored when deterministic); outputs per slot: moves
+ * (action, -1 if the slot was idle), status (0 ongoing / 1 win / 2 draw),
+ * policy [slots][A] f64. */
+int az_tree_play(az_engine* eng, const double* uniforms, int greedy, int deterministic,
+                 int32_t* moves, int32_t* status, double* policy);
+/* Tree snapshot of one slot: info = {arena_top, root_first, root_n, ply,
+ * game_active}; then the edge arrays (length arena_top). */
+int az_tree_info(az_engine* eng, int slot, int64_t* info, float* root_value);
+int az_tree_export(az_engine* eng, int slot, double* prior, double* w, int32_t* n, int32_t* child,
+                   int32_t* child_n, int32_t* action, float* child_value);
+
+int az_stats_get(az_engine* eng, az_stats* st);
+int az_timer_enable(az_engine* eng, int on);
+/* The host-built libm pow(k, 0.5) table the kernels use (tests). */
+int az_pow_table(az_engine* eng, double* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AZ_H_ */

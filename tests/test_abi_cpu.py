@@ -1,0 +1,38 @@
+"""CPU checks of the drop-in boundary: libaz loads and exports every symbol
+include/az.h declares; the ctypes structs match the header layout."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from custom_alphazero import engine as az
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "az.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(az_\w+)\(", src, re.M)))
+
+
+def test_header_and_binding_agree():
+    declared = header_functions()
+    assert declared == sorted(az.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(az.LIB_PATH):
+        pytest.fail("libaz.so missing: run __graft_entry__.build()")
+    lib = ctypes.CDLL(az.LIB_PATH)
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    L = az.load_library()
+    assert L.az_abi_version() == 1
+
+
+def test_struct_sizes_match_header():
+    # az_config: 8 int32 + double + 4 int32 ... computed by hand from az.h
+    assert ctypes.sizeof(az.Config) == 4 * 6 + 8 + 4 * 5 + 4 + 8 + 8 + 8 + 32
+    assert ctypes.sizeof(az.Tensor) == 8 + 8 + 8 + 4 + 4
+    assert ctypes.sizeof(az.Stats) == 8 * 8 + 8 + 8 * 7

@@ -1,0 +1,196 @@
+"""GPU parity of libaz against the reference (golden vectors) and the oracle.
+
+Bar: bit-exact visit counts, W, priors, policies and
+moves; network outputs within 1e-5 of the float64 Keras restatement.
+"""
+import numpy as np
+import pytest
+
+import keras_ref
+import oracle
+from custom_alphazero import engine as az
+from custom_alphazero.model.weights import init_weights, weight_spec
+from test_oracle import MCTS_FIXTURES, check_game_against_golden
+
+pytestmark = pytest.mark.gpu
+
+NET_TOL = 1e-5  # north_star: value/policy outputs within 1e-5 (fp32)
+
+
+def synth_engine(z, slots):
+    H, W, n, grav, S = (int(z[k]) for k in ("height", "width", "n", "gravity", "sims"))
+    return az.Engine(H, W, n, bool(grav), S, slots=slots, evaluator=az.EVAL_SYNTHETIC)
+
+
+def selfplay_games(eng, first, n_games, base_seed=0):
+    eng.selfplay_run(first, n_games, base_seed)
+    r = eng.selfplay_results()
+    games = []
+    for g in range(n_games):
+        T = int(r["lengths"][g])
+        res = int(r["results"][g])
+        rewards = np.full(T, res, np.int64)
+        rewards[-2::-2] *= -1
+        games.append(dict(T=T, moves=r["moves"][g, :T], policy=r["policies"][g, :T],
+                          boards=r["boards"][g, :T], rewards=rewards,
+                          expansions=int(r["expansions"][g])))
+    return games
+
+
+def check_selfplay_game(z, g, got):
+    lens = z["game_len"]
+    off = int(lens[:g].sum())
+    T = int(lens[g])
+    sl = slice(off, off + T)
+    assert got["T"] == T, (g, got["T"], T)
+    np.testing.assert_array_equal(got["moves"], z["moves"][sl])
+    np.testing.assert_array_equal(got["policy"].view(np.uint64), z["policy"][sl].view(np.uint64))
+    np.testing.assert_array_equal(oracle.full_state(got["boards"]), z["state"][sl])
+    np.testing.assert_array_equal(got["rewards"], z["reward"][sl])
+    assert got["expansions"] == z["expansions"][g]
+
+
+@pytest.mark.parametrize("name", MCTS_FIXTURES)
+def test_selfplay_synthetic_matches_reference(golden, name):
+    """Batched device self-play == the reference's play_game, game by game."""
+    z = golden("mcts_" + name)
+    seeds = z["seed"].astype(np.int64)
+    assert np.all(np.diff(seeds) == 1)
+    for slots in sorted({len(seeds), max(1, len(seeds) // 2)}):  # also exercises slot refill
+        eng = synth_engine(z, slots)
+        games = selfplay_games(eng, int(seeds[0]), len(seeds))
+        for g, got in enumerate(games):
+            check_selfplay_game(z, g, got)
+        eng.close()
+
+
+@pytest.mark.parametrize("name", ["c4_s25", "c4_s100", "c5_9x9_s50", "nograv_5x5_s25", "c4_s1"])
+def test_tree_api_edges_match_reference(golden, name):
+    """MCTS.search/play through the tree API: root edge N, W, prior bit-exact."""
+    z = golden("mcts_" + name)
+    H, W, S = int(z["height"]), int(z["width"]), int(z["sims"])
+    A = int(z["action_space"])
+    off = 0
+    for g, seed in enumerate(z["seed"][:3]):
+        eng = synth_engine(z, 1)
+        eng.tree_reset([0], np.zeros((1, H, W), np.int8))
+        rng = np.random.RandomState(int(seed))
+        T = int(z["game_len"][g])
+        for ply in range(T):
+            eng.tree_search(S)
+            t = eng.tree_export(0)
+            k, f = t["root_n"], t["root_first"]
+            gi = off + ply
+            assert k == z["n_edges"][gi]
+            np.testing.assert_array_equal(t["action"][f:f + k], z["edge_action"][gi, :k])
+            np.testing.assert_array_equal(t["n"][f:f + k], z["edge_n"][gi, :k])
+            np.testing.assert_array_equal(t["w"][f:f + k].view(np.uint64), z["edge_w"][gi, :k].view(np.uint64))
+            np.testing.assert_array_equal(t["prior"][f:f + k].view(np.uint64),
+                                          z["edge_prior"][gi, :k].view(np.uint64))
+            moves, status, policy = eng.tree_play([rng.random_sample()], greedy=ply >= 8)
+            assert moves[0] == z["moves"][gi]
+            np.testing.assert_array_equal(policy[0].view(np.uint64), z["policy"][gi].view(np.uint64))
+            assert (status[0] != 0) == (ply == T - 1)
+        off += T
+        eng.close()
+    assert A == z["policy"].shape[1]
+
+
+def test_selfplay_synthetic_many_games_vs_oracle():
+    """256 games at S=50 on 96 slots (heavy refill) == the C oracle, bitwise."""
+    eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC)
+    games = selfplay_games(eng, 1000, 256, base_seed=7)
+    for g, got in enumerate(games):
+        ref = oracle.play_game(6, 7, 4, True, 50, 7 + 1000 + g)
+        assert got["T"] == ref["T"]
+        np.testing.assert_array_equal(got["moves"], ref["moves"])
+        np.testing.assert_array_equal(got["policy"].view(np.uint64), ref["policy"].view(np.uint64))
+        np.testing.assert_array_equal(got["boards"], ref["boards"])
+        assert got["expansions"] == ref["expansions"]
+    st = eng.stats()
+    assert st["games_done"] == 256 and st["errors"] == 0 and st["active_slots"] == 0
+
+
+def test_pow_table_is_python_pow(golden):
+    z = golden("numerics")
+    eng = az.Engine(6, 7, 4, True, 100, slots=1, evaluator=az.EVAL_SYNTHETIC,
+                    max_tree_visits=2_000_001)
+    tab = eng.pow_table(2_000_001)
+    exc = z["pow_exceptions"]
+    np.testing.assert_array_equal(tab[exc].view(np.uint64), z["pow_values"].view(np.uint64))
+    mask = np.ones(len(tab), bool)
+    mask[exc] = False
+    np.testing.assert_array_equal(tab[mask], np.sqrt(np.arange(len(tab), dtype=np.float64))[mask])
+
+
+@pytest.mark.parametrize("name", ["c4", "c5_9x9", "nograv_5x5"])
+def test_encode_and_mask_match_reference(golden, name):
+    z = golden("board_" + name)
+    H, W, grav = int(z["height"]), int(z["width"]), bool(z["gravity"])
+    eng = az.Engine(H, W, int(z["n"]), grav, 4, slots=512, evaluator=az.EVAL_SYNTHETIC)
+    state, mask = eng.encode(z["array"])
+    np.testing.assert_array_equal(state, oracle.full_state(z["array"]))
+    np.testing.assert_array_equal(mask, z["mask"])
+
+
+# ------------------------------------------------------------------ network
+def make_net_engine(H=6, W=7, n=4, grav=True, S=25, slots=256, seed=0, randomize_bn=True, depth=4):
+    A = W if grav else W * H
+    spec = weight_spec(H, W, A, depth=depth)
+    w = init_weights(spec, seed=seed, randomize_bn=randomize_bn)
+    eng = az.Engine(H, W, n, grav, S, slots=slots, evaluator=az.EVAL_NETWORK, depth=depth)
+    eng.set_weights(w.items())
+    return eng, w
+
+
+def random_boards(rng, k, H, W):
+    b = rng.randint(-1, 2, (k, H, W)).astype(np.int8)
+    return b
+
+
+@pytest.mark.parametrize("shape", [(6, 7, True), (9, 9, True)])
+def test_forward_matches_keras_restatement(shape):
+    H, W, grav = shape
+    eng, w = make_net_engine(H, W, 4, grav, slots=300)
+    rng = np.random.RandomState(5)
+    x = oracle.full_state(random_boards(rng, 37, H, W))
+    x[-5:] = rng.rand(5, H, W, 4).astype(np.float32)  # arbitrary (non one-hot) inputs too
+    p, v = eng.forward(x)
+    rp, rv = keras_ref.forward(w, x, depth=4)
+    assert np.abs(p - rp).max() < NET_TOL, np.abs(p - rp).max()
+    assert np.abs(v - rv).max() < NET_TOL, np.abs(v - rv).max()
+    np.testing.assert_allclose(p.sum(axis=1), 1.0, atol=1e-6)
+
+
+def test_forward_is_batch_invariant():
+    eng, _ = make_net_engine(slots=512)
+    rng = np.random.RandomState(11)
+    x = oracle.full_state(random_boards(rng, 700, 6, 7))  # > slots: chunked
+    p_all, v_all = eng.forward(x)
+    for lo, hi in [(0, 1), (3, 4), (100, 229), (511, 513), (699, 700)]:
+        p, v = eng.forward(x[lo:hi])
+        np.testing.assert_array_equal(p, p_all[lo:hi])
+        np.testing.assert_array_equal(v, v_all[lo:hi])
+
+
+def test_selfplay_network_replays_on_oracle():
+    """Device self-play with the real network: the oracle, fed the engine's
+    own batch-1 network outputs for every board it asks about, reproduces every
+    move and visit-count policy bit for bit (replay parity)."""
+    eng, _ = make_net_engine(S=40, slots=16, randomize_bn=False)
+    games = selfplay_games(eng, 0, 6, base_seed=123)
+    cache = {}
+
+    def cb(board):
+        key = board.tobytes()
+        if key not in cache:
+            p, v = eng.forward(oracle.full_state(board[None]))
+            cache[key] = (p[0], float(v[0]))
+        return cache[key]
+
+    for g, got in enumerate(games):
+        ref = oracle.play_game(6, 7, 4, True, 40, 123 + g, evaluator="callback", callback=cb)
+        assert got["T"] == ref["T"]
+        np.testing.assert_array_equal(got["moves"], ref["moves"])
+        np.testing.assert_array_equal(got["policy"].view(np.uint64), ref["policy"].view(np.uint64))
+        assert got["expansions"] == ref["expansions"]
