@@ -160,6 +160,24 @@ int fold_unit(const std::map<std::string, const az_tensor*>& m, const std::strin
   return 0;
 }
 
+// [n][K] (K contiguous) -> MFMA fragment order of conv3x3_mfma_kernel:
+// float4 index ((c*4 + tile)*4 + q)*64 + lane holds W[k][n] for
+// k = 32c + 16*(lane>>5) + 4q + e (e = 0..3), n = 32*tile + (lane&31).
+std::vector<float> pack_fragments(const std::vector<float>& wt, int N, int K) {
+  std::vector<float> p((size_t)N * K);
+  const int chunks = K / 32, tiles = N / 32;
+  for (int c = 0; c < chunks; ++c)
+    for (int t = 0; t < tiles; ++t)
+      for (int q = 0; q < 4; ++q)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 4; ++e) {
+            const int k = 32 * c + 16 * (lane >> 5) + 4 * q + e;
+            const int n = 32 * t + (lane & 31);
+            p[((((size_t)c * tiles + t) * 4 + q) * 64 + lane) * 4 + e] = wt[(size_t)n * K + k];
+          }
+  return p;
+}
+
 int upload(az_engine* e, float** dst, const std::vector<float>& src) {
   int rc;
   if (!*dst && (rc = e->alloc(dst, src.size()))) return rc;
@@ -310,7 +328,9 @@ int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
     for (int n2 = 0; n2 < F; ++n2)
       for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
     for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
-    if ((rc = upload(e, &net.c1_w[d], wt)) || (rc = upload(e, &net.c1_b[d], bt))) return rc;
+    if ((rc = upload(e, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
+        (rc = upload(e, &net.c1_b[d], bt)))
+      return rc;
     if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
     if ((rc = fold_unit(m, p + ".res", 1, F, F, eps, wr, br))) return rc;
     std::vector<float> wt2((size_t)F * 10 * F), bt2(F);
@@ -319,7 +339,9 @@ int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
       for (int c = 0; c < F; ++c) wt2[(size_t)n2 * 10 * F + 9 * F + c] = (float)wr[(size_t)c * F + n2];
     }
     for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
-    if ((rc = upload(e, &net.c2_w[d], wt2)) || (rc = upload(e, &net.c2_b[d], bt2))) return rc;
+    if ((rc = upload(e, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
+        (rc = upload(e, &net.c2_b[d], bt2)))
+      return rc;
   }
   // heads
   if ((rc = fold_unit(m, "policy.conv", 1, F, 2, eps, w, b))) return rc;

@@ -14,8 +14,8 @@ struct NetDev {
   int filters = 128, depth = 0, hidden = 256;
   float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c)
   float* stem_b = nullptr;  // [F]
-  std::vector<float*> c1_w, c1_b;  // [F][9F], [F]
-  std::vector<float*> c2_w, c2_b;  // [F][10F] (conv2 taps, then 1x1 residual), [F]
+  std::vector<float*> c1_w, c1_b;  // fragment-packed [9F x F], [F]
+  std::vector<float*> c2_w, c2_b;  // fragment-packed [10F x F] (conv2 taps, then 1x1 residual), [F]
   float *pc_w = nullptr, *pc_b = nullptr;  // policy conv [F][2], [2]
   float *vc_w = nullptr, *vc_b = nullptr;  // value conv [F], [1]
   float *pd_w = nullptr, *pd_b = nullptr;  // policy dense [2HW][A], [A]

@@ -92,138 +92,152 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
 }
 
 // ------------------------------------------------------------ conv3x3 MFMA
-// out[r][n] = ReLU( sum_k A[r][k] * wt[n][k] + bias[n] )
+// out[r][n] = ReLU( sum_k A[r][k] * W[k][n] + bias[n] )
 //   k in [0, 9F): A = in[neighbour(r, tap)][c], tap = k / F, c = k % F
 //   k in [9F, 10F) (RESIDUAL): A = res_in[r][c]  (fused 1x1 projection)
-// Tile: 128 rows x F=128 columns per 256-thread workgroup; wave w owns rows
-// [32w, 32w+32) and all four 32-column MFMA tiles (64 accumulator VGPRs).
-// K is consumed in chunks of 32 through a double-buffered LDS stage (A and B
-// both [128][32] f32, rows padded to 36 floats: conflict-free ds_read_b128).
-// Inside a chunk, lane half h owns k = 16h .. 16h+15, so MFMA k-step s sums
-// the pair (s, 16+s): fixed order, batch-independent.
-constexpr int kBM = 128;
-constexpr int kKC = 32;
-constexpr int kLdsStride = 36;  // floats per staged row (32 + 4 pad)
+//
+// Workgroup = 4 waves = a 64-row x 128-column output tile.  Wave w owns rows
+// [32*(w>>1), +32) and the two 32-column MFMA tiles 2*(w&1), 2*(w&1)+1.
+//   * A: the tile's input rows plus a halo of W+1 rows on each side are staged
+//     ONCE into LDS (the "slab"); every tap reads its shifted view of it, and
+//     off-board neighbours read a zero row.  Rows are 128 floats = 32 16-byte
+//     chunks, chunk j of slab row r stored at j ^ (r & 15): the 16 distinct
+//     rows a ds_read_b128 lane group touches land on 16 distinct bank quads.
+//   * B: weights are pre-packed on the host in MFMA fragment order
+//     ([chunk][tile][q][lane] float4, az_engine.hip pack_fragments) and stream
+//     straight into registers with fully coalesced 1 KiB loads, one 32-wide K
+//     chunk ahead -- no LDS, no barrier in the K loop.
+// v_mfma_f32_32x32x2_f32 is an exact f32 FMA chain; inside a chunk lane half
+// h owns k = 16h..16h+15 and k-step s sums the pair (s, 16+s): a fixed order
+// per output element, independent of the batch.
+constexpr int kTileRows = 64;
+constexpr int kChunkK = 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+__device__ __forceinline__ int slab_swz(int chunk, int key) {
+  return (chunk & 16) | ((chunk ^ key) & 15);
+}
+
+size_t conv_lds_bytes(int W, bool residual) {
+  const int slab_rows = kTileRows + 2 * (W + 1);
+  return (size_t)(slab_rows + 1 + (residual ? kTileRows : 0)) * 512;
+}
+
 template <int F, bool RESIDUAL>
 __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
-    const float* __restrict__ in, const float* __restrict__ res_in, const float* __restrict__ wt,
-    const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
-    int n_static, int H, int W) {
-  static_assert(F == 128, "tile assumes F = 128 output channels");
-  constexpr int K = (RESIDUAL ? 10 : 9) * F;
-  constexpr int CPT = F / kKC;  // chunks per tap
-  constexpr int NCHUNK = K / kKC;
-  __shared__ __attribute__((aligned(16))) float lds[2][2][kBM * kLdsStride];  // [buf][A/B]
+    const float* __restrict__ in, const float* __restrict__ res_in,
+    const float4* __restrict__ wpack, const float* __restrict__ bias, float* __restrict__ out,
+    const int* __restrict__ count, int n_static, int H, int W) {
+  static_assert(F == 128, "tile assumes F = 128 channels (32 16-byte chunks per row)");
+  constexpr int NCH = (RESIDUAL ? 10 : 9) * (F / kChunkK);
+  extern __shared__ __attribute__((aligned(16))) float4 lds4[];
 
-  const int HW = H * W;
+  const int HW = H * W, halo = W + 1;
   const int n_boards = count ? *count : n_static;
   const int rows = n_boards * HW;
-  const int row0 = blockIdx.x * kBM;
+  const int row0 = blockIdx.x * kTileRows;
   if (row0 >= rows) return;
-
   const int tid = threadIdx.x;
+  const int slab_rows = kTileRows + 2 * halo;
+  float4* slab = lds4;
+  float4* zero_row = lds4 + slab_rows * 32;
+  float4* xslab = zero_row + 32;
+
+  // ---- stage the slab (and the residual rows) once
+  const float4* in4 = reinterpret_cast<const float4*>(in);
+  for (int i = tid; i < slab_rows * 32; i += 256) {
+    const int r = i >> 5, j = i & 31, g = row0 - halo + r;
+    const float4 v = (g >= 0 && g < rows) ? in4[(size_t)g * 32 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    slab[r * 32 + slab_swz(j, r)] = v;
+  }
+  if (tid < 32) zero_row[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (RESIDUAL) {
+    const float4* x4 = reinterpret_cast<const float4*>(res_in);
+    for (int i = tid; i < kTileRows * 32; i += 256) {
+      const int r = i >> 5, j = i & 31, g = row0 + r;
+      const float4 v = g < rows ? x4[(size_t)g * 32 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      xslab[r * 32 + slab_swz(j, r)] = v;
+    }
+  }
+  __syncthreads();
+
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
+  const int rg = wave >> 1, cg = wave & 1;
+  const int rl = rg * 32 + r32;        // local row of this lane's A operand
+  const int grow = row0 + rl;
+  const int pos = grow % HW;
+  const int py = pos / W, px = pos - (pos / W) * W;
+  const bool row_ok = grow < rows;
 
-  // staging geometry: piece q = tid + 256*j  ->  tile row q>>3, 4-float segment q&7
-  const int seg = tid & 7;
-  int src_b[4], src_y[4], src_x[4];
-  bool src_ok[4];
+  f32x16 acc[2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = row0 + (tid >> 3) + 32 * j;
-    src_ok[j] = r < rows;
-    const int b = r / HW, p = r - b * HW;
-    src_b[j] = b;
-    src_y[j] = p / W;
-    src_x[j] = p - (p / W) * W;
-  }
-
-  float4 sa[4], sb[4];
-  auto load_chunk = [&](int c) {
-    const int tap = c / CPT;
-    const int c0 = (c - tap * CPT) * kKC + seg * 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (src_ok[j]) {
-        if (tap < 9) {
-          const int ny = src_y[j] + tap / 3 - 1, nx = src_x[j] + tap % 3 - 1;
-          if (ny >= 0 && ny < H && nx >= 0 && nx < W)
-            v = *reinterpret_cast<const float4*>(in + ((size_t)(src_b[j] * HW + ny * W + nx)) * F + c0);
-        } else {
-          v = *reinterpret_cast<const float4*>(
-              res_in + ((size_t)(src_b[j] * HW + src_y[j] * W + src_x[j])) * F + c0);
-        }
-      }
-      sa[j] = v;
-      const int n = (tid >> 3) + 32 * j;
-      sb[j] = *reinterpret_cast<const float4*>(wt + (size_t)n * K + c * kKC + seg * 4);
-    }
-  };
-  auto store_chunk = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = (tid >> 3) + 32 * j;
-      *reinterpret_cast<float4*>(&lds[buf][0][row * kLdsStride + seg * 4]) = sa[j];
-      *reinterpret_cast<float4*>(&lds[buf][1][row * kLdsStride + seg * 4]) = sb[j];
-    }
-  };
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.0f;
 
-  load_chunk(0);
-  store_chunk(0);
-  __syncthreads();
+  // B fragment stream: float4 index ((c*4 + tile)*4 + q)*64 + lane
+  const float4* wl = wpack + (size_t)(2 * cg) * 256 + lane;
+  float4 bc[2][4], bn[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bc[t][q] = wl[t * 256 + q * 64];
 
-  for (int c = 0; c < NCHUNK; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < NCHUNK) load_chunk(c + 1);
-    const float* As = &lds[buf][0][(wave * 32 + r32) * kLdsStride + h * 16];
-    float a[16];
+  for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) {
+      const float4* wn = wl + (size_t)(c + 1) * 1024;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bn[t][q] = wn[t * 256 + q * 64];
+    }
+    const int tap = c >> 2;
+    const float4* base;
+    int key;
+    if (!RESIDUAL || tap < 9) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const bool ok = row_ok && py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
+      const int sr = rl + halo + dy * W + dx;
+      base = ok ? slab + sr * 32 : zero_row;
+      key = ok ? (sr & 15) : 0;
+    } else {
+      base = xslab + rl * 32;
+      key = rl & 15;
+    }
+    const int cbase = (c & 3) * 8 + h * 4;
+    float4 a4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a4[q] = base[slab_swz(cbase + q, key)];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(As + 4 * q);
-      a[4 * q] = v.x;
-      a[4 * q + 1] = v.y;
-      a[4 * q + 2] = v.z;
-      a[4 * q + 3] = v.w;
-    }
+      const float av[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float* Bs = &lds[buf][1][(t * 32 + r32) * kLdsStride + h * 16];
-      float bv[16];
+      for (int e = 0; e < 4; ++e) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(Bs + 4 * q);
-        bv[4 * q] = v.x;
-        bv[4 * q + 1] = v.y;
-        bv[4 * q + 2] = v.z;
-        bv[4 * q + 3] = v.w;
+        for (int t = 0; t < 2; ++t) {
+          const float bv = e == 0 ? bc[t][q].x : e == 1 ? bc[t][q].y : e == 2 ? bc[t][q].z : bc[t][q].w;
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv, acc[t], 0, 0, 0);
+        }
       }
-#pragma unroll
-      for (int s = 0; s < 16; ++s)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bv[s], acc[t], 0, 0, 0);
     }
-    if (c + 1 < NCHUNK) store_chunk(buf ^ 1);
-    __syncthreads();
+    if (c + 1 < NCH) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bc[t][q] = bn[t][q];
+    }
   }
 
   // epilogue: C/D map col = lane&31, row = (i&3) + 8*(i>>2) + 4*h
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int col = t * 32 + r32;
+  for (int t = 0; t < 2; ++t) {
+    const int col = (2 * cg + t) * 32 + r32;
     const float bcol = bias[col];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int row = row0 + wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      const int row = row0 + rg * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
       if (row < rows) out[(size_t)row * F + col] = fmaxf(acc[t][i] + bcol, 0.0f);
     }
   }
@@ -345,16 +359,19 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
     stem_conv_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(
         reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
   }
-  const int grid = (n_max * HW + kBM - 1) / kBM;
+  const int grid = (n_max * HW + kTileRows - 1) / kTileRows;
+  const size_t lds1 = conv_lds_bytes(W, false), lds2 = conv_lds_bytes(W, true);
   float* cur = act_a;  // block input
   float* mid = act_b;
   float* nxt = act_c;
   if (timer) timer->begin(s);
   for (int d = 0; d < net.depth; ++d) {
-    conv3x3_mfma_kernel<F, false><<<grid, 256, 0, s>>>(cur, nullptr, net.c1_w[d], net.c1_b[d],
-                                                      mid, count, n_max, H, W);
-    conv3x3_mfma_kernel<F, true><<<grid, 256, 0, s>>>(mid, cur, net.c2_w[d], net.c2_b[d], nxt,
-                                                     count, n_max, H, W);
+    conv3x3_mfma_kernel<F, false><<<grid, 256, lds1, s>>>(
+        cur, nullptr, reinterpret_cast<const float4*>(net.c1_w[d]), net.c1_b[d], mid, count, n_max,
+        H, W);
+    conv3x3_mfma_kernel<F, true><<<grid, 256, lds2, s>>>(
+        mid, cur, reinterpret_cast<const float4*>(net.c2_w[d]), net.c2_b[d], nxt, count, n_max, H,
+        W);
     float* t = cur;
     cur = nxt;
     nxt = t;
