@@ -67,6 +67,14 @@ def load_library():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise AzError(f"libaz.so not built at {LIB_PATH}; run __graft_entry__.build()")
+    # One HIP runtime per process: torch's wheel bundles its own libamdhip64 /
+    # libhsa-runtime64 with the same SONAMEs as /opt/rocm's.  Loading torch
+    # first makes libaz bind to that already-loaded runtime (SONAME match);
+    # the reverse order leaves two runtimes and torch then sees no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sig = {

@@ -1,0 +1,123 @@
+"""PolicyValueModel with the reference's call signature
+(custom_alphazero/model/tensorflow/model.py:152-218).
+
+PyTorch-ROCm only *holds* the weights (float32 tensors on the GPU, Keras
+layout, names from model/weights.py); the forward runs in libaz
+(az_forward: fp32-MFMA conv tower + heads, csrc/az_nn.hip).  Calling the
+model returns (probabilities [B, A], value [B, 1]) as torch CPU tensors, so
+the reference's `.numpy()` idiom (mcts.py:134-137) works unchanged.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from custom_alphazero import engine as az
+from custom_alphazero.config import ConfigConnectN, ConfigModel, ConfigPath
+from custom_alphazero.model.weights import init_weights, weight_spec
+
+
+class PolicyValueModel:
+    def __init__(self, input_dim, action_space, seed=None, device=0):
+        import torch
+
+        self.input_dim = tuple(int(d) for d in input_dim)
+        self.action_space = int(action_space)
+        H, W, C = self.input_dim
+        self.depth = ConfigModel.depth
+        self.spec = weight_spec(H, W, self.action_space, ConfigModel.filters, self.depth,
+                                ConfigModel.value_hidden, C)
+        if seed is None:
+            seed = int.from_bytes(os.urandom(4), "little")
+        self.device = torch.device("cuda", device)
+        self.weights = {k: torch.from_numpy(v).to(self.device)
+                        for k, v in init_weights(self.spec, seed).items()}
+        self.steps = 0
+        self.learning_rate = ConfigModel.maximum_learning_rate
+        self._engine = None
+        self._engine_version = -1
+        self._version = 0
+
+    # ------------------------------------------------------------ weights
+    def engine_weights(self):
+        return [(name, self.weights[name]) for name, _ in self.spec]
+
+    def get_weights(self):
+        return [self.weights[name].detach().cpu().numpy().reshape(shape) for name, shape in self.spec]
+
+    def set_weights(self, arrays):
+        import torch
+        arrays = list(arrays)
+        if len(arrays) != len(self.spec):
+            raise ValueError(f"expected {len(self.spec)} arrays, got {len(arrays)}")
+        for (name, shape), a in zip(self.spec, arrays):
+            a = np.asarray(a, np.float32)
+            if a.shape != tuple(shape):
+                raise ValueError(f"{name}: shape {a.shape} != {shape}")
+            self.weights[name] = torch.from_numpy(a.copy()).to(self.device)
+        self._version += 1
+
+    @property
+    def hash(self) -> int:
+        # The reference sums md5(str(weight)) over Keras' get_weights()
+        # (model.py:172-177); that string form is numpy-print dependent, so
+        # this hash is over the raw float32 bytes instead.
+        return sum(int(hashlib.md5(w.tobytes()).hexdigest(), 16) for w in self.get_weights())
+
+    def is_equal(self, other: "PolicyValueModel"):
+        return self.hash == other.hash
+
+    # ------------------------------------------------------------ forward
+    def _eng(self):
+        if self._engine is None:
+            H, W, _ = self.input_dim
+            c = ConfigConnectN
+            self._engine = az.Engine(H, W, min(c.n, H, W), c.gravity, 1,
+                                     slots=ConfigModel.forward_batch, evaluator=az.EVAL_NETWORK,
+                                     filters=ConfigModel.filters, depth=self.depth,
+                                     value_hidden=ConfigModel.value_hidden,
+                                     bn_epsilon=ConfigModel.bn_epsilon,
+                                     device=self.device.index or 0)
+        if self._engine_version != self._version:
+            self._engine.set_weights(self.engine_weights())
+            self._engine_version = self._version
+        return self._engine
+
+    def __call__(self, inputs, training=False):
+        import torch
+        x = inputs.numpy() if hasattr(inputs, "numpy") else np.asarray(inputs)
+        x = np.asarray(x, np.float32).reshape((-1,) + self.input_dim)
+        probs, values = self._eng().forward(x)
+        return torch.from_numpy(probs), torch.from_numpy(values.reshape(-1, 1))
+
+    call = __call__
+
+    # ------------------------------------------------------------ persistence
+    def save_with_meta(self, path):
+        os.makedirs(path, exist_ok=True)
+        np.savez(os.path.join(path, ConfigPath.model_prefix + ".npz"),
+                 **{name: w for (name, _), w in zip(self.spec, self.get_weights())})
+        meta = {"steps": int(self.steps), "learning_rate": float(self.learning_rate),
+                "hash": self.hash}
+        with open(os.path.join(path, ConfigPath.model_meta), "w") as fp:
+            json.dump(meta, fp, sort_keys=True, indent=4)
+        open(os.path.join(path, ConfigPath.model_success), "wb").close()
+
+    def load_with_meta(self, path):
+        if not os.path.exists(os.path.join(path, ConfigPath.model_success)):
+            raise AssertionError(f"No verification file of the model found at {path}!")
+        with np.load(os.path.join(path, ConfigPath.model_prefix + ".npz"), allow_pickle=False) as z:
+            self.set_weights([z[name] for name, _ in self.spec])
+        with open(os.path.join(path, ConfigPath.model_meta)) as fp:
+            meta = json.load(fp)
+        self.steps = int(meta.get("steps", 0))
+        self.learning_rate = float(meta.get("learning_rate", self.learning_rate))
+        if self.hash != meta.get("hash"):
+            raise AssertionError(f"Unexpected weights hash recovered during model loading at {path}!")
+
+    def get_learning_rate(self) -> float:
+        return float(self.learning_rate)
+
+    def update_learning_rate(self, learning_rate: float):
+        self.learning_rate = float(learning_rate)

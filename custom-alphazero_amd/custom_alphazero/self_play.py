@@ -1,0 +1,144 @@
+"""Self-play worker entrypoints with the reference's signatures
+(custom_alphazero/self_play.py:37-119).
+
+* play_game(...) plays ONE game through the MCTS API exactly like the
+  reference loop (seeded np.random, search, greedy from ply 8, alternating
+  rewards), so it is a drop-in for callers that want the tree back.
+* play(...) is the batched path: ConfigSelfPlay.games_per_call games run on
+  the device at once (ConfigSelfPlay.concurrent_games trees in flight, slots
+  refilled as games end), replacing the reference's one-game-per-process
+  joblib fan-out (self_play.py:98-110).  Game g is seeded MT19937(base_seed+g).
+"""
+import os
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from custom_alphazero import engine as az
+from custom_alphazero.config import (ConfigConnectN, ConfigGeneral, ConfigMCTS, ConfigModel,
+                                     ConfigPath, ConfigSelfPlay)
+from custom_alphazero.connect_n.board import Board
+from custom_alphazero.connect_n.move import Move
+from custom_alphazero.mcts.mcts import MCTS, SyntheticEvaluator
+from custom_alphazero.utils import best_saved_model
+
+get_all_possible_moves = Board.get_all_possible_moves
+
+
+def alternating_rewards(result: int, length: int) -> np.ndarray:
+    """self_play.py:71-78: the final result for the last mover, negated every
+    other ply going back, times discounting_factor ** distance."""
+    rewards = np.repeat(result, length)
+    rewards[-2::-2] = -rewards[-2::-2]
+    return rewards * ConfigSelfPlay.discounting_factor ** np.arange(length)[::-1]
+
+
+def play_game(process_id: int, all_possible_moves: List[Move], mcts_iterations: int, run_id: str,
+              plays_inferences: Optional[Dict[str, Tuple[np.ndarray, float]]] = None,
+              model=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray, MCTS]:
+    np.random.seed(int((process_id + 1) * time.time()) % (2 ** 32 - 1))
+    if model is None:
+        model = best_saved_model(run_id)
+    mcts = MCTS(board=Board(), all_possible_moves=all_possible_moves,
+                concurrency=ConfigGeneral.concurrency, plays_inferences=plays_inferences,
+                model=model, use_solver=ConfigMCTS.use_solver)
+    states, policies = [], []
+    while not mcts.board.is_game_over():
+        mcts.search(mcts_iterations)
+        greedy = mcts.board.fullmove_number >= ConfigMCTS.index_move_greedy
+        parent_state, _child_state, policy, _move = mcts.play(greedy, return_details=True)
+        states.append(parent_state)
+        policies.append(policy)
+    states, policies = np.asarray(states), np.asarray(policies)
+    rewards = alternating_rewards(mcts.board.get_result(keep_same_player=True), len(states))
+    return states, policies, rewards, mcts
+
+
+@dataclass
+class GameRecord:
+    """Per-game summary returned by play() in place of the reference's pickled
+    MCTS trees (the device arena is recycled when a slot takes a new game)."""
+    game_id: int
+    seed: int
+    length: int
+    result: int
+    expansions: int
+    moves: np.ndarray
+
+
+_ENGINES = {}
+
+
+def _batched_engine(model, n_slots):
+    c = ConfigConnectN
+    synthetic = isinstance(model, SyntheticEvaluator)
+    key = (c.board_height, c.board_width, c.n, c.gravity, ConfigSelfPlay.mcts_iterations, n_slots,
+           synthetic, ConfigMCTS.index_move_greedy, ConfigMCTS.exploration_constant,
+           ConfigModel.depth)
+    eng = _ENGINES.get(key)
+    if eng is None:
+        eng = az.Engine(c.board_height, c.board_width, c.n, c.gravity,
+                        ConfigSelfPlay.mcts_iterations, slots=n_slots,
+                        evaluator=az.EVAL_SYNTHETIC if synthetic else az.EVAL_NETWORK,
+                        index_move_greedy=ConfigMCTS.index_move_greedy,
+                        exploration_constant=ConfigMCTS.exploration_constant,
+                        filters=ConfigModel.filters, depth=ConfigModel.depth,
+                        value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon)
+        _ENGINES.clear()
+        _ENGINES[key] = eng
+    if not synthetic:
+        eng.set_weights(model.engine_weights())
+    return eng
+
+
+def play(run_id: str, plays_inferences: Optional[Dict[str, Tuple[np.ndarray, float]]] = None,
+         model=None, n_games: Optional[int] = None, base_seed: Optional[int] = None,
+         first_game: int = 0):
+    """Batched self-play.  Returns (states [M,H,W,4] f32, policies [M,A] f64,
+    rewards [M] int64, records) concatenated in game order like the reference
+    (self_play.py:112-118)."""
+    if model is None:
+        model = best_saved_model(run_id)
+    n_games = int(n_games or ConfigSelfPlay.games_per_call)
+    if base_seed is None:
+        base_seed = ConfigSelfPlay.base_seed
+    if base_seed is None:
+        base_seed = int(time.time()) % (2 ** 32 - 1)
+    eng = _batched_engine(model, min(n_games, ConfigSelfPlay.concurrent_games))
+    eng.selfplay_run(first_game, n_games, base_seed)
+    r = eng.selfplay_results()
+    states, policies, rewards, records = [], [], [], []
+    for g in range(n_games):
+        T = int(r["lengths"][g])
+        b = r["boards"][g, :T]
+        s = np.zeros(b.shape + (4,), np.float32)
+        s[..., 0] = b == 0
+        s[..., 1] = b == 1
+        s[..., 2] = b == -1
+        s[..., 3] = 1.0
+        states.append(s)
+        policies.append(r["policies"][g, :T])
+        rewards.append(alternating_rewards(int(r["results"][g]), T))
+        records.append(GameRecord(first_game + g, (base_seed + first_game + g) % 2 ** 32, T,
+                                  int(r["results"][g]), int(r["expansions"][g]),
+                                  r["moves"][g, :T].copy()))
+    return np.vstack(states), np.vstack(policies), np.concatenate(rewards), records
+
+
+def exclude_null_games(states, policies, rewards):
+    """self_play.py:155-162: drop samples of drawn games (reward 0)."""
+    keep = rewards != 0
+    return states[keep], policies[keep], rewards[keep]
+
+
+def save_samples(run_id: str, iteration: int, states, policies, rewards) -> str:
+    """samples.npz with keys states/policies/values (self_play.py:170-178,
+    paths.py:37-40 layout results/{game}/{run_id}/self_play/iteration_k/)."""
+    path = os.path.join(ConfigPath.results_dir, ConfigGeneral.game, run_id,
+                        ConfigPath.self_play_dir, f"iteration_{iteration}")
+    os.makedirs(path, exist_ok=True)
+    out = os.path.join(path, ConfigPath.samples_file)
+    np.savez(out, states=states, policies=policies, values=rewards)
+    return out

@@ -1,0 +1,70 @@
+"""Host-side drop-in API (connect_n Board/Move, normalize_probabilities)
+against the reference's own outputs (golden vectors)."""
+import numpy as np
+import pytest
+
+from custom_alphazero.config import ConfigConnectN
+from custom_alphazero.connect_n.board import Board
+from custom_alphazero.connect_n.move import Move
+from custom_alphazero.mcts.utils import normalize_probabilities
+
+
+@pytest.fixture
+def game_cfg():
+    saved = (ConfigConnectN.board_height, ConfigConnectN.board_width, ConfigConnectN.n,
+             ConfigConnectN.gravity)
+
+    def set_(h, w, n, g):
+        ConfigConnectN.board_height, ConfigConnectN.board_width = h, w
+        ConfigConnectN.n, ConfigConnectN.gravity = n, g
+
+    yield set_
+    set_(*saved)
+
+
+@pytest.mark.parametrize("name", ["c4", "c5_9x9", "nograv_5x5"])
+def test_board_api_matches_reference(golden, game_cfg, name):
+    z = golden("board_" + name)
+    H, W, n, grav = int(z["height"]), int(z["width"]), int(z["n"]), bool(z["gravity"])
+    game_cfg(H, W, n, grav)
+    all_moves = Board.get_all_possible_moves()
+    assert len(all_moves) == (W if grav else W * H)
+    games = z["game"]
+    idx = 0
+    for g in np.unique(games)[:40]:
+        sel = np.flatnonzero(games == g)
+        board = Board()
+        for i in sel:
+            board.play(all_moves[int(z["move"][i])], keep_same_player=True)
+            np.testing.assert_array_equal(board.array, z["array"][i])
+            assert board.is_game_over() == bool(z["game_over"][i])
+            res = board.get_result(keep_same_player=True)
+            assert (-9 if res is None else res) == z["result"][i]
+            np.testing.assert_array_equal(board.legal_moves_mask(all_moves), z["mask"][i])
+            order = [all_moves.index(m) for m in board.moves]
+            k = int(z["n_moves"][i])
+            assert order == z["moves_order"][i][:k].tolist()
+            assert board.fullmove_number == z["fullmove"][i]
+            fs = board.full_state
+            assert fs.dtype == np.float32 and fs.shape == (H, W, 4)
+            idx += 1
+    assert idx > 100
+
+
+def test_board_play_on_copy_and_repr(game_cfg):
+    game_cfg(6, 7, 4, True)
+    b = Board()
+    c = b.play(Move(True, 3), on_copy=True, keep_same_player=True)
+    assert b.fullmove_number == 0 and c.fullmove_number == 1
+    assert repr(c).splitlines()[-1] == "...O..." and b != c
+    assert c.turn == 1 and c.played_moves == [Move(True, 3)]
+    assert Board.from_one_hot(c.array_one_hot)[5, 3] == -1
+
+
+def test_normalize_matches_reference(golden):
+    z = golden("numerics")
+    for vin, vout, n, is64 in zip(z["norm_in"], z["norm_out"], z["norm_len"], z["norm_out_is64"]):
+        r = normalize_probabilities(vin[:n])
+        assert (r.dtype == np.float64) == bool(is64)
+        np.testing.assert_array_equal(np.asarray(r, np.float64).view(np.uint64),
+                                      vout[:n].view(np.uint64))

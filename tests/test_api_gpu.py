@@ -1,0 +1,128 @@
+"""The drop-in Python API on the GPU: MCTS / play_game / play / PolicyValueModel
+against the reference's golden vectors (synthetic evaluator) and the float64
+Keras restatement (network)."""
+import numpy as np
+import pytest
+
+import keras_ref
+import oracle
+from custom_alphazero import self_play
+from custom_alphazero.config import ConfigConnectN, ConfigSelfPlay
+from custom_alphazero.connect_n.board import Board
+from custom_alphazero.mcts.mcts import MCTS, SyntheticEvaluator
+from custom_alphazero.model.tensorflow.model import PolicyValueModel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def game_cfg():
+    saved = (ConfigConnectN.board_height, ConfigConnectN.board_width, ConfigConnectN.n,
+             ConfigConnectN.gravity, ConfigSelfPlay.mcts_iterations)
+
+    def set_(z):
+        ConfigConnectN.board_height, ConfigConnectN.board_width = int(z["height"]), int(z["width"])
+        ConfigConnectN.n, ConfigConnectN.gravity = int(z["n"]), bool(z["gravity"])
+        ConfigSelfPlay.mcts_iterations = int(z["sims"])
+
+    yield set_
+    (ConfigConnectN.board_height, ConfigConnectN.board_width, ConfigConnectN.n,
+     ConfigConnectN.gravity, ConfigSelfPlay.mcts_iterations) = saved
+
+
+@pytest.mark.parametrize("name", ["c4_s25", "c5_9x9_s50", "nograv_5x5_s25"])
+def test_play_game_api_matches_reference(golden, game_cfg, monkeypatch, name):
+    """self_play.play_game with the reference's own seeding (time patched)."""
+    z = golden("mcts_" + name)
+    game_cfg(z)
+    all_moves = Board.get_all_possible_moves()
+    off = 0
+    for g, seed in enumerate(z["seed"][:2]):
+        monkeypatch.setattr(self_play.time, "time", lambda s=seed: float(s))
+        states, policies, rewards, mcts = self_play.play_game(
+            0, all_moves, int(z["sims"]), "test-run", {}, model=SyntheticEvaluator())
+        T = int(z["game_len"][g])
+        sl = slice(off, off + T)
+        np.testing.assert_array_equal(states, z["state"][sl])
+        np.testing.assert_array_equal(policies.view(np.uint64), z["policy"][sl].view(np.uint64))
+        np.testing.assert_array_equal(rewards, z["reward"][sl])
+        # tree views: the played path carries the reference's edge statistics
+        node = mcts.root
+        for ply in range(T):
+            played = [e for e in node.edges if e.played]
+            assert len(played) == 1
+            gi = off + ply
+            k = int(z["n_edges"][gi])
+            assert [e.visit_count for e in node.edges] == z["edge_n"][gi, :k].tolist()
+            np.testing.assert_array_equal(np.array([e.total_action_value for e in node.edges]),
+                                          z["edge_w"][gi, :k])
+            assert played[0].greedily_played == bool(z["greedy"][gi])
+            node = played[0].child
+        off += T
+        monkeypatch.undo()
+
+
+def test_batched_play_matches_reference(golden, game_cfg):
+    z = golden("mcts_c4_s25")
+    game_cfg(z)
+    states, policies, rewards, records = self_play.play(
+        "test-run", {}, model=SyntheticEvaluator(), n_games=16, base_seed=0)
+    np.testing.assert_array_equal(states, z["state"])
+    np.testing.assert_array_equal(policies.view(np.uint64), z["policy"].view(np.uint64))
+    np.testing.assert_array_equal(rewards, z["reward"])
+    assert [r.length for r in records] == z["game_len"].tolist()
+    assert [r.expansions for r in records] == z["expansions"].tolist()
+
+
+def test_mcts_deterministic_play_is_argmax(game_cfg, golden):
+    game_cfg(golden("mcts_c4_s25"))
+    m = MCTS(Board(), Board.get_all_possible_moves(), False, {}, model=SyntheticEvaluator())
+    m.search(30)
+    visits = [e.visit_count for e in m.current_root.edges]
+    state = np.random.get_state()
+    b = m.play(deterministic=True)
+    assert b.played_moves[-1].x == int(np.argmax(visits))
+    assert np.random.get_state()[2] == state[2]  # no RNG draw when deterministic
+
+
+def test_policy_value_model_matches_keras(game_cfg, golden):
+    game_cfg(golden("mcts_c4_s25"))
+    model = PolicyValueModel(input_dim=(6, 7, 4), action_space=7, seed=3)
+    rng = np.random.RandomState(0)
+    x = oracle.full_state(rng.randint(-1, 2, (9, 6, 7)).astype(np.int8))
+    probs, value = model(x)
+    p, v = probs.numpy(), value.numpy()
+    assert p.shape == (9, 7) and v.shape == (9, 1)
+    w = dict(zip([n for n, _ in model.spec], model.get_weights()))
+    w = {n: a for n, a in w.items()}
+    rp, rv = keras_ref.forward(w, x, depth=4)
+    assert np.abs(p - rp).max() < 1e-5 and np.abs(v[:, 0] - rv).max() < 1e-5
+    # the reference's batch-1 idiom (mcts.py:131-137)
+    pp, vv = model(np.expand_dims(x[0], 0))
+    assert pp.numpy().ravel().shape == (7,) and isinstance(vv.numpy().item(), float)
+
+
+def test_model_save_load_roundtrip(tmp_path, game_cfg, golden):
+    game_cfg(golden("mcts_c4_s25"))
+    a = PolicyValueModel((6, 7, 4), 7, seed=1)
+    a.steps = 12
+    a.save_with_meta(str(tmp_path))
+    b = PolicyValueModel((6, 7, 4), 7, seed=2)
+    assert not a.is_equal(b)
+    b.load_with_meta(str(tmp_path))
+    assert a.is_equal(b) and b.steps == 12
+    x = np.zeros((1, 6, 7, 4), np.float32)
+    x[..., 0] = 1
+    x[..., 3] = 1
+    np.testing.assert_array_equal(a(x)[0].numpy(), b(x)[0].numpy())
+
+
+def test_mcts_with_network_model_plays_legal_game(game_cfg, golden):
+    game_cfg(golden("mcts_c4_s25"))
+    model = PolicyValueModel((6, 7, 4), 7, seed=0)
+    np.random.seed(4)
+    states, policies, rewards, mcts = self_play.play_game(0, Board.get_all_possible_moves(), 20,
+                                                          "test-run", {}, model=model)
+    assert len(states) == len(policies) == len(rewards) >= 7
+    np.testing.assert_allclose(policies.sum(axis=1), 1.0)
+    assert abs(int(rewards[-1])) in (0, 1)
