@@ -160,6 +160,12 @@ def main():
     local_exp = st1["expansions"] - st0["expansions"]
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     achieved = (local_exp * conv_flop_per_board) / (conv_ms * 1e-3) / 1e12 if conv_ms else 0.0
+    boards_per_launch = local_exp / max(conv_launches / (2 * args.depth), 1)
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "r1", "pmc_conv_traffic.json")
+    if os.path.exists(pmc):  # PMC bytes/board (rocprofv3 FETCH_SIZE/WRITE_SIZE) x live batch
+        with open(pmc) as fp:
+            traffic = int(json.load(fp)["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
 
     if rank == 0:
         line = {
@@ -193,7 +199,9 @@ def main():
                 "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (PMC per-board bytes from profiles/r1 x live boards/launch)",
+                "boards_per_launch": round(boards_per_launch, 1),
                 "avg_launch_ms": round(conv_avg_ms, 4),
                 "algorithmic_flop_per_board": conv_flop_per_board,
                 "launches_timed": conv_launches,

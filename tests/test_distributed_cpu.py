@@ -1,0 +1,92 @@
+"""N>1 path on CPU (gloo, world_size 2): game sharding, one-collective weight
+broadcast, compact sample gather; samples invariant to the number of ranks.
+
+The per-rank runner here is the oracle (CPU) standing in for a rank's
+engine -- the collectives and the sharding logic are the product code
+(custom_alphazero/distributed.py); the GPU engine behind the same runner
+interface is covered by tests/test_engine_gpu.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+H, W, N, S = 6, 7, 4, 12
+N_GAMES = 7
+BASE_SEED = 40
+
+
+def oracle_runner(first, count, base_seed):
+    import oracle
+    T, A = H * W, W
+    out = dict(lengths=np.zeros(count, np.int32), results=np.zeros(count, np.int32),
+               expansions=np.zeros(count, np.int32), boards=np.zeros((count, T, H, W), np.int8),
+               policies=np.zeros((count, T, A)), moves=np.zeros((count, T), np.int32))
+    for i in range(count):
+        r = oracle.play_game(H, W, N, True, S, base_seed + first + i)
+        t = r["T"]
+        out["lengths"][i], out["results"][i], out["expansions"][i] = t, r["result"], r["expansions"]
+        out["boards"][i, :t], out["policies"][i, :t], out["moves"][i, :t] = r["boards"], r["policy"], r["moves"]
+    return out
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (os.path.join(repo, "custom-alphazero_amd"), os.path.join(repo, "oracle"), here):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from custom_alphazero import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # weights: rank 0 holds them, the others get them from one broadcast
+    named = [("a", torch.arange(6, dtype=torch.float32).reshape(2, 3) if rank == 0 else torch.zeros(2, 3)),
+             ("b", torch.full((4,), 7.0) if rank == 0 else torch.zeros(4))]
+    got = D.broadcast_weights(named)
+    assert torch.equal(got[0][1], torch.arange(6, dtype=torch.float32).reshape(2, 3))
+    assert torch.equal(got[1][1], torch.full((4,), 7.0))
+    g = D.selfplay_sharded(oracle_runner, N_GAMES, BASE_SEED)
+    if rank == 0:
+        states, policies, rewards = D.to_samples(g)
+        np.savez(os.path.join(outdir, f"world{world}.npz"), states=states, policies=policies,
+                 rewards=rewards, lengths=g["lengths"], moves=g["moves"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_selfplay_gloo(tmp_path, world):
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    got = np.load(tmp_path / f"world{world}.npz")
+    # every game, in global order, equals the single-engine reference run
+    ref = oracle_runner(0, N_GAMES, BASE_SEED)
+    np.testing.assert_array_equal(got["lengths"], ref["lengths"])
+    off = 0
+    for g in range(N_GAMES):
+        t = int(ref["lengths"][g])
+        np.testing.assert_array_equal(got["moves"][off:off + t], ref["moves"][g, :t])
+        np.testing.assert_array_equal(got["policies"][off:off + t], ref["policies"][g, :t])
+        off += t
+    assert got["states"].shape == (off, H, W, 4) and got["rewards"].shape == (off,)
+
+
+def test_shard_blocks_cover_all_games():
+    from custom_alphazero.distributed import shard
+    for n in (0, 1, 7, 4096, 32768):
+        for world in (1, 2, 3, 8):
+            blocks = [shard(n, world, r) for r in range(world)]
+            assert sum(c for _, c in blocks) == n
+            assert [f for f, _ in blocks] == sorted(f for f, _ in blocks)
+            for (f0, c0), (f1, _) in zip(blocks, blocks[1:]):
+                assert f0 + c0 == f1
