@@ -22,76 +22,135 @@ import numpy as np
 DIRS = ((0, 1), (1, 1), (1, 0), (1, -1))
 
 
+class PortMove:
+    """Move value object with the reference's fields (connect_n/move.py)."""
+    __slots__ = ("gravity", "x", "y")
+
+    def __init__(self, gravity, x, y=None):
+        self.gravity, self.x, self.y = gravity, x, y
+
+    def __eq__(self, other):
+        return (self.x, self.y) == (other.x, other.y)
+
+    def __hash__(self):
+        return hash((self.x, self.y))
+
+
 class PortBoard:
-    """Connect-N rules, reference connect_n/board.py:12-268 (canonical mirror)."""
+    """Connect-N rules, reference connect_n/board.py:12-268 (canonical mirror).
+
+    Carries the same per-board state as the reference Board (piece tables,
+    played Move objects, colour constants) so copying a board costs what the
+    reference's deepcopy costs (the dominant CPU cost).
+    """
 
     def __init__(self, height, width, n, gravity):
-        self.h, self.w, self.n, self.gravity = height, width, n, gravity
-        self.cells = np.zeros((height, width), np.int8)
+        self.board_height, self.board_width, self.n, self.gravity = height, width, n, gravity
+        self.black, self.empty, self.white = -1, 0, 1
         self.pieces = {-1: "O", 0: ".", 1: "X"}
-        self.played = []
-        self.plies = 0
-        self.over = False
-        self.null = None
+        self.pieces_to_int = {v: k for k, v in self.pieces.items()}
+        self.played_moves = []
+        self.array = np.zeros((height, width)).astype("int8")
+        self.turn = 1
+        self.fullmove_number = 0
+        self.game_over = False
+        self.is_null = None
+
+    # short aliases used by the search
+    @property
+    def h(self):
+        return self.board_height
+
+    @property
+    def w(self):
+        return self.board_width
+
+    @property
+    def cells(self):
+        return self.array
+
+    @cells.setter
+    def cells(self, value):
+        self.array = value
+
+    @property
+    def plies(self):
+        return self.fullmove_number
+
+    @property
+    def over(self):
+        return self.game_over
 
     def key(self):
-        return "\n".join("".join(self.pieces[int(c)] for c in row) for row in self.cells)
+        return "\n".join("".join(map(lambda c: self.pieces[c], row)) for row in self.array)
+
+    def moves(self):
+        if self.gravity:
+            return [PortMove(True, int(x)) for x in np.where(self.array[0, :] == 0)[0]]
+        return [PortMove(False, int(x), int(y)) for y, x in zip(*np.where(self.array == 0))]
+
+    def action_of(self, move):
+        return move.x if self.gravity else move.x * self.board_height + move.y
+
+    def all_moves(self):
+        if self.gravity:
+            return [PortMove(True, x) for x in range(self.board_width)]
+        return [PortMove(False, x, y) for x in range(self.board_width) for y in range(self.board_height)]
 
     def legal(self):
         """Board.moves order, as action indices (x, or x*H+y without gravity)."""
-        if self.gravity:
-            return [int(x) for x in np.flatnonzero(self.cells[0] == 0)]
-        ys, xs = np.nonzero(self.cells == 0)
-        return [int(x) * self.h + int(y) for y, x in zip(ys, xs)]
+        return [self.action_of(m) for m in self.moves()]
 
     def legal_mask(self):
-        mask = np.zeros(self.w if self.gravity else self.w * self.h, bool)
-        mask[self.legal()] = True
-        return mask
+        current = self.moves()
+        return np.asarray([m in current for m in self.all_moves()])
 
     def state(self):
-        one_hot = np.eye(3)[self.cells]
-        return np.dstack([one_hot, np.ones((self.h, self.w))]).astype("float32")
+        one_hot = np.eye(3)[self.array]
+        return np.dstack([one_hot, np.ones((self.board_height, self.board_width)) * self.turn]).astype("float32")
 
     def _place(self, action):
+        h, w = self.board_height, self.board_width
         if self.gravity:
             x = action
-            col = self.cells[:, x]
+            col = self.array[:, x]
             y = -1
-            for r in range(self.h):
+            for r in range(h):
                 if col[r] != 0:
                     break
                 y = r
         else:
-            x, y = action // self.h, action % self.h
-        self.cells[y, x] = 1
+            x, y = action // h, action % h
+        self.array[y, x] = self.turn
         for dx, dy in DIRS:
             run = 1
             for s in (1, -1):
                 cx, cy = x + s * dx, y + s * dy
-                while 0 <= cx < self.w and 0 <= cy < self.h and self.cells[cy, cx] == 1:
+                while 0 <= cx < w and 0 <= cy < h and self.array[cy, cx] == self.array[y, x]:
                     run += 1
                     cx, cy = cx + s * dx, cy + s * dy
             if run >= self.n:
-                self.over, self.null = True, False
+                self.game_over, self.is_null = True, False
                 return
-        if not self.legal():
-            self.over, self.null = True, True
+        if not self.moves():
+            self.game_over, self.is_null = True, True
 
     def play(self, action, on_copy=False):
-        if self.over:
+        if self.game_over:
             return self
         b = deepcopy(self) if on_copy else self
         b._place(action)
-        b.plies += 1
-        b.cells = -b.cells
-        b.played.append(action)
+        b.fullmove_number += 1
+        b.array = np.where(b.array == -1, 1, np.where(b.array == 1, -1, b.array)).astype("int8")
+        b.turn = 1
+        b.played_moves.append(PortMove(self.gravity, action % self.board_width if self.gravity else action // self.board_height,
+                                       None if self.gravity else action % self.board_height))
         return b
 
     def result(self):
-        if not self.over:
+        if not self.game_over:
             return None
-        return 0 if self.null else 1
+        return 0 if self.is_null else 1
 
 
 def normalize(p):
@@ -112,7 +171,10 @@ class Edge:
         self.played = False
 
     def ucb(self, c=1.5):
-        q = self.value_sum / self.visits if self.visits else 0.0
+        try:
+            q = self.value_sum / self.visits
+        except ZeroDivisionError:
+            q = 0.0
         total = sum(e.visits for e in self.parent.edges)
         return q + c * self.prior * (total ** 0.5) / (1 + self.visits)
 
