@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(15, cores-1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
     return ap.parse_args()
 
 
@@ -103,16 +104,24 @@ def main():
     import torch.distributed as dist
     from custom_alphazero import engine as az
 
+    # one rank per GPU; the modulo only matters when rehearsing several ranks
+    # on a one-GPU box
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", dev_index)
     # weights: rank 0's init, one flat RCCL broadcast (~5 MB) to every rank
     flat = torch.cat([torch.from_numpy(host_w[n].reshape(-1)) for n, _ in spec]).to(dev)
     if world > 1:
         if rank != 0:
             flat.zero_()
-        dist.broadcast(flat, src=0)
+        if args.dist_backend == "gloo":
+            host = flat.cpu()
+            dist.broadcast(host, src=0)
+            flat.copy_(host)
+        else:
+            dist.broadcast(flat, src=0)
     named, off = [], 0
     for name, shape in spec:
         k = int(torch.tensor(shape).prod())
@@ -120,7 +129,7 @@ def main():
         off += k
 
     eng = az.Engine(args.height, args.width, args.n, True, args.sims, slots=args.slots,
-                    evaluator=az.EVAL_NETWORK, depth=args.depth, device=local_rank)
+                    evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index)
     eng.set_weights(named)
     budget = args.slots * (2 + (args.warmup + args.steps) // 5)
     eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)
@@ -144,10 +153,11 @@ def main():
                                       "terminal_visits")}
     conv_ms, conv_launches = st1["conv_ms"], st1["conv_launches"]
     if world > 1:
+        red_dev = "cpu" if args.dist_backend == "gloo" else dev
         t = torch.tensor([d["games_done"], d["expansions"], d["simulations"], d["plies"]],
-                         dtype=torch.float64, device=dev)
+                         dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         d["games_done"], d["expansions"], d["simulations"], d["plies"] = (int(v) for v in t.tolist())
         elapsed = float(tmax.item())

@@ -407,7 +407,7 @@ int az_forward(az_engine* e, const float* x, int n, float* probs, float* values)
     AZ_HIP(hipMemcpyAsync(e->x, x + (size_t)off * HW * 4, (size_t)m * HW * 4 * sizeof(float),
                           hipMemcpyHostToDevice, e->stream));
     az::launch_forward(e->net, e->x, nullptr, m, e->g.H, e->g.W, A, e->act[0], e->act[1], e->act[2],
-                       e->probs, e->values, e->stream, nullptr);
+                       e->probs, e->values, e->stream, e->timer.enabled ? &e->timer : nullptr);
     AZ_HIP(hipGetLastError());
     AZ_HIP(hipMemcpyAsync(probs + (size_t)off * A, e->probs, (size_t)m * A * sizeof(float),
                           hipMemcpyDeviceToHost, e->stream));

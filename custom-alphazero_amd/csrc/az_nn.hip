@@ -19,6 +19,8 @@
 //   heads            one wave per board
 // Reduction order is fixed per output element and independent of the batch,
 // so a board's outputs do not depend on what else is in the batch.
+#include <stdlib.h>
+
 #include "az_nn.h"
 
 namespace az {
@@ -100,7 +102,8 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
 // [32*(w>>1), +32) and the two 32-column MFMA tiles 2*(w&1), 2*(w&1)+1.
 //   * A: the tile's input rows plus a halo of W+1 rows on each side are staged
 //     ONCE into LDS (the "slab"); every tap reads its shifted view of it, and
-//     off-board neighbours read a zero row.  Rows are 128 floats = 32 16-byte
+//     off-board neighbours read a zero row (the fused residual's 4 chunks read
+//     the lane's own block-input row from global instead).  Rows are 128 floats = 32 16-byte
 //     chunks, chunk j of slab row r stored at j ^ (r & 15): the 16 distinct
 //     rows a ds_read_b128 lane group touches land on 16 distinct bank quads.
 //   * B: weights are pre-packed on the host in MFMA fragment order
@@ -119,13 +122,19 @@ __device__ __forceinline__ int slab_swz(int chunk, int key) {
   return (chunk & 16) | ((chunk ^ key) & 15);
 }
 
-size_t conv_lds_bytes(int W, bool residual) {
+// Variant flags (A/B-tested in profiles/conv_bench.py via AZ_CONV_VARIANT):
+//   PREA  : read the next chunk's A fragments from LDS one chunk ahead
+//   XSLAB : stage the fused residual's block-input rows in LDS (else: global)
+//   OCC   : __launch_bounds__ waves per SIMD (register cap)
+size_t conv_lds_bytes(int W, bool residual, bool xslab) {
   const int slab_rows = kTileRows + 2 * (W + 1);
-  return (size_t)(slab_rows + 1 + (residual ? kTileRows : 0)) * 512;
+  return (size_t)(slab_rows + 1 + (residual && xslab ? kTileRows : 0)) * 512;
 }
 
-template <int F, bool RESIDUAL>
-__global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
+// DIAG (timing experiments only, wrong outputs): 1 = no B loads after the
+// first two chunks, 2 = no A LDS reads after the first chunk.
+template <int F, bool RESIDUAL, bool PREA, bool XSLAB, int OCC, int DIAG = 0>
+__global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ wpack, const float* __restrict__ bias, float* __restrict__ out,
     const int* __restrict__ count, int n_static, int H, int W) {
@@ -144,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
   float4* zero_row = lds4 + slab_rows * 32;
   float4* xslab = zero_row + 32;
 
-  // ---- stage the slab (and the residual rows) once
+  // ---- stage the slab (and, with XSLAB, the residual rows) once
   const float4* in4 = reinterpret_cast<const float4*>(in);
   for (int i = tid; i < slab_rows * 32; i += 256) {
     const int r = i >> 5, j = i & 31, g = row0 - halo + r;
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     slab[r * 32 + slab_swz(j, r)] = v;
   }
   if (tid < 32) zero_row[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (RESIDUAL) {
+  if constexpr (RESIDUAL && XSLAB) {
     const float4* x4 = reinterpret_cast<const float4*>(res_in);
     for (int i = tid; i < kTileRows * 32; i += 256) {
       const int r = i >> 5, j = i & 31, g = row0 + r;
@@ -177,22 +186,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.0f;
 
-  // B fragment stream: float4 index ((c*4 + tile)*4 + q)*64 + lane
+  // B fragment stream: float4 index ((c*4 + tile)*4 + q)*64 + lane.  Two
+  // register buffers in ping-pong (the loop is unrolled by two, so no copy):
+  // chunk c+1's loads are first consumed a whole chunk of MFMAs later.
   const float4* wl = wpack + (size_t)(2 * cg) * 256 + lane;
-  float4 bc[2][4], bn[2][4];
+  float4 b0[2][4], b1[2][4];
+  auto load_b = [&](int c, float4 (&dst)[2][4]) {
+    if (DIAG == 1 && c >= 2) return;
+    const float4* wn = wl + (size_t)c * 1024;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bc[t][q] = wl[t * 256 + q * 64];
-
-  for (int c = 0; c < NCH; ++c) {
-    if (c + 1 < NCH) {
-      const float4* wn = wl + (size_t)(c + 1) * 1024;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bn[t][q] = wn[t * 256 + q * 64];
-    }
+      for (int q = 0; q < 4; ++q) dst[t][q] = wn[t * 256 + q * 64];
+  };
+  auto load_a = [&](int c, float4 (&dst)[4]) {
+    if (DIAG == 2 && c >= 2) return;
     const int tap = c >> 2;
     const float4* base;
     int key;
@@ -202,14 +210,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
       const int sr = rl + halo + dy * W + dx;
       base = ok ? slab + sr * 32 : zero_row;
       key = ok ? (sr & 15) : 0;
-    } else {
+    } else if constexpr (XSLAB) {
       base = xslab + rl * 32;
       key = rl & 15;
+    } else {
+      // fused 1x1 residual (4 of 40 chunks): this lane's own block-input
+      // row, straight from global
+      const float4* xr =
+          reinterpret_cast<const float4*>(res_in) + (size_t)grow * 32 + (c & 3) * 8 + h * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q] = row_ok ? xr[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      return;
     }
     const int cbase = (c & 3) * 8 + h * 4;
-    float4 a4[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) a4[q] = base[slab_swz(cbase + q, key)];
+    for (int q = 0; q < 4; ++q) dst[q] = base[slab_swz(cbase + q, key)];
+  };
+  auto compute = [&](const float4 (&a4)[4], const float4 (&bc)[2][4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float av[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w};
@@ -222,12 +239,29 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
         }
       }
     }
-    if (c + 1 < NCH) {
+  };
+  static_assert(NCH % 2 == 0, "ping-pong loop needs an even chunk count");
+  float4 a0[4], a1[4];
+  load_b(0, b0);
+  if constexpr (PREA) load_a(0, a0);
+  // fully unrolled: no loop back-edge, so the waitcnt pass sees exactly which
+  // loads each MFMA needs (a rolled loop merged the pending state and waited
+  // on the chunk just issued); tap geometry folds to constants per chunk
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bc[t][q] = bn[t][q];
+  for (int c = 0; c < NCH; c += 2) {
+    load_b(c + 1, b1);
+    if constexpr (PREA) {
+      load_a(c + 1, a1);
+    } else {
+      load_a(c, a0);
     }
+    compute(a0, b0);
+    if (c + 2 < NCH) {
+      load_b(c + 2, b0);
+      if constexpr (PREA) load_a(c + 2, a0);
+    }
+    if constexpr (!PREA) load_a(c + 1, a1);
+    compute(a1, b1);
   }
 
   // epilogue: C/D map col = lane&31, row = (i&3) + 8*(i>>2) + 4*h
@@ -360,18 +394,30 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
         reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
   }
   const int grid = (n_max * HW + kTileRows - 1) / kTileRows;
-  const size_t lds1 = conv_lds_bytes(W, false), lds2 = conv_lds_bytes(W, true);
   float* cur = act_a;  // block input
   float* mid = act_b;
   float* nxt = act_c;
+  static const int variant = [] {
+    const char* v = getenv("AZ_CONV_VARIANT");
+    return v ? atoi(v) : 0;
+  }();
   if (timer) timer->begin(s);
   for (int d = 0; d < net.depth; ++d) {
-    conv3x3_mfma_kernel<F, false><<<grid, 256, lds1, s>>>(
-        cur, nullptr, reinterpret_cast<const float4*>(net.c1_w[d]), net.c1_b[d], mid, count, n_max,
-        H, W);
-    conv3x3_mfma_kernel<F, true><<<grid, 256, lds2, s>>>(
-        mid, cur, reinterpret_cast<const float4*>(net.c2_w[d]), net.c2_b[d], nxt, count, n_max, H,
-        W);
+    const float4* w1 = reinterpret_cast<const float4*>(net.c1_w[d]);
+    const float4* w2 = reinterpret_cast<const float4*>(net.c2_w[d]);
+#define AZ_CONV_PAIR(PREA, XSLAB, OCC, DIAG)                                                    \
+  conv3x3_mfma_kernel<F, false, PREA, XSLAB, OCC, DIAG><<<grid, 256, conv_lds_bytes(W, false, XSLAB), s>>>( \
+      cur, nullptr, w1, net.c1_b[d], mid, count, n_max, H, W);                                  \
+  conv3x3_mfma_kernel<F, true, PREA, XSLAB, OCC, DIAG><<<grid, 256, conv_lds_bytes(W, true, XSLAB), s>>>(   \
+      mid, cur, w2, net.c2_b[d], nxt, count, n_max, H, W)
+    switch (variant) {
+      case 1: AZ_CONV_PAIR(true, true, 2, 0); break;    // + A prefetch
+      case 2: AZ_CONV_PAIR(false, false, 2, 0); break;  // residual from global
+      case 5: AZ_CONV_PAIR(false, true, 2, 1); break;   // DIAG: no B loads
+      case 6: AZ_CONV_PAIR(false, true, 2, 2); break;   // DIAG: no A reads
+      default: AZ_CONV_PAIR(false, true, 2, 0); break;  // r1e: best measured
+    }
+#undef AZ_CONV_PAIR
     float* t = cur;
     cur = nxt;
     nxt = t;
