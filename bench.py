@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(15, cores-1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
+    ap.add_argument("--cache-log2", type=int, default=25,
+                    help="transposition cache (the reference's plays_inferences) entries = 2^N; 0 = off")
+    ap.add_argument("--no-cache-window", action="store_true",
+                    help="skip the second timed window with the cache bypassed")
     return ap.parse_args()
 
 
@@ -80,7 +84,8 @@ def cpu_baseline(args, weights):
         "value": round(games / wall, 4), "unit": "games/s", "cores": workers,
         "kind": "port", "expansions_per_s": round(exps / wall, 1),
         "sample": (f"oracle/refport.py self-play, C4 {args.sims} sims/move, {workers} worker processes "
-                   f"x 1 torch-CPU thread, batch-1 forward, per-game cache; {games} games in "
+                   f"x 1 torch-CPU thread, batch-1 forward, plays_inferences dict kept across each "
+                   f"worker's games; {games} games in "
                    f"{wall:.1f}s ({cpu_model})"),
     }
 
@@ -129,9 +134,10 @@ def main():
         off += k
 
     eng = az.Engine(args.height, args.width, args.n, True, args.sims, slots=args.slots,
-                    evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index)
+                    evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index,
+                    cache_log2=args.cache_log2)
     eng.set_weights(named)
-    budget = args.slots * (2 + (args.warmup + args.steps) // 5)
+    budget = args.slots * (2 + (args.warmup + 2 * args.steps) // 5)
     eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)
 
     eng.selfplay_step(args.warmup)
@@ -149,8 +155,34 @@ def main():
     st1 = eng.stats()
     eng.timer(False)
 
+    # second window, same slots continuing, cache bypassed: the rate without
+    # the reference's plays_inferences semantics (every leaf evaluated)
+    off = None
+    if args.cache_log2 and not args.no_cache_window:
+        eng.cache_enable(False)
+        if world > 1:
+            dist.barrier()
+        s0 = eng.stats()
+        t0 = time.perf_counter()
+        eng.selfplay_step(args.steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el2 = time.perf_counter() - t0
+        s1 = eng.stats()
+        g2 = s1["games_done"] - s0["games_done"]
+        if world > 1:
+            t2 = torch.tensor([g2, el2], dtype=torch.float64,
+                              device="cpu" if args.dist_backend == "gloo" else dev)
+            dist.all_reduce(t2[:1], op=dist.ReduceOp.SUM)
+            tm = t2[1:].clone()
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+            g2, el2 = int(t2[0].item()), float(tm.item())
+        off = {"value": round(g2 / el2, 3), "unit": "games/s", "ms_per_step": round(1e3 * el2 / args.steps, 3),
+               "expansions_per_s": round((s1["expansions"] - s0["expansions"]) / el2 * world, 1)}
+
     d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
-                                      "terminal_visits")}
+                                      "terminal_visits", "cache_hits", "evaluations")}
     conv_ms, conv_launches = st1["conv_ms"], st1["conv_launches"]
     if world > 1:
         red_dev = "cpu" if args.dist_backend == "gloo" else dev
@@ -167,7 +199,7 @@ def main():
     # dominant kernel: conv3x3_mfma (8 launches per forward at depth 4)
     HW, F = args.height * args.width, 128
     conv_flop_per_board = HW * 2 * F * F * 19 * args.depth       # 9F + 10F K per block
-    local_exp = st1["expansions"] - st0["expansions"]
+    local_exp = st1["evaluations"] - st0["evaluations"]  # boards the network computed
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     achieved = (local_exp * conv_flop_per_board) / (conv_ms * 1e-3) / 1e12 if conv_ms else 0.0
     boards_per_launch = local_exp / max(conv_launches / (2 * args.depth), 1)
@@ -202,6 +234,14 @@ def main():
             "simulations_per_s": round(d["simulations"] / elapsed, 1),
             "plies_per_s": round(d["plies"] / elapsed, 1),
             "games_timed": d["games_done"],
+            "network_evaluations_per_s": round(d["evaluations"] / elapsed, 1),
+            "transposition_cache": ({"entries": 2 ** args.cache_log2,
+                                     "hit_rate": round(d["cache_hits"] / max(d["expansions"], 1), 4),
+                                     "semantics": "reference plays_inferences (mcts.py:122-143): board -> "
+                                                  "network output, shared by all games, emptied when "
+                                                  "weights change; bit-identical results"}
+                                    if args.cache_log2 else None),
+            "cache_off": off,
             "roofline": {
                 "kernel": "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)",
                 "bound": "mfma",

@@ -41,6 +41,7 @@ struct az_engine {
   az::GameCfg g{};
   az::TreeDev t{};
   az::SampleDev smp{};
+  az::CacheDev cache{};
   az::NetDev net{};
   az::ConvTimer timer;
   float* x = nullptr;
@@ -99,18 +100,34 @@ void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
 // one simulation for every active slot (MCTS.search body, mcts.py:171-180)
 int simulate(az_engine* e) {
   hipStream_t s = e->stream;
-  AZ_HIP(hipMemsetAsync(e->t.eval_count, 0, sizeof(int32_t), s));
-  az::launch_select(e->g, e->t, s);
+  // eval_count, miss_count, nn_count are one contiguous block
+  AZ_HIP(hipMemsetAsync(e->t.eval_count, 0, 4 * sizeof(int32_t), s));
+  az::launch_select(e->g, e->t, e->cache, s);
+  const az::Board* rows = e->t.eval_board;
+  const int32_t* n_rows = e->t.eval_count;
+  if (e->cache.enabled) {
+    az::launch_dedup(e->g, e->t, s);
+    rows = e->t.nn_board;
+    n_rows = e->t.nn_count;
+  }
   if (e->cfg.evaluator == AZ_EVAL_NETWORK) {
-    az::launch_encode(e->t.eval_board, e->t.eval_count, e->g.slots, e->g.HW, e->x, s);
-    az::launch_forward(e->net, e->x, e->t.eval_count, e->g.slots, e->g.H, e->g.W, e->g.A,
-                       e->act[0], e->act[1], e->act[2], e->probs, e->values, s,
+    az::launch_encode(rows, n_rows, e->g.slots, e->g.HW, e->x, s);
+    az::launch_forward(e->net, e->x, n_rows, e->g.slots, e->g.H, e->g.W, e->g.A, e->act[0],
+                       e->act[1], e->act[2], e->probs, e->values, s,
                        e->timer.enabled ? &e->timer : nullptr);
   } else {
-    az::launch_synth_eval(e->g, e->t, e->probs, e->values, s);
+    az::launch_synth_eval(e->g, rows, n_rows, e->probs, e->values, s);
   }
-  az::launch_expand(e->g, e->t, e->probs, e->values, s);
+  az::launch_expand(e->g, e->t, e->cache, e->probs, e->values, s);
+  if (e->cache.enabled) az::launch_cache_insert(e->g, e->t, e->cache, e->probs, e->values, s);
   AZ_HIP(hipGetLastError());
+  return 0;
+}
+
+int cache_clear(az_engine* e) {
+  if (!e->cache.state) return 0;
+  AZ_HIP(hipMemsetAsync(e->cache.state, 0, ((size_t)e->cache.mask + 1) * sizeof(uint32_t), e->stream));
+  AZ_HIP(hipStreamSynchronize(e->stream));
   return 0;
 }
 
@@ -252,7 +269,9 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       (rc = e->alloc(&t.path, S * g.max_depth)) || (rc = e->alloc(&t.path_len, S)) ||
       (rc = e->alloc(&t.slot_expansions, S)) || (rc = e->alloc(&t.mt, S * (az::kMtN + 1))) ||
       (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_board, S)) ||
-      (rc = e->alloc(&t.eval_count, 1)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
+      (rc = e->alloc(&t.eval_src, S)) || (rc = e->alloc(&t.miss_q, S)) ||
+      (rc = e->alloc(&t.nn_board, S)) ||
+      (rc = e->alloc(&t.eval_count, 4)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
       (rc = e->alloc(&t.last_move, S)) || (rc = e->alloc(&t.last_status, S)) ||
       (rc = e->alloc(&t.last_policy, S * A)))
     return cleanup(rc);
@@ -265,6 +284,20 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       return cleanup(fail(AZ_E_HIP, "pow table upload failed"));
   }
   t.powtab = powtab;
+  t.miss_count = t.eval_count + 1;
+  t.nn_count = t.eval_count + 2;
+  if (c.cache_log2 < 0 || c.cache_log2 > 30) return cleanup(fail(AZ_E_INVALID, "cache_log2 must be 0..30"));
+  if (c.cache_log2 > 0) {
+    const size_t cap = (size_t)1 << c.cache_log2;
+    az::CacheDev& cd = e->cache;
+    if ((rc = e->alloc(&cd.keys, cap)) || (rc = e->alloc(&cd.state, cap)) ||
+        (rc = e->alloc(&cd.pay, cap * (A + 1))))
+      return cleanup(rc);
+    cd.mask = (uint32_t)(cap - 1);
+    cd.enabled = 1;
+    if (hipMemset(cd.state, 0, cap * sizeof(uint32_t)) != hipSuccess)
+      return cleanup(fail(AZ_E_HIP, "cache memset failed"));
+  }
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
     return cleanup(fail(AZ_E_HIP, "memset failed"));
@@ -369,7 +402,7 @@ int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
     if ((rc = upload(e, ds.w, a)) || (rc = upload(e, ds.b, c))) return rc;
   }
   net.ready = true;
-  return 0;
+  return cache_clear(e);  // cached outputs belong to the previous weights
 }
 
 int az_encode(az_engine* e, const int8_t* boards, int n, float* state, uint8_t* mask) {
@@ -437,7 +470,23 @@ int az_stats_get(az_engine* e, az_stats* st) {
   e->timer.flush();
   st->conv_ms = e->timer.total_ms;
   st->conv_launches = e->timer.launches;
+  st->cache_hits = (int64_t)h[az::kStatCacheHits];
+  st->evaluations = (int64_t)h[az::kStatNNEvals];
   return 0;
+}
+
+int az_cache_enable(az_engine* e, int on) {
+  if (!e) return fail(AZ_E_INVALID, "null engine");
+  if (!e->cache.state) return on ? fail(AZ_E_STATE, "engine created with cache_log2 = 0") : 0;
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  e->cache.enabled = on != 0;
+  return 0;
+}
+
+int az_cache_clear(az_engine* e) {
+  if (!e) return fail(AZ_E_INVALID, "null engine");
+  AZ_HIP(hipSetDevice(e->device));
+  return cache_clear(e);
 }
 
 int az_timer_enable(az_engine* e, int on) {

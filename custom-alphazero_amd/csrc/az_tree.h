@@ -28,7 +28,10 @@ enum : int {
   kStatSims = 4,         // per-slot simulations
   kStatPlies = 5,
   kStatNextGame = 6,     // next game id to hand to a free slot
-  kStatCount = 8
+  kStatCacheHits = 7,    // expansions served by the transposition cache
+  kStatNNEvals = 8,      // boards the evaluator actually computed
+  kStatCacheInserts = 9,
+  kStatCount = 12
 };
 enum : unsigned long long {
   kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16
@@ -48,15 +51,34 @@ struct TreeDev {
   int32_t* path_len;           // [slots]
   int32_t* slot_expansions;    // [slots], this game's expansions so far
   uint32_t* mt;                // [625][slots], word-major MT19937 state (+ index)
-  int32_t* eval_slot;          // [slots] compacted eval queue
+  int32_t* eval_slot;          // [slots] compacted eval queue (leaves to expand)
   Board* eval_board;           // [slots]
+  int32_t* eval_src;           // [slots] >= 0: cache entry; < 0: -(evaluator row + 1)
   int32_t* eval_count;         // [1]
+  int32_t* miss_q;             // [slots] eval-queue indices that missed the cache
+  int32_t* miss_count;         // [1]
+  Board* nn_board;             // [slots] unique boards the evaluator computes (cache on)
+  int32_t* nn_count;           // [1]
   unsigned long long* stats;   // [kStatCount]
   const double* powtab;        // [pow_len]: libm pow(n, 0.5), host-built
   // per-move outputs (MCTS API play())
   int32_t* last_move;          // [slots] action played (-1 none)
   int32_t* last_status;        // [slots] 0 ongoing / 1 win / 2 draw
   double* last_policy;         // [slots][A]
+};
+
+// Transposition cache = the reference's plays_inferences (mcts/mcts.py:122-143,
+// utils.py:38-39): board -> (probs[A], value), shared by every game on the
+// device, cleared when the weights change.  Open addressing, linear probing.
+// The evaluator is deterministic per board, so hits never change a search.
+enum : uint32_t { kCacheEmpty = 0, kCacheClaimed = 1, kCacheReady = 2 };
+struct CacheDev {
+  Board* keys = nullptr;       // [cap]
+  uint32_t* state = nullptr;   // [cap]
+  float* pay = nullptr;        // [cap][A+1]: probs then value
+  uint32_t mask = 0;           // cap - 1
+  int enabled = 0;
+  int max_probe = 32;
 };
 
 // Self-play sample sink, indexed by game id - first_game.
@@ -71,11 +93,15 @@ struct SampleDev {
   int32_t* expansions = nullptr;  // [n_games]
 };
 
-void launch_select(const GameCfg& g, const TreeDev& t, hipStream_t s);
-void launch_synth_eval(const GameCfg& g, const TreeDev& t, float* probs, float* values,
-                       hipStream_t s);
-void launch_expand(const GameCfg& g, const TreeDev& t, const float* probs, const float* values,
-                   hipStream_t s);
+void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s);
+// cache on: dedup this simulation's misses into nn_board / nn_count
+void launch_dedup(const GameCfg& g, const TreeDev& t, hipStream_t s);
+void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* count, float* probs,
+                       float* values, hipStream_t s);
+void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
+                   const float* values, hipStream_t s);
+void launch_cache_insert(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
+                         const float* values, hipStream_t s);
 // uniforms: device [slots] draws for play (MCTS API), or null -> per-slot MT19937;
 // greedy_mode -1 = by ply (self-play), 0/1 = caller's flag
 void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const double* uniforms,

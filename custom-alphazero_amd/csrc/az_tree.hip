@@ -93,7 +93,12 @@ __device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gi
 // ------------------------------------------------------------------- select
 // MCTS.select (mcts.py:111-120) + the terminal branch of MCTS.search
 // (mcts.py:176-180).  Non-terminal leaves are appended to the eval queue.
-__global__ __launch_bounds__(256) void select_kernel(GameCfg g, TreeDev t) {
+__device__ __forceinline__ bool same_board(const Board& a, const Board& b) {
+  return a.own[0] == b.own[0] && a.own[1] == b.own[1] && a.opp[0] == b.opp[0] &&
+         a.opp[1] == b.opp[1];
+}
+
+__global__ __launch_bounds__(256) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
   Edge* E = t.edges + (size_t)s * g.arena_cap;
@@ -146,30 +151,177 @@ __global__ __launch_bounds__(256) void select_kernel(GameCfg g, TreeDev t) {
   t.eval_slot[q] = s;
   t.eval_board[q] = b;
   t.path_len[s] = depth;
+  if (!c.enabled) {
+    t.eval_src[q] = -(q + 1);
+    stat_add(t, kStatNNEvals, 1);
+    return;
+  }
+  // repr(board) in plays_inferences (mcts.py:123): entries written by earlier
+  // simulations' insert kernels are complete (kernel boundary)
+  uint32_t idx = (uint32_t)board_hash(b) & c.mask;
+  for (int p = 0; p < c.max_probe; ++p) {
+    const uint32_t st = c.state[idx];
+    if (st == kCacheEmpty) break;
+    if (st == kCacheReady && same_board(c.keys[idx], b)) {
+      t.eval_src[q] = (int32_t)idx;
+      stat_add(t, kStatCacheHits, 1);
+      return;
+    }
+    idx = (idx + 1) & c.mask;
+  }
+  const int m = atomicAdd(t.miss_count, 1);
+  t.miss_q[m] = q;
+}
+
+// ------------------------------------------------------------------- dedup
+// One workgroup: bitonic sort of this simulation's misses by (board hash,
+// position), one evaluator row per distinct board (several games reaching the
+// same leaf in the same simulation share one network evaluation).
+constexpr int kDedupThreads = 1024;
+constexpr int kDedupMax = 8192;
+
+__global__ __launch_bounds__(kDedupThreads) void dedup_kernel(GameCfg g, TreeDev t) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  const int n = *t.miss_count;
+  const int tid = threadIdx.x;
+  if (n > kDedupMax) {  // no room to sort: one row per miss (still exact)
+    for (int i = tid; i < n; i += kDedupThreads) {
+      const int q = t.miss_q[i];
+      t.eval_src[q] = -(i + 1);
+      t.nn_board[i] = t.eval_board[q];
+    }
+    if (tid == 0) {
+      *t.nn_count = n;
+      atomicAdd(t.stats + kStatNNEvals, (unsigned long long)n);
+    }
+    return;
+  }
+  int N2 = 2;
+  while (N2 < n) N2 <<= 1;
+  uint64_t* fp = reinterpret_cast<uint64_t*>(dsm);
+  int32_t* ix = reinterpret_cast<int32_t*>(dsm + (size_t)kDedupMax * 8);
+  int32_t* part = ix + kDedupMax;  // [kDedupThreads] scan scratch
+  for (int i = tid; i < N2; i += kDedupThreads) {
+    if (i < n) {
+      fp[i] = board_hash(t.eval_board[t.miss_q[i]]);
+      ix[i] = i;
+    } else {
+      fp[i] = ~0ull;
+      ix[i] = 0x7fffffff;
+    }
+  }
+  __syncthreads();
+  for (int k = 2; k <= N2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < N2; i += kDedupThreads) {
+        const int p = i ^ j;
+        if (p > i) {
+          const bool up = (i & k) == 0;
+          const bool gt = fp[i] > fp[p] || (fp[i] == fp[p] && ix[i] > ix[p]);
+          if (gt == up) {
+            const uint64_t tf = fp[i];
+            fp[i] = fp[p];
+            fp[p] = tf;
+            const int32_t ti = ix[i];
+            ix[i] = ix[p];
+            ix[p] = ti;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // leaders: first of each run of equal boards; block-wide inclusive scan
+  const int per = (n + kDedupThreads - 1) / kDedupThreads;
+  const int lo = tid * per, hi = min(n, lo + per);
+  int cnt = 0;
+  for (int i = lo; i < hi; ++i) {
+    const bool lead = i == 0 || fp[i] != fp[i - 1] ||
+                      !same_board(t.eval_board[t.miss_q[ix[i]]], t.eval_board[t.miss_q[ix[i - 1]]]);
+    cnt += lead;
+  }
+  part[tid] = cnt;
+  __syncthreads();
+  for (int off = 1; off < kDedupThreads; off <<= 1) {
+    const int v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int u = (tid ? part[tid - 1] : 0) - 1;
+  for (int i = lo; i < hi; ++i) {
+    const int q = t.miss_q[ix[i]];
+    const bool lead = i == 0 || fp[i] != fp[i - 1] ||
+                      !same_board(t.eval_board[q], t.eval_board[t.miss_q[ix[i - 1]]]);
+    if (lead) {
+      ++u;
+      t.nn_board[u] = t.eval_board[q];
+    }
+    t.eval_src[q] = -(u + 1);
+  }
+  if (tid == kDedupThreads - 1) {
+    *t.nn_count = part[kDedupThreads - 1];
+    atomicAdd(t.stats + kStatNNEvals, (unsigned long long)part[kDedupThreads - 1]);
+  }
+}
+
+// ------------------------------------------------------------ cache insert
+// plays_inferences[repr(board)] = probabilities, value (mcts.py:142): one
+// writer per distinct board (dedup), racing only for empty slots.
+__global__ __launch_bounds__(256) void cache_insert_kernel(GameCfg g, TreeDev t, CacheDev c,
+                                                           const float* __restrict__ probs,
+                                                           const float* __restrict__ values) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= *t.nn_count) return;
+  const Board b = t.nn_board[u];
+  uint32_t idx = (uint32_t)board_hash(b) & c.mask;
+  for (int p = 0; p < c.max_probe; ++p) {
+    if (atomicCAS(c.state + idx, kCacheEmpty, kCacheClaimed) == kCacheEmpty) {
+      c.keys[idx] = b;
+      float* dst = c.pay + (size_t)idx * (g.A + 1);
+      for (int a = 0; a < g.A; ++a) dst[a] = probs[(size_t)u * g.A + a];
+      dst[g.A] = values[u];
+      __threadfence();
+      atomicExch(c.state + idx, kCacheReady);
+      stat_add(t, kStatCacheInserts, 1);
+      return;
+    }
+    idx = (idx + 1) & c.mask;
+  }
 }
 
 // ------------------------------------------------------ synthetic evaluator
-__global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, TreeDev t,
+__global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, const Board* __restrict__ boards,
+                                                         const int32_t* __restrict__ count,
                                                          float* __restrict__ probs,
                                                          float* __restrict__ values) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *t.eval_count) return;
-  synth_eval(t.eval_board[i], g.A, probs + (size_t)i * g.A, values + i);
+  if (i >= *count) return;
+  synth_eval(boards[i], g.A, probs + (size_t)i * g.A, values + i);
 }
 
 // ------------------------------------------------------------------- expand
 // MCTS.evaluate_and_expand (mcts.py:145-161) with normalize_probabilities
 // (mcts/utils.py:4-16), then backup(-value) (mcts.py:175, 163-168).
 template <int MAXA>
-__global__ __launch_bounds__(256) void expand_kernel(GameCfg g, TreeDev t,
+__global__ __launch_bounds__(256) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
                                                      const float* __restrict__ probs,
                                                      const float* __restrict__ values) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= *t.eval_count) return;
   const int s = t.eval_slot[i];
   const Board b = t.eval_board[i];
-  const float* p = probs + (size_t)i * g.A;
-  const float v = values[i];
+  const int src = t.eval_src[i];
+  const float* p;
+  float v;
+  if (src >= 0) {  // cache hit
+    p = c.pay + (size_t)src * (g.A + 1);
+    v = p[g.A];
+  } else {
+    const int row = -src - 1;
+    p = probs + (size_t)row * g.A;
+    v = values[row];
+  }
   float masked[MAXA];
   int nl = 0;
   for (int a = 0; a < g.A; ++a)
@@ -333,21 +485,31 @@ __global__ void slot_set_root_kernel(GameCfg g, TreeDev t, const int32_t* slots,
 // ---------------------------------------------------------------- launchers
 static inline int blocks_for(int n) { return (n + 255) / 256; }
 
-void launch_select(const GameCfg& g, const TreeDev& t, hipStream_t s) {
-  select_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t);
+void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s) {
+  select_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, c);
 }
 
-void launch_synth_eval(const GameCfg& g, const TreeDev& t, float* probs, float* values,
-                       hipStream_t s) {
-  synth_eval_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, probs, values);
+void launch_dedup(const GameCfg& g, const TreeDev& t, hipStream_t s) {
+  const size_t lds = (size_t)kDedupMax * 12 + kDedupThreads * 4;
+  dedup_kernel<<<1, kDedupThreads, lds, s>>>(g, t);
 }
 
-void launch_expand(const GameCfg& g, const TreeDev& t, const float* probs, const float* values,
-                   hipStream_t s) {
+void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* count, float* probs,
+                       float* values, hipStream_t s) {
+  synth_eval_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, boards, count, probs, values);
+}
+
+void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
+                   const float* values, hipStream_t s) {
   if (g.A <= 16)
-    expand_kernel<16><<<blocks_for(g.slots), 256, 0, s>>>(g, t, probs, values);
+    expand_kernel<16><<<blocks_for(g.slots), 256, 0, s>>>(g, t, c, probs, values);
   else
-    expand_kernel<kMaxActions><<<blocks_for(g.slots), 256, 0, s>>>(g, t, probs, values);
+    expand_kernel<kMaxActions><<<blocks_for(g.slots), 256, 0, s>>>(g, t, c, probs, values);
+}
+
+void launch_cache_insert(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
+                         const float* values, hipStream_t s) {
+  cache_insert_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, c, probs, values);
 }
 
 void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const double* uniforms,

@@ -28,7 +28,7 @@ class Config(ctypes.Structure):
         ("evaluator", ctypes.c_int32), ("filters", ctypes.c_int32), ("depth", ctypes.c_int32),
         ("value_hidden", ctypes.c_int32), ("bn_epsilon", ctypes.c_double),
         ("arena_edges", ctypes.c_int64), ("max_tree_visits", ctypes.c_int64),
-        ("reserved", ctypes.c_int32 * 8),
+        ("cache_log2", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7),
     ]
 
 
@@ -43,7 +43,8 @@ class Stats(ctypes.Structure):
         ("games_done", ctypes.c_int64), ("simulations", ctypes.c_int64),
         ("plies", ctypes.c_int64), ("active_slots", ctypes.c_int64), ("errors", ctypes.c_int64),
         ("conv_launches", ctypes.c_int64), ("conv_ms", ctypes.c_double),
-        ("reserved", ctypes.c_int64 * 7),
+        ("cache_hits", ctypes.c_int64), ("evaluations", ctypes.c_int64),
+        ("reserved", ctypes.c_int64 * 5),
     ]
 
     def as_dict(self):
@@ -55,6 +56,7 @@ EXPORTED = (
     "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
     "az_selfplay_run", "az_selfplay_results", "az_tree_reset", "az_tree_search", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
+    "az_cache_clear", "az_cache_enable",
 )
 
 _lib = None
@@ -97,6 +99,8 @@ def load_library():
         "az_stats_get": (ctypes.c_int, [P, ctypes.POINTER(Stats)]),
         "az_timer_enable": (ctypes.c_int, [P, ctypes.c_int]),
         "az_pow_table": (ctypes.c_int, [P, P, I64]),
+        "az_cache_clear": (ctypes.c_int, [P]),
+        "az_cache_enable": (ctypes.c_int, [P, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -123,7 +127,7 @@ class Engine:
     def __init__(self, height=6, width=7, n=4, gravity=True, mcts_iterations=100, slots=1,
                  evaluator=EVAL_NETWORK, index_move_greedy=8, exploration_constant=1.5,
                  filters=128, depth=4, value_hidden=256, bn_epsilon=1e-3, arena_edges=0,
-                 max_tree_visits=0, device=0):
+                 max_tree_visits=0, device=0, cache_log2=0):
         L = load_library()
         self.height, self.width, self.n, self.gravity = height, width, n, bool(gravity)
         self.action_space = width if gravity else width * height
@@ -134,7 +138,7 @@ class Engine:
                      exploration_constant=exploration_constant, slots=slots, evaluator=evaluator,
                      filters=filters, depth=depth, value_hidden=value_hidden,
                      bn_epsilon=bn_epsilon, arena_edges=arena_edges,
-                     max_tree_visits=max_tree_visits)
+                     max_tree_visits=max_tree_visits, cache_log2=cache_log2)
         handle = ctypes.c_void_p()
         _check(L.az_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
         self._h = handle
@@ -264,6 +268,12 @@ class Engine:
         st = Stats()
         _check(self._L.az_stats_get(self._h, ctypes.byref(st)))
         return st.as_dict()
+
+    def cache_clear(self):
+        _check(self._L.az_cache_clear(self._h))
+
+    def cache_enable(self, on=True):
+        _check(self._L.az_cache_enable(self._h, int(bool(on))))
 
     def timer(self, on):
         _check(self._L.az_timer_enable(self._h, int(bool(on))))

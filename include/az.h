@@ -53,7 +53,9 @@ typedef struct az_config {
     double bn_epsilon;             /* Keras BatchNormalization epsilon (1e-3) */
     int64_t arena_edges;           /* tree edges per slot; 0 = mcts_iterations*H*W*A */
     int64_t max_tree_visits;       /* bound on visits through one node; 0 = mcts_iterations*H*W */
-    int32_t reserved[8];
+    int32_t cache_log2;            /* transposition cache entries = 2^cache_log2 (the reference's
+                                      plays_inferences, mcts/mcts.py:122-143); 0 = off */
+    int32_t reserved[7];
 } az_config;
 
 /* One named weight tensor in Keras layout ("Weights"). */
@@ -75,7 +77,9 @@ typedef struct az_stats {
     int64_t errors;           /* device error flags (0 = none) */
     int64_t conv_launches;    /* timed conv kernels (az_timer_enable) */
     double conv_ms;           /* their summed device time */
-    int64_t reserved[7];
+    int64_t cache_hits;       /* expansions served by the transposition cache */
+    int64_t evaluations;      /* boards the evaluator computed (network or synthetic) */
+    int64_t reserved[5];
 } az_stats;
 
 int az_abi_version(void);
@@ -132,6 +136,11 @@ int az_tree_export(az_engine* eng, int slot, double* prior, double* w, int32_t* 
                    int32_t* child_n, int32_t* action, float* child_value);
 
 int az_stats_get(az_engine* eng, az_stats* st);
+/* plays_inferences reset (self_play.py:145-146: a new best model empties the
+ * cache); az_engine_set_weights also clears it. */
+int az_cache_clear(az_engine* eng);
+/* Bypass (0) or use (1) an allocated cache; results are identical either way. */
+int az_cache_enable(az_engine* eng, int on);
 int az_timer_enable(az_engine* eng, int on);
 /* The host-built libm pow(k, 0.5) table the kernels use (tests). */
 int az_pow_table(az_engine* eng, double* out, int64_t n);

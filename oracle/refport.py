@@ -334,8 +334,9 @@ def baseline_worker(args):
     net = TorchCPUNet(weights, depth)
     t0 = time.perf_counter()
     games = expansions = 0
+    cache = {}  # plays_inferences: kept across this worker's games (utils.py:38-39)
     while time.perf_counter() - t0 < budget_s:
-        r = play_game(height, width, n, gravity, sims, seed + games, net, cache={})
+        r = play_game(height, width, n, gravity, sims, seed + games, net, cache=cache)
         games += 1
         expansions += r["expansions"]
     return games, expansions, time.perf_counter() - t0
