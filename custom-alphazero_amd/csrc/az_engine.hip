@@ -100,13 +100,14 @@ void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
 // one simulation for every active slot (MCTS.search body, mcts.py:171-180)
 int simulate(az_engine* e) {
   hipStream_t s = e->stream;
-  // eval_count, miss_count, nn_count are one contiguous block
+  // eval_count, miss_count, nn_count, dup_count are one contiguous block
   AZ_HIP(hipMemsetAsync(e->t.eval_count, 0, 4 * sizeof(int32_t), s));
+  e->t.epoch += 1;  // fresh per-simulation dedup table (tags of older epochs read as empty)
   az::launch_select(e->g, e->t, e->cache, s);
   const az::Board* rows = e->t.eval_board;
   const int32_t* n_rows = e->t.eval_count;
   if (e->cache.enabled) {
-    az::launch_dedup(e->g, e->t, s);
+    az::launch_dedup_resolve(e->g, e->t, s);
     rows = e->t.nn_board;
     n_rows = e->t.nn_count;
   }
@@ -286,6 +287,18 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   t.powtab = powtab;
   t.miss_count = t.eval_count + 1;
   t.nn_count = t.eval_count + 2;
+  t.dup_count = t.eval_count + 3;
+  {
+    size_t cap = 1024;
+    while (cap < 4 * S) cap <<= 1;  // load factor <= 25%
+    if ((rc = e->alloc(&t.step_tag, cap)) || (rc = e->alloc(&t.step_row, cap) ) ||
+        (rc = e->alloc(&t.dup_q, S)))
+      return cleanup(rc);
+    if (hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)) != hipSuccess)
+      return cleanup(fail(AZ_E_HIP, "memset failed"));
+    t.step_mask = (uint32_t)(cap - 1);
+    t.epoch = 0;
+  }
   if (c.cache_log2 < 0 || c.cache_log2 > 30) return cleanup(fail(AZ_E_INVALID, "cache_log2 must be 0..30"));
   if (c.cache_log2 > 0) {
     const size_t cap = (size_t)1 << c.cache_log2;

@@ -113,7 +113,6 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
 // v_mfma_f32_32x32x2_f32 is an exact f32 FMA chain; inside a chunk lane half
 // h owns k = 16h..16h+15 and k-step s sums the pair (s, 16+s): a fixed order
 // per output element, independent of the batch.
-constexpr int kTileRows = 64;
 constexpr int kChunkK = 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -126,29 +125,33 @@ __device__ __forceinline__ int slab_swz(int chunk, int key) {
 //   PREA  : read the next chunk's A fragments from LDS one chunk ahead
 //   XSLAB : stage the fused residual's block-input rows in LDS (else: global)
 //   OCC   : __launch_bounds__ waves per SIMD (register cap)
-size_t conv_lds_bytes(int W, bool residual, bool xslab) {
-  const int slab_rows = kTileRows + 2 * (W + 1);
-  return (size_t)(slab_rows + 1 + (residual && xslab ? kTileRows : 0)) * 512;
+size_t conv_lds_bytes(int TR, int W, bool residual, bool xslab) {
+  const int slab_rows = TR + 2 * (W + 1);
+  return (size_t)(slab_rows + 1 + (residual && xslab ? TR : 0)) * 512;
 }
 
 // DIAG (timing experiments only, wrong outputs): 1 = no B loads after the
 // first two chunks, 2 = no A LDS reads after the first chunk.
-template <int F, bool RESIDUAL, bool PREA, bool XSLAB, int OCC, int DIAG = 0>
+// TR = tile rows: 64 -> each wave 32 rows x two 32x32 MFMA tiles; 32 -> each
+// wave 32 rows x one tile (twice the workgroups: better balance for small batches).
+template <int F, bool RESIDUAL, bool PREA, bool XSLAB, int OCC, int DIAG = 0, int TR = 64>
 __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ wpack, const float* __restrict__ bias, float* __restrict__ out,
     const int* __restrict__ count, int n_static, int H, int W) {
   static_assert(F == 128, "tile assumes F = 128 channels (32 16-byte chunks per row)");
   constexpr int NCH = (RESIDUAL ? 10 : 9) * (F / kChunkK);
+  constexpr int TPW = TR / 32;  // MFMA tiles per wave
+  constexpr int CG = 4 / TPW;   // column groups
   extern __shared__ __attribute__((aligned(16))) float4 lds4[];
 
   const int HW = H * W, halo = W + 1;
   const int n_boards = count ? *count : n_static;
   const int rows = n_boards * HW;
-  const int row0 = blockIdx.x * kTileRows;
+  const int row0 = blockIdx.x * TR;
   if (row0 >= rows) return;
   const int tid = threadIdx.x;
-  const int slab_rows = kTileRows + 2 * halo;
+  const int slab_rows = TR + 2 * halo;
   float4* slab = lds4;
   float4* zero_row = lds4 + slab_rows * 32;
   float4* xslab = zero_row + 32;
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
   if (tid < 32) zero_row[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
   if constexpr (RESIDUAL && XSLAB) {
     const float4* x4 = reinterpret_cast<const float4*>(res_in);
-    for (int i = tid; i < kTileRows * 32; i += 256) {
+    for (int i = tid; i < TR * 32; i += 256) {
       const int r = i >> 5, j = i & 31, g = row0 + r;
       const float4 v = g < rows ? x4[(size_t)g * 32 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
       xslab[r * 32 + slab_swz(j, r)] = v;
@@ -173,29 +176,29 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
 
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
-  const int rg = wave >> 1, cg = wave & 1;
+  const int rg = wave / CG, cg = wave % CG;
   const int rl = rg * 32 + r32;        // local row of this lane's A operand
   const int grow = row0 + rl;
   const int pos = grow % HW;
   const int py = pos / W, px = pos - (pos / W) * W;
   const bool row_ok = grow < rows;
 
-  f32x16 acc[2];
+  f32x16 acc[TPW];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < TPW; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.0f;
 
   // B fragment stream: float4 index ((c*4 + tile)*4 + q)*64 + lane.  Two
   // register buffers in ping-pong (the loop is unrolled by two, so no copy):
   // chunk c+1's loads are first consumed a whole chunk of MFMAs later.
-  const float4* wl = wpack + (size_t)(2 * cg) * 256 + lane;
-  float4 b0[2][4], b1[2][4];
-  auto load_b = [&](int c, float4 (&dst)[2][4]) {
+  const float4* wl = wpack + (size_t)(TPW * cg) * 256 + lane;
+  float4 b0[TPW][4], b1[TPW][4];
+  auto load_b = [&](int c, float4 (&dst)[TPW][4]) {
     if (DIAG == 1 && c >= 2) return;
     const float4* wn = wl + (size_t)c * 1024;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < TPW; ++t)
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[t][q] = wn[t * 256 + q * 64];
   };
@@ -226,14 +229,14 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[q] = base[slab_swz(cbase + q, key)];
   };
-  auto compute = [&](const float4 (&a4)[4], const float4 (&bc)[2][4]) {
+  auto compute = [&](const float4 (&a4)[4], const float4 (&bc)[TPW][4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float av[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TPW; ++t) {
           const float bv = e == 0 ? bc[t][q].x : e == 1 ? bc[t][q].y : e == 2 ? bc[t][q].z : bc[t][q].w;
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv, acc[t], 0, 0, 0);
         }
@@ -266,8 +269,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
 
   // epilogue: C/D map col = lane&31, row = (i&3) + 8*(i>>2) + 4*h
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int col = (2 * cg + t) * 32 + r32;
+  for (int t = 0; t < TPW; ++t) {
+    const int col = (TPW * cg + t) * 32 + r32;
     const float bcol = bias[col];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -393,7 +396,7 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
     stem_conv_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(
         reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
   }
-  const int grid = (n_max * HW + kTileRows - 1) / kTileRows;
+  const int grid64 = (n_max * HW + 63) / 64, grid32 = (n_max * HW + 31) / 32;
   float* cur = act_a;  // block input
   float* mid = act_b;
   float* nxt = act_c;
@@ -405,17 +408,21 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   for (int d = 0; d < net.depth; ++d) {
     const float4* w1 = reinterpret_cast<const float4*>(net.c1_w[d]);
     const float4* w2 = reinterpret_cast<const float4*>(net.c2_w[d]);
-#define AZ_CONV_PAIR(PREA, XSLAB, OCC, DIAG)                                                    \
-  conv3x3_mfma_kernel<F, false, PREA, XSLAB, OCC, DIAG><<<grid, 256, conv_lds_bytes(W, false, XSLAB), s>>>( \
-      cur, nullptr, w1, net.c1_b[d], mid, count, n_max, H, W);                                  \
-  conv3x3_mfma_kernel<F, true, PREA, XSLAB, OCC, DIAG><<<grid, 256, conv_lds_bytes(W, true, XSLAB), s>>>(   \
-      mid, cur, w2, net.c2_b[d], nxt, count, n_max, H, W)
+#define AZ_CONV_PAIR(PREA, XSLAB, OCC, DIAG, TR)                                                \
+  conv3x3_mfma_kernel<F, false, PREA, XSLAB, OCC, DIAG, TR>                                     \
+      <<<TR == 64 ? grid64 : grid32, 256, conv_lds_bytes(TR, W, false, XSLAB), s>>>(             \
+          cur, nullptr, w1, net.c1_b[d], mid, count, n_max, H, W);                              \
+  conv3x3_mfma_kernel<F, true, PREA, XSLAB, OCC, DIAG, TR>                                      \
+      <<<TR == 64 ? grid64 : grid32, 256, conv_lds_bytes(TR, W, true, XSLAB), s>>>(              \
+          mid, cur, w2, net.c2_b[d], nxt, count, n_max, H, W)
     switch (variant) {
-      case 1: AZ_CONV_PAIR(true, true, 2, 0); break;    // + A prefetch
-      case 2: AZ_CONV_PAIR(false, false, 2, 0); break;  // residual from global
-      case 5: AZ_CONV_PAIR(false, true, 2, 1); break;   // DIAG: no B loads
-      case 6: AZ_CONV_PAIR(false, true, 2, 2); break;   // DIAG: no A reads
-      default: AZ_CONV_PAIR(false, true, 2, 0); break;  // r1e: best measured
+      case 1: AZ_CONV_PAIR(true, true, 2, 0, 64); break;    // + A prefetch
+      case 2: AZ_CONV_PAIR(false, false, 2, 0, 64); break;  // residual from global
+      case 5: AZ_CONV_PAIR(false, true, 2, 1, 64); break;   // DIAG: no B loads
+      case 6: AZ_CONV_PAIR(false, true, 2, 2, 64); break;   // DIAG: no A reads
+      case 7: AZ_CONV_PAIR(false, true, 2, 0, 64); break;   // 64-row tiles (r1e)
+      case 8: AZ_CONV_PAIR(false, false, 4, 0, 32); break;  // 32-row tiles, residual global, 4 w/SIMD
+      default: AZ_CONV_PAIR(false, true, 2, 0, 32); break;  // 32-row tiles: best measured (r1m)
     }
 #undef AZ_CONV_PAIR
     float* t = cur;

@@ -59,6 +59,12 @@ struct TreeDev {
   int32_t* miss_count;         // [1]
   Board* nn_board;             // [slots] unique boards the evaluator computes (cache on)
   int32_t* nn_count;           // [1]
+  int32_t* dup_q;              // [slots] misses whose board tag matched another miss
+  int32_t* dup_count;          // [1]
+  uint64_t* step_tag;          // [step_cap] per-simulation dedup table: (epoch << 32) | fp32
+  int32_t* step_row;           // [step_cap] evaluator row of the tag's owner
+  uint32_t step_mask;          // step_cap - 1
+  uint32_t epoch;              // simulation counter (tags of older epochs read as empty)
   unsigned long long* stats;   // [kStatCount]
   const double* powtab;        // [pow_len]: libm pow(n, 0.5), host-built
   // per-move outputs (MCTS API play())
@@ -94,8 +100,9 @@ struct SampleDev {
 };
 
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s);
-// cache on: dedup this simulation's misses into nn_board / nn_count
-void launch_dedup(const GameCfg& g, const TreeDev& t, hipStream_t s);
+// cache on: misses are deduplicated inside select (step tag table); this
+// resolves the ones whose tag matched, by full-board compare
+void launch_dedup_resolve(const GameCfg& g, const TreeDev& t, hipStream_t s);
 void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* count, float* probs,
                        float* values, hipStream_t s);
 void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,

@@ -169,99 +169,59 @@ __global__ __launch_bounds__(256) void select_kernel(GameCfg g, TreeDev t, Cache
     }
     idx = (idx + 1) & c.mask;
   }
-  const int m = atomicAdd(t.miss_count, 1);
-  t.miss_q[m] = q;
+  // miss: one evaluator row per distinct board in this simulation.  Tag =
+  // (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
+  // empty, so the table needs no clearing.  A tag match is only a candidate:
+  // dedup_resolve compares the full boards after this kernel.
+  atomicAdd(t.miss_count, 1);
+  const uint64_t h = board_hash(b);
+  const uint64_t tag = ((uint64_t)t.epoch << 32) | (uint32_t)(h >> 32);
+  uint32_t slot = (uint32_t)h & t.step_mask;
+  for (uint32_t p = 0; p <= t.step_mask; ++p) {
+    const uint64_t cur = __hip_atomic_load(t.step_tag + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(cur >> 32) != t.epoch) {  // empty in this epoch: try to own it
+      const uint64_t prev = atomicCAS((unsigned long long*)(t.step_tag + slot), cur, tag);
+      if (prev == cur) {
+        const int row = atomicAdd(t.nn_count, 1);
+        t.nn_board[row] = b;
+        t.step_row[slot] = row;
+        t.eval_src[q] = -(row + 1);
+        return;
+      }
+      if (prev == tag) {  // lost the race to the same tag
+        t.eval_src[q] = (int32_t)(0x80000000u | slot);
+        t.dup_q[atomicAdd(t.dup_count, 1)] = q;
+        return;
+      }
+      continue;  // someone else took this slot with another tag: re-read it
+    }
+    if (cur == tag) {
+      t.eval_src[q] = (int32_t)(0x80000000u | slot);
+      t.dup_q[atomicAdd(t.dup_count, 1)] = q;
+      return;
+    }
+    slot = (slot + 1) & t.step_mask;
+  }
 }
 
-// ------------------------------------------------------------------- dedup
-// One workgroup: bitonic sort of this simulation's misses by (board hash,
-// position), one evaluator row per distinct board (several games reaching the
-// same leaf in the same simulation share one network evaluation).
-constexpr int kDedupThreads = 1024;
-constexpr int kDedupMax = 8192;
-
-__global__ __launch_bounds__(kDedupThreads) void dedup_kernel(GameCfg g, TreeDev t) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  const int n = *t.miss_count;
-  const int tid = threadIdx.x;
-  if (n > kDedupMax) {  // no room to sort: one row per miss (still exact)
-    for (int i = tid; i < n; i += kDedupThreads) {
-      const int q = t.miss_q[i];
-      t.eval_src[q] = -(i + 1);
-      t.nn_board[i] = t.eval_board[q];
-    }
-    if (tid == 0) {
-      *t.nn_count = n;
-      atomicAdd(t.stats + kStatNNEvals, (unsigned long long)n);
-    }
-    return;
-  }
-  int N2 = 2;
-  while (N2 < n) N2 <<= 1;
-  uint64_t* fp = reinterpret_cast<uint64_t*>(dsm);
-  int32_t* ix = reinterpret_cast<int32_t*>(dsm + (size_t)kDedupMax * 8);
-  int32_t* part = ix + kDedupMax;  // [kDedupThreads] scan scratch
-  for (int i = tid; i < N2; i += kDedupThreads) {
-    if (i < n) {
-      fp[i] = board_hash(t.eval_board[t.miss_q[i]]);
-      ix[i] = i;
-    } else {
-      fp[i] = ~0ull;
-      ix[i] = 0x7fffffff;
-    }
-  }
-  __syncthreads();
-  for (int k = 2; k <= N2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < N2; i += kDedupThreads) {
-        const int p = i ^ j;
-        if (p > i) {
-          const bool up = (i & k) == 0;
-          const bool gt = fp[i] > fp[p] || (fp[i] == fp[p] && ix[i] > ix[p]);
-          if (gt == up) {
-            const uint64_t tf = fp[i];
-            fp[i] = fp[p];
-            fp[p] = tf;
-            const int32_t ti = ix[i];
-            ix[i] = ix[p];
-            ix[p] = ti;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // leaders: first of each run of equal boards; block-wide inclusive scan
-  const int per = (n + kDedupThreads - 1) / kDedupThreads;
-  const int lo = tid * per, hi = min(n, lo + per);
-  int cnt = 0;
-  for (int i = lo; i < hi; ++i) {
-    const bool lead = i == 0 || fp[i] != fp[i - 1] ||
-                      !same_board(t.eval_board[t.miss_q[ix[i]]], t.eval_board[t.miss_q[ix[i - 1]]]);
-    cnt += lead;
-  }
-  part[tid] = cnt;
-  __syncthreads();
-  for (int off = 1; off < kDedupThreads; off <<= 1) {
-    const int v = tid >= off ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  int u = (tid ? part[tid - 1] : 0) - 1;
-  for (int i = lo; i < hi; ++i) {
-    const int q = t.miss_q[ix[i]];
-    const bool lead = i == 0 || fp[i] != fp[i - 1] ||
-                      !same_board(t.eval_board[q], t.eval_board[t.miss_q[ix[i - 1]]]);
-    if (lead) {
-      ++u;
-      t.nn_board[u] = t.eval_board[q];
-    }
-    t.eval_src[q] = -(u + 1);
-  }
-  if (tid == kDedupThreads - 1) {
-    *t.nn_count = part[kDedupThreads - 1];
-    atomicAdd(t.stats + kStatNNEvals, (unsigned long long)part[kDedupThreads - 1]);
+// ----------------------------------------------------------- dedup resolve
+// Misses whose step tag matched an owner's: same board -> share the owner's
+// evaluator row; a fingerprint collision (different board) -> its own row.
+__global__ __launch_bounds__(256) void dedup_resolve_kernel(GameCfg g, TreeDev t) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) atomicAdd(t.stats + kStatNNEvals, (unsigned long long)*t.nn_count);
+  if (i >= *t.dup_count) return;
+  const int q = t.dup_q[i];
+  const uint32_t slot = (uint32_t)t.eval_src[q] & 0x7fffffffu;
+  const int row = t.step_row[slot];
+  const Board b = t.eval_board[q];
+  if (same_board(t.nn_board[row], b)) {
+    t.eval_src[q] = -(row + 1);
+  } else {
+    const int r2 = atomicAdd(t.nn_count, 1);
+    t.nn_board[r2] = b;
+    t.eval_src[q] = -(r2 + 1);
+    atomicAdd(t.stats + kStatNNEvals, 1ull);
   }
 }
 
@@ -489,9 +449,8 @@ void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStr
   select_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, c);
 }
 
-void launch_dedup(const GameCfg& g, const TreeDev& t, hipStream_t s) {
-  const size_t lds = (size_t)kDedupMax * 12 + kDedupThreads * 4;
-  dedup_kernel<<<1, kDedupThreads, lds, s>>>(g, t);
+void launch_dedup_resolve(const GameCfg& g, const TreeDev& t, hipStream_t s) {
+  dedup_resolve_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t);
 }
 
 void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* count, float* probs,
