@@ -36,8 +36,8 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=60)
     ap.add_argument("--slots", type=int, default=4096)
     ap.add_argument("--sims", type=int, default=100)
     ap.add_argument("--height", type=int, default=6)
