@@ -59,10 +59,9 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
                                                         const float* __restrict__ bias,
                                                         const int* __restrict__ count, int n_static,
                                                         int H, int W, float* __restrict__ out) {
+  // weights (18 KB) are read through L1 by every thread: no per-block LDS
+  // staging (which cost ~18 KB of L2 traffic per 256 outputs)
   constexpr int G4 = F / 4;
-  __shared__ float w_s[36 * F];
-  for (int i = threadIdx.x; i < 36 * F; i += blockDim.x) w_s[i] = ws[i];
-  __syncthreads();
   const int n = count ? *count : n_static;
   const int HW = H * W;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -79,7 +78,7 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
     const float vin[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float4 wv = *reinterpret_cast<const float4*>(w_s + (tap * 4 + c) * F + cg * 4);
+      const float4 wv = *reinterpret_cast<const float4*>(ws + (tap * 4 + c) * F + cg * 4);
       acc.x += vin[c] * wv.x;
       acc.y += vin[c] * wv.y;
       acc.z += vin[c] * wv.z;
@@ -132,17 +131,20 @@ size_t conv_lds_bytes(int TR, int W, bool residual, bool xslab) {
 
 // DIAG (timing experiments only, wrong outputs): 1 = no B loads after the
 // first two chunks, 2 = no A LDS reads after the first chunk.
-// TR = tile rows: 64 -> each wave 32 rows x two 32x32 MFMA tiles; 32 -> each
-// wave 32 rows x one tile (twice the workgroups: better balance for small batches).
-template <int F, bool RESIDUAL, bool PREA, bool XSLAB, int OCC, int DIAG = 0, int TR = 64>
+// Tile shape: each wave owns RPW x TPW 32x32 MFMA tiles (RPW row tiles that
+// share every B fragment, TPW column tiles that share every A fragment); the
+// four waves of a workgroup are CG = 4/TPW column groups x RG = 4/CG row
+// groups, so a workgroup covers TR = 32*RPW*RG rows x 128 columns.
+template <int F, bool RESIDUAL, bool PREA, bool XSLAB, int OCC, int DIAG, int TPW, int RPW>
 __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ wpack, const float* __restrict__ bias, float* __restrict__ out,
     const int* __restrict__ count, int n_static, int H, int W) {
   static_assert(F == 128, "tile assumes F = 128 channels (32 16-byte chunks per row)");
   constexpr int NCH = (RESIDUAL ? 10 : 9) * (F / kChunkK);
-  constexpr int TPW = TR / 32;  // MFMA tiles per wave
   constexpr int CG = 4 / TPW;   // column groups
+  constexpr int RG = 4 / CG;    // row groups
+  constexpr int TR = 32 * RPW * RG;
   extern __shared__ __attribute__((aligned(16))) float4 lds4[];
 
   const int HW = H * W, halo = W + 1;
@@ -177,17 +179,25 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
   const int rg = wave / CG, cg = wave % CG;
-  const int rl = rg * 32 + r32;        // local row of this lane's A operand
-  const int grow = row0 + rl;
-  const int pos = grow % HW;
-  const int py = pos / W, px = pos - (pos / W) * W;
-  const bool row_ok = grow < rows;
+  int rl[RPW], grow[RPW], py[RPW], px[RPW];
+  bool row_ok[RPW];
+#pragma unroll
+  for (int rt = 0; rt < RPW; ++rt) {
+    rl[rt] = (rg * RPW + rt) * 32 + r32;  // local row of this lane's A operand
+    grow[rt] = row0 + rl[rt];
+    const int pos = grow[rt] % HW;
+    py[rt] = pos / W;
+    px[rt] = pos - (pos / W) * W;
+    row_ok[rt] = grow[rt] < rows;
+  }
 
-  f32x16 acc[TPW];
+  f32x16 acc[RPW][TPW];
 #pragma unroll
-  for (int t = 0; t < TPW; ++t)
+  for (int rt = 0; rt < RPW; ++rt)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[t][i] = 0.0f;
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[rt][t][i] = 0.0f;
 
   // B fragment stream: float4 index ((c*4 + tile)*4 + q)*64 + lane.  Two
   // register buffers in ping-pong (the loop is unrolled by two, so no copy):
@@ -202,49 +212,57 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[t][q] = wn[t * 256 + q * 64];
   };
-  auto load_a = [&](int c, float4 (&dst)[4]) {
+  auto load_a = [&](int c, float4 (&dst)[RPW][4]) {
     if (DIAG == 2 && c >= 2) return;
     const int tap = c >> 2;
-    const float4* base;
-    int key;
-    if (!RESIDUAL || tap < 9) {
-      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-      const bool ok = row_ok && py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
-      const int sr = rl + halo + dy * W + dx;
-      base = ok ? slab + sr * 32 : zero_row;
-      key = ok ? (sr & 15) : 0;
-    } else if constexpr (XSLAB) {
-      base = xslab + rl * 32;
-      key = rl & 15;
-    } else {
-      // fused 1x1 residual (4 of 40 chunks): this lane's own block-input
-      // row, straight from global
-      const float4* xr =
-          reinterpret_cast<const float4*>(res_in) + (size_t)grow * 32 + (c & 3) * 8 + h * 4;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dst[q] = row_ok ? xr[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      return;
+    for (int rt = 0; rt < RPW; ++rt) {
+      const float4* base;
+      int key;
+      if (!RESIDUAL || tap < 9) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const bool ok = row_ok[rt] && py[rt] + dy >= 0 && py[rt] + dy < H && px[rt] + dx >= 0 &&
+                        px[rt] + dx < W;
+        const int sr = rl[rt] + halo + dy * W + dx;
+        base = ok ? slab + sr * 32 : zero_row;
+        key = ok ? (sr & 15) : 0;
+      } else if constexpr (XSLAB) {
+        base = xslab + rl[rt] * 32;
+        key = rl[rt] & 15;
+      } else {
+        // fused 1x1 residual (4 of 40 chunks): this lane's own block-input
+        // row, straight from global
+        const float4* xr = reinterpret_cast<const float4*>(res_in) + (size_t)grow[rt] * 32 +
+                           (c & 3) * 8 + h * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          dst[rt][q] = row_ok[rt] ? xr[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
+      const int cbase = (c & 3) * 8 + h * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[rt][q] = base[slab_swz(cbase + q, key)];
     }
-    const int cbase = (c & 3) * 8 + h * 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = base[slab_swz(cbase + q, key)];
   };
-  auto compute = [&](const float4 (&a4)[4], const float4 (&bc)[TPW][4]) {
+  auto compute = [&](const float4 (&a4)[RPW][4], const float4 (&bc)[TPW][4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float av[4] = {a4[q].x, a4[q].y, a4[q].z, a4[q].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const float bv = e == 0 ? bc[t][q].x : e == 1 ? bc[t][q].y : e == 2 ? bc[t][q].z : bc[t][q].w;
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv, acc[t], 0, 0, 0);
+        for (int rt = 0; rt < RPW; ++rt) {
+          const float av = e == 0 ? a4[rt][q].x : e == 1 ? a4[rt][q].y : e == 2 ? a4[rt][q].z : a4[rt][q].w;
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            const float bv = e == 0 ? bc[t][q].x : e == 1 ? bc[t][q].y : e == 2 ? bc[t][q].z : bc[t][q].w;
+            acc[rt][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[rt][t], 0, 0, 0);
+          }
         }
       }
     }
   };
   static_assert(NCH % 2 == 0, "ping-pong loop needs an even chunk count");
-  float4 a0[4], a1[4];
+  float4 a0[RPW][4], a1[RPW][4];
   load_b(0, b0);
   if constexpr (PREA) load_a(0, a0);
   // fully unrolled: no loop back-edge, so the waitcnt pass sees exactly which
@@ -273,9 +291,12 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
     const int col = (TPW * cg + t) * 32 + r32;
     const float bcol = bias[col];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = row0 + rg * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (row < rows) out[(size_t)row * F + col] = fmaxf(acc[t][i] + bcol, 0.0f);
+    for (int rt = 0; rt < RPW; ++rt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = row0 + (rg * RPW + rt) * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (row < rows) out[(size_t)row * F + col] = fmaxf(acc[rt][t][i] + bcol, 0.0f);
+      }
     }
   }
 }
@@ -396,7 +417,6 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
     stem_conv_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(
         reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
   }
-  const int grid64 = (n_max * HW + 63) / 64, grid32 = (n_max * HW + 31) / 32;
   float* cur = act_a;  // block input
   float* mid = act_b;
   float* nxt = act_c;
@@ -404,25 +424,29 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
     const char* v = getenv("AZ_CONV_VARIANT");
     return v ? atoi(v) : 0;
   }();
+  const int rows = n_max * HW;
   if (timer) timer->begin(s);
   for (int d = 0; d < net.depth; ++d) {
     const float4* w1 = reinterpret_cast<const float4*>(net.c1_w[d]);
     const float4* w2 = reinterpret_cast<const float4*>(net.c2_w[d]);
-#define AZ_CONV_PAIR(PREA, XSLAB, OCC, DIAG, TR)                                                \
-  conv3x3_mfma_kernel<F, false, PREA, XSLAB, OCC, DIAG, TR>                                     \
-      <<<TR == 64 ? grid64 : grid32, 256, conv_lds_bytes(TR, W, false, XSLAB), s>>>(             \
-          cur, nullptr, w1, net.c1_b[d], mid, count, n_max, H, W);                              \
-  conv3x3_mfma_kernel<F, true, PREA, XSLAB, OCC, DIAG, TR>                                      \
-      <<<TR == 64 ? grid64 : grid32, 256, conv_lds_bytes(TR, W, true, XSLAB), s>>>(              \
-          mid, cur, w2, net.c2_b[d], nxt, count, n_max, H, W)
+#define AZ_CONV_PAIR(PREA, XSLAB, OCC, DIAG, TPW, RPW)                                          \
+  {                                                                                             \
+    constexpr int TR_ = 32 * (RPW) * (4 / (4 / (TPW)));                                         \
+    const int grid_ = (rows + TR_ - 1) / TR_;                                                   \
+    conv3x3_mfma_kernel<F, false, PREA, XSLAB, OCC, DIAG, TPW, RPW>                             \
+        <<<grid_, 256, conv_lds_bytes(TR_, W, false, XSLAB), s>>>(cur, nullptr, w1, net.c1_b[d], \
+                                                                 mid, count, n_max, H, W);      \
+    conv3x3_mfma_kernel<F, true, PREA, XSLAB, OCC, DIAG, TPW, RPW>                              \
+        <<<grid_, 256, conv_lds_bytes(TR_, W, true, XSLAB), s>>>(mid, cur, w2, net.c2_b[d], nxt, \
+                                                                count, n_max, H, W);            \
+  }
     switch (variant) {
-      case 1: AZ_CONV_PAIR(true, true, 2, 0, 64); break;    // + A prefetch
-      case 2: AZ_CONV_PAIR(false, false, 2, 0, 64); break;  // residual from global
-      case 5: AZ_CONV_PAIR(false, true, 2, 1, 64); break;   // DIAG: no B loads
-      case 6: AZ_CONV_PAIR(false, true, 2, 2, 64); break;   // DIAG: no A reads
-      case 7: AZ_CONV_PAIR(false, true, 2, 0, 64); break;   // 64-row tiles (r1e)
-      case 8: AZ_CONV_PAIR(false, false, 4, 0, 32); break;  // 32-row tiles, residual global, 4 w/SIMD
-      default: AZ_CONV_PAIR(false, true, 2, 0, 32); break;  // 32-row tiles: best measured (r1m)
+      case 1: AZ_CONV_PAIR(false, true, 2, 0, 2, 1); break;   // 64 rows: waves 2x2, 1x2 tiles
+      case 2: AZ_CONV_PAIR(false, true, 2, 0, 1, 2); break;   // 64 rows: each wave 2x1 tiles
+      case 3: AZ_CONV_PAIR(false, false, 2, 0, 1, 4); break;  // 128 rows: each wave 4x1 tiles
+      case 4: AZ_CONV_PAIR(false, false, 2, 0, 2, 2); break;  // 128 rows: waves 2x2, 2x2 tiles
+      case 5: AZ_CONV_PAIR(false, true, 2, 1, 1, 1); break;   // DIAG: no B loads
+      default: AZ_CONV_PAIR(false, true, 2, 0, 1, 1); break;  // 32 rows, 1 tile per wave (r1m)
     }
 #undef AZ_CONV_PAIR
     float* t = cur;

@@ -98,48 +98,10 @@ __device__ __forceinline__ bool same_board(const Board& a, const Board& b) {
          a.opp[1] == b.opp[1];
 }
 
-__global__ __launch_bounds__(256) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= g.slots || t.game_id[s] < 0) return;
-  Edge* E = t.edges + (size_t)s * g.arena_cap;
-  int32_t* path = t.path + (size_t)s * g.max_depth;
-  Board b = t.root_board[s];
-  int first = t.root_first[s], cnt = t.root_n[s];
-  int depth = 0, status = kOngoing;
-  while (cnt > 0) {
-    int sum = 0;
-    for (int i = 0; i < cnt; ++i) sum += E[first + i].N;
-    if (sum >= g.pow_len) {
-      flag_error(t, kErrPow);
-      return;
-    }
-    const double sq = t.powtab[sum];
-    int best = 0;
-    double best_v = 0.0;
-    for (int i = 0; i < cnt; ++i) {
-      const Edge e = E[first + i];
-      const double q = e.N ? e.W / (double)e.N : 0.0;
-      const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
-      const double ucb = q + u;
-      if (i == 0 || ucb > best_v) {
-        best = i;
-        best_v = ucb;
-      }
-    }
-    if (depth >= g.max_depth) {
-      flag_error(t, kErrPath);
-      return;
-    }
-    const Edge& e = E[first + best];
-    path[depth++] = first + best;
-    status = play(g, b, e.action);
-    if (status < 0) {
-      flag_error(t, kErrIllegal);
-      return;
-    }
-    first = e.child;
-    cnt = e.child_n;
-  }
+// After the descent: the terminal branch of MCTS.search (mcts.py:176-180) or
+// the eval queue + plays_inferences probe + per-simulation dedup.
+__device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c, int s, Edge* E,
+                          const int32_t* path, int depth, int status, const Board& b) {
   stat_add(t, kStatSims, 1);
   if (depth > 0 && status != kOngoing) {
     // get_result(keep_same_player=True): 1 for the player who just moved, 0 draw
@@ -204,6 +166,115 @@ __global__ __launch_bounds__(256) void select_kernel(GameCfg g, TreeDev t, Cache
   }
 }
 
+// Serial descent, one lane per game (used when the action space exceeds 64).
+__global__ __launch_bounds__(64) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.slots || t.game_id[s] < 0) return;
+  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  int32_t* path = t.path + (size_t)s * g.max_depth;
+  Board b = t.root_board[s];
+  int first = t.root_first[s], cnt = t.root_n[s];
+  int depth = 0, status = kOngoing;
+  while (cnt > 0) {
+    int sum = 0;
+    for (int i = 0; i < cnt; ++i) sum += E[first + i].N;
+    if (sum >= g.pow_len) {
+      flag_error(t, kErrPow);
+      return;
+    }
+    const double sq = t.powtab[sum];
+    int best = 0;
+    double best_v = 0.0;
+    for (int i = 0; i < cnt; ++i) {
+      const Edge e = E[first + i];
+      const double q = e.N ? e.W / (double)e.N : 0.0;
+      const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
+      const double ucb = q + u;
+      if (i == 0 || ucb > best_v) {
+        best = i;
+        best_v = ucb;
+      }
+    }
+    if (depth >= g.max_depth) {
+      flag_error(t, kErrPath);
+      return;
+    }
+    const Edge& e = E[first + best];
+    path[depth++] = first + best;
+    status = play(g, b, e.action);
+    if (status < 0) {
+      flag_error(t, kErrIllegal);
+      return;
+    }
+    first = e.child;
+    cnt = e.child_n;
+  }
+  leaf_tail(g, t, c, s, E, path, depth, status, b);
+}
+
+// Group descent: a game is a group of L lanes (L = next power of two >= A).
+// Lane j loads edge j (contiguous, one 32-byte record per lane), the group
+// sums N and takes the first-maximum UCB by shuffles -- the same float64
+// expressions as the serial loop, so the chosen edge is identical.
+template <int L>
+__global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = gid / L, j = gid % L;
+  if (s >= g.slots || t.game_id[s] < 0) return;  // whole groups leave together
+  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  int32_t* path = t.path + (size_t)s * g.max_depth;
+  Board b = t.root_board[s];
+  int first = t.root_first[s], cnt = t.root_n[s];
+  int depth = 0, status = kOngoing;
+  while (cnt > 0) {
+    const bool mine = j < cnt;
+    Edge e;
+    if (mine) e = E[first + j];
+    int sum = mine ? e.N : 0;
+#pragma unroll
+    for (int off = L / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off, L);
+    if (sum >= g.pow_len) {
+      if (j == 0) flag_error(t, kErrPow);
+      return;
+    }
+    const double sq = t.powtab[sum];
+    double best_v = -INFINITY;
+    int best = L;
+    if (mine) {
+      const double q = e.N ? e.W / (double)e.N : 0.0;
+      const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
+      best_v = q + u;
+      best = j;
+    }
+#pragma unroll
+    for (int off = L / 2; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(best_v, off, L);
+      const int oj = __shfl_xor(best, off, L);
+      if (ov > best_v || (ov == best_v && oj < best)) {  // np.argmax: first maximum
+        best_v = ov;
+        best = oj;
+      }
+    }
+    if (depth >= g.max_depth) {
+      if (j == 0) flag_error(t, kErrPath);
+      return;
+    }
+    const int action = __shfl(mine ? (int)e.action : 0, best, L);
+    const int child = __shfl(mine ? e.child : 0, best, L);
+    const int child_n = __shfl(mine ? (int)e.child_n : 0, best, L);
+    if (j == 0) path[depth] = first + best;
+    ++depth;
+    status = play(g, b, action);
+    if (status < 0) {
+      if (j == 0) flag_error(t, kErrIllegal);
+      return;
+    }
+    first = child;
+    cnt = child_n;
+  }
+  if (j == 0) leaf_tail(g, t, c, s, E, path, depth, status, b);
+}
+
 // ----------------------------------------------------------- dedup resolve
 // Misses whose step tag matched an owner's: same board -> share the owner's
 // evaluator row; a fingerprint collision (different board) -> its own row.
@@ -264,7 +335,7 @@ __global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, const Board*
 // MCTS.evaluate_and_expand (mcts.py:145-161) with normalize_probabilities
 // (mcts/utils.py:4-16), then backup(-value) (mcts.py:175, 163-168).
 template <int MAXA>
-__global__ __launch_bounds__(256) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
+__global__ __launch_bounds__(64) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
                                                      const float* __restrict__ probs,
                                                      const float* __restrict__ values) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -331,7 +402,7 @@ __global__ __launch_bounds__(256) void expand_kernel(GameCfg g, TreeDev t, Cache
 // (self_play.py:59-67): greedy one-hot from fullmove_number >= index_move_greedy,
 // else normalised visit counts; one uniform per move even when greedy.
 template <int MAXA>
-__global__ __launch_bounds__(256) void play_kernel(GameCfg g, TreeDev t, SampleDev smp,
+__global__ __launch_bounds__(64) void play_kernel(GameCfg g, TreeDev t, SampleDev smp,
                                                    const double* __restrict__ uniforms,
                                                    int greedy_mode, int deterministic, int refill) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -444,9 +515,21 @@ __global__ void slot_set_root_kernel(GameCfg g, TreeDev t, const int32_t* slots,
 
 // ---------------------------------------------------------------- launchers
 static inline int blocks_for(int n) { return (n + 255) / 256; }
+// per-game kernels are latency-bound chains (one lane = one tree): 64-lane
+// blocks spread 4096 games over 64 CUs instead of 16
+constexpr int kGameBlock = 64;
+static inline int game_blocks(int n) { return (n + kGameBlock - 1) / kGameBlock; }
 
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s) {
-  select_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, c);
+  const int lanes = g.A <= 8 ? 8 : g.A <= 16 ? 16 : g.A <= 32 ? 32 : g.A <= 64 ? 64 : 1;
+  const int blocks = (int)(((int64_t)g.slots * lanes + kGameBlock - 1) / kGameBlock);
+  switch (lanes) {
+    case 8: select_group_kernel<8><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    case 16: select_group_kernel<16><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    case 32: select_group_kernel<32><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    case 64: select_group_kernel<64><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    default: select_kernel<<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c); break;
+  }
 }
 
 void launch_dedup_resolve(const GameCfg& g, const TreeDev& t, hipStream_t s) {
@@ -461,9 +544,9 @@ void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* cou
 void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
                    const float* values, hipStream_t s) {
   if (g.A <= 16)
-    expand_kernel<16><<<blocks_for(g.slots), 256, 0, s>>>(g, t, c, probs, values);
+    expand_kernel<16><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c, probs, values);
   else
-    expand_kernel<kMaxActions><<<blocks_for(g.slots), 256, 0, s>>>(g, t, c, probs, values);
+    expand_kernel<kMaxActions><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c, probs, values);
 }
 
 void launch_cache_insert(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
@@ -474,11 +557,11 @@ void launch_cache_insert(const GameCfg& g, const TreeDev& t, const CacheDev& c, 
 void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const double* uniforms,
                  int greedy_mode, int deterministic, int refill, hipStream_t s) {
   if (g.A <= 16)
-    play_kernel<16><<<blocks_for(g.slots), 256, 0, s>>>(g, t, smp, uniforms, greedy_mode,
-                                                        deterministic, refill);
+    play_kernel<16><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, smp, uniforms, greedy_mode,
+                                                                deterministic, refill);
   else
-    play_kernel<kMaxActions><<<blocks_for(g.slots), 256, 0, s>>>(g, t, smp, uniforms, greedy_mode,
-                                                                 deterministic, refill);
+    play_kernel<kMaxActions><<<game_blocks(g.slots), kGameBlock, 0, s>>>(
+        g, t, smp, uniforms, greedy_mode, deterministic, refill);
 }
 
 void launch_slot_init(const GameCfg& g, const TreeDev& t, const SampleDev& smp, int64_t n_first,
