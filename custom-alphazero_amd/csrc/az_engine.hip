@@ -196,6 +196,52 @@ std::vector<float> pack_fragments(const std::vector<float>& wt, int N, int K) {
   return p;
 }
 
+// Winograd F(2x2,3x3) weights for wino_conv_kernel (az_wino.hip):
+// U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
+// in float64 from the folded Keras kernel, rounded once to float, packed as
+// float4 (((c*16 + xi)*4 + nb)*2 + q)*64 + lane, element e holding
+// cin = 16c + 8*(lane>>5) + 4q + e, cout = 32nb + (lane&31).
+std::vector<float> pack_wino(const std::vector<double>& w, int F) {
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  std::vector<double> U((size_t)16 * F * F, 0.0);
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b)
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx) {
+          const double gg = G[a][ky] * G[b][kx];
+          if (gg == 0.0) continue;
+          const double* src = w.data() + (size_t)(ky * 3 + kx) * F * F;
+          double* dst = U.data() + (size_t)(a * 4 + b) * F * F;
+          for (size_t i = 0; i < (size_t)F * F; ++i) dst[i] += gg * src[i];
+        }
+  std::vector<float> p((size_t)16 * F * F);
+  for (int c = 0; c < F / 16; ++c)
+    for (int xi = 0; xi < 16; ++xi)
+      for (int nb = 0; nb < F / 32; ++nb)
+        for (int q = 0; q < 2; ++q)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int e = 0; e < 4; ++e) {
+              const int cin = 16 * c + 8 * (lane >> 5) + 4 * q + e, co = 32 * nb + (lane & 31);
+              p[(((((size_t)c * 16 + xi) * 4 + nb) * 2 + q) * 64 + lane) * 4 + e] =
+                  (float)U[((size_t)xi * F + cin) * F + co];
+            }
+  return p;
+}
+
+// 1x1 projection residual [cin][cout] in the same fragment order (no xi).
+std::vector<float> pack_wino_res(const std::vector<double>& wr, int F) {
+  std::vector<float> p((size_t)F * F);
+  for (int c = 0; c < F / 16; ++c)
+    for (int nb = 0; nb < F / 32; ++nb)
+      for (int q = 0; q < 2; ++q)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 4; ++e) {
+            const int cin = 16 * c + 8 * (lane >> 5) + 4 * q + e, co = 32 * nb + (lane & 31);
+            p[((((size_t)c * 4 + nb) * 2 + q) * 64 + lane) * 4 + e] = (float)wr[(size_t)cin * F + co];
+          }
+  return p;
+}
+
 int upload(az_engine* e, float** dst, const std::vector<float>& src) {
   int rc;
   if (!*dst && (rc = e->alloc(dst, src.size()))) return rc;
@@ -220,6 +266,10 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   const int A = c.gravity ? c.board_width : c.board_width * c.board_height;
   if (A > az::kMaxActions) return fail(AZ_E_INVALID, "action space too large");
   if (c.slots < 1 || c.mcts_iterations < 1) return fail(AZ_E_INVALID, "slots and mcts_iterations must be >= 1");
+  if (c.conv_algo != AZ_CONV_WINOGRAD && c.conv_algo != AZ_CONV_DIRECT)
+    return fail(AZ_E_INVALID, "conv_algo must be AZ_CONV_WINOGRAD or AZ_CONV_DIRECT");
+  if (c.evaluator == AZ_EVAL_NETWORK && (int64_t)c.slots * c.board_height * c.board_width * 128 >= (1ll << 31))
+    return fail(AZ_E_INVALID, "slots * H * W * 128 must stay below 2^31 (32-bit activation offsets)");
   if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC)
     return fail(AZ_E_INVALID, "unknown evaluator");
   if (c.evaluator == AZ_EVAL_NETWORK && c.filters != 128)
@@ -326,6 +376,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       if ((rc = e->alloc(&e->act[i], act))) return cleanup(rc);
   }
   e->net.depth = c.depth;
+  e->net.algo = c.conv_algo;
   e->net.hidden = c.value_hidden;
   *out = e;
   return 0;
@@ -367,6 +418,9 @@ int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
   net.c1_b.resize(net.depth, nullptr);
   net.c2_w.resize(net.depth, nullptr);
   net.c2_b.resize(net.depth, nullptr);
+  net.u1_w.resize(net.depth, nullptr);
+  net.u2_w.resize(net.depth, nullptr);
+  net.r2_w.resize(net.depth, nullptr);
   for (int d = 0; d < net.depth; ++d) {
     const std::string p = "block" + std::to_string(d);
     if ((rc = fold_unit(m, p + ".conv1", 3, F, F, eps, w, b))) return rc;
@@ -375,7 +429,7 @@ int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
       for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
     for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
     if ((rc = upload(e, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
-        (rc = upload(e, &net.c1_b[d], bt)))
+        (rc = upload(e, &net.u1_w[d], pack_wino(w, F))) || (rc = upload(e, &net.c1_b[d], bt)))
       return rc;
     if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
     if ((rc = fold_unit(m, p + ".res", 1, F, F, eps, wr, br))) return rc;
@@ -386,7 +440,8 @@ int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
     }
     for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
     if ((rc = upload(e, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
-        (rc = upload(e, &net.c2_b[d], bt2)))
+        (rc = upload(e, &net.u2_w[d], pack_wino(w, F))) ||
+        (rc = upload(e, &net.r2_w[d], pack_wino_res(wr, F))) || (rc = upload(e, &net.c2_b[d], bt2)))
       return rc;
   }
   // heads

@@ -12,10 +12,13 @@ namespace az {
 // a [128][32] tile loaded with 16-byte reads.
 struct NetDev {
   int filters = 128, depth = 0, hidden = 256;
+  int algo = 0;  // AZ_CONV_WINOGRAD / AZ_CONV_DIRECT
   float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c)
   float* stem_b = nullptr;  // [F]
   std::vector<float*> c1_w, c1_b;  // fragment-packed [9F x F], [F]
   std::vector<float*> c2_w, c2_b;  // fragment-packed [10F x F] (conv2 taps, then 1x1 residual), [F]
+  std::vector<float*> u1_w, u2_w;  // Winograd U[16][F][F], packed (az_engine.hip pack_wino)
+  std::vector<float*> r2_w;        // 1x1 projection residual [F][F], Winograd fragment order
   float *pc_w = nullptr, *pc_b = nullptr;  // policy conv [F][2], [2]
   float *vc_w = nullptr, *vc_b = nullptr;  // value conv [F], [1]
   float *pd_w = nullptr, *pd_b = nullptr;  // policy dense [2HW][A], [A]
@@ -71,6 +74,9 @@ void launch_encode(const Board* boards, const int* count, int n_max, int HW, flo
                    hipStream_t s);
 void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* mask,
                        hipStream_t s);
+void launch_wino_conv(const float* in, const float* res_in, const float* upack,
+                      const float* rpack, const float* bias, float* out, const int* count,
+                      int n_max, int H, int W, hipStream_t s, int pipe);
 // x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,

@@ -420,10 +420,13 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   float* cur = act_a;  // block input
   float* mid = act_b;
   float* nxt = act_c;
-  static const int variant = [] {
+  // AZ_CONV_VARIANT (A/B experiments, profiles/conv_variants.sh) overrides
+  // the engine's conv_algo: 0 Winograd, 6 direct, 1-5 direct variants
+  static const int env_variant = [] {
     const char* v = getenv("AZ_CONV_VARIANT");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : -1;
   }();
+  const int variant = env_variant >= 0 ? env_variant : (net.algo == 0 ? 0 : 6);
   const int rows = n_max * HW;
   if (timer) timer->begin(s);
   for (int d = 0; d < net.depth; ++d) {
@@ -441,12 +444,19 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
                                                                 count, n_max, H, W);            \
   }
     switch (variant) {
+      case 0:  // Winograd F(2x2,3x3) (az_wino.hip)
+      case 7:  // same, single V buffer (PIPE 0)
+        launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s,
+                         variant == 0);
+        launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s,
+                         variant == 0);
+        break;
       case 1: AZ_CONV_PAIR(false, true, 2, 0, 2, 1); break;   // 64 rows: waves 2x2, 1x2 tiles
       case 2: AZ_CONV_PAIR(false, true, 2, 0, 1, 2); break;   // 64 rows: each wave 2x1 tiles
       case 3: AZ_CONV_PAIR(false, false, 2, 0, 1, 4); break;  // 128 rows: each wave 4x1 tiles
       case 4: AZ_CONV_PAIR(false, false, 2, 0, 2, 2); break;  // 128 rows: waves 2x2, 2x2 tiles
       case 5: AZ_CONV_PAIR(false, true, 2, 1, 1, 1); break;   // DIAG: no B loads
-      default: AZ_CONV_PAIR(false, true, 2, 0, 1, 1); break;  // 32 rows, 1 tile per wave (r1m)
+      default: AZ_CONV_PAIR(false, true, 2, 0, 1, 1); break;  // 6: direct, 32 rows, 1 tile per wave (r1m)
     }
 #undef AZ_CONV_PAIR
     float* t = cur;

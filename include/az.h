@@ -33,6 +33,10 @@ extern "C" {
 #define AZ_EVAL_NETWORK 0    /* the policy/value network (model/tensorflow/model.py) */
 #define AZ_EVAL_SYNTHETIC 1  /* oracle/synth.py's exact evaluator (parity runs) */
 
+/* az_config.conv_algo */
+#define AZ_CONV_WINOGRAD 0   /* Winograd F(2x2,3x3) on fp32 MFMA (default) */
+#define AZ_CONV_DIRECT 1     /* direct implicit GEMM on fp32 MFMA */
+
 typedef struct az_engine az_engine;
 
 /* Engine configuration: the reference's Config* class constants
@@ -55,7 +59,9 @@ typedef struct az_config {
     int64_t max_tree_visits;       /* bound on visits through one node; 0 = mcts_iterations*H*W */
     int32_t cache_log2;            /* transposition cache entries = 2^cache_log2 (the reference's
                                       plays_inferences, mcts/mcts.py:122-143); 0 = off */
-    int32_t reserved[7];
+    int32_t conv_algo;             /* residual-tower 3x3 convs: AZ_CONV_WINOGRAD (0, default) or
+                                      AZ_CONV_DIRECT (1); same layer, outputs within NET_TOL */
+    int32_t reserved[6];
 } az_config;
 
 /* One named weight tensor in Keras layout ("Weights"). */

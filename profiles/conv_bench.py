@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Forward-pass microbenchmark: az_forward on B random Connect-4 boards, the
 conv kernels timed with the engine's HIP events (same method as bench.py).
-Usage: python3 profiles/conv_bench.py [B] [reps]"""
+Usage: python3 profiles/conv_bench.py [B] [reps] [algo: 0 Winograd, 1 direct]
+TFLOP/s are direct-convolution (algorithmic) FLOP per second."""
 import os
 import sys
 import time
@@ -16,7 +17,8 @@ from custom_alphazero.model.weights import init_weights, weight_spec  # noqa: E4
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 H, W = 6, 7
-eng = az.Engine(H, W, 4, True, 1, slots=B, evaluator=az.EVAL_NETWORK)
+algo = int(sys.argv[3]) if len(sys.argv) > 3 else az.CONV_WINOGRAD
+eng = az.Engine(H, W, 4, True, 1, slots=B, evaluator=az.EVAL_NETWORK, conv_algo=algo)
 eng.set_weights(init_weights(weight_spec(H, W, W), seed=0).items())
 rng = np.random.RandomState(0)
 b = rng.randint(-1, 2, (B, H, W)).astype(np.int8)
@@ -31,5 +33,5 @@ wall = time.perf_counter() - t0
 st = eng.stats()
 flop = B * H * W * 2 * 128 * 128 * 19 * 4
 avg = st["conv_ms"] / st["conv_launches"]
-print(f"B={B} reps={reps}: conv {st['conv_ms'] / reps:.3f} ms/forward ({avg * 1e3:.1f} us/launch), "
+print(f"algo={algo} B={B} reps={reps}: conv {st['conv_ms'] / reps:.3f} ms/forward ({avg * 1e3:.1f} us/launch), "
       f"{flop * reps / (st['conv_ms'] * 1e-3) / 1e12:.1f} TFLOP/s; wall {wall / reps * 1e3:.2f} ms/forward incl. H2D/D2H")

@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""Average rocprofv3 counter_collection.csv values per kernel name.
+Usage: python3 profiles/pmc_summary.py <dir> [kernel-substring]"""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+pat = sys.argv[2] if len(sys.argv) > 2 else "conv"
+acc = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+    for row in csv.DictReader(open(f)):
+        k = row["Kernel_Name"]
+        if pat not in k:
+            continue
+        short = k.split("(")[0][-60:]
+        acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
+for k, cs in acc.items():
+    print(k)
+    for c, v in sorted(cs.items()):
+        print(f"   {c:28s} n={len(v):4d} avg={sum(v) / len(v):.4g}")

@@ -145,13 +145,16 @@ def test_encode_and_mask_match_reference(golden, name):
 
 
 # ------------------------------------------------------------------ network
+CONV_ALGOS = [az.CONV_WINOGRAD, az.CONV_DIRECT]
+
+
 def make_net_engine(H=6, W=7, n=4, grav=True, S=25, slots=256, seed=0, randomize_bn=True, depth=4,
-                    cache_log2=0):
+                    cache_log2=0, conv_algo=az.CONV_WINOGRAD):
     A = W if grav else W * H
     spec = weight_spec(H, W, A, depth=depth)
     w = init_weights(spec, seed=seed, randomize_bn=randomize_bn)
     eng = az.Engine(H, W, n, grav, S, slots=slots, evaluator=az.EVAL_NETWORK, depth=depth,
-                    cache_log2=cache_log2)
+                    cache_log2=cache_log2, conv_algo=conv_algo)
     eng.set_weights(w.items())
     return eng, w
 
@@ -161,10 +164,13 @@ def random_boards(rng, k, H, W):
     return b
 
 
-@pytest.mark.parametrize("shape", [(6, 7, True), (9, 9, True)])
-def test_forward_matches_keras_restatement(shape):
+@pytest.mark.parametrize("conv_algo", CONV_ALGOS)
+@pytest.mark.parametrize("shape", [(6, 7, True), (9, 9, True), (5, 5, False), (7, 6, True)])
+def test_forward_matches_keras_restatement(shape, conv_algo):
+    """Both conv algorithms (Winograd F(2x2,3x3), direct) within NET_TOL of the
+    float64 Keras restatement; odd H and W exercise the partial 2x2 tiles."""
     H, W, grav = shape
-    eng, w = make_net_engine(H, W, 4, grav, slots=300)
+    eng, w = make_net_engine(H, W, 4, grav, slots=300, conv_algo=conv_algo)
     rng = np.random.RandomState(5)
     x = oracle.full_state(random_boards(rng, 37, H, W))
     x[-5:] = rng.rand(5, H, W, 4).astype(np.float32)  # arbitrary (non one-hot) inputs too
@@ -175,12 +181,13 @@ def test_forward_matches_keras_restatement(shape):
     np.testing.assert_allclose(p.sum(axis=1), 1.0, atol=1e-6)
 
 
-def test_forward_is_batch_invariant():
-    eng, _ = make_net_engine(slots=512)
+@pytest.mark.parametrize("conv_algo", CONV_ALGOS)
+def test_forward_is_batch_invariant(conv_algo):
+    eng, _ = make_net_engine(slots=512, conv_algo=conv_algo)
     rng = np.random.RandomState(11)
     x = oracle.full_state(random_boards(rng, 700, 6, 7))  # > slots: chunked
     p_all, v_all = eng.forward(x)
-    for lo, hi in [(0, 1), (3, 4), (100, 229), (511, 513), (699, 700)]:
+    for lo, hi in [(0, 1), (3, 4), (2, 5), (100, 229), (511, 513), (699, 700)]:
         p, v = eng.forward(x[lo:hi])
         np.testing.assert_array_equal(p, p_all[lo:hi])
         np.testing.assert_array_equal(v, v_all[lo:hi])
