@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(15, cores-1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=0, help="slot groups on separate HIP streams (0 = auto)")
+    ap.add_argument("--conv-algo", type=int, default=0, help="0 Winograd, 1 direct")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
     ap.add_argument("--cache-log2", type=int, default=25,
                     help="transposition cache (the reference's plays_inferences) entries = 2^N; 0 = off")
@@ -135,7 +137,7 @@ def main():
 
     eng = az.Engine(args.height, args.width, args.n, True, args.sims, slots=args.slots,
                     evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index,
-                    cache_log2=args.cache_log2)
+                    cache_log2=args.cache_log2, lanes=args.lanes, conv_algo=args.conv_algo)
     eng.set_weights(named)
     budget = args.slots * (2 + (args.warmup + 2 * args.steps) // 5)
     eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)

@@ -3,7 +3,11 @@
 #include <math.h>
 #include <string.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <string>
 #include <vector>
@@ -34,9 +38,30 @@ double (*volatile g_pow)(double, double) = pow;
 
 }  // namespace
 
+// A lane = a contiguous group of slots searched on its own HIP stream.  Lanes
+// share the network, the transposition cache, the sample sink and the
+// counters; each owns its eval queue, per-simulation dedup table and slices
+// of the activation buffers.  Two lanes keep the GPU busy across each
+// other's launch tails and small latency-bound kernels; results do not
+// depend on the lane count (each game's search only reads its own tree and
+// the evaluator is deterministic per board).
+struct Lane {
+  int first = 0, n = 0;
+  hipStream_t stream = nullptr;
+  az::GameCfg g{};
+  az::TreeDev t{};
+  float* x = nullptr;
+  float* act[3] = {nullptr, nullptr, nullptr};
+  float* probs = nullptr;
+  float* values = nullptr;
+  az::ConvTimer timer;
+};
+
 struct az_engine {
   int device = 0;
   hipStream_t stream = nullptr;
+  Lane whole;                // every slot on `stream` (tree API; self-play with one lane)
+  std::vector<Lane*> lanes;  // self-play lanes (just &whole when there is one)
   az_config cfg{};
   az::GameCfg g{};
   az::TreeDev t{};
@@ -53,6 +78,7 @@ struct az_engine {
   az::Board* dev_boards = nullptr;
   std::vector<void*> owned;
   std::vector<void*> sample_bufs;
+  std::vector<hipStream_t> lane_streams;
   int64_t sp_first = 0, sp_n = 0;
 
   template <typename T>
@@ -97,36 +123,44 @@ void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
     cells[c] = az::bit(b.own, c) ? 1 : (az::bit(b.opp, c) ? -1 : 0);
 }
 
-// one simulation for every active slot (MCTS.search body, mcts.py:171-180)
-int simulate(az_engine* e) {
-  hipStream_t s = e->stream;
+// one simulation for every active slot of a lane (MCTS.search body,
+// mcts.py:171-180), enqueued on the lane's stream
+int simulate(az_engine* e, Lane& L) {
+  hipStream_t s = L.stream;
   // eval_count, miss_count, nn_count, dup_count are one contiguous block
-  AZ_HIP(hipMemsetAsync(e->t.eval_count, 0, 4 * sizeof(int32_t), s));
-  e->t.epoch += 1;  // fresh per-simulation dedup table (tags of older epochs read as empty)
-  az::launch_select(e->g, e->t, e->cache, s);
-  const az::Board* rows = e->t.eval_board;
-  const int32_t* n_rows = e->t.eval_count;
+  AZ_HIP(hipMemsetAsync(L.t.eval_count, 0, 4 * sizeof(int32_t), s));
+  L.t.epoch += 1;  // fresh per-simulation dedup table (tags of older epochs read as empty)
+  az::launch_select(L.g, L.t, e->cache, s);
+  const az::Board* rows = L.t.eval_board;
+  const int32_t* n_rows = L.t.eval_count;
   if (e->cache.enabled) {
-    az::launch_dedup_resolve(e->g, e->t, s);
-    rows = e->t.nn_board;
-    n_rows = e->t.nn_count;
+    az::launch_dedup_resolve(L.g, L.t, s);
+    rows = L.t.nn_board;
+    n_rows = L.t.nn_count;
   }
   if (e->cfg.evaluator == AZ_EVAL_NETWORK) {
-    az::launch_encode(rows, n_rows, e->g.slots, e->g.HW, e->x, s);
-    az::launch_forward(e->net, e->x, n_rows, e->g.slots, e->g.H, e->g.W, e->g.A, e->act[0],
-                       e->act[1], e->act[2], e->probs, e->values, s,
-                       e->timer.enabled ? &e->timer : nullptr);
+    az::launch_encode(rows, n_rows, L.n, L.g.HW, L.x, s);
+    az::launch_forward(e->net, L.x, n_rows, L.n, L.g.H, L.g.W, L.g.A, L.act[0], L.act[1], L.act[2],
+                       L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr);
   } else {
-    az::launch_synth_eval(e->g, rows, n_rows, e->probs, e->values, s);
+    az::launch_synth_eval(L.g, rows, n_rows, L.probs, L.values, s);
   }
-  az::launch_expand(e->g, e->t, e->cache, e->probs, e->values, s);
-  if (e->cache.enabled) az::launch_cache_insert(e->g, e->t, e->cache, e->probs, e->values, s);
+  az::launch_expand(L.g, L.t, e->cache, L.probs, L.values, s);
+  if (e->cache.enabled) az::launch_cache_insert(L.g, L.t, e->cache, L.probs, L.values, s);
   AZ_HIP(hipGetLastError());
+  return 0;
+}
+
+int sync_all(az_engine* e) {
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  for (hipStream_t s : e->lane_streams) AZ_HIP(hipStreamSynchronize(s));
   return 0;
 }
 
 int cache_clear(az_engine* e) {
   if (!e->cache.state) return 0;
+  int rc;
+  if ((rc = sync_all(e))) return rc;
   AZ_HIP(hipMemsetAsync(e->cache.state, 0, ((size_t)e->cache.mask + 1) * sizeof(uint32_t), e->stream));
   AZ_HIP(hipStreamSynchronize(e->stream));
   return 0;
@@ -249,6 +283,59 @@ int upload(az_engine* e, float** dst, const std::vector<float>& src) {
   return 0;
 }
 
+// Lane views: per-slot arrays offset to the lane's first slot; with more than
+// one lane each gets its own eval-queue counters and dedup table.
+int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
+  const az::GameCfg& g = e->g;
+  L->first = first;
+  L->n = n;
+  L->g = g;
+  L->g.slots = n;
+  az::TreeDev t = e->t;
+  const size_t f = (size_t)first;
+  t.edges += f * g.arena_cap;
+  t.root_board += f;
+  t.root_first += f;
+  t.root_n += f;
+  t.root_value += f;
+  t.arena_top += f;
+  t.ply += f;
+  t.game_id += f;
+  t.path += f * g.max_depth;
+  t.path_len += f;
+  t.slot_expansions += f;
+  t.mt += f;  // word-major: stride stays the whole engine's slot count
+  t.eval_slot += f;
+  t.eval_board += f;
+  t.eval_src += f;
+  t.miss_q += f;
+  t.nn_board += f;
+  t.dup_q += f;
+  t.last_move += f;
+  t.last_status += f;
+  t.last_policy += f * g.A;
+  if (own_queue) {
+    int rc;
+    size_t cap = 1024;
+    while (cap < 4 * (size_t)n) cap <<= 1;
+    if ((rc = e->alloc(&t.eval_count, 4)) || (rc = e->alloc(&t.step_tag, cap)) ||
+        (rc = e->alloc(&t.step_row, cap)))
+      return rc;
+    AZ_HIP(hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)));
+    t.miss_count = t.eval_count + 1;
+    t.nn_count = t.eval_count + 2;
+    t.dup_count = t.eval_count + 3;
+    t.step_mask = (uint32_t)(cap - 1);
+    t.epoch = 0;
+  }
+  L->t = t;
+  L->x = e->x + f * g.HW * 4;
+  for (int i = 0; i < 3; ++i) L->act[i] = e->act[i] ? e->act[i] + f * g.HW * 128 : nullptr;
+  L->probs = e->probs + f * g.A;
+  L->values = e->values + f;
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -311,6 +398,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   int rc;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(AZ_E_HIP, "hipStreamCreate failed"));
+  if (c.lanes < 0) return cleanup(fail(AZ_E_INVALID, "lanes must be >= 0"));
   const size_t S = (size_t)g.slots;
   az::TreeDev& t = e->t;
   if ((rc = e->alloc(&t.edges, S * g.arena_cap)) || (rc = e->alloc(&t.root_board, S)) ||
@@ -335,6 +423,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       return cleanup(fail(AZ_E_HIP, "pow table upload failed"));
   }
   t.powtab = powtab;
+  t.mt_stride = g.slots;
   t.miss_count = t.eval_count + 1;
   t.nn_count = t.eval_count + 2;
   t.dup_count = t.eval_count + 3;
@@ -377,6 +466,26 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   }
   e->net.depth = c.depth;
   e->net.algo = c.conv_algo;
+  // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
+  int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);
+  nl = std::min(nl, std::min(g.slots, 8));
+  if ((rc = make_lane(e, &e->whole, 0, g.slots, false))) return cleanup(rc);
+  e->whole.stream = e->stream;
+  if (nl == 1) {
+    e->lanes.push_back(&e->whole);
+  } else {
+    for (int l = 0; l < nl; ++l) {
+      Lane* L = new Lane();
+      e->lanes.push_back(L);
+      const int lo = (int)((int64_t)g.slots * l / nl), hi = (int)((int64_t)g.slots * (l + 1) / nl);
+      if ((rc = make_lane(e, L, lo, hi - lo, true))) return cleanup(rc);
+      hipStream_t st;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(AZ_E_HIP, "hipStreamCreate failed"));
+      e->lane_streams.push_back(st);
+      L->stream = st;
+    }
+  }
   e->net.hidden = c.value_hidden;
   *out = e;
   return 0;
@@ -386,6 +495,12 @@ int az_engine_destroy(az_engine* eng) {
   if (!eng) return 0;
   (void)hipSetDevice(eng->device);
   if (eng->stream) (void)hipStreamSynchronize(eng->stream);
+  for (hipStream_t s : eng->lane_streams) {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+  }
+  for (Lane* L : eng->lanes)
+    if (L != &eng->whole) delete L;
   for (void* p : eng->sample_bufs) (void)hipFree(p);
   for (void* p : eng->owned) (void)hipFree(p);
   if (eng->stream) (void)hipStreamDestroy(eng->stream);
@@ -522,7 +637,8 @@ int az_forward(az_engine* e, const float* x, int n, float* probs, float* values)
 int az_stats_get(az_engine* e, az_stats* st) {
   if (!e || !st) return fail(AZ_E_INVALID, "null argument");
   AZ_HIP(hipSetDevice(e->device));
-  AZ_HIP(hipStreamSynchronize(e->stream));
+  int rc;
+  if ((rc = sync_all(e))) return rc;
   unsigned long long h[az::kStatCount];
   AZ_HIP(hipMemcpy(h, e->t.stats, sizeof(h), hipMemcpyDeviceToHost));
   std::vector<int64_t> gid(e->g.slots);
@@ -538,6 +654,15 @@ int az_stats_get(az_engine* e, az_stats* st) {
   e->timer.flush();
   st->conv_ms = e->timer.total_ms;
   st->conv_launches = e->timer.launches;
+  e->whole.timer.flush();
+  st->conv_ms += e->whole.timer.total_ms;
+  st->conv_launches += e->whole.timer.launches;
+  for (Lane* L : e->lanes) {
+    if (L == &e->whole) continue;
+    L->timer.flush();
+    st->conv_ms += L->timer.total_ms;
+    st->conv_launches += L->timer.launches;
+  }
   st->cache_hits = (int64_t)h[az::kStatCacheHits];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
   return 0;
@@ -546,7 +671,8 @@ int az_stats_get(az_engine* e, az_stats* st) {
 int az_cache_enable(az_engine* e, int on) {
   if (!e) return fail(AZ_E_INVALID, "null engine");
   if (!e->cache.state) return on ? fail(AZ_E_STATE, "engine created with cache_log2 = 0") : 0;
-  AZ_HIP(hipStreamSynchronize(e->stream));
+  int rc;
+  if ((rc = sync_all(e))) return rc;
   e->cache.enabled = on != 0;
   return 0;
 }
@@ -559,10 +685,18 @@ int az_cache_clear(az_engine* e) {
 
 int az_timer_enable(az_engine* e, int on) {
   if (!e) return fail(AZ_E_INVALID, "null engine");
-  AZ_HIP(hipStreamSynchronize(e->stream));
-  e->timer.flush();
-  e->timer.reset();
-  e->timer.enabled = on != 0;
+  int rc;
+  if ((rc = sync_all(e))) return rc;
+  for (az::ConvTimer* tm : {&e->timer, &e->whole.timer}) {
+    tm->flush();
+    tm->reset();
+    tm->enabled = on != 0;
+  }
+  for (Lane* L : e->lanes) {
+    L->timer.flush();
+    L->timer.reset();
+    L->timer.enabled = on != 0;
+  }
   return 0;
 }
 
@@ -617,13 +751,23 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
   int rc;
   if ((rc = ready_to_search(e))) return rc;
   AZ_HIP(hipSetDevice(e->device));
+  const auto t_start = std::chrono::steady_clock::now();
   for (int mv = 0; mv < n_moves; ++mv) {
+    // lanes interleaved per simulation so every stream always has work queued
     for (int s = 0; s < e->g.sims; ++s)
-      if ((rc = simulate(e))) return rc;
-    az::launch_play(e->g, e->t, e->smp, nullptr, -1, 0, 1, e->stream);
+      for (Lane* L : e->lanes)
+        if ((rc = simulate(e, *L))) return rc;
+    for (Lane* L : e->lanes) az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
     AZ_HIP(hipGetLastError());
   }
-  AZ_HIP(hipStreamSynchronize(e->stream));
+  static const bool dbg = getenv("AZ_DEBUG_TIMING") != nullptr;
+  if (dbg) {
+    const double t_enq = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    if ((rc = sync_all(e))) return rc;
+    const double t_all = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    fprintf(stderr, "selfplay_step: %d moves, enqueue %.1f ms, total %.1f ms\n", n_moves, 1e3 * t_enq, 1e3 * t_all);
+  }
+  if ((rc = sync_all(e))) return rc;
   if ((rc = check_device_errors(e))) return rc;
   if (st) return az_stats_get(e, st);
   return 0;
@@ -691,7 +835,7 @@ int az_tree_search(az_engine* e, int n_sims) {
   if ((rc = ready_to_search(e))) return rc;
   AZ_HIP(hipSetDevice(e->device));
   for (int s = 0; s < n_sims; ++s)
-    if ((rc = simulate(e))) return rc;
+    if ((rc = simulate(e, e->whole))) return rc;
   AZ_HIP(hipStreamSynchronize(e->stream));
   return check_device_errors(e);
 }

@@ -50,7 +50,8 @@ struct TreeDev {
   int32_t* path;               // [slots][max_depth]
   int32_t* path_len;           // [slots]
   int32_t* slot_expansions;    // [slots], this game's expansions so far
-  uint32_t* mt;                // [625][slots], word-major MT19937 state (+ index)
+  uint32_t* mt;                // [625][mt_stride], word-major MT19937 state (+ index)
+  int32_t mt_stride;           // slots of the whole engine (a lane view offsets mt)
   int32_t* eval_slot;          // [slots] compacted eval queue (leaves to expand)
   Board* eval_board;           // [slots]
   int32_t* eval_src;           // [slots] >= 0: cache entry; < 0: -(evaluator row + 1)

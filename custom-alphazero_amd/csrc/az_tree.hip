@@ -87,7 +87,7 @@ __device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gi
   t.game_id[s] = gid;
   t.last_move[s] = -1;
   t.last_status[s] = kOngoing;
-  mt_seed(t, g.slots, s, seed);
+  mt_seed(t, t.mt_stride, s, seed);
 }
 
 // ------------------------------------------------------------------- select
@@ -118,11 +118,13 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
     stat_add(t, kStatNNEvals, 1);
     return;
   }
-  // repr(board) in plays_inferences (mcts.py:123): entries written by earlier
-  // simulations' insert kernels are complete (kernel boundary)
+  // repr(board) in plays_inferences (mcts.py:123).  Entries may be published
+  // concurrently by another lane's insert kernel: the acquire load pairs with
+  // its release exchange, so a Ready entry's key and payload are complete
+  // (a Claimed one reads as absent: the leaf is evaluated here, same result).
   uint32_t idx = (uint32_t)board_hash(b) & c.mask;
   for (int p = 0; p < c.max_probe; ++p) {
-    const uint32_t st = c.state[idx];
+    const uint32_t st = __hip_atomic_load(c.state + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     if (st == kCacheEmpty) break;
     if (st == kCacheReady && same_board(c.keys[idx], b)) {
       t.eval_src[q] = (int32_t)idx;
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(64) void play_kernel(GameCfg g, TreeDev t, SampleDe
     for (int i = 1; i < cnt; ++i)
       if (pr[i] > pr[k]) k = i;
   } else {
-    const double u = uniforms ? uniforms[s] : mt_uniform(t, g.slots, s);
+    const double u = uniforms ? uniforms[s] : mt_uniform(t, t.mt_stride, s);
     double cdf[MAXA];
     double acc = 0.0;
     for (int i = 0; i < cnt; ++i) {

@@ -31,7 +31,7 @@ class Config(ctypes.Structure):
         ("value_hidden", ctypes.c_int32), ("bn_epsilon", ctypes.c_double),
         ("arena_edges", ctypes.c_int64), ("max_tree_visits", ctypes.c_int64),
         ("cache_log2", ctypes.c_int32), ("conv_algo", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("lanes", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
     ]
 
 
@@ -130,7 +130,8 @@ class Engine:
     def __init__(self, height=6, width=7, n=4, gravity=True, mcts_iterations=100, slots=1,
                  evaluator=EVAL_NETWORK, index_move_greedy=8, exploration_constant=1.5,
                  filters=128, depth=4, value_hidden=256, bn_epsilon=1e-3, arena_edges=0,
-                 max_tree_visits=0, device=0, cache_log2=0, conv_algo=CONV_WINOGRAD):
+                 max_tree_visits=0, device=0, cache_log2=0, conv_algo=CONV_WINOGRAD,
+                 lanes=0):
         L = load_library()
         self.height, self.width, self.n, self.gravity = height, width, n, bool(gravity)
         self.action_space = width if gravity else width * height
@@ -141,7 +142,8 @@ class Engine:
                      exploration_constant=exploration_constant, slots=slots, evaluator=evaluator,
                      filters=filters, depth=depth, value_hidden=value_hidden,
                      bn_epsilon=bn_epsilon, arena_edges=arena_edges,
-                     max_tree_visits=max_tree_visits, cache_log2=cache_log2, conv_algo=conv_algo)
+                     max_tree_visits=max_tree_visits, cache_log2=cache_log2, conv_algo=conv_algo,
+                     lanes=lanes)
         handle = ctypes.c_void_p()
         _check(L.az_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
         self._h = handle

@@ -61,7 +61,9 @@ typedef struct az_config {
                                       plays_inferences, mcts/mcts.py:122-143); 0 = off */
     int32_t conv_algo;             /* residual-tower 3x3 convs: AZ_CONV_WINOGRAD (0, default) or
                                       AZ_CONV_DIRECT (1); same layer, outputs within NET_TOL */
-    int32_t reserved[6];
+    int32_t lanes;                 /* self-play slot groups searched on separate HIP streams
+                                      (0 = auto: 2 when slots >= 512); results do not depend on it */
+    int32_t reserved[5];
 } az_config;
 
 /* One named weight tensor in Keras layout ("Weights"). */

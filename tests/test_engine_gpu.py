@@ -17,10 +17,10 @@ pytestmark = pytest.mark.gpu
 NET_TOL = 1e-5  # north_star: value/policy outputs within 1e-5 (fp32)
 
 
-def synth_engine(z, slots, cache_log2=0):
+def synth_engine(z, slots, cache_log2=0, lanes=0):
     H, W, n, grav, S = (int(z[k]) for k in ("height", "width", "n", "gravity", "sims"))
     return az.Engine(H, W, n, bool(grav), S, slots=slots, evaluator=az.EVAL_SYNTHETIC,
-                     cache_log2=cache_log2)
+                     cache_log2=cache_log2, lanes=lanes)
 
 
 def selfplay_games(eng, first, n_games, base_seed=0):
@@ -51,16 +51,17 @@ def check_selfplay_game(z, g, got):
     assert got["expansions"] == z["expansions"][g]
 
 
-@pytest.mark.parametrize("cache_log2", [0, 16])
+@pytest.mark.parametrize("cache_log2,lanes", [(0, 1), (16, 1), (16, 2)])
 @pytest.mark.parametrize("name", MCTS_FIXTURES)
-def test_selfplay_synthetic_matches_reference(golden, name, cache_log2):
+def test_selfplay_synthetic_matches_reference(golden, name, cache_log2, lanes):
     """Batched device self-play == the reference's play_game, game by game,
-    with and without the shared transposition cache (plays_inferences)."""
+    with and without the shared transposition cache (plays_inferences), on one
+    stream or two lanes (slot groups on separate streams sharing the cache)."""
     z = golden("mcts_" + name)
     seeds = z["seed"].astype(np.int64)
     assert np.all(np.diff(seeds) == 1)
     for slots in sorted({len(seeds), max(1, len(seeds) // 2)}):  # also exercises slot refill
-        eng = synth_engine(z, slots, cache_log2)
+        eng = synth_engine(z, slots, cache_log2, lanes)
         games = selfplay_games(eng, int(seeds[0]), len(seeds))
         for g, got in enumerate(games):
             check_selfplay_game(z, g, got)
@@ -99,12 +100,13 @@ def test_tree_api_edges_match_reference(golden, name):
     assert A == z["policy"].shape[1]
 
 
-@pytest.mark.parametrize("cache_log2", [0, 10, 20])
-def test_selfplay_synthetic_many_games_vs_oracle(cache_log2):
+@pytest.mark.parametrize("cache_log2,lanes", [(0, 1), (10, 1), (20, 1), (20, 3), (0, 2)])
+def test_selfplay_synthetic_many_games_vs_oracle(cache_log2, lanes):
     """256 games at S=50 on 96 slots (heavy refill) == the C oracle, bitwise;
-    cache_log2=10 fills the table (probe limit / no-insert path)."""
+    cache_log2=10 fills the table (probe limit / no-insert path); 2-3 lanes
+    race on the shared cache and the refill counter."""
     eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC,
-                    cache_log2=cache_log2)
+                    cache_log2=cache_log2, lanes=lanes)
     games = selfplay_games(eng, 1000, 256, base_seed=7)
     for g, got in enumerate(games):
         ref = oracle.play_game(6, 7, 4, True, 50, 7 + 1000 + g)
@@ -149,12 +151,12 @@ CONV_ALGOS = [az.CONV_WINOGRAD, az.CONV_DIRECT]
 
 
 def make_net_engine(H=6, W=7, n=4, grav=True, S=25, slots=256, seed=0, randomize_bn=True, depth=4,
-                    cache_log2=0, conv_algo=az.CONV_WINOGRAD):
+                    cache_log2=0, conv_algo=az.CONV_WINOGRAD, lanes=0):
     A = W if grav else W * H
     spec = weight_spec(H, W, A, depth=depth)
     w = init_weights(spec, seed=seed, randomize_bn=randomize_bn)
     eng = az.Engine(H, W, n, grav, S, slots=slots, evaluator=az.EVAL_NETWORK, depth=depth,
-                    cache_log2=cache_log2, conv_algo=conv_algo)
+                    cache_log2=cache_log2, conv_algo=conv_algo, lanes=lanes)
     eng.set_weights(w.items())
     return eng, w
 
@@ -193,12 +195,12 @@ def test_forward_is_batch_invariant(conv_algo):
         np.testing.assert_array_equal(v, v_all[lo:hi])
 
 
-@pytest.mark.parametrize("cache_log2", [0, 18])
-def test_selfplay_network_replays_on_oracle(cache_log2):
+@pytest.mark.parametrize("cache_log2,lanes", [(0, 1), (18, 1), (18, 2)])
+def test_selfplay_network_replays_on_oracle(cache_log2, lanes):
     """Device self-play with the real network: the oracle, fed the engine's
     own batch-1 network outputs for every board it asks about, reproduces every
     move and visit-count policy bit for bit (replay parity)."""
-    eng, _ = make_net_engine(S=40, slots=16, randomize_bn=False, cache_log2=cache_log2)
+    eng, _ = make_net_engine(S=40, slots=16, randomize_bn=False, cache_log2=cache_log2, lanes=lanes)
     games = selfplay_games(eng, 0, 6, base_seed=123)
     cache = {}
 
