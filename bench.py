@@ -25,6 +25,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "custom-alphazero_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -198,18 +200,49 @@ def main():
     if st1["active_slots"] < args.slots:
         print(f"warning: rank {rank} ran out of game budget", file=sys.stderr)
 
-    # dominant kernel: conv3x3_mfma (8 launches per forward at depth 4)
+    # dominant kernel: the residual tower's 3x3 convs (8 launches per forward at
+    # depth 4).  Algorithmic FLOP = the direct convolution (SURVEY.md 8d, 19 F*F
+    # MACs per pixel per block: 9F + 9F + the 1x1 F); the Winograd kernel issues
+    # fewer MFMA FLOP (16 points per 2x2 tile + 4 residual rows per conv2).
     HW, F = args.height * args.width, 128
-    conv_flop_per_board = HW * 2 * F * F * 19 * args.depth       # 9F + 10F K per block
+    TB = ((args.height + 1) // 2) * ((args.width + 1) // 2)
+    conv_flop_per_board = HW * 2 * F * F * 19 * args.depth
+    mfma_flop_per_board = (TB * 36 * 2 * F * F * args.depth if args.conv_algo == 0
+                           else conv_flop_per_board)
     local_exp = st1["evaluations"] - st0["evaluations"]  # boards the network computed
     conv_avg_ms = conv_ms / max(conv_launches, 1)
-    achieved = (local_exp * conv_flop_per_board) / (conv_ms * 1e-3) / 1e12 if conv_ms else 0.0
+    busy_ms = st1["conv_busy_ms"]
+    achieved = (local_exp * conv_flop_per_board) / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
+    mfma_achieved = (local_exp * mfma_flop_per_board) / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
     boards_per_launch = local_exp / max(conv_launches / (2 * args.depth), 1)
     traffic = None
     pmc = os.path.join(REPO, "profiles", "r1", "pmc_conv_traffic.json")
     if os.path.exists(pmc):  # PMC bytes/board (rocprofv3 FETCH_SIZE/WRITE_SIZE) x live batch
         with open(pmc) as fp:
-            traffic = int(json.load(fp)["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+            tj = json.load(fp)
+        key = "winograd" if args.conv_algo == 0 else "direct"
+        if key in tj:
+            traffic = int(tj[key]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+
+    # the same kernels alone on one stream at the live per-lane batch (what a
+    # launch costs without the other lane's kernels sharing the CUs)
+    isolated = None
+    if rank == 0:
+        nb = max(1, int(round(boards_per_launch)))
+        rng = np.random.RandomState(1)
+        bx = rng.randint(-1, 2, (nb, args.height, args.width))
+        xin = np.stack([bx == 0, bx == 1, bx == -1, np.ones_like(bx, bool)], -1).astype(np.float32)
+        eng.forward(xin)
+        eng.timer(True)
+        for _ in range(10):
+            eng.forward(xin)
+        si = eng.stats()
+        eng.timer(False)
+        iso = nb * 10 * conv_flop_per_board / (si["conv_busy_ms"] * 1e-3) / 1e12
+        isolated = {"boards": nb, "avg_launch_ms": round(si["conv_ms"] / max(si["conv_launches"], 1), 4),
+                    "achieved": round(iso, 2), "frac": round(iso / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "mfma_frac": round(iso * mfma_flop_per_board / conv_flop_per_board
+                                       / FP32_MFMA_PEAK_TFLOPS, 4)}
 
     if rank == 0:
         line = {
@@ -245,18 +278,28 @@ def main():
                                     if args.cache_log2 else None),
             "cache_off": off,
             "roofline": {
-                "kernel": "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)",
+                "kernel": ("wino_conv_kernel (Winograd F(2x2,3x3) on fp32 MFMA, fused BN/ReLU and 1x1 "
+                           "projection residual)" if args.conv_algo == 0 else
+                           "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"),
                 "bound": "mfma",
                 "achieved": round(achieved, 2),
                 "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (PMC per-board bytes from profiles/r1 x live boards/launch)",
+                "traffic_unit": "HBM bytes per launch (PMC bytes/board, profiles/r1/pmc_conv_traffic.json, "
+                                "x live boards/launch)",
+                "achieved_basis": "algorithmic (direct-convolution) FLOP / conv-busy time (union of the "
+                                  "timed conv intervals of all lanes, HIP events on each lane's stream)",
+                "algorithmic_flop_per_board": conv_flop_per_board,
+                "mfma_flop_per_board": mfma_flop_per_board,
+                "mfma_achieved": round(mfma_achieved, 2),
+                "mfma_frac": round(mfma_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "boards_per_launch": round(boards_per_launch, 1),
                 "avg_launch_ms": round(conv_avg_ms, 4),
-                "algorithmic_flop_per_board": conv_flop_per_board,
+                "conv_busy_ms": round(busy_ms, 2),
                 "launches_timed": conv_launches,
+                "isolated": isolated,
             },
             "cpu_baseline": base,
         }

@@ -79,6 +79,7 @@ struct az_engine {
   std::vector<void*> owned;
   std::vector<void*> sample_bufs;
   std::vector<hipStream_t> lane_streams;
+  hipEvent_t timer_ref = nullptr;  // common origin of every ConvTimer's intervals
   int64_t sp_first = 0, sp_n = 0;
 
   template <typename T>
@@ -232,47 +233,42 @@ std::vector<float> pack_fragments(const std::vector<float>& wt, int N, int K) {
 
 // Winograd F(2x2,3x3) weights for wino_conv_kernel (az_wino.hip):
 // U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
-// in float64 from the folded Keras kernel, rounded once to float, packed as
-// float4 (((c*16 + xi)*4 + nb)*2 + q)*64 + lane, element e holding
-// cin = 16c + 8*(lane>>5) + 4q + e, cout = 32nb + (lane&31).
+// in float64 from the folded Keras kernel (times the sign the kernel expects
+// for corner points), rounded once to float, in the kernel's fragment order.
 std::vector<float> pack_wino(const std::vector<double>& w, int F) {
   static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
-  std::vector<double> U((size_t)16 * F * F, 0.0);
-  for (int a = 0; a < 4; ++a)
-    for (int b = 0; b < 4; ++b)
-      for (int ky = 0; ky < 3; ++ky)
-        for (int kx = 0; kx < 3; ++kx) {
-          const double gg = G[a][ky] * G[b][kx];
-          if (gg == 0.0) continue;
-          const double* src = w.data() + (size_t)(ky * 3 + kx) * F * F;
-          double* dst = U.data() + (size_t)(a * 4 + b) * F * F;
-          for (size_t i = 0; i < (size_t)F * F; ++i) dst[i] += gg * src[i];
-        }
   std::vector<float> p((size_t)16 * F * F);
-  for (int c = 0; c < F / 16; ++c)
-    for (int xi = 0; xi < 16; ++xi)
-      for (int nb = 0; nb < F / 32; ++nb)
-        for (int q = 0; q < 2; ++q)
-          for (int lane = 0; lane < 64; ++lane)
-            for (int e = 0; e < 4; ++e) {
-              const int cin = 16 * c + 8 * (lane >> 5) + 4 * q + e, co = 32 * nb + (lane & 31);
-              p[(((((size_t)c * 16 + xi) * 4 + nb) * 2 + q) * 64 + lane) * 4 + e] =
-                  (float)U[((size_t)xi * F + cin) * F + co];
-            }
+  std::vector<double> U((size_t)F * F);
+  for (int xi = 0; xi < 16; ++xi) {
+    const int a = xi >> 2, b = xi & 3;
+    std::fill(U.begin(), U.end(), 0.0);
+    for (int ky = 0; ky < 3; ++ky)
+      for (int kx = 0; kx < 3; ++kx) {
+        const double gg = G[a][ky] * G[b][kx];
+        if (gg == 0.0) continue;
+        const double* src = w.data() + (size_t)(ky * 3 + kx) * F * F;
+        for (size_t i = 0; i < (size_t)F * F; ++i) U[i] += gg * src[i];
+      }
+    const double sg = az::wino_fold_sign(xi);
+    for (int cin = 0; cin < F; ++cin)
+      for (int co = 0; co < F; ++co) p[az::wino_pack_index(xi, cin, co)] = (float)(sg * U[(size_t)cin * F + co]);
+  }
   return p;
 }
 
-// 1x1 projection residual [cin][cout] in the same fragment order (no xi).
+// 1x1 projection residual [cin][cout] in the same fragment order, as if it
+// were point 0 of a 16-point-per-chunk stream compacted to one point.
 std::vector<float> pack_wino_res(const std::vector<double>& wr, int F) {
   std::vector<float> p((size_t)F * F);
-  for (int c = 0; c < F / 16; ++c)
-    for (int nb = 0; nb < F / 32; ++nb)
-      for (int q = 0; q < 2; ++q)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int e = 0; e < 4; ++e) {
-            const int cin = 16 * c + 8 * (lane >> 5) + 4 * q + e, co = 32 * nb + (lane & 31);
-            p[((((size_t)c * 4 + nb) * 2 + q) * 64 + lane) * 4 + e] = (float)wr[(size_t)cin * F + co];
-          }
+  const int CK = az::kWinoCK;
+  for (int cin = 0; cin < F; ++cin)
+    for (int co = 0; co < F; ++co) {
+      // index within the chunk's 16-point block, then compact chunks to 1 point
+      const size_t i16 = az::wino_pack_index(0, cin, co);
+      const size_t per_point = (size_t)4 * (CK / 8) * 64 * 4;  // floats per point per chunk
+      const size_t c = (size_t)cin / CK;
+      p[i16 - c * 16 * per_point + c * per_point] = (float)wr[(size_t)cin * F + co];
+    }
   return p;
 }
 
@@ -503,6 +499,7 @@ int az_engine_destroy(az_engine* eng) {
     if (L != &eng->whole) delete L;
   for (void* p : eng->sample_bufs) (void)hipFree(p);
   for (void* p : eng->owned) (void)hipFree(p);
+  if (eng->timer_ref) (void)hipEventDestroy(eng->timer_ref);
   if (eng->stream) (void)hipStreamDestroy(eng->stream);
   delete eng;
   return 0;
@@ -651,18 +648,29 @@ int az_stats_get(az_engine* e, az_stats* st) {
   st->plies = (int64_t)h[az::kStatPlies];
   st->errors = (int64_t)h[az::kStatErrors];
   st->active_slots = std::count_if(gid.begin(), gid.end(), [](int64_t v) { return v >= 0; });
-  e->timer.flush();
-  st->conv_ms = e->timer.total_ms;
-  st->conv_launches = e->timer.launches;
-  e->whole.timer.flush();
-  st->conv_ms += e->whole.timer.total_ms;
-  st->conv_launches += e->whole.timer.launches;
-  for (Lane* L : e->lanes) {
-    if (L == &e->whole) continue;
-    L->timer.flush();
-    st->conv_ms += L->timer.total_ms;
-    st->conv_launches += L->timer.launches;
+  std::vector<az::ConvTimer*> timers = {&e->timer, &e->whole.timer};
+  for (Lane* L : e->lanes)
+    if (L != &e->whole) timers.push_back(&L->timer);
+  std::vector<std::pair<double, double>> iv;
+  for (az::ConvTimer* tm : timers) {
+    tm->flush();
+    st->conv_ms += tm->total_ms;
+    st->conv_launches += tm->launches;
+    iv.insert(iv.end(), tm->intervals.begin(), tm->intervals.end());
   }
+  std::sort(iv.begin(), iv.end());
+  double busy = 0.0, lo = 0.0, hi = -1.0;
+  for (const auto& x : iv) {
+    if (x.first > hi) {
+      if (hi > lo) busy += hi - lo;
+      lo = x.first;
+      hi = x.second;
+    } else {
+      hi = std::max(hi, x.second);
+    }
+  }
+  if (hi > lo) busy += hi - lo;
+  st->conv_busy_ms = busy;
   st->cache_hits = (int64_t)h[az::kStatCacheHits];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
   return 0;
@@ -687,15 +695,17 @@ int az_timer_enable(az_engine* e, int on) {
   if (!e) return fail(AZ_E_INVALID, "null engine");
   int rc;
   if ((rc = sync_all(e))) return rc;
-  for (az::ConvTimer* tm : {&e->timer, &e->whole.timer}) {
+  if (!e->timer_ref) AZ_HIP(hipEventCreate(&e->timer_ref));
+  AZ_HIP(hipEventRecord(e->timer_ref, e->stream));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  std::vector<az::ConvTimer*> timers = {&e->timer, &e->whole.timer};
+  for (Lane* L : e->lanes)
+    if (L != &e->whole) timers.push_back(&L->timer);
+  for (az::ConvTimer* tm : timers) {
     tm->flush();
     tm->reset();
+    tm->ref = &e->timer_ref;
     tm->enabled = on != 0;
-  }
-  for (Lane* L : e->lanes) {
-    L->timer.flush();
-    L->timer.reset();
-    L->timer.enabled = on != 0;
   }
   return 0;
 }

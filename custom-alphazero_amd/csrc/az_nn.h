@@ -28,13 +28,18 @@ struct NetDev {
 };
 
 // hipEvent pairs around the conv launches of every forward while enabled, so
-// bench.py can price the dominant kernel live (roofline.achieved).
+// bench.py can price the dominant kernel live (roofline.achieved).  `ref` is
+// an event the engine records when timing starts: intervals of all lanes are
+// placed on one device clock, so their union (time in which any conv ran)
+// can be taken next to the summed durations.
 struct ConvTimer {
   bool enabled = false;
+  hipEvent_t* ref = nullptr;
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   double total_ms = 0.0;
   long long launches = 0;
+  std::vector<std::pair<double, double>> intervals;  // [start, end) ms after *ref
   void begin(hipStream_t s) {
     if (!enabled) return;
     if (used + 2 > pool.size()) {
@@ -54,9 +59,12 @@ struct ConvTimer {
   // call after a stream synchronize: folds recorded pairs into total_ms
   void flush() {
     for (size_t i = 0; i + 1 < used; i += 2) {
-      float ms = 0.f;
+      float ms = 0.f, a = 0.f, b = 0.f;
       (void)hipEventElapsedTime(&ms, pool[i], pool[i + 1]);
       total_ms += ms;
+      if (ref && hipEventElapsedTime(&a, *ref, pool[i]) == hipSuccess &&
+          hipEventElapsedTime(&b, *ref, pool[i + 1]) == hipSuccess)
+        intervals.emplace_back(a, b);
     }
     used = 0;
   }
@@ -64,6 +72,7 @@ struct ConvTimer {
     used = 0;
     total_ms = 0.0;
     launches = 0;
+    intervals.clear();
   }
   ~ConvTimer() {
     for (auto e : pool) (void)hipEventDestroy(e);
@@ -74,6 +83,14 @@ void launch_encode(const Board* boards, const int* count, int n_max, int HW, flo
                    hipStream_t s);
 void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* mask,
                        hipStream_t s);
+// Winograd conv: input channels per LDS chunk (16 or 32; the host packing
+// follows it), packing index and the sign folded into the corner points
+#ifndef AZ_WINO_CK
+#define AZ_WINO_CK 32
+#endif
+constexpr int kWinoCK = AZ_WINO_CK;
+size_t wino_pack_index(int xi, int cin, int cout);
+int wino_fold_sign(int xi);
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
                       int n_max, int H, int W, hipStream_t s, int pipe);

@@ -15,16 +15,18 @@
 //
 // Workgroup = 4 waves = 32 consecutive tiles (one MFMA M block) x 128 output
 // channels; wave w owns output channels [32w, 32w+32).  Input channels run in
-// 8 chunks of 16:
+// chunks of CK:
 //   * produce: the 256 threads turn the chunk's 4x4 input patches (read from
 //     global/L2; a pixel is shared by up to four tiles) into V = B^T d B and
-//     store V[xi][tile][16 cin] in LDS (plus, for the block's second conv, the
-//     4 output pixels' block-input rows for the fused 1x1 projection residual);
-//   * consume: per xi, 8 MFMAs accumulate M = V[xi] U[xi] over the chunk
-//     (A from LDS, B = host-packed U fragments streamed from global two
-//     points ahead), then M is added into the four output-pixel accumulators
-//     with the +-1 coefficients of A^T (x) A^T.  The residual's four pixel
-//     rows accumulate straight into their pixel's accumulator.
+//     store V[xi][tile][CK] in LDS (plus, for the block's second conv, the 4
+//     output pixels' block-input rows for the fused 1x1 projection residual);
+//   * consume, one pipeline stage per point xi: CK/2 MFMAs accumulate
+//     M = V[xi] U[xi] over the chunk (A from LDS, B = host-packed U fragments
+//     streamed from global one stage ahead), and the previous stage's M is
+//     added into the output-pixel accumulators with the +-1 coefficients of
+//     A^T (x) A^T.  The four corner points feed exactly one output pixel each:
+//     their MFMAs accumulate straight into that pixel (the sign folded into U
+//     on the host), no M and no adds; the residual's pixel rows likewise.
 // Reduction order per output element is fixed (chunk, xi, k-step), so a
 // board's outputs do not depend on the rest of the batch.
 #include "az_nn.h"
@@ -33,27 +35,56 @@ namespace az {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kWinoTiles = 32;   // tiles per workgroup (MFMA M)
-constexpr int kWinoCK = 16;      // input channels per chunk
-constexpr int kWinoChunks = 128 / kWinoCK;
+constexpr int kWinoTiles = 32;  // tiles per workgroup (MFMA M)
 
-// V rows are 16 floats = four 16-byte chunks; chunk j of tile row t lives at
-// j ^ ((t >> 2) & 3) so the 16 rows a ds_read_b128 lane group touches fall on
-// 16 distinct bank quads.
-__device__ __forceinline__ int vswz(int j, int t) { return j ^ ((t >> 2) & 3); }
+// A^T = [[1,1,1,0],[0,1,-1,-1]]: sign with which point coordinate a feeds
+// output coordinate i (0 = not at all)
+__host__ __device__ constexpr int wino_sign(int a, int i) {
+  return i == 0 ? (a == 3 ? 0 : 1) : (a == 0 ? 0 : (a == 1 ? 1 : -1));
+}
+// corner points (a, b in {0, 3}) feed one output pixel; returns it, else -1.
+// With AZ_WINO_CORNER their MFMAs accumulate straight into the pixel; off by
+// default: mixing MFMA and VALU writes on the same accumulators serialises
+// the stage (measured 175 -> 148 TFLOP/s at B = 4096).
+#ifndef AZ_WINO_BRING
+#define AZ_WINO_BRING 2  // B register ring (prefetch distance RB/2)
+#endif
+#ifndef AZ_WINO_CORNER
+#define AZ_WINO_CORNER 0
+#endif
+__host__ __device__ constexpr int wino_corner_pixel(int xi) {
+  return AZ_WINO_CORNER && ((xi >> 2) == 0 || (xi >> 2) == 3) && ((xi & 3) == 0 || (xi & 3) == 3)
+             ? 2 * ((xi >> 2) == 3) + ((xi & 3) == 3)
+             : -1;
+}
+
+// V rows are CK floats = CK/4 16-byte chunks; chunk j of tile row t is
+// stored at j ^ f(t) with f(t) = (t / rows-per-256B) mod (CK/4), so the 16
+// rows a ds_read_b128 lane group touches fall on 16 distinct bank quads.
+template <int CK>
+__device__ __forceinline__ int vswz(int j, int t) {
+  constexpr int RC = CK / 4, RPB = 16 / RC;
+  return j ^ ((t / RPB) & (RC - 1));
+}
 
 // PIPE 0: one V buffer, chunk c+1 loaded+transformed between two barriers.
 // PIPE 1: two V buffers; chunk c+1's patch loads are issued a whole chunk
 //         early into registers and transformed after chunk c's MFMAs: one
-//         barrier per chunk, no exposed global latency.
-template <bool RESIDUAL, int PIPE>
+//         barrier per chunk, no exposed global latency (LDS permitting).
+template <bool RESIDUAL, int CK, int PIPE>
 __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
     int n_static, int H, int W) {
-  constexpr int NX = RESIDUAL ? 20 : 16;  // 16 Winograd points (+4 residual pixel rows)
-  constexpr int VB = NX * kWinoTiles * 4;  // float4 per V buffer
+  static_assert(CK == 16 || CK == 32, "chunk of 16 or 32 input channels");
+  constexpr int NX = RESIDUAL ? 20 : 16;   // 16 Winograd points (+4 residual pixel rows)
+  constexpr int RC = CK / 4;               // float4 per V row
+  constexpr int VB = NX * kWinoTiles * RC; // float4 per V buffer
+  constexpr int NCH = 128 / CK;
+  constexpr int KS = CK / 2;               // MFMA k-steps per stage
+  constexpr int QB = CK / 8;               // float4 of B (and of A) per lane per stage
+  constexpr int IPT = 16 * CK / 256;       // producer items per thread (tile, c4, half)
   __shared__ float4 vbuf_all[(PIPE ? 2 : 1) * VB];
 
   const int HW = H * W, TW = (W + 1) >> 1, TH = (H + 1) >> 1, TB = TH * TW;
@@ -63,97 +94,113 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
   if (t0 >= tiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // ---- producer geometry: thread -> (tile pt, 4-channel group pc, half ph)
-  const int pt = tid >> 3, pc = (tid >> 1) & 3, ph = tid & 1;
-  const int ptau = t0 + pt;
-  const bool pvalid = ptau < tiles;
-  int pb = 0, pty = 0, ptx = 0;
-  if (pvalid) {
-    pb = ptau / TB;
-    const int lt = ptau - pb * TB;
-    pty = lt / TW;
-    ptx = lt - pty * TW;
-  }
-  // rows of the 4x4 patch this half needs: V rows i = 2ph, 2ph+1 use d rows
-  // {0,1,2} (ph = 0) or {1,2,3} (ph = 1)
-  int doff[3][4];
+  // ---- producer geometry: item -> (tile pt, 4-channel group pc, half ph)
+  int pt[IPT], pc[IPT], ph[IPT], pbase[IPT], pty[IPT], ptx[IPT];
+  bool pvalid[IPT];
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    const int y = 2 * pty - 1 + ph + r;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int x = 2 * ptx - 1 + c;
-      const bool ok = pvalid && y >= 0 && y < H && x >= 0 && x < W;
-      doff[r][c] = ok ? ((pb * HW + y * W + x) * 128 + pc * 4) : -1;
+  for (int it = 0; it < IPT; ++it) {
+    const int item = tid + 256 * it;
+    ph[it] = item & 1;
+    pc[it] = (item >> 1) & (RC - 1);
+    pt[it] = item / (2 * RC);
+    const int tau = t0 + pt[it];
+    pvalid[it] = tau < tiles;
+    int b = 0, ty = 0, tx = 0;
+    if (pvalid[it]) {
+      b = tau / TB;
+      const int lt = tau - b * TB;
+      ty = lt / TW;
+      tx = lt - ty * TW;
     }
-  }
-  int roff[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int p = 2 * ph + k;
-    const int y = 2 * pty + (p >> 1), x = 2 * ptx + (p & 1);
-    roff[k] = (RESIDUAL && pvalid && y < H && x < W) ? ((pb * HW + y * W + x) * 128 + pc * 4) : -1;
+    pbase[it] = b * HW * 128 + pc[it] * 4;
+    pty[it] = ty;
+    ptx[it] = tx;
   }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   struct Patch {
-    float4 d[3][4];
-    float4 rr[2];
+    float4 d[IPT][3][4];
+    float4 rr[IPT][2];
+    uint32_t ok[IPT];  // bit r*4+x: patch pixel on the board; bits 12,13: residual rows
   };
-  // unconditional loads (clamped address) + select: no branches, all 12-14
-  // loads in flight together
+  // V rows i = 2ph, 2ph+1 need patch rows {0,1,2} (ph = 0) or {1,2,3} (ph = 1).
+  // Unconditional loads from a clamped address: no branches, every load of
+  // the chunk in flight together; off-board pixels are zeroed in
+  // produce_store, so nothing here waits on the loads (PIPE 1 issues them a
+  // whole chunk ahead).
   auto produce_load = [&](int c, Patch& P) {
-    const int cb = c * kWinoCK;
+    const int cb = c * CK;
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+    for (int it = 0; it < IPT; ++it) {
+      P.ok[it] = 0;
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
-        P.d[r][x] = *reinterpret_cast<const float4*>(in + (unsigned)(doff[r][x] >= 0 ? doff[r][x] + cb : 0));
-    if constexpr (RESIDUAL) {
+      for (int r = 0; r < 3; ++r) {
+        const int y = 2 * pty[it] - 1 + ph[it] + r;
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        P.rr[k] = *reinterpret_cast<const float4*>(res_in + (unsigned)(roff[k] >= 0 ? roff[k] + cb : 0));
+        for (int x = 0; x < 4; ++x) {
+          const int xx = 2 * ptx[it] - 1 + x;
+          const bool ok = pvalid[it] && y >= 0 && y < H && xx >= 0 && xx < W;
+          const unsigned o = ok ? (unsigned)(pbase[it] + (y * W + xx) * 128 + cb) : 0u;
+          P.d[it][r][x] = *reinterpret_cast<const float4*>(in + o);
+          P.ok[it] |= (uint32_t)ok << (r * 4 + x);
+        }
+      }
+      if constexpr (RESIDUAL) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int p = 2 * ph[it] + k;
+          const int y = 2 * pty[it] + (p >> 1), xx = 2 * ptx[it] + (p & 1);
+          const bool ok = pvalid[it] && y < H && xx < W;
+          const unsigned o = ok ? (unsigned)(pbase[it] + (y * W + xx) * 128 + cb) : 0u;
+          P.rr[it][k] = *reinterpret_cast<const float4*>(res_in + o);
+          P.ok[it] |= (uint32_t)ok << (12 + k);
+        }
+      }
     }
   };
   auto produce_store = [&](Patch& P, float4* vbuf) {
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+    for (int it = 0; it < IPT; ++it) {
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
-        if (doff[r][x] < 0) P.d[r][x] = z4;
-    if constexpr (RESIDUAL) {
+      for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (roff[k] < 0) P.rr[k] = z4;
-    }
-    // T = B^T d (rows), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
-    float4 T[2][4];
+        for (int x = 0; x < 4; ++x)
+          if (!((P.ok[it] >> (r * 4 + x)) & 1)) P.d[it][r][x] = z4;
+      if constexpr (RESIDUAL) {
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const float4 a = P.d[0][x], b = P.d[1][x], e = P.d[2][x];
-      if (ph == 0) {  // rows 0,1 from d rows 0,1,2
-        T[0][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
-        T[1][x] = make_float4(b.x + e.x, b.y + e.y, b.z + e.z, b.w + e.w);
-      } else {        // rows 2,3 from d rows 1,2,3 (a = d1, b = d2, e = d3)
-        T[0][x] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
-        T[1][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
+        for (int k = 0; k < 2; ++k)
+          if (!((P.ok[it] >> (12 + k)) & 1)) P.rr[it][k] = z4;
       }
-    }
-    const int sw = vswz(pc, pt);
+      // T = B^T d (rows), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
+      float4 T[2][4];
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
-      const int i = 2 * ph + ii;
-      const float4 t0_ = T[ii][0], t1 = T[ii][1], t2 = T[ii][2], t3 = T[ii][3];
-      const float4 v[4] = {
-          make_float4(t0_.x - t2.x, t0_.y - t2.y, t0_.z - t2.z, t0_.w - t2.w),
-          make_float4(t1.x + t2.x, t1.y + t2.y, t1.z + t2.z, t1.w + t2.w),
-          make_float4(t2.x - t1.x, t2.y - t1.y, t2.z - t1.z, t2.w - t1.w),
-          make_float4(t1.x - t3.x, t1.y - t3.y, t1.z - t3.z, t1.w - t3.w)};
+      for (int x = 0; x < 4; ++x) {
+        const float4 a = P.d[it][0][x], b = P.d[it][1][x], e = P.d[it][2][x];
+        if (ph[it] == 0) {  // rows 0,1 from d rows 0,1,2
+          T[0][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
+          T[1][x] = make_float4(b.x + e.x, b.y + e.y, b.z + e.z, b.w + e.w);
+        } else {            // rows 2,3 from d rows 1,2,3 (a = d1, b = d2, e = d3)
+          T[0][x] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
+          T[1][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
+        }
+      }
+      const int sw = vswz<CK>(pc[it], pt[it]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) vbuf[((i * 4 + j) * kWinoTiles + pt) * 4 + sw] = v[j];
-    }
-    if constexpr (RESIDUAL) {
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * ph[it] + ii;
+        const float4 t0_ = T[ii][0], t1 = T[ii][1], t2 = T[ii][2], t3 = T[ii][3];
+        const float4 v[4] = {
+            make_float4(t0_.x - t2.x, t0_.y - t2.y, t0_.z - t2.z, t0_.w - t2.w),
+            make_float4(t1.x + t2.x, t1.y + t2.y, t1.z + t2.z, t1.w + t2.w),
+            make_float4(t2.x - t1.x, t2.y - t1.y, t2.z - t1.z, t2.w - t1.w),
+            make_float4(t1.x - t3.x, t1.y - t3.y, t1.z - t3.z, t1.w - t3.w)};
 #pragma unroll
-      for (int k = 0; k < 2; ++k) vbuf[((16 + 2 * ph + k) * kWinoTiles + pt) * 4 + sw] = P.rr[k];
+        for (int j = 0; j < 4; ++j) vbuf[((i * 4 + j) * kWinoTiles + pt[it]) * RC + sw] = v[j];
+      }
+      if constexpr (RESIDUAL) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          vbuf[((16 + 2 * ph[it] + k) * kWinoTiles + pt[it]) * RC + sw] = P.rr[it][k];
+      }
     }
   };
 
@@ -165,32 +212,33 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) Y[p][i] = 0.0f;
 
-  // B stream: point g = c*NX + xi; two float4 per point.  Four register
-  // buffers, prefetch distance 2 (NX % 4 == 0 keeps the ring position static
-  // inside the unrolled point loop).  32-bit offsets from the uniform base.
-  const unsigned blane = (unsigned)(wave * 128 + lane);
-  auto load_b = [&](int c, int xi, float4 (&dst)[2]) {
-    const float4* base = (RESIDUAL && xi >= 16) ? rpack : upack;
-    const unsigned o = blane + (unsigned)((RESIDUAL && xi >= 16) ? c * 512 : (c * 16 + xi) * 512);
-    dst[0] = base[o];
-    dst[1] = base[o + 64];
+  // B stream: QB float4 per lane per stage in a ring of RB register buffers,
+  // prefetched RB-2... RB/2 stages ahead (NX % RB == 0 keeps the ring slot
+  // static per stage).  32-bit offsets from the uniform base.
+  constexpr int RB = AZ_WINO_BRING, DIST = RB / 2;
+  static_assert(NX % RB == 0, "ring slot must be static per stage");
+  const unsigned blane = (unsigned)(wave * 64 * QB + lane);
+  auto load_b = [&](int c, int xi, float4 (&dst)[QB]) {
+    const bool res = RESIDUAL && xi >= 16;
+    const float4* base = res ? rpack : upack;
+    const unsigned o = blane + (unsigned)(res ? c * 4 * 64 * QB : (c * 16 + xi) * 4 * 64 * QB);
+#pragma unroll
+    for (int q = 0; q < QB; ++q) dst[q] = base[o + q * 64];
   };
-  auto load_a = [&](const float4* vbuf, int xi, float4 (&dst)[2]) {
-    const float4* vrow = vbuf + (xi * kWinoTiles + r) * 4;
-    dst[0] = vrow[vswz(2 * h, r)];
-    dst[1] = vrow[vswz(2 * h + 1, r)];
+  auto load_a = [&](const float4* vbuf, int xi, float4 (&dst)[QB]) {
+    const float4* vrow = vbuf + (xi * kWinoTiles + r) * RC;
+#pragma unroll
+    for (int q = 0; q < QB; ++q) dst[q] = vrow[vswz<CK>(QB * h + q, r)];
   };
-  // Y[p] +-= M for the output pixels point xi feeds:
-  // A^T = [[1,1,1,0],[0,1,-1,-1]] on both axes
   auto scatter = [&](int xi, const f32x16& m) {
     const int a = xi >> 2, bb = xi & 3;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int si = i == 0 ? (a == 3 ? 0 : 1) : (a == 0 ? 0 : (a == 1 ? 1 : -1));
+      const int si = wino_sign(a, i);
       if (si == 0) continue;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int sj = j == 0 ? (bb == 3 ? 0 : 1) : (bb == 0 ? 0 : (bb == 1 ? 1 : -1));
+        const int sj = wino_sign(bb, j);
         if (sj == 0) continue;
         if (si * sj > 0) {
           Y[2 * i + j] += m;
@@ -200,64 +248,75 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
       }
     }
   };
-  float4 bq[4][2], aq[2][2];
+  float4 bq[RB][QB], aq[2][QB];
   f32x16 M[2];
 
   Patch P;
   produce_load(0, P);
   produce_store(P, vbuf_all);
   if (PIPE) produce_load(1, P);
-  load_b(0, 0, bq[0]);
-  load_b(0, 1, bq[1]);
+#pragma unroll
+  for (int k = 0; k < DIST; ++k) load_b(0, k, bq[k]);
   __syncthreads();
 
-  for (int c = 0; c < kWinoChunks; ++c) {
+  // the chunk loop stays rolled: one copy of the 16-20 unrolled stages is
+  // already ~10 KB of code (unrolling it tripled the body and ran 15% slower)
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
     const float4* vbuf = vbuf_all + (PIPE ? (c & 1) * VB : 0);
     load_a(vbuf, 0, aq[0]);
+    int pend = -1;  // point whose M still has to be scattered
 #pragma unroll
     for (int xi = 0; xi < NX; ++xi) {
       // one software-pipeline stage per point: the scheduler may interleave
-      // inside a stage (MFMAs of xi with the adds of xi-1) but not across
+      // inside a stage (MFMAs of xi with the adds of the pending point and
+      // the next stage's loads) but not across
       __builtin_amdgcn_sched_barrier(0);
       {
-        const int nx = xi + 2;
+        const int nx = xi + DIST;
         if (nx < NX) {
-          load_b(c, nx, bq[nx & 3]);
-        } else if (c + 1 < kWinoChunks) {
-          load_b(c + 1, nx - NX, bq[nx & 3]);
+          load_b(c, nx, bq[nx % RB]);
+        } else if (c + 1 < NCH) {
+          load_b(c + 1, nx - NX, bq[nx % RB]);
         }
       }
       if (xi + 1 < NX) load_a(vbuf, xi + 1, aq[(xi + 1) & 1]);
-      const float4 a0 = aq[xi & 1][0], a1 = aq[xi & 1][1];
-      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const float4 b0 = bq[xi & 3][0], b1 = bq[xi & 3][1];
-      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-      if (RESIDUAL && xi >= 16) {
-        // fused 1x1 projection residual: pixel p's own block-input row
-        const int p = xi - 16;
+      float av[KS], bv[KS];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) Y[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], Y[p], 0, 0, 0);
+      for (int q = 0; q < QB; ++q) {
+        const float4 a4 = aq[xi & 1][q], b4 = bq[xi % RB][q];
+        av[4 * q] = a4.x, av[4 * q + 1] = a4.y, av[4 * q + 2] = a4.z, av[4 * q + 3] = a4.w;
+        bv[4 * q] = b4.x, bv[4 * q + 1] = b4.y, bv[4 * q + 2] = b4.z, bv[4 * q + 3] = b4.w;
+      }
+      const int direct = (RESIDUAL && xi >= 16) ? xi - 16 : wino_corner_pixel(xi);
+      if (direct >= 0) {
+        // residual pixel row, or a corner point: straight into its pixel
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          Y[direct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], Y[direct], 0, 0, 0);
       } else {
         f32x16& m = M[xi & 1];
         m = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], bv[0], f32x16{}, 0, 0, 0);
 #pragma unroll
-        for (int s = 1; s < 8; ++s) m = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], m, 0, 0, 0);
+        for (int s = 1; s < KS; ++s) m = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], m, 0, 0, 0);
       }
-      if (xi >= 1 && xi - 1 < 16) {
-        scatter(xi - 1, M[(xi - 1) & 1]);
+      if (pend >= 0) {
+        scatter(pend, M[pend & 1]);
         // pin the adds to this stage (IR-level sinking would otherwise move
-        // every point's adds to the loop latch and keep 16 M blocks live)
+        // every point's adds to the loop latch and keep all M blocks live)
         asm volatile("" ::"v"(Y[0]), "v"(Y[1]), "v"(Y[2]), "v"(Y[3]));
+        pend = -1;
       }
+      if (direct < 0) pend = xi;
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (NX == 16) scatter(15, M[1]);
-    if (c + 1 < kWinoChunks) {
+    if (pend >= 0) scatter(pend, M[pend & 1]);
+    if (c + 1 < NCH) {
       if constexpr (PIPE) {
         // the other buffer was last read in chunk c-1, before the previous
         // barrier: safe to overwrite now
         produce_store(P, vbuf_all + ((c + 1) & 1) * VB);
-        if (c + 2 < kWinoChunks) produce_load(c + 2, P);
+        if (c + 2 < NCH) produce_load(c + 2, P);
         __syncthreads();
       } else {
         __syncthreads();  // every wave is done with chunk c's V
@@ -286,6 +345,23 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
   }
 }
 
+// float index of weight (cin, cout) at point xi in the kernel's B stream:
+// float4 (((c*16 + xi)*4 + nb)*QB + q)*64 + lane, element e, where
+// cin = CK*c + (CK/2)*(lane>>5) + 4q + e and cout = 32nb + (lane&31).
+size_t wino_pack_index(int xi, int cin, int cout) {
+  constexpr int CK = kWinoCK, QB = CK / 8;
+  const int c = cin / CK, rem = cin % CK, hh = rem / (CK / 2), k = rem % (CK / 2);
+  const int q = k / 4, e = k % 4, nb = cout / 32, lane = 32 * hh + cout % 32;
+  return (((((size_t)c * 16 + xi) * 4 + nb) * QB + q) * 64 + lane) * 4 + e;
+}
+
+// sign folded into U for the corner points the kernel accumulates directly
+int wino_fold_sign(int xi) {
+  if (wino_corner_pixel(xi) < 0) return 1;
+  const int a = xi >> 2, b = xi & 3;
+  return wino_sign(a, a == 3 ? 1 : 0) * wino_sign(b, b == 3 ? 1 : 0);
+}
+
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
                       int n_max, int H, int W, hipStream_t s, int pipe) {
@@ -294,16 +370,20 @@ void launch_wino_conv(const float* in, const float* res_in, const float* upack,
   if (grid <= 0) return;
   const float4* u = reinterpret_cast<const float4*>(upack);
   const float4* rp = reinterpret_cast<const float4*>(rpack);
+  constexpr int CK = kWinoCK;
+  // PIPE 1 needs two V buffers: at CK = 32 they would leave one workgroup per
+  // CU, so CK = 32 always runs single-buffered
+  constexpr int P1 = CK == 16 ? 1 : 0;
   if (pipe) {
     if (res_in)
-      wino_conv_kernel<true, 1><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W);
+      wino_conv_kernel<true, CK, P1><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W);
     else
-      wino_conv_kernel<false, 1><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W);
+      wino_conv_kernel<false, CK, P1><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W);
   } else {
     if (res_in)
-      wino_conv_kernel<true, 0><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W);
+      wino_conv_kernel<true, CK, 0><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W);
     else
-      wino_conv_kernel<false, 0><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W);
+      wino_conv_kernel<false, CK, 0><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W);
   }
 }
 

@@ -47,7 +47,7 @@ class Stats(ctypes.Structure):
         ("plies", ctypes.c_int64), ("active_slots", ctypes.c_int64), ("errors", ctypes.c_int64),
         ("conv_launches", ctypes.c_int64), ("conv_ms", ctypes.c_double),
         ("cache_hits", ctypes.c_int64), ("evaluations", ctypes.c_int64),
-        ("reserved", ctypes.c_int64 * 5),
+        ("conv_busy_ms", ctypes.c_double), ("reserved", ctypes.c_int64 * 4),
     ]
 
     def as_dict(self):
@@ -70,8 +70,9 @@ def load_library():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise AzError(f"libaz.so not built at {LIB_PATH}; run __graft_entry__.build()")
+    path = os.environ.get("AZ_LIB_PATH", LIB_PATH)  # A/B builds (profiles/); default in-tree lib
+    if not os.path.exists(path):
+        raise AzError(f"libaz.so not built at {path}; run __graft_entry__.build()")
     # One HIP runtime per process: torch's wheel bundles its own libamdhip64 /
     # libhsa-runtime64 with the same SONAMEs as /opt/rocm's.  Loading torch
     # first makes libaz bind to that already-loaded runtime (SONAME match);
@@ -80,7 +81,7 @@ def load_library():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sig = {
         "az_abi_version": (ctypes.c_int, []),

@@ -87,7 +87,9 @@ typedef struct az_stats {
     double conv_ms;           /* their summed device time */
     int64_t cache_hits;       /* expansions served by the transposition cache */
     int64_t evaluations;      /* boards the evaluator computed (network or synthetic) */
-    int64_t reserved[5];
+    double conv_busy_ms;      /* union of the timed conv intervals over all lanes (device
+                                 time in which at least one lane's conv kernels ran) */
+    int64_t reserved[4];
 } az_stats;
 
 int az_abi_version(void);
