@@ -1,67 +1,75 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 collection (kernel trace/stats + FETCH_SIZE/WRITE_SIZE
-passes) into the table committed under profiles/.
+"""Summarise a collect_r1.sh run into the markdown committed under profiles/.
 
-HBM bytes follow MI355X_MICROARCH.md's HBM/rocprofv3 section: counters are in
-KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane)
-coalesced read, so fetched bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact
-for 16 B/lane stores.  Usage: summarize.py <prof_dir> [boards_per_launch]
-"""
+Usage: summarize.py <prof_dir>   (prof_dir = gpurun_out/prof_r1)
+HBM bytes follow MI355X_MICROARCH.md's HBM/rocprofv3 section (FETCH_SIZE x2
+on gfx950 for 16 B/lane streams, WRITE_SIZE as is; KiB units)."""
 import csv
+import glob
+import json
 import os
+import subprocess
 import sys
-from collections import defaultdict
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def short(name):
-    name = name.replace("void ", "")
-    return name.split("(")[0][:60]
-
-
-def stats(path):
-    rows = list(csv.DictReader(open(path)))
-    return [(short(r["Name"]), int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]),
-             float(r["Percentage"])) for r in rows]
-
-
-def counters(path, name):
-    acc = defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == name:
-            acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return name.replace("void ", "").split("(")[0][:64]
 
 
 def main():
     d = sys.argv[1]
-    boards = float(sys.argv[2]) if len(sys.argv) > 2 else None
-    st = stats(os.path.join(d, "trace", "run_kernel_stats.csv"))
-    print("## Kernel time (rocprofv3 --kernel-trace --stats)\n")
+    st = glob.glob(f"{d}/trace/**/*kernel_stats.csv", recursive=True)[0]
+    tr = glob.glob(f"{d}/trace/**/*kernel_trace.csv", recursive=True)[0]
+    rows = list(csv.DictReader(open(st)))
+    print("## Kernel time (rocprofv3 --kernel-trace --stats, `bench.py --steps 5 --warmup 20`)\n")
     print("| kernel | calls | total ms | avg us | % |")
     print("|---|---:|---:|---:|---:|")
-    for n, c, tot, avg, pct in st[:14]:
+    conv_calls = conv_ns = 0
+    for r in rows[:16]:
+        n, c, tot, avg, pct = short(r["Name"]), int(r["Calls"]), float(r["TotalDurationNs"]), \
+            float(r["AverageNs"]), float(r["Percentage"])
         print(f"| `{n}` | {c} | {tot / 1e6:.1f} | {avg / 1e3:.1f} | {pct:.2f} |")
-    conv = [(c, tot) for n, c, tot, _, _ in st if "conv3x3_mfma" in n]
-    if conv:
-        calls = sum(c for c, _ in conv)
-        tot = sum(t for _, t in conv)
-        print(f"\nconv3x3_mfma (both variants): {calls} launches, average {tot / calls / 1e3:.1f} us")
-    fetch_p = os.path.join(d, "fetch", "run_counter_collection.csv")
-    write_p = os.path.join(d, "write", "run_counter_collection.csv")
-    if os.path.exists(fetch_p) and os.path.exists(write_p):
-        f, w = counters(fetch_p, "FETCH_SIZE"), counters(write_p, "WRITE_SIZE")
-        print("\n## HBM traffic per launch (PMC, separate passes; fetch x2 gfx950 correction)\n")
-        print("| kernel | FETCH_SIZE KiB | WRITE_SIZE KiB | HBM MB/launch (corrected) |"
-              + (" KB/board |" if boards else ""))
-        print("|---|---:|---:|---:|" + ("---:|" if boards else ""))
-        for k in sorted(f, key=lambda k: -f[k]):
-            if k not in w:
+    for r in rows:
+        if "conv_kernel" in r["Name"] or "conv3x3_mfma" in r["Name"]:
+            if "stem" in r["Name"]:
                 continue
-            mb = (2 * f[k] + w[k]) * 1024 / 1e6
-            line = f"| `{k}` | {f[k]:.0f} | {w[k]:.0f} | {mb:.2f} |"
-            if boards:
-                line += f" {mb * 1e3 / boards:.2f} |"
-            print(line)
+            conv_calls += int(r["Calls"])
+            conv_ns += float(r["TotalDurationNs"])
+    print(f"\nresidual-tower conv kernels: {conv_calls} launches, rocprof average "
+          f"{conv_ns / max(conv_calls, 1) / 1e3:.1f} us per launch")
+    try:
+        b = json.loads(open(f"{d}/bench_trace.json").read().strip().splitlines()[-1])
+        rf = b["roofline"]
+        print(f"same run, bench.py HIP events: avg_launch_ms {rf['avg_launch_ms']} "
+              f"({rf['avg_launch_ms'] * 1e3:.1f} us), boards/launch {rf['boards_per_launch']}, "
+              f"achieved {rf['achieved']} TFLOP/s algorithmic, {rf['mfma_achieved']} MFMA-executed; "
+              f"value {b['value']} games/s under the profiler")
+    except Exception as ex:  # noqa: BLE001
+        print(f"(bench_trace.json unreadable: {ex})")
+    print("\n## GPU occupancy over the last 0.5 s of the trace (profiles/busy.py)\n")
+    print("```")
+    print(subprocess.run([sys.executable, os.path.join(HERE, "busy.py"), tr, "0.5"],
+                         capture_output=True, text=True).stdout.rstrip())
+    print("```")
+    tj = os.path.join(HERE, "r1", "pmc_conv_traffic.json")
+    if os.path.exists(tj):
+        t = json.load(open(tj))
+        print("\n## HBM traffic per board (PMC, B = 4096, profiles/r1/pmc_conv_traffic.json)\n")
+        print("| kernel | HBM KB/board |")
+        print("|---|---:|")
+        for algo in ("winograd", "direct"):
+            for k, v in t.get(algo, {}).get("hbm_bytes_per_board", {}).items():
+                print(f"| `{k}` | {v / 1e3:.1f} |")
+    sq = glob.glob(f"{os.path.dirname(d)}/pmc_conv_4096_0/**/*counter_collection.csv", recursive=True)
+    if sq:
+        print("\n## SQ counters, Winograd conv kernels (az_forward, B = 4096)\n")
+        print("```")
+        print(subprocess.run([sys.executable, os.path.join(HERE, "pmc_summary.py"),
+                              f"{os.path.dirname(d)}/pmc_conv_4096_0", "wino"],
+                             capture_output=True, text=True).stdout.rstrip())
+        print("```")
 
 
 if __name__ == "__main__":
