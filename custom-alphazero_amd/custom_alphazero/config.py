@@ -22,6 +22,8 @@ class ConfigSelfPlay:
     games_per_call = 4096        # games per play() call (reference: cpu_count()-1)
     concurrent_games = 4096      # device slots (trees in flight)
     base_seed = None             # None -> time-based like self_play.py:45
+    cache_log2 = 22              # device plays_inferences entries (2^k); 0 = no cache
+    lanes = 0                    # slot groups on separate HIP streams (0 = auto)
 
 
 class ConfigChess:

@@ -69,6 +69,12 @@ class GameRecord:
 
 
 _ENGINES = {}
+# The device transposition cache stands for the caller's plays_inferences
+# dict (mcts.py:122-143): it lives as long as the same dict object is passed
+# (self_play.__main__ keeps one across play() calls) and is emptied when a
+# different dict arrives (utils.reset_plays_inferences_dict, self_play.py:
+# 145-146) or the weights change (az_engine_set_weights clears it).
+_CACHE_OWNER = {"dict": None}
 
 
 def _batched_engine(model, n_slots):
@@ -76,7 +82,7 @@ def _batched_engine(model, n_slots):
     synthetic = isinstance(model, SyntheticEvaluator)
     key = (c.board_height, c.board_width, c.n, c.gravity, ConfigSelfPlay.mcts_iterations, n_slots,
            synthetic, ConfigMCTS.index_move_greedy, ConfigMCTS.exploration_constant,
-           ConfigModel.depth)
+           ConfigModel.depth, ConfigSelfPlay.cache_log2, ConfigSelfPlay.lanes)
     eng = _ENGINES.get(key)
     if eng is None:
         eng = az.Engine(c.board_height, c.board_width, c.n, c.gravity,
@@ -85,11 +91,17 @@ def _batched_engine(model, n_slots):
                         index_move_greedy=ConfigMCTS.index_move_greedy,
                         exploration_constant=ConfigMCTS.exploration_constant,
                         filters=ConfigModel.filters, depth=ConfigModel.depth,
-                        value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon)
+                        value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon,
+                        cache_log2=ConfigSelfPlay.cache_log2, lanes=ConfigSelfPlay.lanes)
+        eng.weights_key = None
         _ENGINES.clear()
         _ENGINES[key] = eng
+        _CACHE_OWNER["dict"] = None
     if not synthetic:
-        eng.set_weights(model.engine_weights())
+        wkey = (id(model), getattr(model, "_version", None))
+        if eng.weights_key != wkey:  # new best model: upload (clears the cache)
+            eng.set_weights(model.engine_weights())
+            eng.weights_key = wkey
     return eng
 
 
@@ -107,6 +119,10 @@ def play(run_id: str, plays_inferences: Optional[Dict[str, Tuple[np.ndarray, flo
     if base_seed is None:
         base_seed = int(time.time()) % (2 ** 32 - 1)
     eng = _batched_engine(model, min(n_games, ConfigSelfPlay.concurrent_games))
+    if ConfigSelfPlay.cache_log2 and (plays_inferences is None
+                                      or plays_inferences is not _CACHE_OWNER["dict"]):
+        eng.cache_clear()
+        _CACHE_OWNER["dict"] = plays_inferences
     eng.selfplay_run(first_game, n_games, base_seed)
     r = eng.selfplay_results()
     states, policies, rewards, records = [], [], [], []

@@ -74,6 +74,26 @@ def test_batched_play_matches_reference(golden, game_cfg):
     assert [r.expansions for r in records] == z["expansions"].tolist()
 
 
+def test_batched_play_cache_follows_plays_inferences(golden, game_cfg):
+    """The device cache is the caller's plays_inferences: kept across calls
+    with the same dict (hits on the second call), emptied for a new dict;
+    results identical either way (self_play.py:145-146, mcts.py:122-143)."""
+    z = golden("mcts_c4_s25")
+    game_cfg(z)
+    shared = {}
+    hits = []  # per call (az_selfplay_begin resets the counters)
+    outs = []
+    for d in (shared, shared, {}):
+        outs.append(self_play.play("test-run", d, model=SyntheticEvaluator(), n_games=16, base_seed=0))
+        hits.append(next(iter(self_play._ENGINES.values())).stats()["cache_hits"])
+    for out in outs[1:]:
+        np.testing.assert_array_equal(out[0], outs[0][0])
+        np.testing.assert_array_equal(out[1].view(np.uint64), outs[0][1].view(np.uint64))
+    # same dict: the replayed games find their boards already cached; a fresh
+    # dict starts empty again
+    assert hits[1] > hits[0] and hits[2] == hits[0]
+
+
 def test_mcts_deterministic_play_is_argmax(game_cfg, golden):
     game_cfg(golden("mcts_c4_s25"))
     m = MCTS(Board(), Board.get_all_possible_moves(), False, {}, model=SyntheticEvaluator())
