@@ -244,9 +244,14 @@ def main():
                     "mfma_frac": round(iso * mfma_flop_per_board / conv_flop_per_board
                                        / FP32_MFMA_PEAK_TFLOPS, 4)}
 
+    game_name = "Connect-4 6x7" if (args.height, args.width, args.n) == (6, 7, 4) else \
+        f"Connect-{args.n} {args.height}x{args.width}"
+    cfg_ref = {(6, 7, 4, 100): "BASELINE.json configs[1]", (9, 9, 5, 200): "BASELINE.json configs[2]",
+               (6, 7, 4, 400): "BASELINE.json configs[3], per-GPU shard"}.get(
+        (args.height, args.width, args.n, args.sims), "custom")
     if rank == 0:
         line = {
-            "metric": "self-play games/s (Connect-4 6x7, 100 sims/move)",
+            "metric": f"self-play games/s ({game_name}, {args.sims} sims/move)",
             "value": round(d["games_done"] / elapsed, 3),
             "unit": "games/s",
             "n_gpus": world,
@@ -259,9 +264,9 @@ def main():
             "dtype": "fp32 network / f64 PUCT",
             "data": "synthetic (self-generated games, random-init Keras-default weights, torch seed 0)",
             "config": {
-                "workload": (f"Connect-4 {args.height}x{args.width} n={args.n} gravity, {args.sims} sims/move, "
+                "workload": (f"{game_name} n={args.n} gravity, {args.sims} sims/move, "
                              f"{args.slots} concurrent games per GPU, 128f x {args.depth}-block net "
-                             "(BASELINE.json configs[1])"),
+                             f"({cfg_ref})"),
                 "global_batch": args.slots * world,
                 "parallelism": f"games sharded over {world} GPU(s)",
             },

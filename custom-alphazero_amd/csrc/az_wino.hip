@@ -49,6 +49,13 @@ __host__ __device__ constexpr int wino_sign(int a, int i) {
 #ifndef AZ_WINO_BRING
 #define AZ_WINO_BRING 2  // B register ring (prefetch distance RB/2)
 #endif
+#ifndef AZ_WINO_SGB
+#define AZ_WINO_SGB 0  // explicit per-stage instruction order (measured -3%: off)
+#endif
+#ifndef AZ_WINO_DIAG
+#define AZ_WINO_DIAG 0  // timing experiments only (wrong outputs): 1 no B stream,
+                        // 2 no producer after chunk 0, 3 no output-transform adds
+#endif
 #ifndef AZ_WINO_CORNER
 #define AZ_WINO_CORNER 0
 #endif
@@ -219,6 +226,7 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
   static_assert(NX % RB == 0, "ring slot must be static per stage");
   const unsigned blane = (unsigned)(wave * 64 * QB + lane);
   auto load_b = [&](int c, int xi, float4 (&dst)[QB]) {
+    if (AZ_WINO_DIAG == 1 && (c > 0 || xi > 1)) return;
     const bool res = RESIDUAL && xi >= 16;
     const float4* base = res ? rpack : upack;
     const unsigned o = blane + (unsigned)(res ? c * 4 * 64 * QB : (c * 16 + xi) * 4 * 64 * QB);
@@ -231,6 +239,10 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
     for (int q = 0; q < QB; ++q) dst[q] = vrow[vswz<CK>(QB * h + q, r)];
   };
   auto scatter = [&](int xi, const f32x16& m) {
+    if (AZ_WINO_DIAG == 3) {
+      Y[xi & 3] += m;
+      return;
+    }
     const int a = xi >> 2, bb = xi & 3;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -308,11 +320,27 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
         pend = -1;
       }
       if (direct < 0) pend = xi;
+#if AZ_WINO_SGB
+      // stage order: the next stage's B (global) and A (LDS) loads first, so
+      // their latency hides behind this stage's MFMAs; then MFMAs with the
+      // pending point's adds spread between them (two MFMAs first: the adds
+      // read the previous stage's last MFMA result)
+      __builtin_amdgcn_sched_group_barrier(0x020, QB, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, QB, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#pragma unroll
+      for (int k = 2; k < KS; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+#endif
     }
     __builtin_amdgcn_sched_barrier(0);
     if (pend >= 0) scatter(pend, M[pend & 1]);
     if (c + 1 < NCH) {
-      if constexpr (PIPE) {
+      if (AZ_WINO_DIAG == 2) {
+        __syncthreads();
+      } else if constexpr (PIPE) {
         // the other buffer was last read in chunk c-1, before the previous
         // barrier: safe to overwrite now
         produce_store(P, vbuf_all + ((c + 1) & 1) * VB);
