@@ -89,11 +89,26 @@ void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* ma
 #define AZ_WINO_CK 32
 #endif
 constexpr int kWinoCK = AZ_WINO_CK;
+#ifndef AZ_WINO_PIPE
+#define AZ_WINO_PIPE 1  // default pipeline (launch_wino_conv); 1 falls back to 0 at CK 32
+#endif
 size_t wino_pack_index(int xi, int cin, int cout);
 int wino_fold_sign(int xi);
+// The heads' 1x1 convolutions (policy F->2, value F->1, each + folded BN +
+// ReLU, model.py:68-149), fused into the last block's conv2 epilogue: feat =
+// [boards][HW] float4 (policy ch 0, policy ch 1, value, 0); the block output
+// itself is then never written.
+struct HeadConv {
+  const float* wpc;  // [F][2]
+  const float* bpc;  // [2]
+  const float* wvc;  // [F]
+  const float* bvc;  // [1]
+  float4* feat;      // null: write the block output instead
+};
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
-                      int n_max, int H, int W, hipStream_t s, int pipe);
+                      int n_max, int H, int W, hipStream_t s, int pipe,
+                      const HeadConv* heads = nullptr);
 // x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,

@@ -23,6 +23,10 @@
 
 #include "az_nn.h"
 
+#ifndef AZ_FUSE_HEADS
+#define AZ_FUSE_HEADS 1
+#endif
+
 namespace az {
 
 // ------------------------------------------------------------------ encode
@@ -329,7 +333,9 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-template <int F>
+// FEAT: the 1x1 head convs already ran in the last conv's epilogue (feat =
+// [boards][HW] float4 from wino_conv_kernel<.., HEADS>); same fmaf chains.
+template <int F, bool FEAT>
 __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ act, HeadWeights hw,
                                                     const int* __restrict__ count, int n_static,
                                                     int HW, int A, int hidden,
@@ -342,8 +348,17 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + wave;
   if (b >= n) return;  // wave-uniform; no block barrier below
+  if constexpr (FEAT) {
+    const float4* feat = reinterpret_cast<const float4*>(act) + (size_t)b * HW;
+    for (int p = lane; p < HW; p += 64) {
+      const float4 f = feat[p];
+      pflat[wave][2 * p] = f.x;
+      pflat[wave][2 * p + 1] = f.y;
+      vflat[wave][p] = f.z;
+    }
+  }
   const float* base = act + (size_t)b * HW * F;
-  for (int p = lane; p < HW; p += 64) {
+  for (int p = lane; p < HW && !FEAT; p += 64) {
     const float4* row = reinterpret_cast<const float4*>(base + (size_t)p * F);
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll 8
@@ -353,9 +368,9 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int c = 4 * q + e;
-        s0 += vv[e] * hw.wpc[2 * c];
-        s1 += vv[e] * hw.wpc[2 * c + 1];
-        s2 += vv[e] * hw.wvc[c];
+        s0 = fmaf(vv[e], hw.wpc[2 * c], s0);
+        s1 = fmaf(vv[e], hw.wpc[2 * c + 1], s1);
+        s2 = fmaf(vv[e], hw.wvc[c], s2);
       }
     }
     pflat[wave][2 * p] = fmaxf(s0 + hw.bpc[0], 0.f);
@@ -428,6 +443,7 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   }();
   const int variant = env_variant >= 0 ? env_variant : (net.algo == 0 ? 0 : 6);
   const int rows = n_max * HW;
+  bool fused_heads = false;
   if (timer) timer->begin(s);
   for (int d = 0; d < net.depth; ++d) {
     const float4* w1 = reinterpret_cast<const float4*>(net.c1_w[d]);
@@ -444,13 +460,20 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
                                                                 count, n_max, H, W);            \
   }
     switch (variant) {
-      case 0:  // Winograd F(2x2,3x3) (az_wino.hip)
-      case 7:  // same, single V buffer (PIPE 0)
-        launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s,
-                         variant == 0);
-        launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s,
-                         variant == 0);
+      case 0:  // Winograd F(2x2,3x3) (az_wino.hip), default pipeline
+      case 7:  // single V buffer
+      case 8:  // warp-specialised producer
+      case 9:  // double buffer + register prefetch
+      {
+        const int pipe = variant == 0 ? AZ_WINO_PIPE : variant == 7 ? 0 : variant == 8 ? 2 : 1;
+        launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s, pipe);
+        // last block: the head 1x1 convs run in conv2's epilogue, features into nxt
+        HeadConv hc{net.pc_w, net.pc_b, net.vc_w, net.vc_b,
+                    d == net.depth - 1 && AZ_FUSE_HEADS ? reinterpret_cast<float4*>(nxt) : nullptr};
+        launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, pipe, &hc);
+        fused_heads = hc.feat != nullptr;
         break;
+      }
       case 1: AZ_CONV_PAIR(false, true, 2, 0, 2, 1); break;   // 64 rows: waves 2x2, 1x2 tiles
       case 2: AZ_CONV_PAIR(false, true, 2, 0, 1, 2); break;   // 64 rows: each wave 2x1 tiles
       case 3: AZ_CONV_PAIR(false, false, 2, 0, 1, 4); break;  // 128 rows: each wave 4x1 tiles
@@ -466,8 +489,12 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   if (timer) timer->end(s, 2 * net.depth);
   HeadWeights hw{net.pc_w, net.pc_b, net.vc_w, net.vc_b, net.pd_w,
                  net.pd_b, net.v1_w, net.v1_b, net.v2_w, net.v2_b};
-  heads_kernel<F><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A, net.hidden, probs,
-                                                 values);
+  if (fused_heads)
+    heads_kernel<F, true><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A, net.hidden, probs,
+                                                        values);
+  else
+    heads_kernel<F, false><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A, net.hidden, probs,
+                                                         values);
 }
 
 }  // namespace az

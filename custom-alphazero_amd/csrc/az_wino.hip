@@ -52,6 +52,9 @@ __host__ __device__ constexpr int wino_sign(int a, int i) {
 #ifndef AZ_WINO_SGB
 #define AZ_WINO_SGB 0  // explicit per-stage instruction order (measured -3%: off)
 #endif
+#ifndef AZ_WINO_STAGE_BARRIER
+#define AZ_WINO_STAGE_BARRIER 1  // sched_barrier between point stages
+#endif
 #ifndef AZ_WINO_DIAG
 #define AZ_WINO_DIAG 0  // timing experiments only (wrong outputs): 1 no B stream,
                         // 2 no producer after chunk 0, 3 no output-transform adds
@@ -74,16 +77,19 @@ __device__ __forceinline__ int vswz(int j, int t) {
   return j ^ ((t / RPB) & (RC - 1));
 }
 
+// PIPE 2: warp-specialised: a fifth wave produces chunk c+1 into the other V
+//         buffer while the four MFMA waves consume chunk c; one barrier per
+//         chunk and no producer work on the MFMA waves.
 // PIPE 0: one V buffer, chunk c+1 loaded+transformed between two barriers.
 // PIPE 1: two V buffers; chunk c+1's patch loads are issued a whole chunk
 //         early into registers and transformed after chunk c's MFMAs: one
 //         barrier per chunk, no exposed global latency (LDS permitting).
-template <bool RESIDUAL, int CK, int PIPE>
-__global__ __launch_bounds__(256, 2) void wino_conv_kernel(
+template <bool RESIDUAL, int CK, int PIPE, bool HEADS = false>
+__global__ __launch_bounds__(PIPE == 2 ? 320 : 256, 2) void wino_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
-    int n_static, int H, int W) {
+    int n_static, int H, int W, HeadConv hc) {
   static_assert(CK == 16 || CK == 32, "chunk of 16 or 32 input channels");
   constexpr int NX = RESIDUAL ? 20 : 16;   // 16 Winograd points (+4 residual pixel rows)
   constexpr int RC = CK / 4;               // float4 per V row
@@ -93,6 +99,7 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
   constexpr int QB = CK / 8;               // float4 of B (and of A) per lane per stage
   constexpr int IPT = 16 * CK / 256;       // producer items per thread (tile, c4, half)
   __shared__ float4 vbuf_all[(PIPE ? 2 : 1) * VB];
+  constexpr bool WS = PIPE == 2;
 
   const int HW = H * W, TW = (W + 1) >> 1, TH = (H + 1) >> 1, TB = TH * TW;
   const int n_boards = count ? *count : n_static;
@@ -226,7 +233,7 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
   static_assert(NX % RB == 0, "ring slot must be static per stage");
   const unsigned blane = (unsigned)(wave * 64 * QB + lane);
   auto load_b = [&](int c, int xi, float4 (&dst)[QB]) {
-    if (AZ_WINO_DIAG == 1 && (c > 0 || xi > 1)) return;
+    if ((AZ_WINO_DIAG == 1 || AZ_WINO_DIAG == 4) && (c > 0 || xi > 1)) return;
     const bool res = RESIDUAL && xi >= 16;
     const float4* base = res ? rpack : upack;
     const unsigned o = blane + (unsigned)(res ? c * 4 * 64 * QB : (c * 16 + xi) * 4 * 64 * QB);
@@ -239,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
     for (int q = 0; q < QB; ++q) dst[q] = vrow[vswz<CK>(QB * h + q, r)];
   };
   auto scatter = [&](int xi, const f32x16& m) {
-    if (AZ_WINO_DIAG == 3) {
+    if (AZ_WINO_DIAG == 3 || AZ_WINO_DIAG == 4) {
       Y[xi & 3] += m;
       return;
     }
@@ -263,13 +270,123 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
   float4 bq[RB][QB], aq[2][QB];
   f32x16 M[2];
 
+  // warp-specialised producer: wave 4 builds a whole chunk, two items
+  // (tile, 4 channels, half) per lane at a time
+  struct Patch2 {
+    float4 d[2][3][4];
+    float4 rr[2][2];
+    uint32_t ok[2];
+  };
+  auto ws_produce = [&](int c, float4* vbuf) {
+    constexpr int ITEMS = 16 * CK;  // per chunk
+#pragma unroll 1
+    for (int i0 = lane; i0 < ITEMS; i0 += 128) {
+      Patch2 Q;
+      int qt[2], qc[2], qh[2];
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int item = i0 + 64 * g;
+        qh[g] = item & 1;
+        qc[g] = (item >> 1) & (RC - 1);
+        qt[g] = item / (2 * RC);
+        const int tau = t0 + qt[g];
+        const bool v = tau < tiles;
+        int b = 0, ty = 0, tx = 0;
+        if (v) {
+          b = tau / TB;
+          const int lt = tau - b * TB;
+          ty = lt / TW;
+          tx = lt - ty * TW;
+        }
+        const int base = b * HW * 128 + qc[g] * 4 + c * CK;
+        Q.ok[g] = 0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const int y = 2 * ty - 1 + qh[g] + r;
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const int xx = 2 * tx - 1 + x;
+            const bool ok = v && y >= 0 && y < H && xx >= 0 && xx < W;
+            Q.d[g][r][x] = *reinterpret_cast<const float4*>(in + (ok ? (unsigned)(base + (y * W + xx) * 128) : 0u));
+            Q.ok[g] |= (uint32_t)ok << (r * 4 + x);
+          }
+        }
+        if constexpr (RESIDUAL) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int pp = 2 * qh[g] + k;
+            const int y = 2 * ty + (pp >> 1), xx = 2 * tx + (pp & 1);
+            const bool ok = v && y < H && xx < W;
+            Q.rr[g][k] = *reinterpret_cast<const float4*>(res_in + (ok ? (unsigned)(base + (y * W + xx) * 128) : 0u));
+            Q.ok[g] |= (uint32_t)ok << (12 + k);
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+            if (!((Q.ok[g] >> (r * 4 + x)) & 1)) Q.d[g][r][x] = z4;
+        float4 T[2][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const float4 a = Q.d[g][0][x], b = Q.d[g][1][x], e = Q.d[g][2][x];
+          if (qh[g] == 0) {
+            T[0][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
+            T[1][x] = make_float4(b.x + e.x, b.y + e.y, b.z + e.z, b.w + e.w);
+          } else {
+            T[0][x] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
+            T[1][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
+          }
+        }
+        const int sw = vswz<CK>(qc[g], qt[g]);
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const int i = 2 * qh[g] + ii;
+          const float4 t0_ = T[ii][0], t1 = T[ii][1], t2 = T[ii][2], t3 = T[ii][3];
+          const float4 vv[4] = {
+              make_float4(t0_.x - t2.x, t0_.y - t2.y, t0_.z - t2.z, t0_.w - t2.w),
+              make_float4(t1.x + t2.x, t1.y + t2.y, t1.z + t2.z, t1.w + t2.w),
+              make_float4(t2.x - t1.x, t2.y - t1.y, t2.z - t1.z, t2.w - t1.w),
+              make_float4(t1.x - t3.x, t1.y - t3.y, t1.z - t3.z, t1.w - t3.w)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vbuf[((i * 4 + j) * kWinoTiles + qt[g]) * RC + sw] = vv[j];
+        }
+        if constexpr (RESIDUAL) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const float4 rv = ((Q.ok[g] >> (12 + k)) & 1) ? Q.rr[g][k] : z4;
+            vbuf[((16 + 2 * qh[g] + k) * kWinoTiles + qt[g]) * RC + sw] = rv;
+          }
+        }
+      }
+    }
+  };
+
+  if constexpr (WS) {
+    if (wave == 4) {
+      ws_produce(0, vbuf_all);
+      __syncthreads();
+#pragma unroll 1
+      for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) ws_produce(c + 1, vbuf_all + ((c + 1) & 1) * VB);
+        __syncthreads();
+      }
+      return;  // the producer wave has no outputs
+    }
+  }
+
   Patch P;
-  produce_load(0, P);
-  produce_store(P, vbuf_all);
-  if (PIPE) produce_load(1, P);
+  if constexpr (!WS) {
+    produce_load(0, P);
+    produce_store(P, vbuf_all);
+    if (PIPE) produce_load(1, P);
+  }
 #pragma unroll
   for (int k = 0; k < DIST; ++k) load_b(0, k, bq[k]);
-  __syncthreads();
+  __syncthreads();  // (WS: pairs with the producer's first barrier)
 
   // the chunk loop stays rolled: one copy of the 16-20 unrolled stages is
   // already ~10 KB of code (unrolling it tripled the body and ran 15% slower)
@@ -283,7 +400,7 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
       // one software-pipeline stage per point: the scheduler may interleave
       // inside a stage (MFMAs of xi with the adds of the pending point and
       // the next stage's loads) but not across
-      __builtin_amdgcn_sched_barrier(0);
+      if (AZ_WINO_STAGE_BARRIER) __builtin_amdgcn_sched_barrier(0);
       {
         const int nx = xi + DIST;
         if (nx < NX) {
@@ -337,8 +454,12 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
     }
     __builtin_amdgcn_sched_barrier(0);
     if (pend >= 0) scatter(pend, M[pend & 1]);
+    if constexpr (WS) {
+      __syncthreads();  // chunk c+1 is in the other buffer; chunk c's is free
+      continue;
+    }
     if (c + 1 < NCH) {
-      if (AZ_WINO_DIAG == 2) {
+      if (AZ_WINO_DIAG == 2 || AZ_WINO_DIAG == 4) {
         __syncthreads();
       } else if constexpr (PIPE) {
         // the other buffer was last read in chunk c-1, before the previous
@@ -359,6 +480,43 @@ __global__ __launch_bounds__(256, 2) void wino_conv_kernel(
   // C/D map: column = lane & 31, tile row = (i & 3) + 8*(i >> 2) + 4*h
   const int col = wave * 32 + r;
   const float bcol = bias[col];
+  if constexpr (HEADS) {
+    // fused head 1x1 convs: the block output goes through LDS (transposed to
+    // [tile pixel][channel], row pitch 129 floats: conflict-free both ways)
+    // and thread tp sums its pixel's 128 channels in channel order -- the
+    // same fmaf chains as heads_kernel on the stored output
+    static_assert(RESIDUAL && PIPE == 0, "heads fuse into the single-buffered conv2");
+    static_assert(128 * 129 * 4 <= VB * 16, "transpose buffer fits the V buffer");
+    float* tb = reinterpret_cast<float*>(vbuf_all);
+    __syncthreads();  // every wave is done with the last chunk's V
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int tau = t0 + (tid >> 2), p = tid & 3;
+      if (tau < tiles) {
+        const int b = tau / TB, lt = tau - b * TB;
+        const int ty = lt / TW, tx = lt - ty * TW;
+        const int y = 2 * ty + (p >> 1), x = 2 * tx + (p & 1);
+        if (y < H && x < W) {
+          const float* v = tb + tid * 129;
+          float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+          for (int c = 0; c < 128; ++c) {
+            s0 = fmaf(v[c], hc.wpc[2 * c], s0);
+            s1 = fmaf(v[c], hc.wpc[2 * c + 1], s1);
+            s2 = fmaf(v[c], hc.wvc[c], s2);
+          }
+          hc.feat[b * HW + y * W + x] = make_float4(fmaxf(s0 + hc.bpc[0], 0.f), fmaxf(s1 + hc.bpc[1], 0.f),
+                                                    fmaxf(s2 + hc.bvc[0], 0.f), 0.f);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int tau = t0 + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -392,26 +550,38 @@ int wino_fold_sign(int xi) {
 
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
-                      int n_max, int H, int W, hipStream_t s, int pipe) {
+                      int n_max, int H, int W, hipStream_t s, int pipe, const HeadConv* heads) {
   const int TB = ((H + 1) / 2) * ((W + 1) / 2);
   const int grid = (n_max * TB + kWinoTiles - 1) / kWinoTiles;
   if (grid <= 0) return;
   const float4* u = reinterpret_cast<const float4*>(upack);
   const float4* rp = reinterpret_cast<const float4*>(rpack);
   constexpr int CK = kWinoCK;
-  // PIPE 1 needs two V buffers: at CK = 32 they would leave one workgroup per
-  // CU, so CK = 32 always runs single-buffered
-  constexpr int P1 = CK == 16 ? 1 : 0;
-  if (pipe) {
+  HeadConv hc{};
+  if (heads && heads->feat) {
+    hc = *heads;
+    wino_conv_kernel<true, CK, 0, true><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
+    return;
+  }
+  // pipe: 0 = single V buffer, 1 = double buffer + register prefetch (CK 16
+  // only: at CK 32 the buffers would leave one workgroup per CU), 2 = warp-
+  // specialised producer wave (double buffer)
+  if (pipe == 2) {
     if (res_in)
-      wino_conv_kernel<true, CK, P1><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W);
+      wino_conv_kernel<true, CK, 2><<<grid, 320, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
     else
-      wino_conv_kernel<false, CK, P1><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W);
+      wino_conv_kernel<false, CK, 2><<<grid, 320, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
+  } else if (CK == 16 && pipe == 1) {
+    constexpr int P1 = CK == 16 ? 1 : 0;  // (no double-buffered instantiation at CK 32)
+    if (res_in)
+      wino_conv_kernel<true, CK, P1><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
+    else
+      wino_conv_kernel<false, CK, P1><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
   } else {
     if (res_in)
-      wino_conv_kernel<true, CK, 0><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W);
+      wino_conv_kernel<true, CK, 0><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
     else
-      wino_conv_kernel<false, CK, 0><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W);
+      wino_conv_kernel<false, CK, 0><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
   }
 }
 

@@ -15,7 +15,7 @@ def per_kernel(d, name):
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if r["Counter_Name"] != name or ("conv" not in k):
+            if r["Counter_Name"] != name or "conv" not in k or "stem" in k:
                 continue
             k = k.split("(")[0].replace("void ", "")
             acc.setdefault(k, []).append(float(r["Counter_Value"]))

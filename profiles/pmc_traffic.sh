@@ -18,4 +18,5 @@ for algo in 0 1; do
 done
 cd $R
 python3 profiles/pmc_traffic.py $OUT $B > profiles/r1/pmc_conv_traffic.json
+cp profiles/r1/pmc_conv_traffic.json $OUT/  # gpurun only brings gpurun_out/ back
 cat profiles/r1/pmc_conv_traffic.json
