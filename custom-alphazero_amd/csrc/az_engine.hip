@@ -140,9 +140,14 @@ int simulate(az_engine* e, Lane& L) {
     n_rows = L.t.nn_count;
   }
   if (e->cfg.evaluator == AZ_EVAL_NETWORK) {
-    az::launch_encode(rows, n_rows, L.n, L.g.HW, L.x, s);
+    static const bool stem_boards = [] {  // AZ_STEM_BOARDS=0: encode + float stem (A/B)
+      const char* v = getenv("AZ_STEM_BOARDS");
+      return !v || atoi(v) != 0;
+    }();
+    if (!stem_boards) az::launch_encode(rows, n_rows, L.n, L.g.HW, L.x, s);
     az::launch_forward(e->net, L.x, n_rows, L.n, L.g.H, L.g.W, L.g.A, L.act[0], L.act[1], L.act[2],
-                       L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr);
+                       L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr,
+                       stem_boards ? rows : nullptr);
   } else {
     az::launch_synth_eval(L.g, rows, n_rows, L.probs, L.values, s);
   }

@@ -110,8 +110,10 @@ void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       int n_max, int H, int W, hipStream_t s, int pipe,
                       const HeadConv* heads = nullptr);
 // x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
+// boards (optional): one-hot input straight from the eval queue's boards
+// (bitwise the same outputs as encoding them into x first)
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
-                    hipStream_t s, ConvTimer* timer);
+                    hipStream_t s, ConvTimer* timer, const Board* boards = nullptr);
 
 }  // namespace az

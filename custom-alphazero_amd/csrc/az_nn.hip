@@ -96,6 +96,52 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
   *reinterpret_cast<float4*>(out + (size_t)r * F + cg * 4) = acc;
 }
 
+// Same layer straight from the boards (self-play): the input is one-hot, so
+// each in-board tap contributes w[tap][state] then w[tap][3] (the turn
+// plane) -- exactly the nonzero terms of stem_conv_kernel's fmaf chain in its
+// channel order (a zero term leaves the accumulator unchanged: it is never
+// -0), so outputs are bitwise those of encode + stem_conv.  Saves the encode
+// pass and the float4 input reads.
+template <int F>
+__global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict__ boards,
+                                                         const float* __restrict__ ws,
+                                                         const float* __restrict__ bias,
+                                                         const int* __restrict__ count, int n_static,
+                                                         int H, int W, float* __restrict__ out) {
+  constexpr int G4 = F / 4;
+  const int n = count ? *count : n_static;
+  const int HW = H * W;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * HW * G4) return;
+  const int r = idx / G4, cg = idx - r * G4;
+  const int b = r / HW, p = r - b * HW;
+  const int y = p / W, xx = p - y * W;
+  const Board bd = boards[b];
+  float4 acc = *reinterpret_cast<const float4*>(bias + cg * 4);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int ny = y + tap / 3 - 1, nx = xx + tap % 3 - 1;
+    if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
+    const int q = ny * W + nx;
+    const int st = bit(bd.own, q) ? 1 : (bit(bd.opp, q) ? 2 : 0);
+    const float4 w1 = *reinterpret_cast<const float4*>(ws + (tap * 4 + st) * F + cg * 4);
+    const float4 w3 = *reinterpret_cast<const float4*>(ws + (tap * 4 + 3) * F + cg * 4);
+    acc.x = fmaf(1.0f, w1.x, acc.x);
+    acc.y = fmaf(1.0f, w1.y, acc.y);
+    acc.z = fmaf(1.0f, w1.z, acc.z);
+    acc.w = fmaf(1.0f, w1.w, acc.w);
+    acc.x = fmaf(1.0f, w3.x, acc.x);
+    acc.y = fmaf(1.0f, w3.y, acc.y);
+    acc.z = fmaf(1.0f, w3.z, acc.z);
+    acc.w = fmaf(1.0f, w3.w, acc.w);
+  }
+  acc.x = fmaxf(acc.x, 0.0f);
+  acc.y = fmaxf(acc.y, 0.0f);
+  acc.z = fmaxf(acc.z, 0.0f);
+  acc.w = fmaxf(acc.w, 0.0f);
+  *reinterpret_cast<float4*>(out + (size_t)r * F + cg * 4) = acc;
+}
+
 // ------------------------------------------------------------ conv3x3 MFMA
 // out[r][n] = ReLU( sum_k A[r][k] * W[k][n] + bias[n] )
 //   k in [0, 9F): A = in[neighbour(r, tap)][c], tap = k / F, c = k % F
@@ -423,14 +469,18 @@ void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* ma
 
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
-                    hipStream_t s, ConvTimer* timer) {
+                    hipStream_t s, ConvTimer* timer, const Board* boards) {
   if (n_max <= 0) return;
   const int HW = H * W;
   constexpr int F = 128;
   {
     const int total = n_max * HW * (F / 4);
-    stem_conv_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(
-        reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
+    if (boards)
+      stem_board_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(boards, net.stem_w, net.stem_b, count,
+                                                               n_max, H, W, act_a);
+    else
+      stem_conv_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(
+          reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
   }
   float* cur = act_a;  // block input
   float* mid = act_b;
