@@ -9,6 +9,7 @@
   refilled as games end), replacing the reference's one-game-per-process
   joblib fan-out (self_play.py:98-110).  Game g is seeded MT19937(base_seed+g).
 """
+import json
 import os
 import time
 from dataclasses import dataclass
@@ -98,7 +99,9 @@ def _batched_engine(model, n_slots):
         _ENGINES[key] = eng
         _CACHE_OWNER["dict"] = None
     if not synthetic:
-        wkey = (id(model), getattr(model, "_version", None))
+        # content hash: play() reloads the best model from disk every call like
+        # the reference (utils.py:42-48); unchanged weights keep the cache
+        wkey = model.hash if hasattr(model, "hash") else (id(model), getattr(model, "_version", None))
         if eng.weights_key != wkey:  # new best model: upload (clears the cache)
             eng.set_weights(model.engine_weights())
             eng.weights_key = wkey
@@ -147,6 +150,48 @@ def exclude_null_games(states, policies, rewards):
     """self_play.py:155-162: drop samples of drawn games (reward 0)."""
     keep = rewards != 0
     return states[keep], policies[keep], rewards[keep]
+
+
+def queue_payload(states, policies, values) -> dict:
+    """The append_queue request body (serving/factory.py:69-80; schema
+    ModelAppendQueueInputs, serving/schemas/schemas.py:27-30)."""
+    return {"states": np.asarray(states).tolist(), "policies": np.asarray(policies).tolist(),
+            "values": np.asarray(values).tolist()}
+
+
+def write_queue_payload(path: str, states, policies, values) -> str:
+    """File sink for the queue payload (the HTTP control plane is out of scope)."""
+    with open(path, "w") as fp:
+        json.dump(queue_payload(states, policies, values), fp)
+    return path
+
+
+def run(run_id: str, iterations: int = 1, queue_sink=None, model_loader=None):
+    """self_play.__main__'s loop (self_play.py:128-185) without the HTTP
+    control plane: poll the best model's hash (utils.best_saved_model_hash),
+    reset plays_inferences when it changes, play a batch, drop draws
+    (ConfigSelfPlay.exclude_null_games), checkpoint samples.npz every
+    samples_checkpoint_frequency iterations, and hand the append_queue payload
+    to `queue_sink` (a callable, e.g. list.append or an HTTP client).
+    Returns the per-iteration sample counts."""
+    from custom_alphazero.utils import best_saved_model_hash, reset_plays_inferences_dict
+    load = model_loader or best_saved_model
+    previous_hash, plays_inferences, model, counts = object(), None, None, []
+    for it in range(iterations):
+        current = best_saved_model_hash(run_id)
+        if current != previous_hash or model is None:
+            plays_inferences = reset_plays_inferences_dict()
+            model = load(run_id)
+            previous_hash = current
+        states, policies, rewards, _records = play(run_id, plays_inferences, model=model)
+        if ConfigSelfPlay.exclude_null_games:
+            states, policies, rewards = exclude_null_games(states, policies, rewards)
+        if (it + 1) % ConfigSelfPlay.samples_checkpoint_frequency == 0:
+            save_samples(run_id, it, states, policies, rewards)
+        if queue_sink is not None:
+            queue_sink(queue_payload(states, policies, rewards))
+        counts.append(len(states))
+    return counts
 
 
 def save_samples(run_id: str, iteration: int, states, policies, rewards) -> str:

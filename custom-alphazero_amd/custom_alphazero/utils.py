@@ -13,9 +13,9 @@ def set_gpu_index(gpu_index: Union[int, str]):
 
 def reset_plays_inferences_dict() -> dict:
     """The reference returns a Manager().dict() shared by its worker processes
-    (utils.py:38-39).  The device engine needs no host cache (the evaluator
-    is deterministic per board, so a cache never changes a search); a plain
-    dict keeps the call signature."""
+    (utils.py:38-39).  Here the cache lives on the device (self_play.play):
+    the returned dict is a token -- passing the same object to play() keeps
+    the device cache, a new one empties it."""
     return {}
 
 

@@ -68,3 +68,23 @@ def test_normalize_matches_reference(golden):
         assert (r.dtype == np.float64) == bool(is64)
         np.testing.assert_array_equal(np.asarray(r, np.float64).view(np.uint64),
                                       vout[:n].view(np.uint64))
+
+
+def test_queue_payload_matches_append_queue_schema(tmp_path):
+    """append_queue's JSON body (serving/factory.py:69-80): nested lists with
+    ModelAppendQueueInputs' shapes; round-trips to the same arrays."""
+    import json
+
+    from custom_alphazero import self_play
+    rng = np.random.RandomState(0)
+    states = rng.rand(3, 6, 7, 4).astype(np.float32)
+    policies = rng.rand(3, 7)
+    values = np.array([1, -1, 1])
+    body = self_play.queue_payload(states, policies, values)
+    assert set(body) == {"states", "policies", "values"}
+    assert len(body["states"]) == 3 and len(body["states"][0]) == 6 and len(body["states"][0][0][0]) == 4
+    path = self_play.write_queue_payload(str(tmp_path / "q.json"), states, policies, values)
+    back = json.load(open(path))
+    np.testing.assert_array_equal(np.asarray(back["states"], np.float32), states)
+    np.testing.assert_array_equal(np.asarray(back["policies"]), policies)
+    np.testing.assert_array_equal(np.asarray(back["values"]), values)

@@ -146,3 +146,25 @@ def test_mcts_with_network_model_plays_legal_game(game_cfg, golden):
     assert len(states) == len(policies) == len(rewards) >= 7
     np.testing.assert_allclose(policies.sum(axis=1), 1.0)
     assert abs(int(rewards[-1])) in (0, 1)
+
+
+def test_self_play_run_loop(tmp_path, golden, game_cfg, monkeypatch):
+    """self_play.run = the reference __main__ loop: samples.npz checkpoints,
+    draws dropped, the queue payload handed to the sink, plays_inferences kept
+    while the best model's hash is unchanged."""
+    from custom_alphazero.config import ConfigPath
+    z = golden("mcts_c4_s25")
+    game_cfg(z)
+    monkeypatch.setattr(ConfigPath, "results_dir", str(tmp_path))
+    monkeypatch.setattr(ConfigSelfPlay, "games_per_call", 16)
+    monkeypatch.setattr(ConfigSelfPlay, "base_seed", 0)
+    sink = []
+    counts = self_play.run("run-x", iterations=2, queue_sink=sink.append,
+                           model_loader=lambda run_id: SyntheticEvaluator())
+    keep = z["reward"] != 0
+    assert counts == [int(keep.sum())] * 2
+    assert len(sink) == 2
+    np.testing.assert_array_equal(np.asarray(sink[0]["states"], np.float32), z["state"][keep])
+    saved = np.load(tmp_path / "connect_n" / "run-x" / ConfigPath.self_play_dir / "iteration_1" /
+                    ConfigPath.samples_file)
+    np.testing.assert_array_equal(saved["values"], z["reward"][keep])
