@@ -84,8 +84,11 @@ __device__ __forceinline__ int vswz(int j, int t) {
 // PIPE 1: two V buffers; chunk c+1's patch loads are issued a whole chunk
 //         early into registers and transformed after chunk c's MFMAs: one
 //         barrier per chunk, no exposed global latency (LDS permitting).
+#ifndef AZ_WINO_OCC
+#define AZ_WINO_OCC 2  // workgroups per CU the register budget is sized for
+#endif
 template <bool RESIDUAL, int CK, int PIPE, bool HEADS = false>
-__global__ __launch_bounds__(PIPE == 2 ? 320 : 256, 2) void wino_conv_kernel(
+__global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
@@ -486,32 +489,36 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, 2) void wino_conv_kernel(
     // and thread tp sums its pixel's 128 channels in channel order -- the
     // same fmaf chains as heads_kernel on the stored output
     static_assert(RESIDUAL && PIPE == 0, "heads fuse into the single-buffered conv2");
-    static_assert(128 * 129 * 4 <= VB * 16, "transpose buffer fits the V buffer");
+    static_assert(64 * 129 * 4 <= VB * 16, "half the transpose fits the V buffer");
     float* tb = reinterpret_cast<float*>(vbuf_all);
-    __syncthreads();  // every wave is done with the last chunk's V
+    // two passes of 16 tile rows (64 tile pixels) each
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    for (int half = 0; half < 2; ++half) {
+      __syncthreads();  // V (or the previous pass) no longer read
 #pragma unroll
-      for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
-    }
-    __syncthreads();
-    if (tid < 128) {
-      const int tau = t0 + (tid >> 2), p = tid & 3;
-      if (tau < tiles) {
-        const int b = tau / TB, lt = tau - b * TB;
-        const int ty = lt / TW, tx = lt - ty * TW;
-        const int y = 2 * ty + (p >> 1), x = 2 * tx + (p & 1);
-        if (y < H && x < W) {
-          const float* v = tb + tid * 129;
-          float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-          for (int c = 0; c < 128; ++c) {
-            s0 = fmaf(v[c], hc.wpc[2 * c], s0);
-            s1 = fmaf(v[c], hc.wpc[2 * c + 1], s1);
-            s2 = fmaf(v[c], hc.wvc[c], s2);
+      for (int i = 8 * half; i < 8 * half + 8; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h - 16 * half;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const int tau = t0 + 16 * half + (tid >> 2), p = tid & 3;
+        if (tau < tiles) {
+          const int b = tau / TB, lt = tau - b * TB;
+          const int ty = lt / TW, tx = lt - ty * TW;
+          const int y = 2 * ty + (p >> 1), x = 2 * tx + (p & 1);
+          if (y < H && x < W) {
+            const float* v = tb + tid * 129;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            for (int c = 0; c < 128; ++c) {
+              s0 = fmaf(v[c], hc.wpc[2 * c], s0);
+              s1 = fmaf(v[c], hc.wpc[2 * c + 1], s1);
+              s2 = fmaf(v[c], hc.wvc[c], s2);
+            }
+            hc.feat[b * HW + y * W + x] = make_float4(fmaxf(s0 + hc.bpc[0], 0.f), fmaxf(s1 + hc.bpc[1], 0.f),
+                                                      fmaxf(s2 + hc.bvc[0], 0.f), 0.f);
           }
-          hc.feat[b * HW + y * W + x] = make_float4(fmaxf(s0 + hc.bpc[0], 0.f), fmaxf(s1 + hc.bpc[1], 0.f),
-                                                    fmaxf(s2 + hc.bvc[0], 0.f), 0.f);
         }
       }
     }
