@@ -844,6 +844,18 @@ int az_tree_reset(az_engine* e, int n, const int32_t* slots, const int8_t* board
   return 0;
 }
 
+int az_tree_release(az_engine* e, int n, const int32_t* slots) {
+  if (!e || n < 0 || n > e->g.slots || (n && !slots)) return fail(AZ_E_INVALID, "bad arguments");
+  AZ_HIP(hipSetDevice(e->device));
+  for (int i = 0; i < n; ++i)
+    if (slots[i] < 0 || slots[i] >= e->g.slots) return fail(AZ_E_INVALID, "slot out of range");
+  AZ_HIP(hipMemcpyAsync(e->dev_i32, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+  az::launch_slot_release(e->t, e->dev_i32, n, e->stream);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
 int az_tree_search(az_engine* e, int n_sims) {
   if (!e || n_sims < 0) return fail(AZ_E_INVALID, "bad arguments");
   int rc;

@@ -116,6 +116,7 @@ void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const
                  int greedy_mode, int deterministic, int refill, hipStream_t s);
 void launch_slot_init(const GameCfg& g, const TreeDev& t, const SampleDev& smp, int64_t n_first,
                       hipStream_t s);
+void launch_slot_release(const TreeDev& t, const int32_t* slots, int n, hipStream_t s);
 void launch_slot_set_root(const GameCfg& g, const TreeDev& t, const int32_t* slots,
                           const Board* boards, int n, hipStream_t s);
 

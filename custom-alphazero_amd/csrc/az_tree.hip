@@ -515,6 +515,11 @@ __global__ void slot_set_root_kernel(GameCfg g, TreeDev t, const int32_t* slots,
   t.root_board[s] = boards[i];
 }
 
+__global__ void slot_release_kernel(TreeDev t, const int32_t* slots, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) t.game_id[slots[i]] = -1;
+}
+
 // ---------------------------------------------------------------- launchers
 static inline int blocks_for(int n) { return (n + 255) / 256; }
 // per-game kernels are latency-bound chains (one lane = one tree): 64-lane
@@ -569,6 +574,10 @@ void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const
 void launch_slot_init(const GameCfg& g, const TreeDev& t, const SampleDev& smp, int64_t n_first,
                       hipStream_t s) {
   slot_init_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, smp, n_first);
+}
+
+void launch_slot_release(const TreeDev& t, const int32_t* slots, int n, hipStream_t s) {
+  if (n > 0) slot_release_kernel<<<(n + 255) / 256, 256, 0, s>>>(t, slots, n);
 }
 
 void launch_slot_set_root(const GameCfg& g, const TreeDev& t, const int32_t* slots,

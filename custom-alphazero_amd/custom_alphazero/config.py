@@ -69,6 +69,12 @@ class ConfigModel:
     forward_batch = 1024          # az_forward chunk (device buffer rows)
 
 
+class ConfigServing:
+    evaluation_games_number = 150   # config.py:89
+    replace_min_score = 0.55        # config.py:90
+    evaluate_with_mcts = False      # config.py:92
+
+
 class ConfigPath:
     results_dir = "results"
     self_play_dir = "self_play"

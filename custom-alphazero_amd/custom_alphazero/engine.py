@@ -57,7 +57,7 @@ class Stats(ctypes.Structure):
 EXPORTED = (
     "az_abi_version", "az_last_error", "az_engine_create", "az_engine_destroy",
     "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
-    "az_selfplay_run", "az_selfplay_results", "az_tree_reset", "az_tree_search", "az_tree_play",
+    "az_selfplay_run", "az_selfplay_results", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
     "az_cache_clear", "az_cache_enable",
 )
@@ -96,6 +96,7 @@ def load_library():
         "az_selfplay_run": (ctypes.c_int, [P, I64, I64, ctypes.c_uint32, ctypes.POINTER(Stats)]),
         "az_selfplay_results": (ctypes.c_int, [P, P, P, P, P, P, P]),
         "az_tree_reset": (ctypes.c_int, [P, ctypes.c_int, P, P]),
+        "az_tree_release": (ctypes.c_int, [P, ctypes.c_int, P]),
         "az_tree_search": (ctypes.c_int, [P, ctypes.c_int]),
         "az_tree_play": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, P, P, P]),
         "az_tree_info": (ctypes.c_int, [P, ctypes.c_int, P, P]),
@@ -237,6 +238,10 @@ class Engine:
         slots = np.ascontiguousarray(slots, np.int32)
         b = np.ascontiguousarray(boards, np.int8).reshape(len(slots), self.height, self.width)
         _check(self._L.az_tree_reset(self._h, len(slots), _ptr(slots), _ptr(b)))
+
+    def tree_release(self, slots):
+        slots = np.ascontiguousarray(slots, np.int32)
+        _check(self._L.az_tree_release(self._h, len(slots), _ptr(slots)))
 
     def tree_search(self, n_sims):
         _check(self._L.az_tree_search(self._h, int(n_sims)))

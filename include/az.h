@@ -131,6 +131,10 @@ int az_selfplay_results(az_engine* eng, int32_t* lengths, int32_t* results, int3
 
 /* MCTS tree API (mcts/mcts.py:88-222) over the engine's slots. */
 int az_tree_reset(az_engine* eng, int n, const int32_t* slots, const int8_t* boards);
+/* Idle the given slots (search and play skip them) until the next reset:
+ * an arena's per-move MCTS objects (evaluation/evaluate.py:64-83) use one
+ * engine per model and hand each game to the engine whose model moves. */
+int az_tree_release(az_engine* eng, int n, const int32_t* slots);
 int az_tree_search(az_engine* eng, int n_sims);
 /* MCTS.play(greedy, deterministic) (mcts.py:182-222) on every active slot:
  * uniforms [slots] are the np.random.random_sample draws np.random.choice
