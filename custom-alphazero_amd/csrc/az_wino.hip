@@ -35,7 +35,12 @@ namespace az {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kWinoTiles = 32;  // tiles per workgroup (MFMA M)
+#ifndef AZ_WINO_MB
+#define AZ_WINO_MB 1  // MFMA M blocks (32 tiles each) per workgroup
+#endif
+constexpr int kWinoMB = AZ_WINO_MB;
+constexpr int kWinoTiles = 32 * kWinoMB;  // tiles per workgroup
+constexpr int kWinoThreads = 256 * kWinoMB;
 
 // A^T = [[1,1,1,0],[0,1,-1,-1]]: sign with which point coordinate a feeds
 // output coordinate i (0 = not at all)
@@ -88,7 +93,7 @@ __device__ __forceinline__ int vswz(int j, int t) {
 #define AZ_WINO_OCC 2  // workgroups per CU the register budget is sized for
 #endif
 template <bool RESIDUAL, int CK, int PIPE, bool HEADS = false>
-__global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_kernel(
+__global__ __launch_bounds__(PIPE == 2 ? 320 : kWinoThreads, AZ_WINO_OCC / kWinoMB) void wino_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_
   bool pvalid[IPT];
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
-    const int item = tid + 256 * it;
+    const int item = tid + kWinoThreads * it;
     ph[it] = item & 1;
     pc[it] = (item >> 1) & (RC - 1);
     pt[it] = item / (2 * RC);
@@ -222,7 +227,11 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_
   };
 
   // ---- consumer geometry: lane -> tile row r, k half h; wave -> columns
+  // wave -> (M block mb, 32 output channels nbw): the M blocks' waves read
+  // the same B fragments at about the same time (one L2 fetch, L1 hits)
   const int r = lane & 31, h = lane >> 5;
+  const int mb = wave >> 2, nbw = wave & 3;
+  const int vr = mb * 32 + r;  // this lane's tile row in the workgroup
   f32x16 Y[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p)
@@ -234,7 +243,7 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_
   // static per stage).  32-bit offsets from the uniform base.
   constexpr int RB = AZ_WINO_BRING, DIST = RB / 2;
   static_assert(NX % RB == 0, "ring slot must be static per stage");
-  const unsigned blane = (unsigned)(wave * 64 * QB + lane);
+  const unsigned blane = (unsigned)(nbw * 64 * QB + lane);
   auto load_b = [&](int c, int xi, float4 (&dst)[QB]) {
     if ((AZ_WINO_DIAG == 1 || AZ_WINO_DIAG == 4) && (c > 0 || xi > 1)) return;
     const bool res = RESIDUAL && xi >= 16;
@@ -244,9 +253,9 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_
     for (int q = 0; q < QB; ++q) dst[q] = base[o + q * 64];
   };
   auto load_a = [&](const float4* vbuf, int xi, float4 (&dst)[QB]) {
-    const float4* vrow = vbuf + (xi * kWinoTiles + r) * RC;
+    const float4* vrow = vbuf + (xi * kWinoTiles + vr) * RC;
 #pragma unroll
-    for (int q = 0; q < QB; ++q) dst[q] = vrow[vswz<CK>(QB * h + q, r)];
+    for (int q = 0; q < QB; ++q) dst[q] = vrow[vswz<CK>(QB * h + q, vr)];
   };
   auto scatter = [&](int xi, const f32x16& m) {
     if (AZ_WINO_DIAG == 3 || AZ_WINO_DIAG == 4) {
@@ -481,7 +490,7 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_
 
   // ---- epilogue: bias (+ residual bias, folded on the host), ReLU, store
   // C/D map: column = lane & 31, tile row = (i & 3) + 8*(i >> 2) + 4*h
-  const int col = wave * 32 + r;
+  const int col = nbw * 32 + r;
   const float bcol = bias[col];
   if constexpr (HEADS) {
     // fused head 1x1 convs: the block output goes through LDS (transposed to
@@ -493,17 +502,20 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_
     float* tb = reinterpret_cast<float*>(vbuf_all);
     // two passes of 16 tile rows (64 tile pixels) each
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    for (int pass = 0; pass < 2 * kWinoMB; ++pass) {
+      const int half = pass & 1;
       __syncthreads();  // V (or the previous pass) no longer read
+      if (mb == (pass >> 1)) {
 #pragma unroll
-      for (int i = 8 * half; i < 8 * half + 8; ++i) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * h - 16 * half;
+        for (int i = 8 * half; i < 8 * half + 8; ++i) {
+          const int row = (i & 3) + 8 * (i >> 2) + 4 * h - 16 * half;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
+          for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
+        }
       }
       __syncthreads();
       if (tid < 64) {
-        const int tau = t0 + 16 * half + (tid >> 2), p = tid & 3;
+        const int tau = t0 + 16 * pass + (tid >> 2), p = tid & 3;
         if (tau < tiles) {
           const int b = tau / TB, lt = tau - b * TB;
           const int ty = lt / TW, tx = lt - ty * TW;
@@ -526,7 +538,7 @@ __global__ __launch_bounds__(PIPE == 2 ? 320 : 256, AZ_WINO_OCC) void wino_conv_
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int tau = t0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    const int tau = t0 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
     if (tau >= tiles) continue;
     const int b = tau / TB, lt = tau - b * TB;
     const int ty = lt / TW, tx = lt - ty * TW;
@@ -567,28 +579,32 @@ void launch_wino_conv(const float* in, const float* res_in, const float* upack,
   HeadConv hc{};
   if (heads && heads->feat) {
     hc = *heads;
-    wino_conv_kernel<true, CK, 0, true><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
+    wino_conv_kernel<true, CK, 0, true><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
     return;
   }
   // pipe: 0 = single V buffer, 1 = double buffer + register prefetch (CK 16
   // only: at CK 32 the buffers would leave one workgroup per CU), 2 = warp-
   // specialised producer wave (double buffer)
-  if (pipe == 2) {
-    if (res_in)
-      wino_conv_kernel<true, CK, 2><<<grid, 320, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
-    else
-      wino_conv_kernel<false, CK, 2><<<grid, 320, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
-  } else if (CK == 16 && pipe == 1) {
+  if constexpr (kWinoMB == 1) {  // the producer wave is wave 4: one M block only
+    if (pipe == 2) {
+      if (res_in)
+        wino_conv_kernel<true, CK, 2><<<grid, 320, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
+      else
+        wino_conv_kernel<false, CK, 2><<<grid, 320, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
+      return;
+    }
+  }
+  if (CK == 16 && pipe == 1) {
     constexpr int P1 = CK == 16 ? 1 : 0;  // (no double-buffered instantiation at CK 32)
     if (res_in)
-      wino_conv_kernel<true, CK, P1><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
+      wino_conv_kernel<true, CK, P1><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
     else
-      wino_conv_kernel<false, CK, P1><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
+      wino_conv_kernel<false, CK, P1><<<grid, kWinoThreads, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
   } else {
     if (res_in)
-      wino_conv_kernel<true, CK, 0><<<grid, 256, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
+      wino_conv_kernel<true, CK, 0><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
     else
-      wino_conv_kernel<false, CK, 0><<<grid, 256, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
+      wino_conv_kernel<false, CK, 0><<<grid, kWinoThreads, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
   }
 }
 
