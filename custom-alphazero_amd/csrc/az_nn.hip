@@ -21,6 +21,8 @@
 // so a board's outputs do not depend on what else is in the batch.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "az_nn.h"
 
 #ifndef AZ_FUSE_HEADS
@@ -102,6 +104,9 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
 // channel order (a zero term leaves the accumulator unchanged: it is never
 // -0), so outputs are bitwise those of encode + stem_conv.  Saves the encode
 // pass and the float4 input reads.
+// Blocks loop over pixels (8 per pass: lane group = 32 channel quads) with
+// the 18 KB of stem weights staged once per block in LDS (read per pixel
+// through L1 the kernel was L1-bandwidth bound).
 template <int F>
 __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict__ boards,
                                                          const float* __restrict__ ws,
@@ -109,37 +114,45 @@ __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict
                                                          const int* __restrict__ count, int n_static,
                                                          int H, int W, float* __restrict__ out) {
   constexpr int G4 = F / 4;
+  static_assert(256 % G4 == 0, "a pass covers whole pixels");
+  constexpr int PPB = 256 / G4;  // pixels per pass
+  __shared__ float4 wsh[36 * G4];
   const int n = count ? *count : n_static;
   const int HW = H * W;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n * HW * G4) return;
-  const int r = idx / G4, cg = idx - r * G4;
-  const int b = r / HW, p = r - b * HW;
-  const int y = p / W, xx = p - y * W;
-  const Board bd = boards[b];
-  float4 acc = *reinterpret_cast<const float4*>(bias + cg * 4);
+  const int npix = n * HW;
+  if ((int)blockIdx.x * PPB >= npix) return;  // block-uniform
+  for (int i = threadIdx.x; i < 36 * G4; i += 256) wsh[i] = reinterpret_cast<const float4*>(ws)[i];
+  __syncthreads();
+  const int cg = threadIdx.x % G4;
+  const float4 b4 = reinterpret_cast<const float4*>(bias)[cg];
+  for (int r = blockIdx.x * PPB + threadIdx.x / G4; r < npix; r += gridDim.x * PPB) {
+    const int b = r / HW, p = r - b * HW;
+    const int y = p / W, xx = p - y * W;
+    const Board bd = boards[b];
+    float4 acc = b4;
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    const int ny = y + tap / 3 - 1, nx = xx + tap % 3 - 1;
-    if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
-    const int q = ny * W + nx;
-    const int st = bit(bd.own, q) ? 1 : (bit(bd.opp, q) ? 2 : 0);
-    const float4 w1 = *reinterpret_cast<const float4*>(ws + (tap * 4 + st) * F + cg * 4);
-    const float4 w3 = *reinterpret_cast<const float4*>(ws + (tap * 4 + 3) * F + cg * 4);
-    acc.x = fmaf(1.0f, w1.x, acc.x);
-    acc.y = fmaf(1.0f, w1.y, acc.y);
-    acc.z = fmaf(1.0f, w1.z, acc.z);
-    acc.w = fmaf(1.0f, w1.w, acc.w);
-    acc.x = fmaf(1.0f, w3.x, acc.x);
-    acc.y = fmaf(1.0f, w3.y, acc.y);
-    acc.z = fmaf(1.0f, w3.z, acc.z);
-    acc.w = fmaf(1.0f, w3.w, acc.w);
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ny = y + tap / 3 - 1, nx = xx + tap % 3 - 1;
+      if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
+      const int q = ny * W + nx;
+      const int st = bit(bd.own, q) ? 1 : (bit(bd.opp, q) ? 2 : 0);
+      const float4 w1 = wsh[(tap * 4 + st) * G4 + cg];
+      const float4 w3 = wsh[(tap * 4 + 3) * G4 + cg];
+      acc.x = fmaf(1.0f, w1.x, acc.x);
+      acc.y = fmaf(1.0f, w1.y, acc.y);
+      acc.z = fmaf(1.0f, w1.z, acc.z);
+      acc.w = fmaf(1.0f, w1.w, acc.w);
+      acc.x = fmaf(1.0f, w3.x, acc.x);
+      acc.y = fmaf(1.0f, w3.y, acc.y);
+      acc.z = fmaf(1.0f, w3.z, acc.z);
+      acc.w = fmaf(1.0f, w3.w, acc.w);
+    }
+    acc.x = fmaxf(acc.x, 0.0f);
+    acc.y = fmaxf(acc.y, 0.0f);
+    acc.z = fmaxf(acc.z, 0.0f);
+    acc.w = fmaxf(acc.w, 0.0f);
+    *reinterpret_cast<float4*>(out + (size_t)r * F + cg * 4) = acc;
   }
-  acc.x = fmaxf(acc.x, 0.0f);
-  acc.y = fmaxf(acc.y, 0.0f);
-  acc.z = fmaxf(acc.z, 0.0f);
-  acc.w = fmaxf(acc.w, 0.0f);
-  *reinterpret_cast<float4*>(out + (size_t)r * F + cg * 4) = acc;
 }
 
 // ------------------------------------------------------------ conv3x3 MFMA
@@ -381,7 +394,11 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // FEAT: the 1x1 head convs already ran in the last conv's epilogue (feat =
 // [boards][HW] float4 from wino_conv_kernel<.., HEADS>); same fmaf chains.
-template <int F, bool FEAT>
+// Blocks loop over boards (4 per pass, one per wave); with STAGE the dense
+// layers' weights (policy [2HW][A], value1 [HW][hidden]) are copied into LDS
+// once per block instead of being re-read through L1 for every board.  The
+// per-board arithmetic is unchanged.
+template <int F, bool FEAT, bool STAGE>
 __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ act, HeadWeights hw,
                                                     const int* __restrict__ count, int n_static,
                                                     int HW, int A, int hidden,
@@ -390,10 +407,21 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
   __shared__ float pflat[4][2 * kMaxCells];
   __shared__ float vflat[4][kMaxCells];
   __shared__ float logits[4][kMaxActions];
+  extern __shared__ float wsm[];
   const int n = count ? *count : n_static;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + wave;
-  if (b >= n) return;  // wave-uniform; no block barrier below
+  const float* wpd = hw.wpd;
+  const float* wv1 = hw.wv1;
+  if constexpr (STAGE) {
+    if ((int)blockIdx.x * 4 >= n) return;  // block-uniform
+    const int npd = 2 * HW * A, nv1 = HW * hidden;
+    for (int i = threadIdx.x; i < npd; i += 256) wsm[i] = hw.wpd[i];
+    for (int i = threadIdx.x; i < nv1; i += 256) wsm[npd + i] = hw.wv1[i];
+    __syncthreads();
+    wpd = wsm;
+    wv1 = wsm + npd;
+  }
+  for (int b = blockIdx.x * 4 + wave; b < n; b += gridDim.x * 4) {  // wave-uniform
   if constexpr (FEAT) {
     const float4* feat = reinterpret_cast<const float4*>(act) + (size_t)b * HW;
     for (int p = lane; p < HW; p += 64) {
@@ -428,7 +456,7 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
   // policy dense + softmax
   for (int a = lane; a < A; a += 64) {
     float s = hw.bpd[a];
-    for (int i = 0; i < 2 * HW; ++i) s += pflat[wave][i] * hw.wpd[i * A + a];
+    for (int i = 0; i < 2 * HW; ++i) s += pflat[wave][i] * wpd[i * A + a];
     logits[wave][a] = s;
   }
   __builtin_amdgcn_wave_barrier();
@@ -444,11 +472,13 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
   float part = 0.f;
   for (int j = lane; j < hidden; j += 64) {
     float s = hw.bv1[j];
-    for (int p = 0; p < HW; ++p) s += vflat[wave][p] * hw.wv1[p * hidden + j];
+    for (int p = 0; p < HW; ++p) s += vflat[wave][p] * wv1[p * hidden + j];
     part += fmaxf(s, 0.f) * hw.wv2[j];
   }
   part = wave_sum(part);
   if (lane == 0) values[b] = tanhf(part + hw.bv2[0]);
+  __builtin_amdgcn_wave_barrier();  // pflat/vflat/logits are reused by the next board
+  }
 }
 
 // --------------------------------------------------------------- launchers
@@ -476,8 +506,8 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   {
     const int total = n_max * HW * (F / 4);
     if (boards)
-      stem_board_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(boards, net.stem_w, net.stem_b, count,
-                                                               n_max, H, W, act_a);
+      stem_board_kernel<F><<<std::min((n_max * HW + 7) / 8, 1024), 256, 0, s>>>(
+          boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a);
     else
       stem_conv_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(
           reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
@@ -539,12 +569,18 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   if (timer) timer->end(s, 2 * net.depth);
   HeadWeights hw{net.pc_w, net.pc_b, net.vc_w, net.vc_b, net.pd_w,
                  net.pd_b, net.v1_w, net.v1_b, net.v2_w, net.v2_b};
-  if (fused_heads)
-    heads_kernel<F, true><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A, net.hidden, probs,
-                                                        values);
-  else
-    heads_kernel<F, false><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A, net.hidden, probs,
-                                                         values);
+  const size_t wbytes = (size_t)(2 * HW * A + HW * net.hidden) * sizeof(float);
+  const bool stage = wbytes <= 64 * 1024;
+  const int hblocks = stage ? std::min((n_max + 3) / 4, 512) : (n_max + 3) / 4;
+#define AZ_HEADS(FEAT_, STAGE_)                                                                      \
+  heads_kernel<F, FEAT_, STAGE_><<<hblocks, 256, STAGE_ ? wbytes : 0, s>>>(cur, hw, count, n_max, HW, A, \
+                                                                         net.hidden, probs, values)
+  if (fused_heads) {
+    if (stage) AZ_HEADS(true, true); else AZ_HEADS(true, false);
+  } else {
+    if (stage) AZ_HEADS(false, true); else AZ_HEADS(false, false);
+  }
+#undef AZ_HEADS
 }
 
 }  // namespace az
