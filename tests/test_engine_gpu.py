@@ -217,3 +217,25 @@ def test_selfplay_network_replays_on_oracle(cache_log2, lanes):
         np.testing.assert_array_equal(got["moves"], ref["moves"])
         np.testing.assert_array_equal(got["policy"].view(np.uint64), ref["policy"].view(np.uint64))
         assert got["expansions"] == ref["expansions"]
+
+
+@pytest.mark.parametrize("cfg", [(9, 9, 5, False, 30), (11, 11, 5, True, 30), (8, 8, 4, True, 40),
+                                 (4, 4, 3, False, 20)])
+@pytest.mark.parametrize("cache_log2", [0, 16])
+def test_selfplay_synthetic_board_shapes_vs_oracle(cfg, cache_log2):
+    """Shapes beyond the fixtures: A = 81 (serial select / wide expand and play
+    kernels), the largest 11x11 board (121 of 128 cells), 8x8; slot refill."""
+    H, W, n, grav, S = cfg
+    games = 4
+    for slots in (games, 2):
+        eng = az.Engine(H, W, n, grav, S, slots=slots, evaluator=az.EVAL_SYNTHETIC,
+                        cache_log2=cache_log2)
+        got = selfplay_games(eng, 0, games, base_seed=31)
+        for g in range(games):
+            ref = oracle.play_game(H, W, n, grav, S, 31 + g)
+            assert got[g]["T"] == ref["T"]
+            np.testing.assert_array_equal(got[g]["moves"], ref["moves"])
+            np.testing.assert_array_equal(got[g]["policy"].view(np.uint64), ref["policy"].view(np.uint64))
+            np.testing.assert_array_equal(got[g]["boards"], ref["boards"])
+            assert got[g]["expansions"] == ref["expansions"]
+        eng.close()
