@@ -57,6 +57,9 @@ __host__ __device__ constexpr int wino_sign(int a, int i) {
 #ifndef AZ_WINO_SGB
 #define AZ_WINO_SGB 0  // explicit per-stage instruction order (measured -3%: off)
 #endif
+#ifndef AZ_WINO_WS_WAVES
+#define AZ_WINO_WS_WAVES 2  // warp-specialised variant: min waves/SIMD to size registers for
+#endif
 #ifndef AZ_WINO_STAGE_BARRIER
 #define AZ_WINO_STAGE_BARRIER 1  // sched_barrier between point stages
 #endif
@@ -90,10 +93,12 @@ __device__ __forceinline__ int vswz(int j, int t) {
 //         early into registers and transformed after chunk c's MFMAs: one
 //         barrier per chunk, no exposed global latency (LDS permitting).
 #ifndef AZ_WINO_OCC
-#define AZ_WINO_OCC 2  // workgroups per CU the register budget is sized for
+#define AZ_WINO_OCC 2  // waves per SIMD the register budget is sized for
 #endif
 template <bool RESIDUAL, int CK, int PIPE, bool HEADS = false>
-__global__ __launch_bounds__(PIPE == 2 ? 320 : kWinoThreads, AZ_WINO_OCC / kWinoMB) void wino_conv_kernel(
+// (HIP's second launch-bounds argument is the minimum waves per SIMD)
+__global__ __launch_bounds__(PIPE == 2 ? 320 : kWinoThreads, PIPE == 2 ? AZ_WINO_WS_WAVES : AZ_WINO_OCC)
+void wino_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
