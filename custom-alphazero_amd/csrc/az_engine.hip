@@ -238,8 +238,8 @@ std::vector<float> pack_fragments(const std::vector<float>& wt, int N, int K) {
 
 // Winograd F(2x2,3x3) weights for wino_conv_kernel (az_wino.hip):
 // U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
-// in float64 from the folded Keras kernel (times the sign the kernel expects
-// for corner points), rounded once to float, in the kernel's fragment order.
+// in float64 from the folded Keras kernel, rounded once to float, in the
+// kernel's fragment order.
 std::vector<float> pack_wino(const std::vector<double>& w, int F) {
   static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   std::vector<float> p((size_t)16 * F * F);
@@ -254,9 +254,8 @@ std::vector<float> pack_wino(const std::vector<double>& w, int F) {
         const double* src = w.data() + (size_t)(ky * 3 + kx) * F * F;
         for (size_t i = 0; i < (size_t)F * F; ++i) U[i] += gg * src[i];
       }
-    const double sg = az::wino_fold_sign(xi);
     for (int cin = 0; cin < F; ++cin)
-      for (int co = 0; co < F; ++co) p[az::wino_pack_index(xi, cin, co)] = (float)(sg * U[(size_t)cin * F + co]);
+      for (int co = 0; co < F; ++co) p[az::wino_pack_index(xi, cin, co)] = (float)U[(size_t)cin * F + co];
   }
   return p;
 }

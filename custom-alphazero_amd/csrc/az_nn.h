@@ -84,16 +84,12 @@ void launch_encode(const Board* boards, const int* count, int n_max, int HW, flo
 void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* mask,
                        hipStream_t s);
 // Winograd conv: input channels per LDS chunk (16 or 32; the host packing
-// follows it), packing index and the sign folded into the corner points
+// follows it) and the packing index of a weight in the kernel's B stream
 #ifndef AZ_WINO_CK
 #define AZ_WINO_CK 32
 #endif
 constexpr int kWinoCK = AZ_WINO_CK;
-#ifndef AZ_WINO_PIPE
-#define AZ_WINO_PIPE 1  // default pipeline (launch_wino_conv); 1 falls back to 0 at CK 32
-#endif
 size_t wino_pack_index(int xi, int cin, int cout);
-int wino_fold_sign(int xi);
 // The heads' 1x1 convolutions (policy F->2, value F->1, each + folded BN +
 // ReLU, model.py:68-149), fused into the last block's conv2 epilogue: feat =
 // [boards][HW] float4 (policy ch 0, policy ch 1, value, 0); the block output
@@ -107,8 +103,7 @@ struct HeadConv {
 };
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
-                      int n_max, int H, int W, hipStream_t s, int pipe,
-                      const HeadConv* heads = nullptr);
+                      int n_max, int H, int W, hipStream_t s, const HeadConv* heads = nullptr);
 // x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
 // boards (optional): one-hot input straight from the eval queue's boards
 // (bitwise the same outputs as encoding them into x first)

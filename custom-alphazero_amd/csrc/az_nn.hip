@@ -540,17 +540,13 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
                                                                 count, n_max, H, W);            \
   }
     switch (variant) {
-      case 0:  // Winograd F(2x2,3x3) (az_wino.hip), default pipeline
-      case 7:  // single V buffer
-      case 8:  // warp-specialised producer
-      case 9:  // double buffer + register prefetch
+      case 0:  // Winograd F(2x2,3x3) (az_wino.hip)
       {
-        const int pipe = variant == 0 ? AZ_WINO_PIPE : variant == 7 ? 0 : variant == 8 ? 2 : 1;
-        launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s, pipe);
+        launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s);
         // last block: the head 1x1 convs run in conv2's epilogue, features into nxt
         HeadConv hc{net.pc_w, net.pc_b, net.vc_w, net.vc_b,
                     d == net.depth - 1 && AZ_FUSE_HEADS ? reinterpret_cast<float4*>(nxt) : nullptr};
-        launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, pipe, &hc);
+        launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc);
         fused_heads = hc.feat != nullptr;
         break;
       }

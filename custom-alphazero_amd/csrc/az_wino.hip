@@ -13,9 +13,9 @@
 // stays within ~1e-7 relative of the float64 Keras restatement, like the
 // direct kernel (tests/test_engine_gpu.py, NET_TOL = 1e-5).
 //
-// Workgroup = 4 waves = 32 consecutive tiles (one MFMA M block) x 128 output
-// channels; wave w owns output channels [32w, 32w+32).  Input channels run in
-// chunks of CK:
+// Workgroup = 4 waves = 32 consecutive tiles (one MFMA M block; tiles cross
+// board boundaries freely) x 128 output channels; wave w owns output
+// channels [32w, 32w+32).  Input channels run in chunks of CK:
 //   * produce: the 256 threads turn the chunk's 4x4 input patches (read from
 //     global/L2; a pixel is shared by up to four tiles) into V = B^T d B and
 //     store V[xi][tile][CK] in LDS (plus, for the block's second conv, the 4
@@ -23,57 +23,34 @@
 //   * consume, one pipeline stage per point xi: CK/2 MFMAs accumulate
 //     M = V[xi] U[xi] over the chunk (A from LDS, B = host-packed U fragments
 //     streamed from global one stage ahead), and the previous stage's M is
-//     added into the output-pixel accumulators with the +-1 coefficients of
-//     A^T (x) A^T.  The four corner points feed exactly one output pixel each:
-//     their MFMAs accumulate straight into that pixel (the sign folded into U
-//     on the host), no M and no adds; the residual's pixel rows likewise.
+//     added into the four output-pixel accumulators with the +-1
+//     coefficients of A^T (x) A^T.  The residual's pixel rows accumulate
+//     straight into their pixel.
 // Reduction order per output element is fixed (chunk, xi, k-step), so a
 // board's outputs do not depend on the rest of the batch.
+//
+// The A/B record behind these choices (chunk 32 single-buffered over chunk
+// 16 double-buffered, warp-specialised producers, corner points straight
+// into their pixel, explicit instruction groups, two M blocks per workgroup)
+// is in DESIGN.md section 5; those variants lost and were removed.
 #include "az_nn.h"
 
 namespace az {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-#ifndef AZ_WINO_MB
-#define AZ_WINO_MB 1  // MFMA M blocks (32 tiles each) per workgroup
+constexpr int kWinoTiles = 32;   // tiles per workgroup (MFMA M)
+constexpr int kWinoThreads = 256;
+
+#ifndef AZ_WINO_DIAG
+#define AZ_WINO_DIAG 0  // timing experiments only (wrong outputs): 1 no B stream, 2 no
+                        // producer after chunk 0, 3 no output-transform adds, 4 = 1+2+3
 #endif
-constexpr int kWinoMB = AZ_WINO_MB;
-constexpr int kWinoTiles = 32 * kWinoMB;  // tiles per workgroup
-constexpr int kWinoThreads = 256 * kWinoMB;
 
 // A^T = [[1,1,1,0],[0,1,-1,-1]]: sign with which point coordinate a feeds
 // output coordinate i (0 = not at all)
 __host__ __device__ constexpr int wino_sign(int a, int i) {
   return i == 0 ? (a == 3 ? 0 : 1) : (a == 0 ? 0 : (a == 1 ? 1 : -1));
-}
-// corner points (a, b in {0, 3}) feed one output pixel; returns it, else -1.
-// With AZ_WINO_CORNER their MFMAs accumulate straight into the pixel; off by
-// default: mixing MFMA and VALU writes on the same accumulators serialises
-// the stage (measured 175 -> 148 TFLOP/s at B = 4096).
-#ifndef AZ_WINO_BRING
-#define AZ_WINO_BRING 2  // B register ring (prefetch distance RB/2)
-#endif
-#ifndef AZ_WINO_SGB
-#define AZ_WINO_SGB 0  // explicit per-stage instruction order (measured -3%: off)
-#endif
-#ifndef AZ_WINO_WS_WAVES
-#define AZ_WINO_WS_WAVES 2  // warp-specialised variant: min waves/SIMD to size registers for
-#endif
-#ifndef AZ_WINO_STAGE_BARRIER
-#define AZ_WINO_STAGE_BARRIER 1  // sched_barrier between point stages
-#endif
-#ifndef AZ_WINO_DIAG
-#define AZ_WINO_DIAG 0  // timing experiments only (wrong outputs): 1 no B stream,
-                        // 2 no producer after chunk 0, 3 no output-transform adds
-#endif
-#ifndef AZ_WINO_CORNER
-#define AZ_WINO_CORNER 0
-#endif
-__host__ __device__ constexpr int wino_corner_pixel(int xi) {
-  return AZ_WINO_CORNER && ((xi >> 2) == 0 || (xi >> 2) == 3) && ((xi & 3) == 0 || (xi & 3) == 3)
-             ? 2 * ((xi >> 2) == 3) + ((xi & 3) == 3)
-             : -1;
 }
 
 // V rows are CK floats = CK/4 16-byte chunks; chunk j of tile row t is
@@ -85,20 +62,12 @@ __device__ __forceinline__ int vswz(int j, int t) {
   return j ^ ((t / RPB) & (RC - 1));
 }
 
-// PIPE 2: warp-specialised: a fifth wave produces chunk c+1 into the other V
-//         buffer while the four MFMA waves consume chunk c; one barrier per
-//         chunk and no producer work on the MFMA waves.
-// PIPE 0: one V buffer, chunk c+1 loaded+transformed between two barriers.
-// PIPE 1: two V buffers; chunk c+1's patch loads are issued a whole chunk
-//         early into registers and transformed after chunk c's MFMAs: one
-//         barrier per chunk, no exposed global latency (LDS permitting).
-#ifndef AZ_WINO_OCC
-#define AZ_WINO_OCC 2  // waves per SIMD the register budget is sized for
-#endif
-template <bool RESIDUAL, int CK, int PIPE, bool HEADS = false>
-// (HIP's second launch-bounds argument is the minimum waves per SIMD)
-__global__ __launch_bounds__(PIPE == 2 ? 320 : kWinoThreads, PIPE == 2 ? AZ_WINO_WS_WAVES : AZ_WINO_OCC)
-void wino_conv_kernel(
+// HEADS: the last block's conv2 also runs the heads' 1x1 convolutions in its
+// epilogue (feat, az_nn.h HeadConv) and never writes the block output.
+// (HIP's second launch-bounds argument is the minimum waves per SIMD: two,
+// i.e. two workgroups per CU, which the V buffer's LDS also allows.)
+template <bool RESIDUAL, int CK, bool HEADS>
+__global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
@@ -106,13 +75,12 @@ void wino_conv_kernel(
   static_assert(CK == 16 || CK == 32, "chunk of 16 or 32 input channels");
   constexpr int NX = RESIDUAL ? 20 : 16;   // 16 Winograd points (+4 residual pixel rows)
   constexpr int RC = CK / 4;               // float4 per V row
-  constexpr int VB = NX * kWinoTiles * RC; // float4 per V buffer
+  constexpr int VB = NX * kWinoTiles * RC; // float4 in the V buffer
   constexpr int NCH = 128 / CK;
   constexpr int KS = CK / 2;               // MFMA k-steps per stage
   constexpr int QB = CK / 8;               // float4 of B (and of A) per lane per stage
-  constexpr int IPT = 16 * CK / 256;       // producer items per thread (tile, c4, half)
-  __shared__ float4 vbuf_all[(PIPE ? 2 : 1) * VB];
-  constexpr bool WS = PIPE == 2;
+  constexpr int IPT = 16 * CK / kWinoThreads;  // producer items per thread (tile, c4, half)
+  __shared__ float4 vbuf[VB];
 
   const int HW = H * W, TW = (W + 1) >> 1, TH = (H + 1) >> 1, TB = TH * TW;
   const int n_boards = count ? *count : n_static;
@@ -152,8 +120,7 @@ void wino_conv_kernel(
   // V rows i = 2ph, 2ph+1 need patch rows {0,1,2} (ph = 0) or {1,2,3} (ph = 1).
   // Unconditional loads from a clamped address: no branches, every load of
   // the chunk in flight together; off-board pixels are zeroed in
-  // produce_store, so nothing here waits on the loads (PIPE 1 issues them a
-  // whole chunk ahead).
+  // produce_store (zeroing right after each load made it a stall: -15%).
   auto produce_load = [&](int c, Patch& P) {
     const int cb = c * CK;
 #pragma unroll
@@ -184,7 +151,7 @@ void wino_conv_kernel(
       }
     }
   };
-  auto produce_store = [&](Patch& P, float4* vbuf) {
+  auto produce_store = [&](Patch& P) {
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
 #pragma unroll
@@ -232,23 +199,17 @@ void wino_conv_kernel(
   };
 
   // ---- consumer geometry: lane -> tile row r, k half h; wave -> columns
-  // wave -> (M block mb, 32 output channels nbw): the M blocks' waves read
-  // the same B fragments at about the same time (one L2 fetch, L1 hits)
   const int r = lane & 31, h = lane >> 5;
-  const int mb = wave >> 2, nbw = wave & 3;
-  const int vr = mb * 32 + r;  // this lane's tile row in the workgroup
   f32x16 Y[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p)
 #pragma unroll
     for (int i = 0; i < 16; ++i) Y[p][i] = 0.0f;
 
-  // B stream: QB float4 per lane per stage in a ring of RB register buffers,
-  // prefetched RB-2... RB/2 stages ahead (NX % RB == 0 keeps the ring slot
-  // static per stage).  32-bit offsets from the uniform base.
-  constexpr int RB = AZ_WINO_BRING, DIST = RB / 2;
-  static_assert(NX % RB == 0, "ring slot must be static per stage");
-  const unsigned blane = (unsigned)(nbw * 64 * QB + lane);
+  // B stream: QB float4 per lane per stage, two register buffers (one stage
+  // ahead; NX is even, so the buffer of a stage is static).  32-bit offsets
+  // from the uniform base.
+  const unsigned blane = (unsigned)(wave * 64 * QB + lane);
   auto load_b = [&](int c, int xi, float4 (&dst)[QB]) {
     if ((AZ_WINO_DIAG == 1 || AZ_WINO_DIAG == 4) && (c > 0 || xi > 1)) return;
     const bool res = RESIDUAL && xi >= 16;
@@ -257,10 +218,10 @@ void wino_conv_kernel(
 #pragma unroll
     for (int q = 0; q < QB; ++q) dst[q] = base[o + q * 64];
   };
-  auto load_a = [&](const float4* vbuf, int xi, float4 (&dst)[QB]) {
-    const float4* vrow = vbuf + (xi * kWinoTiles + vr) * RC;
+  auto load_a = [&](int xi, float4 (&dst)[QB]) {
+    const float4* vrow = vbuf + (xi * kWinoTiles + r) * RC;
 #pragma unroll
-    for (int q = 0; q < QB; ++q) dst[q] = vrow[vswz<CK>(QB * h + q, vr)];
+    for (int q = 0; q < QB; ++q) dst[q] = vrow[vswz<CK>(QB * h + q, r)];
   };
   auto scatter = [&](int xi, const f32x16& m) {
     if (AZ_WINO_DIAG == 3 || AZ_WINO_DIAG == 4) {
@@ -284,243 +245,94 @@ void wino_conv_kernel(
       }
     }
   };
-  float4 bq[RB][QB], aq[2][QB];
+  float4 bq[2][QB], aq[2][QB];
   f32x16 M[2];
 
-  // warp-specialised producer: wave 4 builds a whole chunk, two items
-  // (tile, 4 channels, half) per lane at a time
-  struct Patch2 {
-    float4 d[2][3][4];
-    float4 rr[2][2];
-    uint32_t ok[2];
-  };
-  auto ws_produce = [&](int c, float4* vbuf) {
-    constexpr int ITEMS = 16 * CK;  // per chunk
-#pragma unroll 1
-    for (int i0 = lane; i0 < ITEMS; i0 += 128) {
-      Patch2 Q;
-      int qt[2], qc[2], qh[2];
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        const int item = i0 + 64 * g;
-        qh[g] = item & 1;
-        qc[g] = (item >> 1) & (RC - 1);
-        qt[g] = item / (2 * RC);
-        const int tau = t0 + qt[g];
-        const bool v = tau < tiles;
-        int b = 0, ty = 0, tx = 0;
-        if (v) {
-          b = tau / TB;
-          const int lt = tau - b * TB;
-          ty = lt / TW;
-          tx = lt - ty * TW;
-        }
-        const int base = b * HW * 128 + qc[g] * 4 + c * CK;
-        Q.ok[g] = 0;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const int y = 2 * ty - 1 + qh[g] + r;
-#pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            const int xx = 2 * tx - 1 + x;
-            const bool ok = v && y >= 0 && y < H && xx >= 0 && xx < W;
-            Q.d[g][r][x] = *reinterpret_cast<const float4*>(in + (ok ? (unsigned)(base + (y * W + xx) * 128) : 0u));
-            Q.ok[g] |= (uint32_t)ok << (r * 4 + x);
-          }
-        }
-        if constexpr (RESIDUAL) {
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int pp = 2 * qh[g] + k;
-            const int y = 2 * ty + (pp >> 1), xx = 2 * tx + (pp & 1);
-            const bool ok = v && y < H && xx < W;
-            Q.rr[g][k] = *reinterpret_cast<const float4*>(res_in + (ok ? (unsigned)(base + (y * W + xx) * 128) : 0u));
-            Q.ok[g] |= (uint32_t)ok << (12 + k);
-          }
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int x = 0; x < 4; ++x)
-            if (!((Q.ok[g] >> (r * 4 + x)) & 1)) Q.d[g][r][x] = z4;
-        float4 T[2][4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const float4 a = Q.d[g][0][x], b = Q.d[g][1][x], e = Q.d[g][2][x];
-          if (qh[g] == 0) {
-            T[0][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
-            T[1][x] = make_float4(b.x + e.x, b.y + e.y, b.z + e.z, b.w + e.w);
-          } else {
-            T[0][x] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
-            T[1][x] = make_float4(a.x - e.x, a.y - e.y, a.z - e.z, a.w - e.w);
-          }
-        }
-        const int sw = vswz<CK>(qc[g], qt[g]);
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii) {
-          const int i = 2 * qh[g] + ii;
-          const float4 t0_ = T[ii][0], t1 = T[ii][1], t2 = T[ii][2], t3 = T[ii][3];
-          const float4 vv[4] = {
-              make_float4(t0_.x - t2.x, t0_.y - t2.y, t0_.z - t2.z, t0_.w - t2.w),
-              make_float4(t1.x + t2.x, t1.y + t2.y, t1.z + t2.z, t1.w + t2.w),
-              make_float4(t2.x - t1.x, t2.y - t1.y, t2.z - t1.z, t2.w - t1.w),
-              make_float4(t1.x - t3.x, t1.y - t3.y, t1.z - t3.z, t1.w - t3.w)};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) vbuf[((i * 4 + j) * kWinoTiles + qt[g]) * RC + sw] = vv[j];
-        }
-        if constexpr (RESIDUAL) {
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const float4 rv = ((Q.ok[g] >> (12 + k)) & 1) ? Q.rr[g][k] : z4;
-            vbuf[((16 + 2 * qh[g] + k) * kWinoTiles + qt[g]) * RC + sw] = rv;
-          }
-        }
-      }
-    }
-  };
-
-  if constexpr (WS) {
-    if (wave == 4) {
-      ws_produce(0, vbuf_all);
-      __syncthreads();
-#pragma unroll 1
-      for (int c = 0; c < NCH; ++c) {
-        if (c + 1 < NCH) ws_produce(c + 1, vbuf_all + ((c + 1) & 1) * VB);
-        __syncthreads();
-      }
-      return;  // the producer wave has no outputs
-    }
-  }
-
   Patch P;
-  if constexpr (!WS) {
-    produce_load(0, P);
-    produce_store(P, vbuf_all);
-    if (PIPE) produce_load(1, P);
-  }
-#pragma unroll
-  for (int k = 0; k < DIST; ++k) load_b(0, k, bq[k]);
-  __syncthreads();  // (WS: pairs with the producer's first barrier)
+  produce_load(0, P);
+  produce_store(P);
+  load_b(0, 0, bq[0]);
+  __syncthreads();
 
   // the chunk loop stays rolled: one copy of the 16-20 unrolled stages is
-  // already ~10 KB of code (unrolling it tripled the body and ran 15% slower)
+  // already ~10 KB of code
 #pragma unroll 1
   for (int c = 0; c < NCH; ++c) {
-    const float4* vbuf = vbuf_all + (PIPE ? (c & 1) * VB : 0);
-    load_a(vbuf, 0, aq[0]);
-    int pend = -1;  // point whose M still has to be scattered
+    load_a(0, aq[0]);
 #pragma unroll
     for (int xi = 0; xi < NX; ++xi) {
       // one software-pipeline stage per point: the scheduler may interleave
-      // inside a stage (MFMAs of xi with the adds of the pending point and
-      // the next stage's loads) but not across
-      if (AZ_WINO_STAGE_BARRIER) __builtin_amdgcn_sched_barrier(0);
-      {
-        const int nx = xi + DIST;
-        if (nx < NX) {
-          load_b(c, nx, bq[nx % RB]);
-        } else if (c + 1 < NCH) {
-          load_b(c + 1, nx - NX, bq[nx % RB]);
-        }
+      // inside a stage (MFMAs of xi with the adds of xi-1 and the next
+      // stage's loads) but not across
+      __builtin_amdgcn_sched_barrier(0);
+      if (xi + 1 < NX) {
+        load_b(c, xi + 1, bq[(xi + 1) & 1]);
+        load_a(xi + 1, aq[(xi + 1) & 1]);
+      } else if (c + 1 < NCH) {
+        load_b(c + 1, 0, bq[(xi + 1) & 1]);
       }
-      if (xi + 1 < NX) load_a(vbuf, xi + 1, aq[(xi + 1) & 1]);
       float av[KS], bv[KS];
 #pragma unroll
       for (int q = 0; q < QB; ++q) {
-        const float4 a4 = aq[xi & 1][q], b4 = bq[xi % RB][q];
+        const float4 a4 = aq[xi & 1][q], b4 = bq[xi & 1][q];
         av[4 * q] = a4.x, av[4 * q + 1] = a4.y, av[4 * q + 2] = a4.z, av[4 * q + 3] = a4.w;
         bv[4 * q] = b4.x, bv[4 * q + 1] = b4.y, bv[4 * q + 2] = b4.z, bv[4 * q + 3] = b4.w;
       }
-      const int direct = (RESIDUAL && xi >= 16) ? xi - 16 : wino_corner_pixel(xi);
-      if (direct >= 0) {
-        // residual pixel row, or a corner point: straight into its pixel
+      if (RESIDUAL && xi >= 16) {
+        // fused 1x1 projection residual: pixel p's own block-input row
+        const int p = xi - 16;
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
-          Y[direct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], Y[direct], 0, 0, 0);
+        for (int s = 0; s < KS; ++s) Y[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], Y[p], 0, 0, 0);
       } else {
         f32x16& m = M[xi & 1];
         m = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0], bv[0], f32x16{}, 0, 0, 0);
 #pragma unroll
         for (int s = 1; s < KS; ++s) m = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], m, 0, 0, 0);
       }
-      if (pend >= 0) {
-        scatter(pend, M[pend & 1]);
+      if (xi >= 1 && xi - 1 < 16) {
+        scatter(xi - 1, M[(xi - 1) & 1]);
         // pin the adds to this stage (IR-level sinking would otherwise move
         // every point's adds to the loop latch and keep all M blocks live)
         asm volatile("" ::"v"(Y[0]), "v"(Y[1]), "v"(Y[2]), "v"(Y[3]));
-        pend = -1;
       }
-      if (direct < 0) pend = xi;
-#if AZ_WINO_SGB
-      // stage order: the next stage's B (global) and A (LDS) loads first, so
-      // their latency hides behind this stage's MFMAs; then MFMAs with the
-      // pending point's adds spread between them (two MFMAs first: the adds
-      // read the previous stage's last MFMA result)
-      __builtin_amdgcn_sched_group_barrier(0x020, QB, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, QB, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-#pragma unroll
-      for (int k = 2; k < KS; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
-#endif
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (pend >= 0) scatter(pend, M[pend & 1]);
-    if constexpr (WS) {
-      __syncthreads();  // chunk c+1 is in the other buffer; chunk c's is free
-      continue;
-    }
+    if (NX == 16) scatter(15, M[1]);
     if (c + 1 < NCH) {
-      if (AZ_WINO_DIAG == 2 || AZ_WINO_DIAG == 4) {
-        __syncthreads();
-      } else if constexpr (PIPE) {
-        // the other buffer was last read in chunk c-1, before the previous
-        // barrier: safe to overwrite now
-        produce_store(P, vbuf_all + ((c + 1) & 1) * VB);
-        if (c + 2 < NCH) produce_load(c + 2, P);
-        __syncthreads();
-      } else {
-        __syncthreads();  // every wave is done with chunk c's V
+      __syncthreads();  // every wave is done with chunk c's V
+      if (AZ_WINO_DIAG != 2 && AZ_WINO_DIAG != 4) {
         produce_load(c + 1, P);
-        produce_store(P, vbuf_all);
-        __syncthreads();
+        produce_store(P);
       }
+      __syncthreads();
     }
   }
 
   // ---- epilogue: bias (+ residual bias, folded on the host), ReLU, store
   // C/D map: column = lane & 31, tile row = (i & 3) + 8*(i >> 2) + 4*h
-  const int col = nbw * 32 + r;
+  const int col = wave * 32 + r;
   const float bcol = bias[col];
   if constexpr (HEADS) {
     // fused head 1x1 convs: the block output goes through LDS (transposed to
     // [tile pixel][channel], row pitch 129 floats: conflict-free both ways)
     // and thread tp sums its pixel's 128 channels in channel order -- the
-    // same fmaf chains as heads_kernel on the stored output
-    static_assert(RESIDUAL && PIPE == 0, "heads fuse into the single-buffered conv2");
+    // same fmaf chains as heads_kernel on a stored output
+    static_assert(RESIDUAL, "heads fuse into the block's second conv");
     static_assert(64 * 129 * 4 <= VB * 16, "half the transpose fits the V buffer");
-    float* tb = reinterpret_cast<float*>(vbuf_all);
+    float* tb = reinterpret_cast<float*>(vbuf);
     // two passes of 16 tile rows (64 tile pixels) each
 #pragma unroll
-    for (int pass = 0; pass < 2 * kWinoMB; ++pass) {
-      const int half = pass & 1;
+    for (int half = 0; half < 2; ++half) {
       __syncthreads();  // V (or the previous pass) no longer read
-      if (mb == (pass >> 1)) {
 #pragma unroll
-        for (int i = 8 * half; i < 8 * half + 8; ++i) {
-          const int row = (i & 3) + 8 * (i >> 2) + 4 * h - 16 * half;
+      for (int i = 8 * half; i < 8 * half + 8; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h - 16 * half;
 #pragma unroll
-          for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
-        }
+        for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
       }
       __syncthreads();
       if (tid < 64) {
-        const int tau = t0 + 16 * pass + (tid >> 2), p = tid & 3;
+        const int tau = t0 + 16 * half + (tid >> 2), p = tid & 3;
         if (tau < tiles) {
           const int b = tau / TB, lt = tau - b * TB;
           const int ty = lt / TW, tx = lt - ty * TW;
@@ -543,7 +355,7 @@ void wino_conv_kernel(
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int tau = t0 + mb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    const int tau = t0 + (i & 3) + 8 * (i >> 2) + 4 * h;
     if (tau >= tiles) continue;
     const int b = tau / TB, lt = tau - b * TB;
     const int ty = lt / TW, tx = lt - ty * TW;
@@ -565,16 +377,9 @@ size_t wino_pack_index(int xi, int cin, int cout) {
   return (((((size_t)c * 16 + xi) * 4 + nb) * QB + q) * 64 + lane) * 4 + e;
 }
 
-// sign folded into U for the corner points the kernel accumulates directly
-int wino_fold_sign(int xi) {
-  if (wino_corner_pixel(xi) < 0) return 1;
-  const int a = xi >> 2, b = xi & 3;
-  return wino_sign(a, a == 3 ? 1 : 0) * wino_sign(b, b == 3 ? 1 : 0);
-}
-
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
-                      int n_max, int H, int W, hipStream_t s, int pipe, const HeadConv* heads) {
+                      int n_max, int H, int W, hipStream_t s, const HeadConv* heads) {
   const int TB = ((H + 1) / 2) * ((W + 1) / 2);
   const int grid = (n_max * TB + kWinoTiles - 1) / kWinoTiles;
   if (grid <= 0) return;
@@ -584,32 +389,14 @@ void launch_wino_conv(const float* in, const float* res_in, const float* upack,
   HeadConv hc{};
   if (heads && heads->feat) {
     hc = *heads;
-    wino_conv_kernel<true, CK, 0, true><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
-    return;
-  }
-  // pipe: 0 = single V buffer, 1 = double buffer + register prefetch (CK 16
-  // only: at CK 32 the buffers would leave one workgroup per CU), 2 = warp-
-  // specialised producer wave (double buffer)
-  if constexpr (kWinoMB == 1) {  // the producer wave is wave 4: one M block only
-    if (pipe == 2) {
-      if (res_in)
-        wino_conv_kernel<true, CK, 2><<<grid, 320, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
-      else
-        wino_conv_kernel<false, CK, 2><<<grid, 320, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
-      return;
-    }
-  }
-  if (CK == 16 && pipe == 1) {
-    constexpr int P1 = CK == 16 ? 1 : 0;  // (no double-buffered instantiation at CK 32)
-    if (res_in)
-      wino_conv_kernel<true, CK, P1><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
-    else
-      wino_conv_kernel<false, CK, P1><<<grid, kWinoThreads, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
+    wino_conv_kernel<true, CK, true><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count,
+                                                                  n_max, H, W, hc);
+  } else if (res_in) {
+    wino_conv_kernel<true, CK, false><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count,
+                                                                   n_max, H, W, hc);
   } else {
-    if (res_in)
-      wino_conv_kernel<true, CK, 0><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H, W, hc);
-    else
-      wino_conv_kernel<false, CK, 0><<<grid, kWinoThreads, 0, s>>>(in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
+    wino_conv_kernel<false, CK, false><<<grid, kWinoThreads, 0, s>>>(in, nullptr, u, nullptr, bias, out,
+                                                                    count, n_max, H, W, hc);
   }
 }
 
