@@ -36,3 +36,14 @@ def test_struct_sizes_match_header():
     assert ctypes.sizeof(az.Config) == 4 * 6 + 8 + 4 * 5 + 4 + 8 + 8 + 8 + 32
     assert ctypes.sizeof(az.Tensor) == 8 + 8 + 8 + 4 + 4
     assert ctypes.sizeof(az.Stats) == 8 * 8 + 8 + 8 * 7
+
+
+def test_engine_fails_loudly_without_gpu():
+    """No CPU fallback: without a visible HIP device the engine refuses to
+    start (the product path never routes through the oracle)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from custom_alphazero import engine as az
+    with pytest.raises(az.AzError, match="no HIP device"):
+        az.Engine(6, 7, 4, True, 10, slots=4, evaluator=az.EVAL_SYNTHETIC)

@@ -239,3 +239,31 @@ def test_selfplay_synthetic_board_shapes_vs_oracle(cfg, cache_log2):
             np.testing.assert_array_equal(got[g]["boards"], ref["boards"])
             assert got[g]["expansions"] == ref["expansions"]
         eng.close()
+
+
+def test_abi_error_behaviour():
+    """Invalid arguments and states come back as AzError with a message (the
+    ABI returns a negative code + az_last_error); nothing aborts."""
+    with pytest.raises(az.AzError, match="n <= min"):
+        az.Engine(6, 7, 7, True, 10, slots=4, evaluator=az.EVAL_SYNTHETIC)
+    with pytest.raises(az.AzError, match="conv_algo"):
+        az.Engine(6, 7, 4, True, 10, slots=4, evaluator=az.EVAL_NETWORK, conv_algo=5)
+    with pytest.raises(az.AzError, match="lanes"):
+        az.Engine(6, 7, 4, True, 10, slots=4, evaluator=az.EVAL_SYNTHETIC, lanes=-1)
+    eng = az.Engine(6, 7, 4, True, 10, slots=4, evaluator=az.EVAL_NETWORK)
+    with pytest.raises(az.AzError, match="set_weights"):
+        eng.forward(np.zeros((1, 6, 7, 4), np.float32))
+    with pytest.raises(az.AzError, match="set_weights"):
+        eng.selfplay_run(0, 2, 0)
+    eng.close()
+    # a tree arena too small for the search is reported, not overrun
+    eng = az.Engine(6, 7, 4, True, 50, slots=2, evaluator=az.EVAL_SYNTHETIC, arena_edges=64)
+    with pytest.raises(az.AzError, match="arena-overflow"):
+        eng.selfplay_run(0, 2, 0)
+    eng.close()
+    # play before any search
+    eng = az.Engine(6, 7, 4, True, 10, slots=1, evaluator=az.EVAL_SYNTHETIC)
+    eng.tree_reset([0], np.zeros((1, 6, 7), np.int8))
+    with pytest.raises(az.AzError, match="play-before-search"):
+        eng.tree_play([0.5])
+    eng.close()
