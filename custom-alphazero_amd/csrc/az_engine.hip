@@ -7,7 +7,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <chrono>
 #include <map>
 #include <string>
 #include <vector>
@@ -765,7 +764,6 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
   int rc;
   if ((rc = ready_to_search(e))) return rc;
   AZ_HIP(hipSetDevice(e->device));
-  const auto t_start = std::chrono::steady_clock::now();
   for (int mv = 0; mv < n_moves; ++mv) {
     // lanes interleaved per simulation so every stream always has work queued
     for (int s = 0; s < e->g.sims; ++s)
@@ -774,10 +772,7 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
     for (Lane* L : e->lanes) az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
     AZ_HIP(hipGetLastError());
   }
-  static const bool dbg = getenv("AZ_DEBUG_TIMING") != nullptr;
-  if (dbg) {
-    const double t_enq = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-    if ((rc = sync_all(e))) return rc;
+  if ((rc = sync_all(e))) return rc;
     const double t_all = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     fprintf(stderr, "selfplay_step: %d moves, enqueue %.1f ms, total %.1f ms\n", n_moves, 1e3 * t_enq, 1e3 * t_all);
   }
