@@ -773,10 +773,6 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
     AZ_HIP(hipGetLastError());
   }
   if ((rc = sync_all(e))) return rc;
-    const double t_all = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-    fprintf(stderr, "selfplay_step: %d moves, enqueue %.1f ms, total %.1f ms\n", n_moves, 1e3 * t_enq, 1e3 * t_all);
-  }
-  if ((rc = sync_all(e))) return rc;
   if ((rc = check_device_errors(e))) return rc;
   if (st) return az_stats_get(e, st);
   return 0;
