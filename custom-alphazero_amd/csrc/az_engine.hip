@@ -37,6 +37,11 @@ double (*volatile g_pow)(double, double) = pow;
 
 }  // namespace
 
+namespace az {
+// error reporting for the other ABI translation units (az_chess.hip)
+int fail_abi(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace az
+
 // A lane = a contiguous group of slots searched on its own HIP stream.  Lanes
 // share the network, the transposition cache, the sample sink and the
 // counters; each owns its eval queue, per-simulation dedup table and slices

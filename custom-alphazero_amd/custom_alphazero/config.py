@@ -29,8 +29,15 @@ class ConfigSelfPlay:
 class ConfigChess:
     piece_symbols = [None, "p", "n", "b", "r", "q", "k"]
     initial_board_fen = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR"
+    initial_turn = "w"
+    initial_castling_rights = "KQkq"
+    initial_ep_quare = "-"
+    initial_halfmove_clock = "0"
+    initial_fullmove_number = "1"
     board_size = 8
     number_unique_pieces = 12
+    # addition: HIP device the chess board kernels run on (include/az_chess.h)
+    device = 0
 
 
 class ConfigConnectN:

@@ -60,6 +60,8 @@ EXPORTED = (
     "az_selfplay_run", "az_selfplay_results", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
     "az_cache_clear", "az_cache_enable",
+    # include/az_chess.h
+    "az_chess_all_moves", "az_chess_legal", "az_chess_encode", "az_chess_play", "az_chess_perft",
 )
 
 _lib = None
@@ -106,6 +108,11 @@ def load_library():
         "az_pow_table": (ctypes.c_int, [P, P, I64]),
         "az_cache_clear": (ctypes.c_int, [P]),
         "az_cache_enable": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_chess_all_moves": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_chess_legal": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P, P, P, P]),
+        "az_chess_encode": (ctypes.c_int, [ctypes.c_int, P, P, ctypes.c_int, P]),
+        "az_chess_play": (ctypes.c_int, [ctypes.c_int, P, P, ctypes.c_int, ctypes.c_int]),
+        "az_chess_perft": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

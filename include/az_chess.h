@@ -1,0 +1,86 @@
+/*
+ * az_chess.h -- C ABI of libaz's chess board kernels (gfx950).
+ *
+ * Replaces the reference's chess board seam (custom_alphazero/chess/), which
+ * is a subclass of python-chess 1.9.4 (poetry.lock:227-228): the hot path's
+ * "board-tensor encode + legal-move mask" for chess.
+ * Each call below is batched over n positions and runs on the GPU; the Python
+ * drop-in (custom_alphazero/chess/board.py) binds them with ctypes.
+ *
+ * Conventions as in az.h: 0 or a negative AZ_E* code, az_last_error() holds
+ * the message; host buffers owned by the caller; synchronous.  `device` is a
+ * HIP device ordinal; each call uses a per-device stream and scratch of the
+ * library's own.
+ *
+ * Squares are python-chess's (A1 = 0 .. H8 = 63).  A move is a uint16:
+ * from | to << 6 | promotion << 12, promotion = python-chess piece type
+ * (0 none, 2 knight, 3 bishop, 4 rook, 5 queen).
+ */
+#ifndef AZ_CHESS_H_
+#define AZ_CHESS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AZ_CHESS_MAX_MOVES 256  /* > 218, the most legal moves of any position */
+#define AZ_CHESS_ACTIONS 1880   /* len(get_all_possible_moves()) (chess/utils.py:11-32) */
+#define AZ_CHESS_HISTORY 8      /* Board(history_size=8) (chess/board.py:17) */
+#define AZ_CHESS_PLANES 118     /* 8 x (13 one-hot + repetition) + 6 (chess/board.py:55-73) */
+
+/* A python-chess Board's position state (80 bytes).  The repetition flag is
+ * the value Board.state's last plane carries (is_repetition()). */
+typedef struct az_chess_pos {
+    uint64_t pieces[6];        /* pawns, knights, bishops, rooks, queens, kings */
+    uint64_t occupied_co[2];   /* [0] BLACK, [1] WHITE */
+    uint64_t castling_rights;  /* rook squares (python-chess Board.castling_rights) */
+    int16_t ep_square;         /* -1 = None */
+    uint8_t turn;              /* 1 = WHITE */
+    uint8_t repetition;
+    uint16_t halfmove_clock;
+    uint16_t fullmove_number;
+} az_chess_pos;
+
+/* Termination codes of python-chess Board.outcome() (checked in this order) */
+#define AZ_CHESS_ONGOING 0
+#define AZ_CHESS_CHECKMATE 1
+#define AZ_CHESS_INSUFFICIENT 2
+#define AZ_CHESS_STALEMATE 3
+#define AZ_CHESS_SEVENTYFIVE 4
+
+/* get_all_possible_moves() (chess/utils.py:11-32): the action list, sorted by
+ * Move.__lt__ (chess/move.py:33-37).  cap >= AZ_CHESS_ACTIONS; returns the
+ * count (host-side table, no device work). */
+int az_chess_all_moves(uint16_t* out, int cap);
+
+/* Board.moves (chess/board.py:46-48: python-chess legal_moves, generation
+ * order), Board.legal_moves_mask(all_possible_moves) (:111-112) and
+ * is_game_over()/outcome() for n positions: moves [n][AZ_CHESS_MAX_MOVES],
+ * counts [n], mask [n][AZ_CHESS_ACTIONS] u8, outcome [n].  Any output except
+ * counts may be NULL. */
+int az_chess_legal(int device, const az_chess_pos* pos, int n, uint16_t* moves, int32_t* counts,
+                   uint8_t* mask, int32_t* outcome);
+
+/* Board.full_state (chess/board.py:55-73) for n boards: hist [n][8] oldest
+ * first (the state_history deque), valid [n][8] (0 = a zero-filled entry),
+ * the board itself is hist[i][7] (castling planes, fullmove, halfmove) ->
+ * state [n][8][8][118] f32, rows = ranks 8..1 as Board.array (every value is
+ * a small integer: exact in f32; the reference's float64 casts exactly). */
+int az_chess_encode(int device, const az_chess_pos* hist, const uint8_t* valid, int n,
+                    float* state);
+
+/* Board.play(move, keep_same_player=...) (chess/board.py:162-173) in place on
+ * n positions: push, then (keep_same_player) mirror + turn = WHITE. */
+int az_chess_play(int device, az_chess_pos* pos, const uint16_t* moves, int n,
+                  int keep_same_player);
+
+/* perft(depth) node count (legal move generation + push, breadth first on the
+ * device): the size-independent check of the move generator. */
+int az_chess_perft(int device, const az_chess_pos* pos, int depth, uint64_t* nodes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,179 @@
+"""ctypes front-end of the chess oracle (oracle/chess_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ and __graft_entry__.smoke(),
+never by the product package.  It checks the HIP chess kernels
+(csrc/az_chess.hip).  Its legal-move sets are pinned by published perft
+counts (tests/test_chess_oracle.py); generation order, history planes and
+outcome rules restate python-chess 1.9.4 and are "parity unpinned" (python-chess
+is absent here, the reference holds no chess fixture).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libchess_oracle.so")
+
+# az_chess_pos (include/az_chess.h) as a numpy record: 80 bytes
+POS_DTYPE = np.dtype([
+    ("pieces", "<u8", (6,)), ("occupied_co", "<u8", (2,)), ("castling_rights", "<u8"),
+    ("ep_square", "<i2"), ("turn", "u1"), ("repetition", "u1"),
+    ("halfmove_clock", "<u2"), ("fullmove_number", "<u2"),
+])
+assert POS_DTYPE.itemsize == 80
+
+START_FEN = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+PIECE_TYPES = {0: "", 2: "n", 3: "b", 4: "r", 5: "q"}
+OUTCOMES = {0: None, 1: "checkmate", 2: "insufficient_material", 3: "stalemate",
+            4: "seventyfive_moves"}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.orc_chess_pos_size.restype = ctypes.c_int
+        assert L.orc_chess_pos_size() == POS_DTYPE.itemsize
+        L.orc_chess_from_fen.argtypes = [ctypes.c_char_p, P]
+        L.orc_chess_legal.argtypes = [P, P]
+        L.orc_chess_legal.restype = ctypes.c_int
+        L.orc_chess_push.argtypes = [P, ctypes.c_uint16]
+        L.orc_chess_mirror.argtypes = [P]
+        L.orc_chess_play_canonical.argtypes = [P, ctypes.c_uint16]
+        L.orc_chess_outcome.argtypes = [P]
+        L.orc_chess_outcome.restype = ctypes.c_int
+        L.orc_chess_perft.argtypes = [P, ctypes.c_int]
+        L.orc_chess_perft.restype = ctypes.c_uint64
+        L.orc_chess_array.argtypes = [P, P]
+        L.orc_chess_full_state.argtypes = [P, P, P, P]
+        L.orc_chess_all_moves.argtypes = [P]
+        L.orc_chess_all_moves.restype = ctypes.c_int
+        L.orc_chess_legal_mask.argtypes = [P, P, ctypes.c_int, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def from_fen(fen=START_FEN):
+    p = np.zeros(1, POS_DTYPE)
+    if lib().orc_chess_from_fen(fen.encode(), _p(p)) != 0:
+        raise ValueError(fen)
+    return p[0]
+
+
+def _one(pos):
+    return np.array([pos], POS_DTYPE)
+
+
+def legal_moves(pos):
+    out = np.zeros(256, np.uint16)
+    n = lib().orc_chess_legal(_p(_one(pos)), _p(out))
+    return out[:n].copy()
+
+
+def push(pos, move):
+    p = _one(pos)
+    lib().orc_chess_push(_p(p), int(move))
+    return p[0]
+
+
+def mirror(pos):
+    p = _one(pos)
+    lib().orc_chess_mirror(_p(p))
+    return p[0]
+
+
+def play_canonical(pos, move):
+    """Board.play(move, keep_same_player=True) (chess/board.py:162-173)."""
+    p = _one(pos)
+    lib().orc_chess_play_canonical(_p(p), int(move))
+    return p[0]
+
+
+def outcome(pos):
+    return lib().orc_chess_outcome(_p(_one(pos)))
+
+
+def perft(pos, depth):
+    return int(lib().orc_chess_perft(_p(_one(pos)), depth))
+
+
+def array(pos):
+    out = np.zeros(64, np.int8)
+    lib().orc_chess_array(_p(_one(pos)), _p(out))
+    return out.reshape(8, 8)
+
+
+def full_state(hist, valid, cur):
+    """hist: 8 positions oldest first; valid: 8 flags; -> float64 [8][8][118]."""
+    h = np.array(hist, POS_DTYPE)
+    v = np.ascontiguousarray(valid, np.uint8)
+    out = np.zeros((8, 8, 118), np.float64)
+    lib().orc_chess_full_state(_p(h), _p(v), _p(_one(cur)), _p(out))
+    return out
+
+
+def reference_history(pos, is_root):
+    """The history deque the reference's boards carry in MCTS use: a fresh
+    Board() holds [0 x 7, state]; every board made by play() comes out of
+    python-chess's copy(), which re-runs the subclass __init__ (start
+    position), so it holds [0 x 6, start-position state, state]."""
+    start = from_fen(START_FEN)
+    hist = [start] * 8
+    valid = [0] * 8
+    hist[7], valid[7] = pos, 1
+    if not is_root:
+        hist[6], valid[6] = start, 1
+    return hist, valid
+
+
+def all_moves():
+    out = np.zeros(4096, np.uint16)
+    n = lib().orc_chess_all_moves(_p(out))
+    return out[:n].copy()
+
+
+def legal_mask(pos, all_mv):
+    all_mv = np.ascontiguousarray(all_mv, np.uint16)
+    mask = np.zeros(len(all_mv), np.uint8)
+    lib().orc_chess_legal_mask(_p(_one(pos)), _p(all_mv), len(all_mv), _p(mask))
+    return mask
+
+
+def uci(move):
+    f, t, pr = int(move) & 63, (int(move) >> 6) & 63, int(move) >> 12
+    sq = lambda s: "abcdefgh"[s & 7] + str((s >> 3) + 1)
+    return sq(f) + sq(t) + PIECE_TYPES[pr]
+
+
+def random_positions(n, seed, max_plies=200, canonical=True):
+    """Positions reached by seeded random playouts from the start position
+    (canonical = Board.play(keep_same_player=True) after every move, as in
+    MCTS).  Returns (positions, is_root flags)."""
+    rng = np.random.default_rng(seed)
+    out, roots = [], []
+    pos = from_fen()
+    is_root = True
+    ply = 0
+    while len(out) < n:
+        out.append(pos)
+        roots.append(is_root)
+        mv = legal_moves(pos)
+        if len(mv) == 0 or outcome(pos) != 0 or ply >= max_plies:
+            pos, is_root, ply = from_fen(), True, 0
+            continue
+        m = mv[rng.integers(len(mv))]
+        pos = play_canonical(pos, m) if canonical else push(pos, m)
+        is_root = False
+        ply += 1
+    return np.array(out, POS_DTYPE), np.array(roots, bool)

@@ -1,9 +1,10 @@
 """CPU checks of the drop-in boundary: libaz loads and exports every symbol
-include/az.h declares; the ctypes structs match the header layout."""
+include/*.h declares (az.h, az_chess.h); the ctypes structs match the header layout."""
 import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 from custom_alphazero import engine as az
@@ -12,8 +13,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    src = open(os.path.join(REPO, "include", "az.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(az_\w+)\(", src, re.M)))
+    names = set()
+    for h in sorted(os.listdir(os.path.join(REPO, "include"))):
+        if h.endswith(".h"):
+            src = open(os.path.join(REPO, "include", h)).read()
+            names |= set(re.findall(r"^(?:int|const char\*)\s+(az_\w+)\(", src, re.M))
+    return sorted(names)
 
 
 def test_header_and_binding_agree():
@@ -47,3 +52,17 @@ def test_engine_fails_loudly_without_gpu():
     from custom_alphazero import engine as az
     with pytest.raises(az.AzError, match="no HIP device"):
         az.Engine(6, 7, 4, True, 10, slots=4, evaluator=az.EVAL_SYNTHETIC)
+
+
+def test_chess_kernels_fail_loudly_without_gpu():
+    """The chess board seam has no CPU fallback either."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from custom_alphazero.chess import kernels as K
+    from custom_alphazero.chess.board import Board
+    b = Board()  # construction is host bookkeeping only
+    with pytest.raises(az.AzError, match="no HIP device"):
+        b.moves
+    with pytest.raises(az.AzError, match="no HIP device"):
+        K.encode(np.zeros((1, 8), K.POS_DTYPE), np.ones((1, 8), np.uint8))
