@@ -33,7 +33,30 @@ constexpr bb DARK = 0xAA55AA55AA55AA55ull;
 // direction rays from each square, empty board, origin excluded.
 // d: 0 N(+8) 1 NE(+9) 2 E(+1) 3 NW(+7) | 4 S(-8) 5 SW(-9) 6 W(-1) 7 SE(-7)
 // (0-3 increase the square index: first blocker = lowest bit; 4-7: highest)
-extern __constant__ bb c_rays[8][64];
+// Each translation unit that includes this header owns a copy and uploads it
+// with upload_rays() once per device before its first launch.
+static __constant__ bb c_rays[8][64];
+
+static inline void host_rays(uint64_t rays[8][64]) {
+  const int dirs[8][2] = {{0, 1}, {1, 1}, {1, 0}, {-1, 1}, {0, -1}, {-1, -1}, {-1, 0}, {1, -1}};
+  for (int d = 0; d < 8; ++d)
+    for (int s = 0; s < 64; ++s) {
+      uint64_t r = 0;
+      int f = (s & 7) + dirs[d][0], k = (s >> 3) + dirs[d][1];
+      while (f >= 0 && f < 8 && k >= 0 && k < 8) {
+        r |= 1ull << (k * 8 + f);
+        f += dirs[d][0];
+        k += dirs[d][1];
+      }
+      rays[d][s] = r;
+    }
+}
+// for the current device (hipSetDevice first)
+static inline hipError_t upload_rays() {
+  uint64_t rays[8][64];
+  host_rays(rays);
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_rays), rays, sizeof(rays));
+}
 
 AZC_HD bb sq_bb(int s) { return 1ull << s; }
 AZC_HD int msb(bb x) { return 63 - __clzll(x); }

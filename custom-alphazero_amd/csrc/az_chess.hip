@@ -18,25 +18,7 @@ int fail_abi(int code, const std::string& msg);  // az_engine.hip (az_last_error
 
 namespace azc {
 
-__constant__ bb c_rays[8][64];
-
 namespace {
-
-constexpr int kDirs[8][2] = {{0, 1}, {1, 1}, {1, 0}, {-1, 1}, {0, -1}, {-1, -1}, {-1, 0}, {1, -1}};
-
-void host_rays(uint64_t rays[8][64]) {
-  for (int d = 0; d < 8; ++d)
-    for (int s = 0; s < 64; ++s) {
-      uint64_t r = 0;
-      int f = (s & 7) + kDirs[d][0], k = (s >> 3) + kDirs[d][1];
-      while (f >= 0 && f < 8 && k >= 0 && k < 8) {
-        r |= 1ull << (k * 8 + f);
-        f += kDirs[d][0];
-        k += kDirs[d][1];
-      }
-      rays[d][s] = r;
-    }
-}
 
 // get_all_possible_moves() (chess/utils.py:11-32), derived directly: queen
 // and knight moves from every square of an empty board, plus the white
@@ -84,6 +66,8 @@ const std::vector<uint16_t>& all_moves() {
   return mv;
 }
 
+}  // namespace
+
 // move -> action index table [from][to][promo slot], -1 = not an action
 std::vector<int16_t> action_lut() {
   std::vector<int16_t> lut(64 * 64 * 5, -1);
@@ -95,6 +79,8 @@ std::vector<int16_t> action_lut() {
   }
   return lut;
 }
+
+namespace {
 
 // per-device state: stream, tables, action table
 struct DevCtx {
@@ -122,9 +108,7 @@ int ctx_for(int device, DevCtx** out) {
   std::lock_guard<std::mutex> lk(g_mu);
   DevCtx& c = g_ctx[device];
   if (!c.ready) {
-    uint64_t rays[8][64];
-    host_rays(rays);
-    AZC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_rays), rays, sizeof(rays)));
+    AZC_HIP(upload_rays());
     AZC_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     std::vector<int16_t> lut = action_lut();
     AZC_HIP(hipMalloc(&c.lut, lut.size() * sizeof(int16_t)));

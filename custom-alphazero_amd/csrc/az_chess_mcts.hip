@@ -1,0 +1,943 @@
+// az_chess_mcts.hip -- chess self-play on gfx950 (BASELINE configs[4]):
+// the MCTS of custom_alphazero/mcts/mcts.py over the chess rules of
+// az_chess.h, with the policy/value network of az_nn.hip on 118-plane states.
+//
+// One simulation for every game slot per step, as in the Connect-N engine
+// (az_tree.hip), but a chess node has up to 218 edges and a game has no fixed
+// length, so:
+//   select   one wave per slot: PUCT over the node's edges (4 per lane),
+//            ΣN and first-max argmax by wave shuffles, the position replayed
+//            along the path with push + mirror (no boards stored per node)
+//   leaf     one thread per slot: legal moves + outcome of the leaf; terminal
+//            leaves back up get_result's value, the rest join the eval queue
+//   encode   one workgroup per queued board: Board.full_state planes straight
+//            into the network input (padded to 128 channels)
+//   expand   one wave per queued board: priors = probs[mask] renormalised in
+//            action order (float32 pairwise sum) and zipped positionally with
+//            python-chess's move order (mcts.py:147-160), edges allocated, backup
+//   play     one wave per slot: MCTS.play policy + np.random.choice, sample
+//            record, and the chosen child's subtree copied (Cheney scan) into
+//            the other half of the slot's edge arena (tree reuse,
+//            mcts.py:212), then the new root's game-over check and slot refill.
+// Arithmetic contract as az_tree.hip (this file builds with -ffp-contract=off).
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/az_chess.h"
+#include "az_chess.h"
+#include "az_nn.h"
+#include "az_tree.h"
+
+namespace az {
+int fail_abi(int code, const std::string& msg);
+}
+
+namespace azc {
+std::vector<int16_t> action_lut();  // az_chess.hip
+
+namespace {
+
+using az::Edge;
+
+struct CCfg {
+  int slots, sims, greedy_ply, half_cap, max_depth, max_plies, pow_len, evaluator;
+  double c_puct;
+};
+
+struct CTree {
+  Edge* edges;             // [slots][2][half_cap]
+  az_chess_pos* root;      // [slots]
+  int32_t* root_first;     // [slots]
+  int32_t* root_n;         // [slots]
+  int32_t* half;           // [slots] arena half holding the live tree
+  int32_t* top;            // [slots] edges used in that half
+  int32_t* ply;            // [slots]
+  int32_t* initial;        // [slots] root is the game's Board() (history [0 x 7, state])
+  int64_t* game_id;        // [slots], -1 idle
+  int32_t* path;           // [slots][max_depth]
+  int32_t* path_len;       // [slots]
+  az_chess_pos* leaf;      // [slots]
+  uint16_t* leaf_moves;    // [slots][AZ_CHESS_MAX_MOVES]
+  int32_t* leaf_n;         // [slots]
+  int32_t* slot_exp;       // [slots]
+  uint32_t* mt;            // [625][slots] word-major MT19937
+  int32_t* eval_slot;      // [slots]
+  int32_t* eval_count;     // [1]
+  unsigned long long* stats;
+  const double* powtab;
+  const int16_t* lut;
+};
+
+struct CSamples {
+  int64_t first_game = 0, n_games = 0;
+  uint32_t base_seed = 0;
+  int plies = 0;
+  az_chess_pos* pos = nullptr;   // [G][P]
+  uint16_t* moves = nullptr;     // [G][P]
+  int32_t* pol_n = nullptr;      // [G][P]
+  int16_t* pol_a = nullptr;      // [G][P][256]
+  double* pol_p = nullptr;       // [G][P][256]
+  int32_t* length = nullptr;     // [G]
+  int32_t* result = nullptr;
+  int32_t* term = nullptr;
+  int32_t* expansions = nullptr;
+};
+
+constexpr int kMtN = 624;
+
+__device__ __forceinline__ Edge* arena(const CCfg& g, const CTree& t, int s, int h) {
+  return t.edges + ((size_t)s * 2 + h) * g.half_cap;
+}
+__device__ __forceinline__ void flag(const CTree& t, unsigned long long f) {
+  atomicOr(t.stats + az::kStatErrors, f);
+}
+
+// MT19937 per slot, word-major (az_tree.hip layout)
+__device__ void mt_seed(const CTree& t, int slots, int s, uint32_t seed) {
+  uint32_t prev = seed;
+  t.mt[s] = seed;
+  for (int i = 1; i < kMtN; ++i) {
+    prev = 1812433253u * (prev ^ (prev >> 30)) + (uint32_t)i;
+    t.mt[(size_t)i * slots + s] = prev;
+  }
+  t.mt[(size_t)kMtN * slots + s] = kMtN;
+}
+__device__ uint32_t mt_next(const CTree& t, int slots, int s) {
+  uint32_t* m = t.mt;
+  uint32_t pos = m[(size_t)kMtN * slots + s];
+  if (pos >= (uint32_t)kMtN) {
+    for (int i = 0; i < kMtN; ++i) {
+      const uint32_t y = (m[(size_t)i * slots + s] & 0x80000000u) |
+                         (m[(size_t)((i + 1) % kMtN) * slots + s] & 0x7fffffffu);
+      m[(size_t)i * slots + s] =
+          m[(size_t)((i + 397) % kMtN) * slots + s] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    pos = 0;
+  }
+  const uint32_t y = m[(size_t)pos * slots + s];
+  m[(size_t)kMtN * slots + s] = pos + 1;
+  return az::mt_temper(y);
+}
+__device__ double mt_uniform(const CTree& t, int slots, int s) {
+  const uint32_t a = mt_next(t, slots, s) >> 5;
+  const uint32_t b = mt_next(t, slots, s) >> 6;
+  return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+
+// numpy pairwise add.reduce (identity 0 + pairwise_sum, blocks of 128, 8
+// accumulators) for n <= 256 (at most two levels of splitting)
+template <typename T>
+__device__ T pw_block(const T* a, int n) {
+  if (n < 8) {
+    T r = (T)0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  T r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+template <typename T>
+__device__ T pw_136(const T* a, int n) {
+  if (n <= 128) return pw_block(a, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_block(a, n2) + pw_block(a + n2, n - n2);
+}
+template <typename T>
+__device__ T pairwise(const T* a, int n) {
+  if (n <= 128) return pw_block(a, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_136(a, n2) + pw_136(a + n2, n - n2);
+}
+
+__device__ __forceinline__ void backup(Edge* E, const int32_t* path, int depth, double v) {
+  for (int d = depth - 1; d >= 0; --d) {
+    Edge& e = E[path[d]];
+    e.N += 1;
+    e.W += v;
+    v = -v;
+  }
+}
+
+__device__ Pos start_pos() {
+  Pos q;
+  q.p[0] = 0x00FF00000000FF00ull;  // pawns
+  q.p[1] = 0x4200000000000042ull;  // knights
+  q.p[2] = 0x2400000000000024ull;  // bishops
+  q.p[3] = 0x8100000000000081ull;  // rooks
+  q.p[4] = 0x0800000000000008ull;  // queens
+  q.p[5] = 0x1000000000000010ull;  // kings
+  q.co[1] = 0x000000000000FFFFull;
+  q.co[0] = 0xFFFF000000000000ull;
+  q.castling = 0x8100000000000081ull;
+  q.ep = -1;
+  q.turn = 1;
+  q.rep = 0;
+  q.half = 0;
+  q.full = 1;
+  return q;
+}
+
+__device__ void slot_reset(const CCfg& g, const CTree& t, const CSamples& smp, int s, int64_t gid) {
+  az_chess_pos a;
+  store_pos(start_pos(), a);
+  t.root[s] = a;
+  t.root_first[s] = 0;
+  t.root_n[s] = 0;
+  t.half[s] = 0;
+  t.top[s] = 0;
+  t.ply[s] = 0;
+  t.initial[s] = 1;
+  t.path_len[s] = 0;
+  t.slot_exp[s] = 0;
+  t.game_id[s] = gid;
+  mt_seed(t, g.slots, s, smp.base_seed + (uint32_t)gid);
+}
+
+// synthetic evaluator (oracle/chess_oracle.c orc_chess_synth): dyadic priors
+// k/64 and values k/128 from a hash of the position the network would see
+__device__ uint64_t pos_hash(const Pos& q, int initial) {
+  uint64_t h = az::splitmix64(q.p[0]);
+  for (int i = 1; i < 6; ++i) h = az::splitmix64(h ^ q.p[i]);
+  h = az::splitmix64(h ^ q.co[0]);
+  h = az::splitmix64(h ^ q.co[1]);
+  h = az::splitmix64(h ^ q.castling);
+  const uint64_t misc = (uint64_t)(uint16_t)q.ep | ((uint64_t)(uint16_t)q.half << 16) |
+                        ((uint64_t)(uint16_t)q.full << 32) | ((uint64_t)initial << 48);
+  return az::splitmix64(h ^ misc);
+}
+
+// ----------------------------------------------------------------- kernels
+
+__global__ void slot_init_kernel(CCfg g, CTree t, CSamples smp, int64_t n_first) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.slots) return;
+  if (s < n_first) slot_reset(g, t, smp, s, smp.first_game + s);
+  else t.game_id[s] = -1;
+}
+
+// MCTS.select (mcts.py:111-120): one wave per slot
+__global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  if (t.game_id[s] < 0) return;
+  const Edge* E = arena(g, t, s, t.half[s]);
+  int32_t* path = t.path + (size_t)s * g.max_depth;
+  Pos q = load_pos(t.root[s]);
+  int first = t.root_first[s], cnt = t.root_n[s];
+  int depth = 0;
+  while (cnt > 0) {
+    int sum = 0;
+    for (int j = lane; j < cnt; j += 64) sum += E[first + j].N;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    if (sum >= g.pow_len) {
+      if (lane == 0) flag(t, az::kErrPow);
+      return;
+    }
+    const double sq = t.powtab[sum];
+    double best_v = -INFINITY;
+    int best = 1 << 30;
+    for (int j = lane; j < cnt; j += 64) {
+      const Edge e = E[first + j];
+      const double qv = e.N ? e.W / (double)e.N : 0.0;
+      const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
+      const double v = qv + u;
+      if (v > best_v) {  // within a lane j increases: strict > keeps the first
+        best_v = v;
+        best = j;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(best_v, off, 64);
+      const int oj = __shfl_xor(best, off, 64);
+      if (ov > best_v || (ov == best_v && oj < best)) {  // np.argmax: first maximum
+        best_v = ov;
+        best = oj;
+      }
+    }
+    if (depth >= g.max_depth) {
+      if (lane == 0) flag(t, az::kErrPath);
+      return;
+    }
+    const Edge e = E[first + best];
+    if (lane == 0) path[depth] = first + best;
+    ++depth;
+    play(q, (uint16_t)e.action, true);  // Board.play(keep_same_player=True)
+    first = e.child;
+    cnt = e.child < 0 ? 0 : e.child_n;
+  }
+  if (lane == 0) {
+    store_pos(q, t.leaf[s]);
+    t.path_len[s] = depth;
+  }
+}
+
+// the leaf's is_game_over() (mcts.py:173-179): terminal leaves back up the
+// canonical get_result (1 checkmate, 0 draw); others are queued for evaluation
+__global__ __launch_bounds__(128) void leaf_kernel(CCfg g, CTree t) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.slots || t.game_id[s] < 0) return;
+  const Pos q = load_pos(t.leaf[s]);
+  bool check;
+  const int n = legal_moves(q, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check);
+  if (n < 0) {
+    flag(t, az::kErrIllegal);
+    return;
+  }
+  t.leaf_n[s] = n;
+  const int oc = outcome(q, n, check);
+  if (oc != AZ_CHESS_ONGOING) {
+    Edge* E = arena(g, t, s, t.half[s]);
+    backup(E, t.path + (size_t)s * g.max_depth, t.path_len[s], oc == AZ_CHESS_CHECKMATE ? 1.0 : 0.0);
+    atomicAdd(t.stats + az::kStatTerminal, 1ull);
+  } else {
+    const int qi = atomicAdd(t.eval_count, 1);
+    t.eval_slot[qi] = s;
+  }
+  atomicAdd(t.stats + az::kStatSims, 1ull);
+}
+
+// Board.full_state of the queued leaves into the network input [q][64][128]:
+// history [0 x 6, start position, board] (every board made by play(), see
+// chess/board.py docstring) or [0 x 7, board] for a game's first Board();
+// planes 118..127 are the zero padding of the stem.
+__global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, float4* __restrict__ x) {
+  __shared__ Pos sp[2];
+  __shared__ float feat[6];
+  __shared__ int initial;
+  const int n = *t.eval_count;
+  for (int b = blockIdx.x; b < n; b += gridDim.x) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int s = t.eval_slot[b];
+      sp[0] = start_pos();
+      sp[1] = load_pos(t.leaf[s]);
+      initial = t.path_len[s] == 0 && t.initial[s];
+      const Pos& cur = sp[1];
+      const bb c = clean_castling(cur);
+      const bb back_t = cur.turn ? RANK_1 : RANK_8, back_o = cur.turn ? RANK_8 : RANK_1;
+      feat[0] = (c & FILE_A & back_t) != 0;
+      feat[1] = (c & FILE_H & back_t) != 0;
+      feat[2] = (c & FILE_A & back_o) != 0;
+      feat[3] = (c & FILE_H & back_o) != 0;
+      feat[4] = (float)cur.full;
+      feat[5] = (float)cur.half;
+    }
+    __syncthreads();
+    float4* o = x + (size_t)b * 64 * 32;
+    for (int e = threadIdx.x; e < 64 * 32; e += blockDim.x) {
+      const int pix = e >> 5, k0 = (e & 31) * 4;
+      const int sq = (7 - (pix >> 3)) * 8 + (pix & 7);
+      const int cur_idx = onehot_index(sp[1], sq), st_idx = onehot_index(sp[0], sq);
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + i;
+        float val = 0.f;
+        if (k >= 112 && k < 118) val = feat[k - 112];
+        else if (k >= 98 && k < 112) val = k - 98 == 13 ? (float)sp[1].rep : (cur_idx == k - 98 ? 1.f : 0.f);
+        else if (k >= 84 && k < 98 && !initial) val = k - 84 == 13 ? 0.f : (st_idx == k - 84 ? 1.f : 0.f);
+        v[i] = val;
+      }
+      o[e] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(CCfg g, CTree t, float* probs, float* values) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= *t.eval_count) return;
+  const int s = t.eval_slot[b];
+  const Pos q = load_pos(t.leaf[s]);
+  const uint64_t h = pos_hash(q, t.path_len[s] == 0 && t.initial[s]);
+  const uint64_t vh = az::splitmix64(h ^ 0x5555555555555555ull);
+  values[b] = (float)(((double)(vh >> 56) - 128.0) / 128.0);
+  float* p = probs + (size_t)b * AZ_CHESS_ACTIONS;
+  if ((vh & 0x3F) == 0) {
+    for (int a = 0; a < AZ_CHESS_ACTIONS; ++a) p[a] = 0.f;
+    return;
+  }
+  uint64_t w = h;
+  for (int a = 0; a < AZ_CHESS_ACTIONS; ++a) {
+    if (a && a % 12 == 0) w = az::splitmix64(w);
+    p[a] = (float)((double)(((w >> (5 * (a % 12))) & 31) + 1) / 64.0);
+  }
+}
+
+// MCTS.evaluate_and_expand (mcts.py:145-161) + backup, one wave per queued leaf
+__global__ __launch_bounds__(64) void expand_kernel(CCfg g, CTree t, const float* __restrict__ probs,
+                                                    const float* __restrict__ values) {
+  __shared__ int act[AZ_CHESS_MAX_MOVES];
+  __shared__ float sorted[AZ_CHESS_MAX_MOVES];
+  __shared__ double prior[AZ_CHESS_MAX_MOVES];
+  __shared__ int first_s;
+  const int lane = threadIdx.x;
+  const int n_q = *t.eval_count;
+  for (int b = blockIdx.x; b < n_q; b += gridDim.x) {
+    const int s = t.eval_slot[b];
+    const int n = t.leaf_n[s];
+    const uint16_t* mv = t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES;
+    const float* pr = probs + (size_t)b * AZ_CHESS_ACTIONS;
+    __syncthreads();
+    for (int j = lane; j < n; j += 64) {
+      const int a = action_of(t.lut, mv[j]);
+      act[j] = a;
+      if (a < 0) flag(t, az::kErrIllegal);
+    }
+    __syncthreads();
+    // probabilities[legal_moves_mask]: the legal actions in action order
+    for (int j = lane; j < n; j += 64) {
+      const int a = act[j];
+      int r = 0;
+      for (int i = 0; i < n; ++i) r += act[i] < a;
+      sorted[r] = a >= 0 ? pr[a] : 0.f;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      // normalize_probabilities (mcts/utils.py:4-16)
+      const float sum = pairwise(sorted, n);
+      if (sum == 0.0f) {
+        for (int i = 0; i < n; ++i) prior[i] = 1.0 / (double)n;
+      } else {
+        for (int i = 0; i < n; ++i) prior[i] = (double)(float)(sorted[i] / sum);
+      }
+      const int first = t.top[s];
+      if (first + n > g.half_cap) {
+        flag(t, az::kErrArena);
+        first_s = -1;
+      } else {
+        t.top[s] = first + n;
+        first_s = first;
+      }
+    }
+    __syncthreads();
+    const int first = first_s;
+    if (first < 0) continue;
+    Edge* E = arena(g, t, s, t.half[s]);
+    // zip(probabilities, node.board.moves): positional, python-chess move order
+    for (int j = lane; j < n; j += 64) {
+      Edge e;
+      e.W = 0.0;
+      e.prior = prior[j];
+      e.N = 0;
+      e.child = az::kNoChild;
+      e.child_n = 0;
+      e.action = (int16_t)mv[j];
+      e.child_value = 0.f;
+      E[first + j] = e;
+    }
+    if (lane == 0) {
+      const int depth = t.path_len[s];
+      const int32_t* path = t.path + (size_t)s * g.max_depth;
+      const float value = values[b];
+      if (depth == 0) {
+        t.root_first[s] = first;
+        t.root_n[s] = n;
+      } else {
+        Edge& pe = E[path[depth - 1]];
+        pe.child = first;
+        pe.child_n = (int16_t)n;
+        pe.child_value = value;
+      }
+      backup(E, path, depth, -(double)value);
+      t.slot_exp[s] += 1;
+      atomicAdd(t.stats + az::kStatExpansions, 1ull);
+      atomicAdd(t.stats + az::kStatNNEvals, 1ull);
+    }
+  }
+}
+
+// MCTS.play (mcts.py:182-222) for every active slot + the self-play loop's
+// bookkeeping (self_play.py:59-82); one wave per slot
+__global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp) {
+  __shared__ double pi[AZ_CHESS_MAX_MOVES];
+  __shared__ int chosen;
+  __shared__ int done_code;
+  const int s = blockIdx.x, lane = threadIdx.x;
+  if (t.game_id[s] < 0) return;
+  const int h = t.half[s];
+  Edge* E = arena(g, t, s, h);
+  Edge* D = arena(g, t, s, 1 - h);
+  const int first = t.root_first[s], n = t.root_n[s];
+  if (n <= 0) {
+    if (lane == 0) flag(t, az::kErrNoRoot);
+    return;
+  }
+  const Pos root = load_pos(t.root[s]);
+  const int64_t gid = t.game_id[s];
+  const int64_t gi = gid - smp.first_game;
+  const int ply = t.ply[s];
+  for (int j = lane; j < n; j += 64) pi[j] = (double)E[first + j].N;
+  __syncthreads();
+  if (lane == 0) {
+    const bool greedy = root.full >= g.greedy_ply;  // self_play.py:62
+    if (greedy) {
+      int im = 0;
+      for (int i = 1; i < n; ++i)
+        if (pi[i] > pi[im]) im = i;
+      for (int i = 0; i < n; ++i) pi[i] = i == im ? 1.0 : 0.0;
+    } else {
+      const double sum = pairwise(pi, n);  // normalize_probabilities on float64 counts
+      for (int i = 0; i < n; ++i) pi[i] = sum == 0.0 ? 1.0 / (double)n : pi[i] / sum;
+    }
+    // np.random.choice(edges, 1, p): one random_sample, cumsum, normalise, searchsorted right
+    const double u = mt_uniform(t, g.slots, s);
+    double cdf[1];
+    double acc = 0.0, last;
+    for (int i = 0; i < n; ++i) acc += pi[i];
+    last = acc;
+    acc = 0.0;
+    int idx = 0;
+    for (int i = 0; i < n; ++i) {
+      acc += pi[i];
+      cdf[0] = acc / last;
+      if (cdf[0] <= u) idx = i + 1;
+    }
+    chosen = idx < n ? idx : n - 1;
+  }
+  __syncthreads();
+  const int c_idx = chosen;
+  const Edge c = E[first + c_idx];
+  // sample record (MCTS.play return_details: parent state, policy, move)
+  if (gi >= 0 && gi < smp.n_games && ply < smp.plies) {
+    const size_t r = (size_t)gi * smp.plies + ply;
+    for (int j = lane; j < n; j += 64) {
+      smp.pol_a[r * AZ_CHESS_MAX_MOVES + j] = (int16_t)action_of(t.lut, (uint16_t)E[first + j].action);
+      smp.pol_p[r * AZ_CHESS_MAX_MOVES + j] = pi[j];
+    }
+    if (lane == 0) {
+      smp.pos[r] = t.root[s];
+      smp.moves[r] = (uint16_t)c.action;
+      smp.pol_n[r] = n;
+    }
+  }
+  // tree reuse: copy the chosen child's subtree into the other half
+  // (Cheney scan: edges before `scan` point into D, edges after it into E)
+  int top = 0;
+  if (c.child >= 0) {
+    for (int j = lane; j < c.child_n; j += 64) D[j] = E[c.child + j];
+    top = c.child_n;
+  }
+  __syncthreads();
+  int scan = 0;
+  bool overflow = false;
+  while (scan < top) {
+    const int top0 = top;
+    const int j = scan + lane;
+    Edge e;
+    int need = 0;
+    if (j < top0) {
+      e = D[j];
+      if (e.child >= 0) need = e.child_n;
+    }
+    int incl = need;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    const int total = __shfl(incl, 63, 64);
+    if (top0 + total > g.half_cap) {
+      overflow = true;
+      break;
+    }
+    if (need) {
+      const int nf = top0 + incl - need;
+      for (int k = 0; k < need; ++k) D[nf + k] = E[e.child + k];
+      e.child = nf;
+      D[j] = e;
+    }
+    top = top0 + total;
+    scan = min(scan + 64, top0);
+    __syncthreads();
+  }
+  if (lane == 0) {
+    if (overflow) flag(t, az::kErrArena);
+    Pos nr = root;
+    play(nr, (uint16_t)c.action, true);
+    az_chess_pos a;
+    store_pos(nr, a);
+    t.root[s] = a;
+    t.half[s] = 1 - h;
+    t.top[s] = overflow ? 0 : top;
+    t.root_first[s] = 0;
+    t.root_n[s] = (c.child >= 0 && !overflow) ? c.child_n : 0;
+    t.ply[s] = ply + 1;
+    t.initial[s] = 0;
+    atomicAdd(t.stats + az::kStatPlies, 1ull);
+    // while not mcts.board.is_game_over() (self_play.py:59)
+    bool check;
+    const int nl = legal_moves(nr, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check);
+    int oc = nl < 0 ? AZ_CHESS_ONGOING : outcome(nr, nl, check);
+    if (oc == AZ_CHESS_ONGOING && ply + 1 >= g.max_plies) oc = AZ_CHESS_MAX_PLIES;
+    done_code = oc;
+  }
+  __syncthreads();
+  if (done_code != AZ_CHESS_ONGOING && lane == 0) {
+    if (gi >= 0 && gi < smp.n_games) {
+      smp.length[gi] = ply + 1;
+      smp.result[gi] = done_code == AZ_CHESS_CHECKMATE ? 1 : 0;
+      smp.term[gi] = done_code;
+      smp.expansions[gi] = t.slot_exp[s];
+    }
+    atomicAdd(t.stats + az::kStatGamesDone, 1ull);
+    const unsigned long long next = atomicAdd(t.stats + az::kStatNextGame, 1ull);
+    if ((int64_t)next < smp.first_game + smp.n_games) slot_reset(g, t, smp, s, (int64_t)next);
+    else t.game_id[s] = -1;
+  }
+}
+
+#define AZC_HIP(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t err__ = (expr);                                                             \
+    if (err__ != hipSuccess)                                                               \
+      return az::fail_abi(AZ_E_HIP, std::string(#expr) + ": " + hipGetErrorString(err__)); \
+  } while (0)
+
+}  // namespace
+}  // namespace azc
+
+using namespace azc;
+
+struct az_chess_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  az_chess_config cfg{};
+  CCfg g{};
+  CTree t{};
+  CSamples smp{};
+  az::NetDev net{};
+  az::ConvTimer timer;
+  hipEvent_t timer_ref = nullptr;
+  float* x = nullptr;
+  float* act[3] = {nullptr, nullptr, nullptr};
+  float* probs = nullptr;
+  float* values = nullptr;
+  std::vector<void*> owned, sample_bufs;
+  int64_t sp_n = 0;
+
+  template <typename T>
+  int alloc(T** p, size_t count) {
+    void* q = nullptr;
+    AZC_HIP(hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)));
+    owned.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+  }
+};
+
+namespace {
+
+int check_errors(az_chess_engine* e) {
+  unsigned long long err = 0;
+  AZC_HIP(hipMemcpy(&err, e->t.stats + az::kStatErrors, sizeof(err), hipMemcpyDeviceToHost));
+  if (!err) return 0;
+  std::string m = "device error flags:";
+  if (err & az::kErrArena) m += " arena-overflow(raise az_chess_config.arena_edges)";
+  if (err & az::kErrPow) m += " visit-table-overflow";
+  if (err & az::kErrPath) m += " path-overflow";
+  if (err & az::kErrIllegal) m += " illegal-move";
+  if (err & az::kErrNoRoot) m += " play-before-search";
+  return az::fail_abi(AZ_E_DEVICE, m);
+}
+
+int simulate(az_chess_engine* e) {
+  hipStream_t s = e->stream;
+  const int S = e->g.slots;
+  select_kernel<<<S, 64, 0, s>>>(e->g, e->t);
+  AZC_HIP(hipMemsetAsync(e->t.eval_count, 0, sizeof(int32_t), s));
+  leaf_kernel<<<(S + 127) / 128, 128, 0, s>>>(e->g, e->t);
+  if (e->g.evaluator == AZ_EVAL_NETWORK) {
+    encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(e->g, e->t, reinterpret_cast<float4*>(e->x));
+    az::launch_forward(e->net, e->x, e->t.eval_count, S, 8, 8, AZ_CHESS_ACTIONS, e->act[0], e->act[1],
+                       e->act[2], e->probs, e->values, s, e->timer.enabled ? &e->timer : nullptr);
+  } else {
+    synth_kernel<<<(S + 255) / 256, 256, 0, s>>>(e->g, e->t, e->probs, e->values);
+  }
+  expand_kernel<<<S, 64, 0, s>>>(e->g, e->t, e->probs, e->values);
+  AZC_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engine** out) {
+  if (!cfg || !out) return az::fail_abi(AZ_E_INVALID, "null argument");
+  const az_chess_config& c = *cfg;
+  if (c.slots < 1 || c.mcts_iterations < 1) return az::fail_abi(AZ_E_INVALID, "slots and mcts_iterations must be >= 1");
+  if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC)
+    return az::fail_abi(AZ_E_INVALID, "unknown evaluator");
+  if (c.evaluator == AZ_EVAL_NETWORK && c.filters != 128)
+    return az::fail_abi(AZ_E_INVALID, "network evaluator supports filters == 128 (ConfigModel.filters)");
+  if (c.conv_algo != AZ_CONV_WINOGRAD && c.conv_algo != AZ_CONV_DIRECT)
+    return az::fail_abi(AZ_E_INVALID, "conv_algo must be AZ_CONV_WINOGRAD or AZ_CONV_DIRECT");
+  if (c.max_plies < 0 || c.arena_edges < 0) return az::fail_abi(AZ_E_INVALID, "negative bound");
+  if ((int64_t)c.slots * 64 * 128 >= (1ll << 31))
+    return az::fail_abi(AZ_E_INVALID, "slots * 64 * 128 must stay below 2^31 (32-bit activation offsets)");
+  int dev_count = 0;
+  if (hipGetDeviceCount(&dev_count) != hipSuccess || dev_count == 0)
+    return az::fail_abi(AZ_E_HIP, "no HIP device visible: libaz has no CPU fallback");
+  if (device < 0 || device >= dev_count) return az::fail_abi(AZ_E_INVALID, "bad device index");
+  AZC_HIP(hipSetDevice(device));
+  AZC_HIP(upload_rays());
+  az_chess_engine* e = new az_chess_engine();
+  e->device = device;
+  e->cfg = c;
+  CCfg& g = e->g;
+  g.slots = c.slots;
+  g.sims = c.mcts_iterations;
+  g.greedy_ply = c.index_move_greedy;
+  g.c_puct = c.exploration_constant;
+  g.evaluator = c.evaluator;
+  g.max_plies = c.max_plies > 0 ? c.max_plies : 512;
+  g.max_depth = 512;
+  const int64_t half = c.arena_edges > 0 ? c.arena_edges : (int64_t)96 * c.mcts_iterations + 256;
+  const int64_t visits = (int64_t)c.mcts_iterations * g.max_plies + 2;
+  if (half > (1 << 30) || visits > (1 << 28) || (int64_t)c.slots * 2 * half > (1ll << 36)) {
+    delete e;
+    return az::fail_abi(AZ_E_INVALID, "tree bounds too large");
+  }
+  g.half_cap = (int)half;
+  g.pow_len = (int)visits;
+  auto cleanup = [&](int rc) {
+    az_chess_engine_destroy(e);
+    return rc;
+  };
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(az::fail_abi(AZ_E_HIP, "hipStreamCreate failed"));
+  const size_t S = (size_t)g.slots;
+  CTree& t = e->t;
+  int rc;
+  if ((rc = e->alloc(&t.edges, S * 2 * (size_t)g.half_cap)) || (rc = e->alloc(&t.root, S)) ||
+      (rc = e->alloc(&t.root_first, S)) || (rc = e->alloc(&t.root_n, S)) || (rc = e->alloc(&t.half, S)) ||
+      (rc = e->alloc(&t.top, S)) || (rc = e->alloc(&t.ply, S)) || (rc = e->alloc(&t.initial, S)) ||
+      (rc = e->alloc(&t.game_id, S)) || (rc = e->alloc(&t.path, S * g.max_depth)) ||
+      (rc = e->alloc(&t.path_len, S)) || (rc = e->alloc(&t.leaf, S)) ||
+      (rc = e->alloc(&t.leaf_moves, S * AZ_CHESS_MAX_MOVES)) || (rc = e->alloc(&t.leaf_n, S)) ||
+      (rc = e->alloc(&t.slot_exp, S)) || (rc = e->alloc(&t.mt, S * (kMtN + 1))) ||
+      (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_count, 1)) ||
+      (rc = e->alloc(&t.stats, az::kStatCount)))
+    return cleanup(rc);
+  {
+    double* powtab = nullptr;
+    if ((rc = e->alloc(&powtab, g.pow_len))) return cleanup(rc);
+    std::vector<double> hp(g.pow_len);
+    double (*volatile pw)(double, double) = pow;  // libm pow, as Python `** 0.5` (mcts.py:50)
+    for (int k = 0; k < g.pow_len; ++k) hp[k] = k == 0 ? 0.0 : pw((double)k, 0.5);
+    if (hipMemcpy(powtab, hp.data(), hp.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(az::fail_abi(AZ_E_HIP, "pow table upload failed"));
+    t.powtab = powtab;
+    int16_t* lut = nullptr;
+    std::vector<int16_t> hl = action_lut();
+    if ((rc = e->alloc(&lut, hl.size()))) return cleanup(rc);
+    if (hipMemcpy(lut, hl.data(), hl.size() * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(az::fail_abi(AZ_E_HIP, "action table upload failed"));
+    t.lut = lut;
+  }
+  if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
+    return cleanup(az::fail_abi(AZ_E_HIP, "memset failed"));
+  if ((rc = e->alloc(&e->probs, S * AZ_CHESS_ACTIONS)) || (rc = e->alloc(&e->values, S))) return cleanup(rc);
+  if (c.evaluator == AZ_EVAL_NETWORK) {
+    if ((rc = e->alloc(&e->x, S * 64 * 128))) return cleanup(rc);
+    if (hipMemset(e->x, 0, S * 64 * 128 * sizeof(float)) != hipSuccess)
+      return cleanup(az::fail_abi(AZ_E_HIP, "memset failed"));
+    for (int i = 0; i < 3; ++i)
+      if ((rc = e->alloc(&e->act[i], S * 64 * 128))) return cleanup(rc);
+  }
+  e->net.depth = c.depth;
+  e->net.algo = c.conv_algo;
+  e->net.hidden = c.value_hidden;
+  *out = e;
+  return 0;
+}
+
+int az_chess_engine_destroy(az_chess_engine* e) {
+  if (!e) return 0;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (void* p : e->sample_bufs) (void)hipFree(p);
+  for (void* p : e->owned) (void)hipFree(p);
+  if (e->timer_ref) (void)hipEventDestroy(e->timer_ref);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return 0;
+}
+
+int az_chess_engine_set_weights(az_chess_engine* e, const az_tensor* tensors, int n) {
+  if (!e || (!tensors && n)) return az::fail_abi(AZ_E_INVALID, "null argument");
+  if (e->cfg.evaluator != AZ_EVAL_NETWORK) return az::fail_abi(AZ_E_STATE, "engine has no network evaluator");
+  AZC_HIP(hipSetDevice(e->device));
+  return az::load_network(e->net, tensors, n, AZ_CHESS_PLANES, 64, AZ_CHESS_ACTIONS, e->cfg.bn_epsilon,
+                          e->owned);
+}
+
+int az_chess_forward(az_chess_engine* e, const float* x, int n, float* probs, float* values) {
+  if (!e || n < 0 || (n && (!x || !probs || !values))) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  if (!e->net.ready) return az::fail_abi(AZ_E_STATE, "az_chess_engine_set_weights was not called");
+  AZC_HIP(hipSetDevice(e->device));
+  const int chunk = e->g.slots;
+  for (int off = 0; off < n; off += chunk) {
+    const int m = std::min(chunk, n - off);
+    // [m][64][118] -> [m][64][128] (planes 118..127 stay zero)
+    AZC_HIP(hipMemcpy2DAsync(e->x, 128 * sizeof(float), x + (size_t)off * 64 * AZ_CHESS_PLANES,
+                             AZ_CHESS_PLANES * sizeof(float), AZ_CHESS_PLANES * sizeof(float), (size_t)m * 64,
+                             hipMemcpyHostToDevice, e->stream));
+    az::launch_forward(e->net, e->x, nullptr, m, 8, 8, AZ_CHESS_ACTIONS, e->act[0], e->act[1], e->act[2],
+                       e->probs, e->values, e->stream, e->timer.enabled ? &e->timer : nullptr);
+    AZC_HIP(hipGetLastError());
+    AZC_HIP(hipMemcpyAsync(probs + (size_t)off * AZ_CHESS_ACTIONS, e->probs,
+                           (size_t)m * AZ_CHESS_ACTIONS * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    AZC_HIP(hipMemcpyAsync(values + off, e->values, (size_t)m * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    AZC_HIP(hipStreamSynchronize(e->stream));
+  }
+  return 0;
+}
+
+int az_chess_selfplay_begin(az_chess_engine* e, int64_t first_game, int64_t n_games, uint32_t base_seed) {
+  if (!e || n_games < 0 || first_game < 0) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
+    return az::fail_abi(AZ_E_STATE, "network evaluator selected but az_chess_engine_set_weights was not called");
+  AZC_HIP(hipSetDevice(e->device));
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  for (void* p : e->sample_bufs) (void)hipFree(p);
+  e->sample_bufs.clear();
+  CSamples& smp = e->smp;
+  smp = CSamples{};
+  smp.first_game = first_game;
+  smp.n_games = n_games;
+  smp.base_seed = base_seed;
+  smp.plies = e->g.max_plies;
+  const size_t G = (size_t)std::max<int64_t>(n_games, 1), P = (size_t)smp.plies, M = AZ_CHESS_MAX_MOVES;
+  auto get = [&](void** p, size_t bytes) -> int {
+    AZC_HIP(hipMalloc(p, std::max<size_t>(bytes, 16)));
+    e->sample_bufs.push_back(*p);
+    AZC_HIP(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 16), e->stream));
+    return 0;
+  };
+  int rc;
+  if ((rc = get((void**)&smp.pos, G * P * sizeof(az_chess_pos))) ||
+      (rc = get((void**)&smp.moves, G * P * sizeof(uint16_t))) ||
+      (rc = get((void**)&smp.pol_n, G * P * sizeof(int32_t))) ||
+      (rc = get((void**)&smp.pol_a, G * P * M * sizeof(int16_t))) ||
+      (rc = get((void**)&smp.pol_p, G * P * M * sizeof(double))) ||
+      (rc = get((void**)&smp.length, G * sizeof(int32_t))) || (rc = get((void**)&smp.result, G * sizeof(int32_t))) ||
+      (rc = get((void**)&smp.term, G * sizeof(int32_t))) || (rc = get((void**)&smp.expansions, G * sizeof(int32_t))))
+    return rc;
+  unsigned long long st[az::kStatCount] = {0};
+  const int64_t first_wave = std::min<int64_t>(n_games, e->g.slots);
+  st[az::kStatNextGame] = (unsigned long long)(first_game + first_wave);
+  AZC_HIP(hipMemcpyAsync(e->t.stats, st, sizeof(st), hipMemcpyHostToDevice, e->stream));
+  slot_init_kernel<<<(e->g.slots + 255) / 256, 256, 0, e->stream>>>(e->g, e->t, smp, first_wave);
+  AZC_HIP(hipGetLastError());
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  e->sp_n = n_games;
+  return 0;
+}
+
+int az_chess_stats(az_chess_engine* e, az_stats* st) {
+  if (!e || !st) return az::fail_abi(AZ_E_INVALID, "null argument");
+  AZC_HIP(hipSetDevice(e->device));
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  unsigned long long h[az::kStatCount];
+  AZC_HIP(hipMemcpy(h, e->t.stats, sizeof(h), hipMemcpyDeviceToHost));
+  std::vector<int64_t> gid(e->g.slots);
+  AZC_HIP(hipMemcpy(gid.data(), e->t.game_id, gid.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+  memset(st, 0, sizeof(*st));
+  st->expansions = (int64_t)h[az::kStatExpansions];
+  st->terminal_visits = (int64_t)h[az::kStatTerminal];
+  st->games_done = (int64_t)h[az::kStatGamesDone];
+  st->simulations = (int64_t)h[az::kStatSims];
+  st->plies = (int64_t)h[az::kStatPlies];
+  st->errors = (int64_t)h[az::kStatErrors];
+  st->evaluations = (int64_t)h[az::kStatNNEvals];
+  st->active_slots = std::count_if(gid.begin(), gid.end(), [](int64_t v) { return v >= 0; });
+  e->timer.flush();
+  st->conv_ms = e->timer.total_ms;
+  st->conv_launches = e->timer.launches;
+  double busy = 0.0;
+  for (const auto& iv : e->timer.intervals) busy += iv.second - iv.first;  // one stream: no overlap
+  st->conv_busy_ms = busy;
+  return 0;
+}
+
+int az_chess_selfplay_step(az_chess_engine* e, int n_moves, az_stats* st) {
+  if (!e || n_moves < 0) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  for (int mv = 0; mv < n_moves; ++mv) {
+    for (int s = 0; s < e->g.sims; ++s)
+      if ((rc = simulate(e))) return rc;
+    play_kernel<<<e->g.slots, 64, 0, e->stream>>>(e->g, e->t, e->smp);
+    AZC_HIP(hipGetLastError());
+  }
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  if ((rc = check_errors(e))) return rc;
+  if (st) return az_chess_stats(e, st);
+  return 0;
+}
+
+int az_chess_selfplay_run(az_chess_engine* e, int64_t first_game, int64_t n_games, uint32_t base_seed,
+                          az_stats* st) {
+  int rc;
+  if ((rc = az_chess_selfplay_begin(e, first_game, n_games, base_seed))) return rc;
+  az_stats tmp;
+  for (;;) {
+    if ((rc = az_chess_selfplay_step(e, 1, &tmp))) return rc;
+    if (tmp.active_slots == 0) break;
+  }
+  if (st) *st = tmp;
+  return 0;
+}
+
+int az_chess_selfplay_results(az_chess_engine* e, int32_t* lengths, int32_t* results, int32_t* terminations,
+                              int32_t* expansions, az_chess_pos* positions, uint16_t* moves, int32_t* policy_n,
+                              int16_t* policy_actions, double* policy_probs) {
+  if (!e) return az::fail_abi(AZ_E_INVALID, "null engine");
+  AZC_HIP(hipSetDevice(e->device));
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  const size_t G = (size_t)e->sp_n, P = (size_t)e->smp.plies, M = AZ_CHESS_MAX_MOVES;
+  if (G == 0) return 0;
+  const CSamples& s = e->smp;
+  if (lengths) AZC_HIP(hipMemcpy(lengths, s.length, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (results) AZC_HIP(hipMemcpy(results, s.result, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (terminations) AZC_HIP(hipMemcpy(terminations, s.term, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (expansions) AZC_HIP(hipMemcpy(expansions, s.expansions, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (positions) AZC_HIP(hipMemcpy(positions, s.pos, G * P * sizeof(az_chess_pos), hipMemcpyDeviceToHost));
+  if (moves) AZC_HIP(hipMemcpy(moves, s.moves, G * P * sizeof(uint16_t), hipMemcpyDeviceToHost));
+  if (policy_n) AZC_HIP(hipMemcpy(policy_n, s.pol_n, G * P * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (policy_actions)
+    AZC_HIP(hipMemcpy(policy_actions, s.pol_a, G * P * M * sizeof(int16_t), hipMemcpyDeviceToHost));
+  if (policy_probs) AZC_HIP(hipMemcpy(policy_probs, s.pol_p, G * P * M * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int az_chess_timer_enable(az_chess_engine* e, int on) {
+  if (!e) return az::fail_abi(AZ_E_INVALID, "null engine");
+  AZC_HIP(hipSetDevice(e->device));
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  if (!e->timer_ref) AZC_HIP(hipEventCreate(&e->timer_ref));
+  AZC_HIP(hipEventRecord(e->timer_ref, e->stream));
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  e->timer.flush();
+  e->timer.reset();
+  e->timer.ref = &e->timer_ref;
+  e->timer.enabled = on != 0;
+  return 0;
+}
+
+}  // extern "C"

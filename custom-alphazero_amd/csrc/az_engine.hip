@@ -183,7 +183,7 @@ int ready_to_search(az_engine* e) {
 }
 
 // ------------------------------------------------------------ weight folding
-int fetch(const std::map<std::string, const az_tensor*>& m, const std::string& name,
+[[maybe_unused]] int fetch(const std::map<std::string, const az_tensor*>& m, const std::string& name,
           int64_t numel, std::vector<double>& out) {
   auto it = m.find(name);
   if (it == m.end()) return fail(AZ_E_INVALID, "missing weight tensor '" + name + "'");
@@ -204,7 +204,7 @@ int fetch(const std::map<std::string, const az_tensor*>& m, const std::string& n
 // InnerConvBlock (base_layers.py:20-66): conv kernel [kh][kw][cin][cout] +
 // bias, BatchNorm(gamma, beta, moving mean/var).  Returns the folded kernel in
 // Keras layout (double) and folded bias.
-int fold_unit(const std::map<std::string, const az_tensor*>& m, const std::string& u, int kk,
+[[maybe_unused]] int fold_unit(const std::map<std::string, const az_tensor*>& m, const std::string& u, int kk,
               int cin, int cout, double eps, std::vector<double>& w, std::vector<double>& b) {
   std::vector<double> gamma, beta, mean, var;
   int rc;
@@ -225,7 +225,7 @@ int fold_unit(const std::map<std::string, const az_tensor*>& m, const std::strin
 // [n][K] (K contiguous) -> MFMA fragment order of conv3x3_mfma_kernel:
 // float4 index ((c*4 + tile)*4 + q)*64 + lane holds W[k][n] for
 // k = 32c + 16*(lane>>5) + 4q + e (e = 0..3), n = 32*tile + (lane&31).
-std::vector<float> pack_fragments(const std::vector<float>& wt, int N, int K) {
+[[maybe_unused]] std::vector<float> pack_fragments(const std::vector<float>& wt, int N, int K) {
   std::vector<float> p((size_t)N * K);
   const int chunks = K / 32, tiles = N / 32;
   for (int c = 0; c < chunks; ++c)
@@ -244,7 +244,7 @@ std::vector<float> pack_fragments(const std::vector<float>& wt, int N, int K) {
 // U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
 // in float64 from the folded Keras kernel, rounded once to float, in the
 // kernel's fragment order.
-std::vector<float> pack_wino(const std::vector<double>& w, int F) {
+[[maybe_unused]] std::vector<float> pack_wino(const std::vector<double>& w, int F) {
   static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   std::vector<float> p((size_t)16 * F * F);
   std::vector<double> U((size_t)F * F);
@@ -266,7 +266,7 @@ std::vector<float> pack_wino(const std::vector<double>& w, int F) {
 
 // 1x1 projection residual [cin][cout] in the same fragment order, as if it
 // were point 0 of a 16-point-per-chunk stream compacted to one point.
-std::vector<float> pack_wino_res(const std::vector<double>& wr, int F) {
+[[maybe_unused]] std::vector<float> pack_wino_res(const std::vector<double>& wr, int F) {
   std::vector<float> p((size_t)F * F);
   const int CK = az::kWinoCK;
   for (int cin = 0; cin < F; ++cin)
@@ -280,9 +280,13 @@ std::vector<float> pack_wino_res(const std::vector<double>& wr, int F) {
   return p;
 }
 
-int upload(az_engine* e, float** dst, const std::vector<float>& src) {
-  int rc;
-  if (!*dst && (rc = e->alloc(dst, src.size()))) return rc;
+[[maybe_unused]] int upload(std::vector<void*>& owned, float** dst, const std::vector<float>& src) {
+  if (!*dst) {
+    void* q = nullptr;
+    AZ_HIP(hipMalloc(&q, std::max<size_t>(src.size(), 1) * sizeof(float)));
+    owned.push_back(q);
+    *dst = reinterpret_cast<float*>(q);
+  }
   AZ_HIP(hipMemcpy(*dst, src.data(), src.size() * sizeof(float), hipMemcpyHostToDevice));
   return 0;
 }
@@ -341,6 +345,101 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
 }
 
 }  // namespace
+
+namespace az {
+// Folds (BatchNorm into conv) and uploads the network weights, Keras names
+// of custom_alphazero/model/weights.py.  in_ch = 4: the Connect-N stem
+// kernels (stem_w [36][F]); in_ch > 4 (chess, 118 planes): the stem is a
+// Winograd conv over the input zero-padded to F channels (stem_u).
+int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW, int A, double eps,
+                 std::vector<void*>& owned) {
+  std::map<std::string, const az_tensor*> m;
+  for (int i = 0; i < n; ++i) {
+    if (!tensors[i].name || !tensors[i].data) return fail(AZ_E_INVALID, "tensor without name/data");
+    m[tensors[i].name] = &tensors[i];
+  }
+  const int F = 128, hidden = net.hidden;
+  if (in_ch < 1 || in_ch > F) return fail(AZ_E_INVALID, "input planes must be 1..128");
+  std::vector<double> w, b, wr, br;
+  int rc;
+  if ((rc = fold_unit(m, "stem", 3, in_ch, F, eps, w, b))) return rc;
+  {
+    std::vector<float> bs(F);
+    for (int i = 0; i < F; ++i) bs[i] = (float)b[i];
+    if ((rc = upload(owned, &net.stem_b, bs))) return rc;
+    if (in_ch == 4) {  // [3][3][4][F] -> [tap*4 + c][F]
+      std::vector<float> ws(36 * F);
+      for (int i = 0; i < 36 * F; ++i) ws[i] = (float)w[i];  // Keras order == (tap, c, n)
+      if ((rc = upload(owned, &net.stem_w, ws))) return rc;
+    } else {  // [3][3][in_ch][F] zero-padded to [3][3][F][F]
+      std::vector<double> wp((size_t)9 * F * F, 0.0);
+      for (int tap = 0; tap < 9; ++tap)
+        for (int c = 0; c < in_ch; ++c)
+          for (int o = 0; o < F; ++o)
+            wp[((size_t)tap * F + c) * F + o] = w[((size_t)tap * in_ch + c) * F + o];
+      if ((rc = upload(owned, &net.stem_u, pack_wino(wp, F)))) return rc;
+    }
+    net.in_ch = in_ch;
+  }
+  net.c1_w.resize(net.depth, nullptr);
+  net.c1_b.resize(net.depth, nullptr);
+  net.c2_w.resize(net.depth, nullptr);
+  net.c2_b.resize(net.depth, nullptr);
+  net.u1_w.resize(net.depth, nullptr);
+  net.u2_w.resize(net.depth, nullptr);
+  net.r2_w.resize(net.depth, nullptr);
+  for (int d = 0; d < net.depth; ++d) {
+    const std::string p = "block" + std::to_string(d);
+    if ((rc = fold_unit(m, p + ".conv1", 3, F, F, eps, w, b))) return rc;
+    std::vector<float> wt((size_t)F * 9 * F), bt(F);
+    for (int n2 = 0; n2 < F; ++n2)
+      for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
+    for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
+    if ((rc = upload(owned, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
+        (rc = upload(owned, &net.u1_w[d], pack_wino(w, F))) || (rc = upload(owned, &net.c1_b[d], bt)))
+      return rc;
+    if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
+    if ((rc = fold_unit(m, p + ".res", 1, F, F, eps, wr, br))) return rc;
+    std::vector<float> wt2((size_t)F * 10 * F), bt2(F);
+    for (int n2 = 0; n2 < F; ++n2) {
+      for (int k = 0; k < 9 * F; ++k) wt2[(size_t)n2 * 10 * F + k] = (float)w[(size_t)k * F + n2];
+      for (int c = 0; c < F; ++c) wt2[(size_t)n2 * 10 * F + 9 * F + c] = (float)wr[(size_t)c * F + n2];
+    }
+    for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
+    if ((rc = upload(owned, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
+        (rc = upload(owned, &net.u2_w[d], pack_wino(w, F))) ||
+        (rc = upload(owned, &net.r2_w[d], pack_wino_res(wr, F))) || (rc = upload(owned, &net.c2_b[d], bt2)))
+      return rc;
+  }
+  // heads
+  if ((rc = fold_unit(m, "policy.conv", 1, F, 2, eps, w, b))) return rc;
+  {
+    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    if ((rc = upload(owned, &net.pc_w, a)) || (rc = upload(owned, &net.pc_b, c))) return rc;
+  }
+  if ((rc = fold_unit(m, "value.conv", 1, F, 1, eps, w, b))) return rc;
+  {
+    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    if ((rc = upload(owned, &net.vc_w, a)) || (rc = upload(owned, &net.vc_b, c))) return rc;
+  }
+  struct DenseSpec {
+    const char* name;
+    int in, out;
+    float** w;
+    float** b;
+  } dense[] = {{"policy.dense", 2 * HW, A, &net.pd_w, &net.pd_b},
+               {"value.dense1", HW, hidden, &net.v1_w, &net.v1_b},
+               {"value.dense2", hidden, 1, &net.v2_w, &net.v2_b}};
+  for (auto& ds : dense) {
+    if ((rc = fetch(m, std::string(ds.name) + ".kernel", (int64_t)ds.in * ds.out, w))) return rc;
+    if ((rc = fetch(m, std::string(ds.name) + ".bias", ds.out, b))) return rc;
+    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    if ((rc = upload(owned, ds.w, a)) || (rc = upload(owned, ds.b, c))) return rc;
+  }
+  net.ready = true;
+  return 0;
+}
+}  // namespace az
 
 extern "C" {
 
@@ -516,80 +615,9 @@ int az_engine_destroy(az_engine* eng) {
 int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
   if (!e || (!tensors && n)) return fail(AZ_E_INVALID, "null argument");
   AZ_HIP(hipSetDevice(e->device));
-  std::map<std::string, const az_tensor*> m;
-  for (int i = 0; i < n; ++i) {
-    if (!tensors[i].name || !tensors[i].data) return fail(AZ_E_INVALID, "tensor without name/data");
-    m[tensors[i].name] = &tensors[i];
-  }
-  const int F = 128, HW = e->g.HW, A = e->g.A, hidden = e->net.hidden;
-  const double eps = e->cfg.bn_epsilon;
-  az::NetDev& net = e->net;
-  std::vector<double> w, b, wr, br;
   int rc;
-  // stem: [3][3][4][F] -> [tap*4 + c][F]
-  if ((rc = fold_unit(m, "stem", 3, 4, F, eps, w, b))) return rc;
-  {
-    std::vector<float> ws(36 * F), bs(F);
-    for (int i = 0; i < 36 * F; ++i) ws[i] = (float)w[i];  // Keras order == (tap, c, n)
-    for (int i = 0; i < F; ++i) bs[i] = (float)b[i];
-    if ((rc = upload(e, &net.stem_w, ws)) || (rc = upload(e, &net.stem_b, bs))) return rc;
-  }
-  net.c1_w.resize(net.depth, nullptr);
-  net.c1_b.resize(net.depth, nullptr);
-  net.c2_w.resize(net.depth, nullptr);
-  net.c2_b.resize(net.depth, nullptr);
-  net.u1_w.resize(net.depth, nullptr);
-  net.u2_w.resize(net.depth, nullptr);
-  net.r2_w.resize(net.depth, nullptr);
-  for (int d = 0; d < net.depth; ++d) {
-    const std::string p = "block" + std::to_string(d);
-    if ((rc = fold_unit(m, p + ".conv1", 3, F, F, eps, w, b))) return rc;
-    std::vector<float> wt((size_t)F * 9 * F), bt(F);
-    for (int n2 = 0; n2 < F; ++n2)
-      for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
-    for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
-    if ((rc = upload(e, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
-        (rc = upload(e, &net.u1_w[d], pack_wino(w, F))) || (rc = upload(e, &net.c1_b[d], bt)))
-      return rc;
-    if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
-    if ((rc = fold_unit(m, p + ".res", 1, F, F, eps, wr, br))) return rc;
-    std::vector<float> wt2((size_t)F * 10 * F), bt2(F);
-    for (int n2 = 0; n2 < F; ++n2) {
-      for (int k = 0; k < 9 * F; ++k) wt2[(size_t)n2 * 10 * F + k] = (float)w[(size_t)k * F + n2];
-      for (int c = 0; c < F; ++c) wt2[(size_t)n2 * 10 * F + 9 * F + c] = (float)wr[(size_t)c * F + n2];
-    }
-    for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
-    if ((rc = upload(e, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
-        (rc = upload(e, &net.u2_w[d], pack_wino(w, F))) ||
-        (rc = upload(e, &net.r2_w[d], pack_wino_res(wr, F))) || (rc = upload(e, &net.c2_b[d], bt2)))
-      return rc;
-  }
-  // heads
-  if ((rc = fold_unit(m, "policy.conv", 1, F, 2, eps, w, b))) return rc;
-  {
-    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
-    if ((rc = upload(e, &net.pc_w, a)) || (rc = upload(e, &net.pc_b, c))) return rc;
-  }
-  if ((rc = fold_unit(m, "value.conv", 1, F, 1, eps, w, b))) return rc;
-  {
-    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
-    if ((rc = upload(e, &net.vc_w, a)) || (rc = upload(e, &net.vc_b, c))) return rc;
-  }
-  struct DenseSpec {
-    const char* name;
-    int in, out;
-    float** w;
-    float** b;
-  } dense[] = {{"policy.dense", 2 * HW, A, &net.pd_w, &net.pd_b},
-               {"value.dense1", HW, hidden, &net.v1_w, &net.v1_b},
-               {"value.dense2", hidden, 1, &net.v2_w, &net.v2_b}};
-  for (auto& ds : dense) {
-    if ((rc = fetch(m, std::string(ds.name) + ".kernel", (int64_t)ds.in * ds.out, w))) return rc;
-    if ((rc = fetch(m, std::string(ds.name) + ".bias", ds.out, b))) return rc;
-    std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
-    if ((rc = upload(e, ds.w, a)) || (rc = upload(e, ds.b, c))) return rc;
-  }
-  net.ready = true;
+  if ((rc = az::load_network(e->net, tensors, n, 4, e->g.HW, e->g.A, e->cfg.bn_epsilon, e->owned)))
+    return rc;
   return cache_clear(e);  // cached outputs belong to the previous weights
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <vector>
 
+#include "../../include/az.h"
 #include "az_device.h"
 
 namespace az {
@@ -13,7 +14,9 @@ namespace az {
 struct NetDev {
   int filters = 128, depth = 0, hidden = 256;
   int algo = 0;  // AZ_CONV_WINOGRAD / AZ_CONV_DIRECT
-  float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c)
+  int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
+  float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c), in_ch == 4
+  float* stem_u = nullptr;  // Winograd U of the zero-padded stem [3][3][F][F], in_ch > 4
   float* stem_b = nullptr;  // [F]
   std::vector<float*> c1_w, c1_b;  // fragment-packed [9F x F], [F]
   std::vector<float*> c2_w, c2_b;  // fragment-packed [10F x F] (conv2 taps, then 1x1 residual), [F]
@@ -107,6 +110,11 @@ void launch_wino_conv(const float* in, const float* res_in, const float* upack,
 // x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
 // boards (optional): one-hot input straight from the eval queue's boards
 // (bitwise the same outputs as encoding them into x first)
+// Folds and uploads the network weights (Keras names, model/weights.py);
+// device buffers are appended to `owned` (az_engine.hip)
+int load_network(NetDev& net, const ::az_tensor* tensors, int n, int in_ch, int HW, int A,
+                 double eps, std::vector<void*>& owned);
+// x: [n][HW][4] (in_ch == 4) or [n][HW][F] zero-padded planes (in_ch > 4)
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
                     hipStream_t s, ConvTimer* timer, const Board* boards = nullptr);

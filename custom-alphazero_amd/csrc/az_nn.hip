@@ -398,7 +398,7 @@ __device__ __forceinline__ float wave_max(float v) {
 // layers' weights (policy [2HW][A], value1 [HW][hidden]) are copied into LDS
 // once per block instead of being re-read through L1 for every board.  The
 // per-board arithmetic is unchanged.
-template <int F, bool FEAT, bool STAGE>
+template <int F, bool FEAT, bool STAGE, int AMAX>
 __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ act, HeadWeights hw,
                                                     const int* __restrict__ count, int n_static,
                                                     int HW, int A, int hidden,
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
                                                     float* __restrict__ values) {
   __shared__ float pflat[4][2 * kMaxCells];
   __shared__ float vflat[4][kMaxCells];
-  __shared__ float logits[4][kMaxActions];
+  __shared__ float logits[4][AMAX];  // AMAX = kMaxActions, or 2048 for chess (A = 1880)
   extern __shared__ float wsm[];
   const int n = count ? *count : n_static;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -503,7 +503,10 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   if (n_max <= 0) return;
   const int HW = H * W;
   constexpr int F = 128;
-  {
+  if (net.stem_u) {
+    // chess: 118 input planes zero-padded to F, the stem is one more Winograd conv
+    launch_wino_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s);
+  } else {
     const int total = n_max * HW * (F / 4);
     if (boards)
       stem_board_kernel<F><<<std::min((n_max * HW + 7) / 8, 1024), 256, 0, s>>>(
@@ -569,9 +572,16 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   const bool stage = wbytes <= 64 * 1024;
   const int hblocks = stage ? std::min((n_max + 3) / 4, 512) : (n_max + 3) / 4;
 #define AZ_HEADS(FEAT_, STAGE_)                                                                      \
-  heads_kernel<F, FEAT_, STAGE_><<<hblocks, 256, STAGE_ ? wbytes : 0, s>>>(cur, hw, count, n_max, HW, A, \
-                                                                         net.hidden, probs, values)
-  if (fused_heads) {
+  heads_kernel<F, FEAT_, STAGE_, kMaxActions><<<hblocks, 256, STAGE_ ? wbytes : 0, s>>>(           \
+      cur, hw, count, n_max, HW, A, net.hidden, probs, values)
+  if (A > kMaxActions) {  // chess: 1880 logits per board in LDS, weights through L1/L2
+    if (fused_heads)
+      heads_kernel<F, true, false, 2048><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A,
+                                                                         net.hidden, probs, values);
+    else
+      heads_kernel<F, false, false, 2048><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A,
+                                                                          net.hidden, probs, values);
+  } else if (fused_heads) {
     if (stage) AZ_HEADS(true, true); else AZ_HEADS(true, false);
   } else {
     if (stage) AZ_HEADS(false, true); else AZ_HEADS(false, false);

@@ -35,6 +35,18 @@ class Config(ctypes.Structure):
     ]
 
 
+class ChessConfig(ctypes.Structure):
+    """az_chess_config (include/az_chess.h)."""
+    _fields_ = [
+        ("mcts_iterations", ctypes.c_int32), ("index_move_greedy", ctypes.c_int32),
+        ("exploration_constant", ctypes.c_double), ("slots", ctypes.c_int32),
+        ("evaluator", ctypes.c_int32), ("filters", ctypes.c_int32), ("depth", ctypes.c_int32),
+        ("value_hidden", ctypes.c_int32), ("max_plies", ctypes.c_int32),
+        ("bn_epsilon", ctypes.c_double), ("arena_edges", ctypes.c_int64),
+        ("conv_algo", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7),
+    ]
+
+
 class Tensor(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64),
                 ("on_device", ctypes.c_int32), ("reserved", ctypes.c_int32)]
@@ -62,6 +74,9 @@ EXPORTED = (
     "az_cache_clear", "az_cache_enable",
     # include/az_chess.h
     "az_chess_all_moves", "az_chess_legal", "az_chess_encode", "az_chess_play", "az_chess_perft",
+    "az_chess_engine_create", "az_chess_engine_destroy", "az_chess_engine_set_weights",
+    "az_chess_forward", "az_chess_selfplay_begin", "az_chess_selfplay_step", "az_chess_selfplay_run",
+    "az_chess_selfplay_results", "az_chess_stats", "az_chess_timer_enable",
 )
 
 _lib = None
@@ -113,6 +128,17 @@ def load_library():
         "az_chess_encode": (ctypes.c_int, [ctypes.c_int, P, P, ctypes.c_int, P]),
         "az_chess_play": (ctypes.c_int, [ctypes.c_int, P, P, ctypes.c_int, ctypes.c_int]),
         "az_chess_perft": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P]),
+        "az_chess_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ChessConfig),
+                                                  ctypes.POINTER(P)]),
+        "az_chess_engine_destroy": (ctypes.c_int, [P]),
+        "az_chess_engine_set_weights": (ctypes.c_int, [P, ctypes.POINTER(Tensor), ctypes.c_int]),
+        "az_chess_forward": (ctypes.c_int, [P, P, ctypes.c_int, P, P]),
+        "az_chess_selfplay_begin": (ctypes.c_int, [P, I64, I64, ctypes.c_uint32]),
+        "az_chess_selfplay_step": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(Stats)]),
+        "az_chess_selfplay_run": (ctypes.c_int, [P, I64, I64, ctypes.c_uint32, ctypes.POINTER(Stats)]),
+        "az_chess_selfplay_results": (ctypes.c_int, [P] + [P] * 9),
+        "az_chess_stats": (ctypes.c_int, [P, ctypes.POINTER(Stats)]),
+        "az_chess_timer_enable": (ctypes.c_int, [P, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -131,6 +157,31 @@ def _check(rc):
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def tensor_array(named):
+    """(name, numpy array or torch tensor) pairs -> az_tensor array; torch
+    CUDA tensors are passed as device pointers (the engine copies them)."""
+    keep, items = [], []
+    for name, t in named:
+        on_dev = 0
+        if hasattr(t, "is_cuda"):
+            t = t.detach().float().contiguous()
+            on_dev = int(t.is_cuda)
+            if not on_dev:
+                t = t.numpy()
+        if on_dev:
+            ptr, numel = t.data_ptr(), t.numel()
+        else:
+            t = np.ascontiguousarray(t, np.float32)
+            ptr, numel = t.ctypes.data, t.size
+        keep.append(t)
+        items.append(Tensor(name.encode(), ptr, numel, on_dev, 0))
+    arr = (Tensor * len(items))(*items)
+    if any(i.on_device for i in items):
+        import torch
+        torch.cuda.synchronize()
+    return arr, len(items), keep
 
 
 class Engine:
@@ -173,26 +224,8 @@ class Engine:
     # ------------------------------------------------------------- weights
     def set_weights(self, named):
         """named: iterable of (name, array-like or torch tensor)."""
-        keep, items = [], []
-        for name, t in named:
-            on_dev = 0
-            if hasattr(t, "is_cuda"):
-                t = t.detach().float().contiguous()
-                on_dev = int(t.is_cuda)
-                if not on_dev:
-                    t = t.numpy()
-            if on_dev:
-                ptr, numel = t.data_ptr(), t.numel()
-            else:
-                t = np.ascontiguousarray(t, np.float32)
-                ptr, numel = t.ctypes.data, t.size
-            keep.append(t)
-            items.append(Tensor(name.encode(), ptr, numel, on_dev, 0))
-        arr = (Tensor * len(items))(*items)
-        if any(i.on_device for i in items):
-            import torch
-            torch.cuda.synchronize()
-        _check(self._L.az_engine_set_weights(self._h, arr, len(items)))
+        arr, n, _keep = tensor_array(named)
+        _check(self._L.az_engine_set_weights(self._h, arr, n))
 
     # ------------------------------------------------------------- eval
     def encode(self, boards):
@@ -300,3 +333,92 @@ class Engine:
         out = np.zeros(int(n), np.float64)
         _check(self._L.az_pow_table(self._h, _ptr(out), int(n)))
         return out
+
+
+class ChessEngine:
+    """libaz chess self-play engine (include/az_chess.h): `slots` concurrent
+    chess games on one device, MCTS with the policy/value network on the
+    (8, 8, 118) Board.full_state planes and the 1880-move action space."""
+
+    ACTIONS = 1880
+    MAX_MOVES = 256
+
+    def __init__(self, mcts_iterations=800, slots=256, evaluator=EVAL_NETWORK, max_plies=512,
+                 index_move_greedy=8, exploration_constant=1.5, filters=128, depth=4,
+                 value_hidden=256, bn_epsilon=1e-3, arena_edges=0, conv_algo=CONV_WINOGRAD,
+                 device=0):
+        L = load_library()
+        self.slots, self.mcts_iterations = slots, mcts_iterations
+        self.max_plies = max_plies if max_plies > 0 else 512
+        cfg = ChessConfig(mcts_iterations=mcts_iterations, index_move_greedy=index_move_greedy,
+                          exploration_constant=exploration_constant, slots=slots,
+                          evaluator=evaluator, filters=filters, depth=depth,
+                          value_hidden=value_hidden, max_plies=max_plies, bn_epsilon=bn_epsilon,
+                          arena_edges=arena_edges, conv_algo=conv_algo)
+        handle = ctypes.c_void_p()
+        _check(L.az_chess_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
+        self._h, self._L, self._n_games = handle, L, 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.az_chess_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+    def set_weights(self, named):
+        arr, n, _keep = tensor_array(named)
+        _check(self._L.az_chess_engine_set_weights(self._h, arr, n))
+
+    def forward(self, x):
+        x = np.ascontiguousarray(x, np.float32).reshape(-1, 8, 8, 118)
+        probs = np.zeros((len(x), self.ACTIONS), np.float32)
+        values = np.zeros(len(x), np.float32)
+        _check(self._L.az_chess_forward(self._h, _ptr(x), len(x), _ptr(probs), _ptr(values)))
+        return probs, values
+
+    def selfplay_begin(self, first_game, n_games, base_seed):
+        _check(self._L.az_chess_selfplay_begin(self._h, int(first_game), int(n_games),
+                                               int(base_seed) & 0xFFFFFFFF))
+        self._n_games = int(n_games)
+
+    def selfplay_step(self, n_moves=1):
+        st = Stats()
+        _check(self._L.az_chess_selfplay_step(self._h, int(n_moves), ctypes.byref(st)))
+        return st.as_dict()
+
+    def selfplay_run(self, first_game, n_games, base_seed):
+        st = Stats()
+        _check(self._L.az_chess_selfplay_run(self._h, int(first_game), int(n_games),
+                                             int(base_seed) & 0xFFFFFFFF, ctypes.byref(st)))
+        self._n_games = int(n_games)
+        return st.as_dict()
+
+    def selfplay_results(self, with_samples=True):
+        from custom_alphazero.chess.kernels import POS_DTYPE
+        G, P, M = self._n_games, self.max_plies, self.MAX_MOVES
+        out = {k: np.zeros(G, np.int32) for k in ("lengths", "results", "terminations", "expansions")}
+        if with_samples:
+            out["positions"] = np.zeros((G, P), POS_DTYPE)
+            out["moves"] = np.zeros((G, P), np.uint16)
+            out["policy_n"] = np.zeros((G, P), np.int32)
+            out["policy_actions"] = np.zeros((G, P, M), np.int16)
+            out["policy_probs"] = np.zeros((G, P, M), np.float64)
+        g = out.get
+        _check(self._L.az_chess_selfplay_results(
+            self._h, _ptr(g("lengths")), _ptr(g("results")), _ptr(g("terminations")),
+            _ptr(g("expansions")), _ptr(g("positions")), _ptr(g("moves")), _ptr(g("policy_n")),
+            _ptr(g("policy_actions")), _ptr(g("policy_probs"))))
+        return out
+
+    def stats(self):
+        st = Stats()
+        _check(self._L.az_chess_stats(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def timer(self, on):
+        _check(self._L.az_chess_timer_enable(self._h, int(bool(on))))

@@ -21,6 +21,8 @@
 
 #include <stdint.h>
 
+#include "az.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -79,6 +81,70 @@ int az_chess_play(int device, az_chess_pos* pos, const uint16_t* moves, int n,
 /* perft(depth) node count (legal move generation + push, breadth first on the
  * device): the size-independent check of the move generator. */
 int az_chess_perft(int device, const az_chess_pos* pos, int depth, uint64_t* nodes);
+
+
+/* ------------------------------------------------------------ self-play
+ * Chess self-play (BASELINE configs[4]): the batched
+ * replacement of self_play.play_game / MCTS on chess boards
+ * (self_play.py:37-82, mcts/mcts.py:88-222, chess/board.py).  Same tree
+ * arithmetic as the Connect-N engine (f64 PUCT, libm pow, first-max argmax,
+ * float32 pairwise prior normalisation with the reference's positional
+ * prior/move zip, np.random.choice on MT19937); subtrees are reused across
+ * moves (current_root = edge.child) and compacted into the other half of the
+ * slot's edge arena.  The reference's chess path cannot finish a game under
+ * MCTS (get_result() takes no keep_same_player, chess/board.py:178 vs
+ * mcts.py:179); here a terminal board scores as get_result does in the
+ * canonical form: 1 for checkmate (a win for the side that just moved), 0 for
+ * every draw. */
+typedef struct az_chess_engine az_chess_engine;
+
+typedef struct az_chess_config {
+    int32_t mcts_iterations;      /* sims per move (ConfigSelfPlay.mcts_iterations) */
+    int32_t index_move_greedy;    /* greedy once fullmove_number >= this (self_play.py:62) */
+    double exploration_constant;  /* ConfigMCTS.exploration_constant */
+    int32_t slots;                /* concurrent games on this device */
+    int32_t evaluator;            /* AZ_EVAL_NETWORK or AZ_EVAL_SYNTHETIC */
+    int32_t filters, depth, value_hidden;  /* ConfigModel (filters must be 128) */
+    int32_t max_plies;            /* addition: games stop (as draws) after this many plies;
+                                     the reference has no cap (0 = 512) */
+    double bn_epsilon;
+    int64_t arena_edges;          /* edges per arena half per slot (0 = 96 * mcts_iterations) */
+    int32_t conv_algo;            /* AZ_CONV_WINOGRAD / AZ_CONV_DIRECT (tower; the padded
+                                     118-plane stem is always Winograd) */
+    int32_t reserved[7];
+} az_chess_config;
+
+/* Termination of a finished self-play game: AZ_CHESS_* above, or this */
+#define AZ_CHESS_MAX_PLIES 5
+
+int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engine** out);
+int az_chess_engine_destroy(az_chess_engine* eng);
+/* PolicyValueModel weights for input_dim (8, 8, 118), action_space 1880
+ * (model/tensorflow/model.py:152-188; names of custom_alphazero/model/weights.py) */
+int az_chess_engine_set_weights(az_chess_engine* eng, const az_tensor* tensors, int n);
+/* PolicyValueModel.__call__ on chess states: x [n][8][8][118] f32 (Board.full_state)
+ * -> probs [n][1880] f32, values [n] f32 */
+int az_chess_forward(az_chess_engine* eng, const float* x, int n, float* probs, float* values);
+/* Games first_game .. first_game + n_games - 1 from the start position, game g
+ * seeded with MT19937(base_seed + g); slots refilled as games end. */
+int az_chess_selfplay_begin(az_chess_engine* eng, int64_t first_game, int64_t n_games,
+                            uint32_t base_seed);
+int az_chess_selfplay_step(az_chess_engine* eng, int n_moves, az_stats* st);
+int az_chess_selfplay_run(az_chess_engine* eng, int64_t first_game, int64_t n_games,
+                          uint32_t base_seed, az_stats* st);
+/* Per game g (P = max_plies): lengths[g] plies; results[g] (1 checkmate, 0
+ * draw or cap); terminations[g] (AZ_CHESS_*); expansions[g]; positions
+ * [g][P] (canonical root before each move, MCTS.play's parent board); moves
+ * [g][P]; the MCTS.play policy sparsely: policy_n [g][P] root edges,
+ * policy_actions [g][P][AZ_CHESS_MAX_MOVES] action indices (edge order),
+ * policy_probs [g][P][AZ_CHESS_MAX_MOVES] f64.  Any pointer may be NULL. */
+int az_chess_selfplay_results(az_chess_engine* eng, int32_t* lengths, int32_t* results,
+                              int32_t* terminations, int32_t* expansions, az_chess_pos* positions,
+                              uint16_t* moves, int32_t* policy_n, int16_t* policy_actions,
+                              double* policy_probs);
+int az_chess_stats(az_chess_engine* eng, az_stats* st);
+/* HIP-event timing of the residual-tower conv launches (bench.py roofline) */
+int az_chess_timer_enable(az_chess_engine* eng, int on);
 
 #ifdef __cplusplus
 }

@@ -683,3 +683,293 @@ int orc_chess_from_fen(const char* fen, cpos* p) {
 }
 
 int orc_chess_pos_size(void) { return (int)sizeof(cpos); }
+
+/* =====================================================================
+ * Chess self-play MCTS (BASELINE configs[4]), restating
+ *   MCTS.select / search / evaluate_and_expand / backup / play
+ *                                custom_alphazero/mcts/mcts.py:111-222
+ *   normalize_probabilities     custom_alphazero/mcts/utils.py:4-16
+ *   play_game                   custom_alphazero/self_play.py:37-82
+ * over the chess rules above.  The tree arithmetic is the Connect-N
+ * oracle's (az_oracle.c, linked in): float64 UCB with libm pow, first-max
+ * argmax, float32 pairwise prior normalisation, positional zip of the
+ * action-ordered priors with the python-chess move order (mcts.py:151),
+ * float64 backup, np.random.choice on MT19937.  The reference cannot finish
+ * a chess game under MCTS (chess Board.get_result() takes no
+ * keep_same_player, chess/board.py:178 vs mcts.py:179): terminal boards
+ * score as get_result does in the canonical form (checkmate 1, draw 0).
+ * Games stop after max_plies (termination 5), a cap the reference lacks.
+ * ===================================================================== */
+#include <math.h>
+
+typedef struct {
+    uint32_t mt[624];
+    int pos;
+} orc_mt; /* az_oracle.c */
+void orc_mt_seed(orc_mt* s, uint32_t seed);
+double orc_mt_uniform(orc_mt* s);
+int orc_normalize_f32(const float* p, int n, double* out);
+void orc_normalize_f64(const double* p, int n, double* out);
+double orc_pow_half(int64_t n);
+
+#define ORC_CHESS_ACTIONS 1880
+
+typedef struct {
+    double W, prior;
+    int64_t N;
+    int child;       /* node id */
+    uint16_t action; /* move code */
+} cedge;
+
+typedef struct {
+    int first, count; /* edges (count 0: unexpanded or terminal) */
+    int initial;      /* the game's Board(): history [0 x 7, state] */
+    cpos pos;
+} cnode;
+
+typedef struct {
+    cnode* nodes;
+    cedge* edges;
+    int n_nodes, cap_nodes, n_edges, cap_edges;
+    double c_puct;
+    int eval_kind; /* 0 synthetic, 1 callback */
+    int (*cb)(void* ctx, const cpos* pos, int initial, float* probs, float* value);
+    void* ctx;
+    int64_t expansions, terminal_visits;
+    int error;
+} ctree;
+
+static uint64_t c_splitmix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* synthetic evaluator: dyadic priors k/64, values k/128, from a hash of
+ * what the network would see (position, counters, root-history flag) */
+void orc_chess_synth(const cpos* p, int initial, float* probs, float* value) {
+    uint64_t h = c_splitmix(p->pieces[0]);
+    for (int i = 1; i < 6; ++i) h = c_splitmix(h ^ p->pieces[i]);
+    h = c_splitmix(h ^ p->occupied_co[0]);
+    h = c_splitmix(h ^ p->occupied_co[1]);
+    h = c_splitmix(h ^ p->castling_rights);
+    uint64_t misc = (uint64_t)(uint16_t)p->ep_square | ((uint64_t)p->halfmove_clock << 16) |
+                    ((uint64_t)p->fullmove_number << 32) | ((uint64_t)initial << 48);
+    h = c_splitmix(h ^ misc);
+    uint64_t vh = c_splitmix(h ^ 0x5555555555555555ull);
+    *value = (float)(((double)(vh >> 56) - 128.0) / 128.0);
+    if ((vh & 0x3F) == 0) {
+        for (int a = 0; a < ORC_CHESS_ACTIONS; ++a) probs[a] = 0.0f;
+        return;
+    }
+    uint64_t w = h;
+    for (int a = 0; a < ORC_CHESS_ACTIONS; ++a) {
+        if (a && a % 12 == 0) w = c_splitmix(w);
+        probs[a] = (float)((double)(((w >> (5 * (a % 12))) & 31) + 1) / 64.0);
+    }
+}
+
+static int g_lut_ready = 0;
+static int16_t g_lut[64 * 64 * 5];
+static int action_index(uint16_t m) {
+    if (!g_lut_ready) {
+        uint16_t all[2048];
+        int n = orc_chess_all_moves(all);
+        for (int i = 0; i < 64 * 64 * 5; ++i) g_lut[i] = -1;
+        for (int i = 0; i < n; ++i) {
+            int pr = all[i] >> 12;
+            g_lut[((all[i] & 63) * 64 + ((all[i] >> 6) & 63)) * 5 + (pr ? pr - 1 : 0)] = (int16_t)i;
+        }
+        g_lut_ready = 1;
+    }
+    int pr = m >> 12;
+    return g_lut[((m & 63) * 64 + ((m >> 6) & 63)) * 5 + (pr ? pr - 1 : 0)];
+}
+
+static int ct_new_node(ctree* t, const cpos* pos, int initial) {
+    if (t->n_nodes == t->cap_nodes) {
+        t->cap_nodes = t->cap_nodes ? 2 * t->cap_nodes : 4096;
+        t->nodes = (cnode*)realloc(t->nodes, sizeof(cnode) * (size_t)t->cap_nodes);
+    }
+    int id = t->n_nodes++;
+    t->nodes[id].first = 0;
+    t->nodes[id].count = 0;
+    t->nodes[id].initial = initial;
+    t->nodes[id].pos = *pos;
+    return id;
+}
+
+static int ct_best_edge(const ctree* t, const cnode* node) {
+    const cedge* e = t->edges + node->first;
+    int64_t sum = 0;
+    for (int i = 0; i < node->count; ++i) sum += e[i].N;
+    double sq = orc_pow_half(sum);
+    int best = 0;
+    double best_v = 0.0;
+    for (int i = 0; i < node->count; ++i) {
+        double q = e[i].N ? e[i].W / (double)e[i].N : 0.0;
+        double u = t->c_puct * e[i].prior * sq / (double)(1 + e[i].N);
+        double ucb = q + u;
+        if (i == 0 || ucb > best_v) {
+            best = i;
+            best_v = ucb;
+        }
+    }
+    return best;
+}
+
+static double ct_expand(ctree* t, int node_id) {
+    float probs[ORC_CHESS_ACTIONS], value = 0.0f;
+    cpos pos = t->nodes[node_id].pos;
+    if (t->eval_kind == 0) {
+        orc_chess_synth(&pos, t->nodes[node_id].initial, probs, &value);
+    } else if (t->cb(t->ctx, &pos, t->nodes[node_id].initial, probs, &value) != 0) {
+        t->error = 1;
+    }
+    uint16_t mv[256];
+    int n = orc_chess_legal(&pos, mv);
+    /* probabilities[legal_moves_mask]: legal actions in action order */
+    int act[256];
+    for (int i = 0; i < n; ++i) act[i] = action_index(mv[i]);
+    float sorted[256];
+    for (int i = 0; i < n; ++i) {
+        int r = 0;
+        for (int j = 0; j < n; ++j) r += act[j] < act[i];
+        sorted[r] = probs[act[i]];
+    }
+    double priors[256];
+    orc_normalize_f32(sorted, n, priors);
+    if (t->n_edges + n > t->cap_edges) {
+        while (t->n_edges + n > t->cap_edges) t->cap_edges = t->cap_edges ? 2 * t->cap_edges : 16384;
+        t->edges = (cedge*)realloc(t->edges, sizeof(cedge) * (size_t)t->cap_edges);
+    }
+    int first = t->n_edges;
+    for (int i = 0; i < n; ++i) {
+        cpos child = pos;
+        orc_chess_play_canonical(&child, mv[i]);
+        int c = ct_new_node(t, &child, 0);
+        cedge* e = t->edges + first + i;
+        e->W = 0.0;
+        e->prior = priors[i]; /* zip(probabilities, node.board.moves) */
+        e->N = 0;
+        e->child = c;
+        e->action = mv[i];
+    }
+    t->n_edges += n;
+    t->nodes[node_id].first = first;
+    t->nodes[node_id].count = n;
+    t->expansions++;
+    return (double)value;
+}
+
+static void ct_search(ctree* t, int root, int sims) {
+    int path[4096];
+    for (int s = 0; s < sims; ++s) {
+        int depth = 0, node = root;
+        while (t->nodes[node].count) {
+            int k = ct_best_edge(t, t->nodes + node);
+            int e = t->nodes[node].first + k;
+            if (depth < 4096) path[depth++] = e;
+            node = t->edges[e].child;
+        }
+        double v;
+        int oc = orc_chess_outcome(&t->nodes[node].pos);
+        if (oc == 0) {
+            v = -ct_expand(t, node);
+        } else {
+            v = oc == 1 ? 1.0 : 0.0;
+            t->terminal_visits++;
+        }
+        for (int i = depth - 1; i >= 0; --i) {
+            t->edges[path[i]].N += 1;
+            t->edges[path[i]].W += v;
+            v = -v;
+        }
+    }
+}
+
+typedef struct {
+    int32_t T, result, termination;
+    int64_t expansions, terminal_visits;
+} orc_chess_game_out;
+
+/* One chess self-play game.  Outputs per ply t < max_plies: positions[t]
+ * (root before the move), moves[t], pol_n[t], pol_a[t][256] (action of each
+ * root edge, edge order), pol_p[t][256] (MCTS.play probabilities), root
+ * visit counts root_n[t][256]. */
+int orc_chess_play_game(int sims, uint32_t seed, int max_plies, int greedy_ply, double c_puct,
+                        int eval_kind,
+                        int (*cb)(void*, const cpos*, int, float*, float*), void* ctx,
+                        cpos* positions, uint16_t* moves, int32_t* pol_n, int16_t* pol_a,
+                        double* pol_p, int64_t* root_visits, orc_chess_game_out* out) {
+    init_tables();
+    ctree t;
+    memset(&t, 0, sizeof(t));
+    t.c_puct = c_puct;
+    t.eval_kind = eval_kind;
+    t.cb = cb;
+    t.ctx = ctx;
+    orc_mt rng;
+    orc_mt_seed(&rng, seed);
+    cpos start;
+    orc_chess_from_fen("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", &start);
+    int root = ct_new_node(&t, &start, 1);
+    int T = 0, term = 0;
+    for (;;) {
+        term = orc_chess_outcome(&t.nodes[root].pos);
+        if (term != 0) break;
+        if (T >= max_plies) {
+            term = 5;
+            break;
+        }
+        ct_search(&t, root, sims);
+        cnode* node = t.nodes + root;
+        int n = node->count;
+        if (n == 0) {
+            t.error = 1;
+            break;
+        }
+        double counts[256], pi[256];
+        for (int i = 0; i < n; ++i) counts[i] = (double)t.edges[node->first + i].N;
+        int greedy = node->pos.fullmove_number >= greedy_ply;
+        if (greedy) {
+            int im = 0;
+            for (int i = 1; i < n; ++i)
+                if (counts[i] > counts[im]) im = i;
+            for (int i = 0; i < n; ++i) pi[i] = i == im ? 1.0 : 0.0;
+        } else {
+            orc_normalize_f64(counts, n, pi);
+        }
+        double u = orc_mt_uniform(&rng);
+        double acc = 0.0, cdf[256];
+        for (int i = 0; i < n; ++i) {
+            acc += pi[i];
+            cdf[i] = acc;
+        }
+        double last = cdf[n - 1];
+        int idx = 0;
+        for (int i = 0; i < n; ++i)
+            if (cdf[i] / last <= u) idx = i + 1;
+        if (idx >= n) idx = n - 1;
+        positions[T] = node->pos;
+        moves[T] = t.edges[node->first + idx].action;
+        pol_n[T] = n;
+        for (int i = 0; i < n; ++i) {
+            pol_a[(size_t)T * 256 + i] = (int16_t)action_index(t.edges[node->first + i].action);
+            pol_p[(size_t)T * 256 + i] = pi[i];
+            if (root_visits) root_visits[(size_t)T * 256 + i] = t.edges[node->first + i].N;
+        }
+        root = t.edges[node->first + idx].child;
+        T++;
+    }
+    out->T = T;
+    out->termination = term;
+    out->result = term == 1 ? 1 : 0;
+    out->expansions = t.expansions;
+    out->terminal_visits = t.terminal_visits;
+    int err = t.error;
+    free(t.nodes);
+    free(t.edges);
+    return err ? -1 : 0;
+}

@@ -177,3 +177,65 @@ def random_positions(n, seed, max_plies=200, canonical=True):
         is_root = False
         ply += 1
     return np.array(out, POS_DTYPE), np.array(roots, bool)
+
+
+class ChessGameOut(ctypes.Structure):
+    _fields_ = [("T", ctypes.c_int32), ("result", ctypes.c_int32), ("termination", ctypes.c_int32),
+                ("expansions", ctypes.c_int64), ("terminal_visits", ctypes.c_int64)]
+
+
+CHESS_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float))
+
+
+def play_game(sims, seed, max_plies, greedy_ply=8, c_puct=1.5, callback=None):
+    """One chess self-play game on the oracle.  callback(pos, initial) ->
+    (probs f32[1880], value) replaces the synthetic evaluator (network replay)."""
+    L = lib()
+    fn = L.orc_chess_play_game
+    fn.restype = ctypes.c_int
+    P = ctypes.c_void_p
+    fn.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                   ctypes.c_int, CHESS_CB, P, P, P, P, P, P, P, ctypes.POINTER(ChessGameOut)]
+    positions = np.zeros(max_plies, POS_DTYPE)
+    moves = np.zeros(max_plies, np.uint16)
+    pol_n = np.zeros(max_plies, np.int32)
+    pol_a = np.zeros((max_plies, 256), np.int16)
+    pol_p = np.zeros((max_plies, 256), np.float64)
+    visits = np.zeros((max_plies, 256), np.int64)
+    out = ChessGameOut()
+    err = []
+
+    def _cb(ctx, pos_ptr, initial, probs_ptr, value_ptr):
+        try:
+            raw = ctypes.string_at(pos_ptr, POS_DTYPE.itemsize)
+            pos = np.frombuffer(raw, POS_DTYPE)[0]
+            p, v = callback(pos, int(initial))
+            p = np.ascontiguousarray(p, np.float32)
+            ctypes.memmove(probs_ptr, p.ctypes.data, 4 * 1880)
+            value_ptr[0] = float(v)
+            return 0
+        except Exception as e:  # pragma: no cover - surfaced below
+            err.append(e)
+            return 1
+
+    cb = CHESS_CB(_cb) if callback is not None else CHESS_CB()
+    rc = fn(sims, seed & 0xFFFFFFFF, max_plies, greedy_ply, c_puct, 1 if callback else 0, cb, None,
+            _p(positions), _p(moves), _p(pol_n), _p(pol_a), _p(pol_p), _p(visits), ctypes.byref(out))
+    if err:
+        raise err[0]
+    assert rc == 0, "oracle chess game failed"
+    T = out.T
+    return dict(T=T, result=out.result, termination=out.termination, expansions=out.expansions,
+                terminal_visits=out.terminal_visits, positions=positions[:T], moves=moves[:T],
+                policy_n=pol_n[:T], policy_actions=pol_a[:T], policy_probs=pol_p[:T],
+                root_visits=visits[:T])
+
+
+def synth(pos, initial):
+    L = lib()
+    L.orc_chess_synth.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    probs = np.zeros(1880, np.float32)
+    v = np.zeros(1, np.float32)
+    L.orc_chess_synth(_p(_one(pos)), int(initial), _p(probs), _p(v))
+    return probs, float(v[0])

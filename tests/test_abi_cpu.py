@@ -41,6 +41,8 @@ def test_struct_sizes_match_header():
     assert ctypes.sizeof(az.Config) == 4 * 6 + 8 + 4 * 5 + 4 + 8 + 8 + 8 + 32
     assert ctypes.sizeof(az.Tensor) == 8 + 8 + 8 + 4 + 4
     assert ctypes.sizeof(az.Stats) == 8 * 8 + 8 + 8 * 7
+    # az_chess_config: 2 int32, double, 6 int32, double, int64, int32 + 7 reserved
+    assert ctypes.sizeof(az.ChessConfig) == 8 + 8 + 24 + 8 + 8 + 4 + 28
 
 
 def test_engine_fails_loudly_without_gpu():

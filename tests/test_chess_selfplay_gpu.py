@@ -1,0 +1,123 @@
+"""Chess self-play on the GPU (csrc/az_chess_mcts.hip, BASELINE configs[4])
+against the chess oracle's MCTS (oracle/chess_oracle.c): the synthetic
+evaluator pins the tree arithmetic bit for bit (moves, root positions,
+MCTS.play policies, expansion counts, terminations); the network evaluator
+is checked against the float64 Keras restatement (1e-5) and replayed through
+the oracle with the engine's own batch-1 outputs."""
+import numpy as np
+import pytest
+
+import chess_oracle as C
+
+pytestmark = pytest.mark.gpu
+NET_TOL = 1e-5
+
+
+def _engine(**kw):
+    from custom_alphazero import engine as az
+    return az.ChessEngine(**kw)
+
+
+def _compare(r, g, ref, tag):
+    T = int(r["lengths"][g])
+    assert T == ref["T"], (tag, g, T, ref["T"])
+    assert r["terminations"][g] == ref["termination"], (tag, g)
+    assert r["results"][g] == ref["result"], (tag, g)
+    assert r["expansions"][g] == ref["expansions"], (tag, g)
+    assert np.array_equal(r["moves"][g, :T], ref["moves"]), (tag, g)
+    assert r["positions"][g, :T].tobytes() == ref["positions"].tobytes(), (tag, g)
+    assert np.array_equal(r["policy_n"][g, :T], ref["policy_n"]), (tag, g)
+    for t in range(T):
+        n = ref["policy_n"][t]
+        assert np.array_equal(r["policy_actions"][g, t, :n], ref["policy_actions"][t, :n]), (tag, g, t)
+        assert np.array_equal(r["policy_probs"][g, t, :n].view(np.uint64),
+                              ref["policy_probs"][t, :n].view(np.uint64)), (tag, g, t)
+
+
+@pytest.mark.parametrize("sims,plies,slots,games,greedy", [
+    (24, 40, 3, 5, 8),      # slot refill, the reference's greedy threshold (never reached)
+    (16, 30, 4, 4, 1),      # greedy from the first move (one-hot policy, one draw consumed)
+    (8, 400, 4, 6, 8),      # long games: checkmate / stalemate / 75-move / cap terminations
+    (2, 60, 2, 2, 8),       # S=2: the root expansion plus one visit
+])
+def test_chess_selfplay_synthetic_matches_oracle(sims, plies, slots, games, greedy):
+    from custom_alphazero import engine as az
+    eng = _engine(mcts_iterations=sims, slots=slots, evaluator=az.EVAL_SYNTHETIC, max_plies=plies,
+                  index_move_greedy=greedy)
+    st = eng.selfplay_run(0, games, 1000)
+    r = eng.selfplay_results()
+    assert st["errors"] == 0 and st["games_done"] == games
+    for g in range(games):
+        ref = C.play_game(sims, 1000 + g, plies, greedy_ply=greedy)
+        _compare(r, g, ref, "synthetic")
+    eng.close()
+
+
+def test_chess_synthetic_evaluator_matches_oracle():
+    """The device synthetic evaluator = orc_chess_synth (indirectly: one
+    expansion's priors are its normalised output)."""
+    p, v = C.synth(C.from_fen(), 1)
+    assert p.dtype == np.float32 and -1 <= v < 1 and ((p * 64) % 1 == 0).all()
+
+
+@pytest.fixture(scope="module")
+def chess_net():
+    from custom_alphazero import engine as az
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    spec = weight_spec(8, 8, 1880, in_channels=118)
+    w = init_weights(spec, seed=3)
+    # non-trivial BatchNorm statistics so the folding is exercised
+    rng = np.random.default_rng(0)
+    for k in list(w):
+        if k.endswith(".mean"):
+            w[k] = rng.normal(0, 0.1, w[k].shape).astype(np.float32)
+        elif k.endswith(".var"):
+            w[k] = rng.uniform(0.5, 1.5, w[k].shape).astype(np.float32)
+    eng = _engine(mcts_iterations=16, slots=64, evaluator=az.EVAL_NETWORK, max_plies=12)
+    eng.set_weights(w.items())
+    yield eng, w
+    eng.close()
+
+
+def _states(n, seed):
+    pos, roots = C.random_positions(n, seed=seed)
+    x = np.stack([C.full_state(*C.reference_history(p, bool(r)), p) for p, r in zip(pos, roots)])
+    return x.astype(np.float32)
+
+
+def test_chess_forward_matches_keras_restatement(chess_net):
+    import keras_ref
+    eng, w = chess_net
+    x = _states(96, seed=21)  # more than one engine chunk (64 slots)
+    probs, values = eng.forward(x)
+    rp, rv = keras_ref.forward(w, x, depth=4)
+    assert np.abs(probs - rp).max() < NET_TOL
+    assert np.abs(values - rv).max() < NET_TOL
+    # batch invariance (the replay parity below depends on it)
+    p1, v1 = eng.forward(x[5:6])
+    assert np.array_equal(p1[0], probs[5]) and v1[0] == values[5]
+
+
+def test_chess_selfplay_network_replays_on_oracle(chess_net):
+    eng, _ = chess_net
+    eng.selfplay_run(0, 3, 77)
+    r = eng.selfplay_results()
+
+    def cb(pos, initial):
+        x = C.full_state(*C.reference_history(pos, bool(initial)), pos)[None].astype(np.float32)
+        p, v = eng.forward(x)
+        return p[0], float(v[0])
+
+    for g in range(3):
+        ref = C.play_game(16, 77 + g, 12, callback=cb)
+        _compare(r, g, ref, "network")
+
+
+def test_chess_engine_errors():
+    from custom_alphazero import engine as az
+    with pytest.raises(az.AzError, match="az_chess_engine_set_weights"):
+        eng = _engine(mcts_iterations=4, slots=2, evaluator=az.EVAL_NETWORK)
+        eng.selfplay_begin(0, 1, 0)
+    with pytest.raises(az.AzError, match="arena"):
+        eng = _engine(mcts_iterations=64, slots=2, evaluator=az.EVAL_SYNTHETIC, arena_edges=300)
+        eng.selfplay_run(0, 2, 0)
