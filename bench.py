@@ -38,10 +38,12 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=60)
-    ap.add_argument("--slots", type=int, default=4096)
-    ap.add_argument("--sims", type=int, default=100)
+    ap.add_argument("--game", choices=("connect_n", "chess"), default="connect_n",
+                    help="chess: BASELINE configs[4] per-GPU shard (256 games, 800 sims/move)")
+    ap.add_argument("--steps", type=int, default=None, help="timed moves (30; chess 3)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed moves first (60; chess 2)")
+    ap.add_argument("--slots", type=int, default=None, help="concurrent games per GPU (4096; chess 256)")
+    ap.add_argument("--sims", type=int, default=None, help="sims per move (100; chess 800)")
     ap.add_argument("--height", type=int, default=6)
     ap.add_argument("--width", type=int, default=7)
     ap.add_argument("--n", type=int, default=4)
@@ -56,7 +58,12 @@ def parse():
                     help="transposition cache (the reference's plays_inferences) entries = 2^N; 0 = off")
     ap.add_argument("--no-cache-window", action="store_true",
                     help="skip the second timed window with the cache bypassed")
-    return ap.parse_args()
+    args = ap.parse_args()
+    chess = args.game == "chess"
+    for k, c4, ch in (("steps", 30, 3), ("warmup", 60, 2), ("slots", 4096, 256), ("sims", 100, 800)):
+        if getattr(args, k) is None:
+            setattr(args, k, ch if chess else c4)
+    return args
 
 
 def cpu_baseline(args, weights):
@@ -94,8 +101,169 @@ def cpu_baseline(args, weights):
     }
 
 
+def _device_weights(spec, host_w, rank, world, args, dev):
+    """Rank 0's init reaches every rank by one flat RCCL broadcast over xGMI."""
+    import torch
+    import torch.distributed as dist
+    flat = torch.cat([torch.from_numpy(host_w[n].reshape(-1)) for n, _ in spec]).to(dev)
+    if world > 1:
+        if rank != 0:
+            flat.zero_()
+        if args.dist_backend == "gloo":
+            host = flat.cpu()
+            dist.broadcast(host, src=0)
+            flat.copy_(host)
+        else:
+            dist.broadcast(flat, src=0)
+    named, off = [], 0
+    for name, shape in spec:
+        k = int(np.prod(shape))
+        named.append((name, flat[off:off + k]))
+        off += k
+    return named, flat
+
+
+def chess_cpu_baseline(args, weights):
+    import multiprocessing as mp
+
+    import refport
+    cores = len(os.sched_getaffinity(0))
+    workers = args.cpu_workers or max(1, min(15, cores - 1))
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(refport.chess_baseline_worker,
+                       [(args.sims, weights, args.depth, args.cpu_baseline_seconds, 20_000_000 + i)
+                        for i in range(workers)])
+    wall = time.perf_counter() - t0
+    exps = sum(r[0] for r in res)
+    return {"value": round(exps / wall, 2), "unit": "expansions/s", "cores": workers, "kind": "port",
+            "plies_per_s_est": round(sum(r[1] for r in res) / wall, 4),
+            "sample": (f"oracle chess MCTS (C tree, reference arithmetic) + torch-CPU network at batch 1 "
+                       f"on Board.full_state, {workers} worker processes x 1 thread, {args.sims} sims/move, "
+                       f"{exps} expansions in {wall:.1f}s; the reference's own chess path cannot run "
+                       f"under MCTS (chess/board.py:178 vs mcts.py:179)")}
+
+
+def chess_main(args):
+    """BASELINE configs[4]: chess, 800 sims/move, 2048 games over 8 GPUs =
+    256 concurrent games per GPU (weak scaling).  A game outlasts any short
+    window (hundreds of plies x 800 simulations), so value is the MCTS
+    node-expansion rate, the metric's second half; plies/s and completed
+    games are reported next to it."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    spec = weight_spec(8, 8, 1880, depth=args.depth, in_channels=118)
+    host_w = init_weights(spec, seed=0)
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = chess_cpu_baseline(args, host_w)
+    import torch
+    import torch.distributed as dist
+    from custom_alphazero import engine as az
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    if world > 1:
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", dev_index)
+    named, _flat = _device_weights(spec, host_w, rank, world, args, dev)
+    eng = az.ChessEngine(mcts_iterations=args.sims, slots=args.slots, evaluator=az.EVAL_NETWORK,
+                         max_plies=512, depth=args.depth, device=dev_index, conv_algo=args.conv_algo,
+                         lanes=args.lanes)
+    eng.set_weights(named)
+    budget = args.slots * 2
+    eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)
+    eng.selfplay_step(args.warmup)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.timer(True)
+    st0 = eng.stats()
+    t0 = time.perf_counter()
+    eng.selfplay_step(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st1 = eng.stats()
+    eng.timer(False)
+    d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
+                                      "terminal_visits", "evaluations")}
+    local_evals = d["evaluations"]
+    if world > 1:
+        red_dev = "cpu" if args.dist_backend == "gloo" else dev
+        t = torch.tensor([d["games_done"], d["expansions"], d["simulations"], d["plies"]],
+                         dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        d["games_done"], d["expansions"], d["simulations"], d["plies"] = (int(v) for v in t.tolist())
+        elapsed = float(tmax.item())
+    F, HW, TB = 128, 64, 16
+    conv_flop_per_board = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
+    mfma_flop_per_board = (TB * 36 * 2 * F * F * args.depth if args.conv_algo == 0
+                           else conv_flop_per_board)
+    busy = st1["conv_busy_ms"]
+    launches = st1["conv_launches"]
+    achieved = local_evals * conv_flop_per_board / (busy * 1e-3) / 1e12 if busy else 0.0
+    if rank == 0:
+        line = {
+            "metric": f"MCTS node-expansions/s (Chess, {args.sims} sims/move)",
+            "value": round(d["expansions"] / elapsed, 1),
+            "unit": "expansions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32 network / f64 PUCT",
+            "data": "synthetic (self-generated games, random-init Keras-default weights, torch seed 0)",
+            "config": {
+                "workload": (f"Chess (custom_alphazero/chess), {args.sims} sims/move, {args.slots} concurrent "
+                             f"games per GPU, (8,8,118) planes, 1880 actions, 128f x {args.depth}-block net "
+                             f"(BASELINE.json configs[4], per-GPU shard of 2048 games over 8 GPUs)"),
+                "global_batch": args.slots * world,
+                "parallelism": f"games sharded over {world} GPU(s)",
+            },
+            "plies_per_s": round(d["plies"] / elapsed, 2),
+            "simulations_per_s": round(d["simulations"] / elapsed, 1),
+            "games_timed": d["games_done"],
+            "terminal_visits": d["terminal_visits"],
+            "lanes": args.lanes or "auto",
+            "roofline": {
+                "kernel": "wino_conv_kernel (residual tower, 8 launches per forward)",
+                "bound": "mfma",
+                "achieved": round(achieved, 2),
+                "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": None,
+                "achieved_basis": "algorithmic (direct-convolution) FLOP of the tower / conv-busy time (HIP events)",
+                "algorithmic_flop_per_board": conv_flop_per_board,
+                "mfma_flop_per_board": mfma_flop_per_board,
+                "mfma_frac": round(achieved * mfma_flop_per_board / conv_flop_per_board
+                                   / FP32_MFMA_PEAK_TFLOPS, 4),
+                "boards_per_launch": round(local_evals / max(launches / (2 * args.depth), 1), 1),
+                "avg_launch_ms": round(st1["conv_ms"] / max(launches, 1), 4),
+                "conv_busy_ms": round(busy, 2),
+            },
+            "cpu_baseline": base,
+        }
+        if base:
+            line["gpu_over_cpu"] = round(line["value"] / base["value"], 1) if base["value"] else None
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.game == "chess":
+        return chess_main(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -121,21 +289,7 @@ def main():
         dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", dev_index)
     # weights: rank 0's init, one flat RCCL broadcast (~5 MB) to every rank
-    flat = torch.cat([torch.from_numpy(host_w[n].reshape(-1)) for n, _ in spec]).to(dev)
-    if world > 1:
-        if rank != 0:
-            flat.zero_()
-        if args.dist_backend == "gloo":
-            host = flat.cpu()
-            dist.broadcast(host, src=0)
-            flat.copy_(host)
-        else:
-            dist.broadcast(flat, src=0)
-    named, off = [], 0
-    for name, shape in spec:
-        k = int(torch.tensor(shape).prod())
-        named.append((name, flat[off:off + k]))
-        off += k
+    named, _flat = _device_weights(spec, host_w, rank, world, args, dev)
 
     eng = az.Engine(args.height, args.width, args.n, True, args.sims, slots=args.slots,
                     evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index,

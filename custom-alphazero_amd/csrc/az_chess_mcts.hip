@@ -64,7 +64,8 @@ struct CTree {
   uint16_t* leaf_moves;    // [slots][AZ_CHESS_MAX_MOVES]
   int32_t* leaf_n;         // [slots]
   int32_t* slot_exp;       // [slots]
-  uint32_t* mt;            // [625][slots] word-major MT19937
+  uint32_t* mt;            // [625][mt_stride] word-major MT19937 (a lane view offsets it)
+  int32_t mt_stride;       // slots of the whole engine
   int32_t* eval_slot;      // [slots]
   int32_t* eval_count;     // [1]
   unsigned long long* stats;
@@ -97,7 +98,8 @@ __device__ __forceinline__ void flag(const CTree& t, unsigned long long f) {
 }
 
 // MT19937 per slot, word-major (az_tree.hip layout)
-__device__ void mt_seed(const CTree& t, int slots, int s, uint32_t seed) {
+__device__ void mt_seed(const CTree& t, int s, uint32_t seed) {
+  const int slots = t.mt_stride;
   uint32_t prev = seed;
   t.mt[s] = seed;
   for (int i = 1; i < kMtN; ++i) {
@@ -106,7 +108,8 @@ __device__ void mt_seed(const CTree& t, int slots, int s, uint32_t seed) {
   }
   t.mt[(size_t)kMtN * slots + s] = kMtN;
 }
-__device__ uint32_t mt_next(const CTree& t, int slots, int s) {
+__device__ uint32_t mt_next(const CTree& t, int s) {
+  const int slots = t.mt_stride;
   uint32_t* m = t.mt;
   uint32_t pos = m[(size_t)kMtN * slots + s];
   if (pos >= (uint32_t)kMtN) {
@@ -122,9 +125,9 @@ __device__ uint32_t mt_next(const CTree& t, int slots, int s) {
   m[(size_t)kMtN * slots + s] = pos + 1;
   return az::mt_temper(y);
 }
-__device__ double mt_uniform(const CTree& t, int slots, int s) {
-  const uint32_t a = mt_next(t, slots, s) >> 5;
-  const uint32_t b = mt_next(t, slots, s) >> 6;
+__device__ double mt_uniform(const CTree& t, int s) {
+  const uint32_t a = mt_next(t, s) >> 5;
+  const uint32_t b = mt_next(t, s) >> 6;
   return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
 }
 
@@ -202,7 +205,7 @@ __device__ void slot_reset(const CCfg& g, const CTree& t, const CSamples& smp, i
   t.path_len[s] = 0;
   t.slot_exp[s] = 0;
   t.game_id[s] = gid;
-  mt_seed(t, g.slots, s, smp.base_seed + (uint32_t)gid);
+  mt_seed(t, s, smp.base_seed + (uint32_t)gid);
 }
 
 // synthetic evaluator (oracle/chess_oracle.c orc_chess_synth): dyadic priors
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp)
       for (int i = 0; i < n; ++i) pi[i] = sum == 0.0 ? 1.0 / (double)n : pi[i] / sum;
     }
     // np.random.choice(edges, 1, p): one random_sample, cumsum, normalise, searchsorted right
-    const double u = mt_uniform(t, g.slots, s);
+    const double u = mt_uniform(t, s);
     double cdf[1];
     double acc = 0.0, last;
     for (int i = 0; i < n; ++i) acc += pi[i];
@@ -611,12 +614,28 @@ __global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp)
 
 using namespace azc;
 
+// A lane = a contiguous slot group searched on its own HIP stream: its
+// simulations' tree kernels and network launches overlap the other lanes'
+// (a 256-game step is latency-bound: one launch fills half the CUs).
+struct CLane {
+  int first = 0;
+  hipStream_t stream = nullptr;
+  CCfg g{};
+  CTree t{};
+  float* x = nullptr;
+  float* act[3] = {nullptr, nullptr, nullptr};
+  float* probs = nullptr;
+  float* values = nullptr;
+  az::ConvTimer timer;
+};
+
 struct az_chess_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   az_chess_config cfg{};
   CCfg g{};
   CTree t{};
+  std::vector<CLane*> lanes;
   CSamples smp{};
   az::NetDev net{};
   az::ConvTimer timer;
@@ -653,21 +672,64 @@ int check_errors(az_chess_engine* e) {
   return az::fail_abi(AZ_E_DEVICE, m);
 }
 
-int simulate(az_chess_engine* e) {
-  hipStream_t s = e->stream;
-  const int S = e->g.slots;
-  select_kernel<<<S, 64, 0, s>>>(e->g, e->t);
-  AZC_HIP(hipMemsetAsync(e->t.eval_count, 0, sizeof(int32_t), s));
-  leaf_kernel<<<(S + 127) / 128, 128, 0, s>>>(e->g, e->t);
-  if (e->g.evaluator == AZ_EVAL_NETWORK) {
-    encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(e->g, e->t, reinterpret_cast<float4*>(e->x));
-    az::launch_forward(e->net, e->x, e->t.eval_count, S, 8, 8, AZ_CHESS_ACTIONS, e->act[0], e->act[1],
-                       e->act[2], e->probs, e->values, s, e->timer.enabled ? &e->timer : nullptr);
+int simulate(az_chess_engine* e, CLane& L) {
+  hipStream_t s = L.stream;
+  const int S = L.g.slots;
+  select_kernel<<<S, 64, 0, s>>>(L.g, L.t);
+  AZC_HIP(hipMemsetAsync(L.t.eval_count, 0, sizeof(int32_t), s));
+  leaf_kernel<<<(S + 63) / 64, 64, 0, s>>>(L.g, L.t);
+  if (L.g.evaluator == AZ_EVAL_NETWORK) {
+    encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, reinterpret_cast<float4*>(L.x));
+    az::launch_forward(e->net, L.x, L.t.eval_count, S, 8, 8, AZ_CHESS_ACTIONS, L.act[0], L.act[1],
+                       L.act[2], L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr);
   } else {
-    synth_kernel<<<(S + 255) / 256, 256, 0, s>>>(e->g, e->t, e->probs, e->values);
+    synth_kernel<<<(S + 255) / 256, 256, 0, s>>>(L.g, L.t, L.probs, L.values);
   }
-  expand_kernel<<<S, 64, 0, s>>>(e->g, e->t, e->probs, e->values);
+  expand_kernel<<<S, 64, 0, s>>>(L.g, L.t, L.probs, L.values);
   AZC_HIP(hipGetLastError());
+  return 0;
+}
+
+int sync_lanes(az_chess_engine* e) {
+  for (CLane* L : e->lanes) AZC_HIP(hipStreamSynchronize(L->stream));
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+// lane view: per-slot arrays offset to the lane's first slot, its own eval
+// queue counter and evaluator buffer slices
+int make_lane(az_chess_engine* e, CLane* L, int first, int n) {
+  L->first = first;
+  L->g = e->g;
+  L->g.slots = n;
+  CTree t = e->t;
+  const size_t f = (size_t)first;
+  t.edges += f * 2 * e->g.half_cap;
+  t.root += f;
+  t.root_first += f;
+  t.root_n += f;
+  t.half += f;
+  t.top += f;
+  t.ply += f;
+  t.initial += f;
+  t.game_id += f;
+  t.path += f * e->g.max_depth;
+  t.path_len += f;
+  t.leaf += f;
+  t.leaf_moves += f * AZ_CHESS_MAX_MOVES;
+  t.leaf_n += f;
+  t.slot_exp += f;
+  t.mt += f;
+  t.eval_slot += f;
+  int rc;
+  if ((rc = e->alloc(&t.eval_count, 1))) return rc;
+  L->t = t;
+  if (e->x) L->x = e->x + f * 64 * 128;
+  for (int i = 0; i < 3; ++i) L->act[i] = e->act[i] ? e->act[i] + f * 64 * 128 : nullptr;
+  L->probs = e->probs + f * AZ_CHESS_ACTIONS;
+  L->values = e->values + f;
+  if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess)
+    return az::fail_abi(AZ_E_HIP, "hipStreamCreate failed");
   return 0;
 }
 
@@ -759,9 +821,23 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
     for (int i = 0; i < 3; ++i)
       if ((rc = e->alloc(&e->act[i], S * 64 * 128))) return cleanup(rc);
   }
+  t.mt_stride = g.slots;
   e->net.depth = c.depth;
   e->net.algo = c.conv_algo;
   e->net.hidden = c.value_hidden;
+  if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));
+  // auto = 1: at 256 games a chess step is bound by its launch chain; extra
+  // streams measured slower (375k expansions/s with 1 lane, 311k with 2,
+  // 159k with 4: more launches per simulation from one host thread, streams
+  // sharing the 4 hardware queues)
+  int nl = c.lanes > 0 ? c.lanes : 1;
+  nl = std::min(nl, std::min(g.slots, 16));
+  for (int l = 0; l < nl; ++l) {
+    CLane* L = new CLane();
+    e->lanes.push_back(L);
+    const int lo = (int)((int64_t)g.slots * l / nl), hi = (int)((int64_t)g.slots * (l + 1) / nl);
+    if ((rc = make_lane(e, L, lo, hi - lo))) return cleanup(rc);
+  }
   *out = e;
   return 0;
 }
@@ -770,6 +846,13 @@ int az_chess_engine_destroy(az_chess_engine* e) {
   if (!e) return 0;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (CLane* L : e->lanes) {
+    if (L->stream) {
+      (void)hipStreamSynchronize(L->stream);
+      (void)hipStreamDestroy(L->stream);
+    }
+    delete L;
+  }
   for (void* p : e->sample_bufs) (void)hipFree(p);
   for (void* p : e->owned) (void)hipFree(p);
   if (e->timer_ref) (void)hipEventDestroy(e->timer_ref);
@@ -813,7 +896,8 @@ int az_chess_selfplay_begin(az_chess_engine* e, int64_t first_game, int64_t n_ga
   if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
     return az::fail_abi(AZ_E_STATE, "network evaluator selected but az_chess_engine_set_weights was not called");
   AZC_HIP(hipSetDevice(e->device));
-  AZC_HIP(hipStreamSynchronize(e->stream));
+  int rc;
+  if ((rc = sync_lanes(e))) return rc;
   for (void* p : e->sample_bufs) (void)hipFree(p);
   e->sample_bufs.clear();
   CSamples& smp = e->smp;
@@ -829,7 +913,6 @@ int az_chess_selfplay_begin(az_chess_engine* e, int64_t first_game, int64_t n_ga
     AZC_HIP(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 16), e->stream));
     return 0;
   };
-  int rc;
   if ((rc = get((void**)&smp.pos, G * P * sizeof(az_chess_pos))) ||
       (rc = get((void**)&smp.moves, G * P * sizeof(uint16_t))) ||
       (rc = get((void**)&smp.pol_n, G * P * sizeof(int32_t))) ||
@@ -852,7 +935,8 @@ int az_chess_selfplay_begin(az_chess_engine* e, int64_t first_game, int64_t n_ga
 int az_chess_stats(az_chess_engine* e, az_stats* st) {
   if (!e || !st) return az::fail_abi(AZ_E_INVALID, "null argument");
   AZC_HIP(hipSetDevice(e->device));
-  AZC_HIP(hipStreamSynchronize(e->stream));
+  int rc;
+  if ((rc = sync_lanes(e))) return rc;
   unsigned long long h[az::kStatCount];
   AZC_HIP(hipMemcpy(h, e->t.stats, sizeof(h), hipMemcpyDeviceToHost));
   std::vector<int64_t> gid(e->g.slots);
@@ -866,11 +950,28 @@ int az_chess_stats(az_chess_engine* e, az_stats* st) {
   st->errors = (int64_t)h[az::kStatErrors];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
   st->active_slots = std::count_if(gid.begin(), gid.end(), [](int64_t v) { return v >= 0; });
-  e->timer.flush();
-  st->conv_ms = e->timer.total_ms;
-  st->conv_launches = e->timer.launches;
-  double busy = 0.0;
-  for (const auto& iv : e->timer.intervals) busy += iv.second - iv.first;  // one stream: no overlap
+  // conv-busy time = union of the timed conv intervals over all lanes
+  std::vector<az::ConvTimer*> timers = {&e->timer};
+  for (CLane* L : e->lanes) timers.push_back(&L->timer);
+  std::vector<std::pair<double, double>> iv;
+  for (az::ConvTimer* tm : timers) {
+    tm->flush();
+    st->conv_ms += tm->total_ms;
+    st->conv_launches += tm->launches;
+    iv.insert(iv.end(), tm->intervals.begin(), tm->intervals.end());
+  }
+  std::sort(iv.begin(), iv.end());
+  double busy = 0.0, lo = 0.0, hi = -1.0;
+  for (const auto& x : iv) {
+    if (x.first > hi) {
+      if (hi > lo) busy += hi - lo;
+      lo = x.first;
+      hi = x.second;
+    } else {
+      hi = std::max(hi, x.second);
+    }
+  }
+  if (hi > lo) busy += hi - lo;
   st->conv_busy_ms = busy;
   return 0;
 }
@@ -880,12 +981,14 @@ int az_chess_selfplay_step(az_chess_engine* e, int n_moves, az_stats* st) {
   AZC_HIP(hipSetDevice(e->device));
   int rc;
   for (int mv = 0; mv < n_moves; ++mv) {
+    // lanes interleaved per simulation so every stream always has work queued
     for (int s = 0; s < e->g.sims; ++s)
-      if ((rc = simulate(e))) return rc;
-    play_kernel<<<e->g.slots, 64, 0, e->stream>>>(e->g, e->t, e->smp);
+      for (CLane* L : e->lanes)
+        if ((rc = simulate(e, *L))) return rc;
+    for (CLane* L : e->lanes) play_kernel<<<L->g.slots, 64, 0, L->stream>>>(L->g, L->t, e->smp);
     AZC_HIP(hipGetLastError());
   }
-  AZC_HIP(hipStreamSynchronize(e->stream));
+  if ((rc = sync_lanes(e))) return rc;
   if ((rc = check_errors(e))) return rc;
   if (st) return az_chess_stats(e, st);
   return 0;
@@ -909,7 +1012,8 @@ int az_chess_selfplay_results(az_chess_engine* e, int32_t* lengths, int32_t* res
                               int16_t* policy_actions, double* policy_probs) {
   if (!e) return az::fail_abi(AZ_E_INVALID, "null engine");
   AZC_HIP(hipSetDevice(e->device));
-  AZC_HIP(hipStreamSynchronize(e->stream));
+  int rc;
+  if ((rc = sync_lanes(e))) return rc;
   const size_t G = (size_t)e->sp_n, P = (size_t)e->smp.plies, M = AZ_CHESS_MAX_MOVES;
   if (G == 0) return 0;
   const CSamples& s = e->smp;
@@ -933,10 +1037,16 @@ int az_chess_timer_enable(az_chess_engine* e, int on) {
   if (!e->timer_ref) AZC_HIP(hipEventCreate(&e->timer_ref));
   AZC_HIP(hipEventRecord(e->timer_ref, e->stream));
   AZC_HIP(hipStreamSynchronize(e->stream));
-  e->timer.flush();
-  e->timer.reset();
-  e->timer.ref = &e->timer_ref;
-  e->timer.enabled = on != 0;
+  int rc;
+  if ((rc = sync_lanes(e))) return rc;
+  std::vector<az::ConvTimer*> timers = {&e->timer};
+  for (CLane* L : e->lanes) timers.push_back(&L->timer);
+  for (az::ConvTimer* tm : timers) {
+    tm->flush();
+    tm->reset();
+    tm->ref = &e->timer_ref;
+    tm->enabled = on != 0;
+  }
   return 0;
 }
 

@@ -481,6 +481,92 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
   }
 }
 
+// Chess-size heads (A = 1880), used when the 1x1 head convs ran in the last
+// conv's epilogue (feat = [boards][HW] float4: policy ch 0, ch 1, value, 0).
+// policy_dense_kernel: Dense(2HW -> A) as a tiled GEMM over the live batch --
+// a workgroup owns 64 actions x 32 boards, stages the weight tile [2HW][64]
+// and the boards' flattened policy features [32][2HW] in LDS, and each thread
+// accumulates one action for 8 boards, s = bias + sum_i p[i] * w[i][a] in i
+// order, into `logits` (the probs buffer).  One wave per board could not hide
+// the 962 KB weight stream (60% of a chess step); here every weight is read
+// once per 32 boards.
+template <int K>
+__global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restrict__ feat,
+                                                           const float* __restrict__ wpd,
+                                                           const float* __restrict__ bpd,
+                                                           const int* __restrict__ count, int n_static,
+                                                           int HW, int A, float* __restrict__ logits) {
+  __shared__ float ws[K][64];
+  __shared__ float ps[32][K];
+  const int n = count ? *count : n_static;
+  const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 32;
+  if (b0 >= n) return;  // block-uniform
+  const int t = threadIdx.x;
+  for (int idx = t; idx < K * 64; idx += 256) {
+    const int i = idx >> 6, a = idx & 63;
+    ws[i][a] = a0 + a < A ? wpd[(size_t)i * A + a0 + a] : 0.f;
+  }
+  for (int idx = t; idx < 32 * HW; idx += 256) {
+    const int b = idx / HW, p = idx - b * HW;
+    const float4 f = b0 + b < n ? feat[(size_t)(b0 + b) * HW + p] : make_float4(0.f, 0.f, 0.f, 0.f);
+    ps[b][2 * p] = f.x;
+    ps[b][2 * p + 1] = f.y;
+  }
+  __syncthreads();
+  const int a = t & 63, bg = (t >> 6) * 8;
+  if (a0 + a >= A) return;
+  const float bias = bpd[a0 + a];
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = bias;
+  for (int i = 0; i < 2 * HW; ++i) {
+    const float w = ws[i][a];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = fmaf(ps[bg + j][i], w, acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (b0 + bg + j < n) logits[(size_t)(b0 + bg + j) * A + a0 + a] = acc[j];
+}
+
+// softmax over the logits in place + the value head (Dense(hidden) ReLU ->
+// Dense(1) tanh), one wave per board, heads_kernel's arithmetic; the value
+// layer's weights [HW][hidden] are staged in LDS once per workgroup.
+__global__ __launch_bounds__(256) void heads_tail_kernel(const float4* __restrict__ feat, HeadWeights hw,
+                                                         const int* __restrict__ count, int n_static, int HW,
+                                                         int A, int hidden, float* __restrict__ probs,
+                                                         float* __restrict__ values) {
+  __shared__ float vflat[4][kMaxCells];
+  extern __shared__ float wv1[];
+  const int n = count ? *count : n_static;
+  if ((int)blockIdx.x * 4 >= n) return;  // block-uniform
+  for (int i = threadIdx.x; i < HW * hidden; i += 256) wv1[i] = hw.wv1[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int b = blockIdx.x * 4 + wave; b < n; b += gridDim.x * 4) {  // wave-uniform
+    for (int p = lane; p < HW; p += 64) vflat[wave][p] = feat[(size_t)b * HW + p].z;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    float* row = probs + (size_t)b * A;
+    float m = -INFINITY;
+    for (int a = lane; a < A; a += 64) m = fmaxf(m, row[a]);
+    m = wave_max(m);
+    float z = 0.f;
+    for (int a = lane; a < A; a += 64) z += expf(row[a] - m);
+    z = wave_sum(z);
+    for (int a = lane; a < A; a += 64) row[a] = expf(row[a] - m) / z;
+    float part = 0.f;
+    for (int j = lane; j < hidden; j += 64) {
+      float s = hw.bv1[j];
+      for (int p = 0; p < HW; ++p) s += vflat[wave][p] * wv1[p * hidden + j];
+      part += fmaxf(s, 0.f) * hw.wv2[j];
+    }
+    part = wave_sum(part);
+    if (lane == 0) values[b] = tanhf(part + hw.bv2[0]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // --------------------------------------------------------------- launchers
 void launch_encode(const Board* boards, const int* count, int n_max, int HW, float* x,
                    hipStream_t s) {
@@ -574,11 +660,14 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
 #define AZ_HEADS(FEAT_, STAGE_)                                                                      \
   heads_kernel<F, FEAT_, STAGE_, kMaxActions><<<hblocks, 256, STAGE_ ? wbytes : 0, s>>>(           \
       cur, hw, count, n_max, HW, A, net.hidden, probs, values)
-  if (A > kMaxActions) {  // chess: 1880 logits per board in LDS, weights through L1/L2
-    if (fused_heads)
-      heads_kernel<F, true, false, 2048><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A,
-                                                                         net.hidden, probs, values);
-    else
+  if (A > kMaxActions) {  // chess: 1880 actions
+    if (fused_heads && HW == 64) {
+      const float4* feat = reinterpret_cast<const float4*>(cur);
+      policy_dense_kernel<128><<<dim3((A + 63) / 64, (n_max + 31) / 32), 256, 0, s>>>(
+          feat, net.pd_w, net.pd_b, count, n_max, HW, A, probs);
+      heads_tail_kernel<<<std::min((n_max + 3) / 4, 256), 256, (size_t)HW * net.hidden * sizeof(float), s>>>(
+          feat, hw, count, n_max, HW, A, net.hidden, probs, values);
+    } else
       heads_kernel<F, false, false, 2048><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A,
                                                                           net.hidden, probs, values);
   } else if (fused_heads) {

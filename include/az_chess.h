@@ -111,7 +111,9 @@ typedef struct az_chess_config {
     int64_t arena_edges;          /* edges per arena half per slot (0 = 96 * mcts_iterations) */
     int32_t conv_algo;            /* AZ_CONV_WINOGRAD / AZ_CONV_DIRECT (tower; the padded
                                      118-plane stem is always Winograd) */
-    int32_t reserved[7];
+    int32_t lanes;                /* slot groups searched on separate HIP streams (0 = auto = 1);
+                                     results do not depend on it */
+    int32_t reserved[6];
 } az_chess_config;
 
 /* Termination of a finished self-play game: AZ_CHESS_* above, or this */

@@ -308,10 +308,14 @@ class TorchCPUNet:
         self.v2 = (t("value.dense2.kernel"), t("value.dense2.bias"))
 
     def __call__(self, board):
+        return self.forward_state(board.state())
+
+    def forward_state(self, state):
+        """One [H, W, C] state (batch 1) -> (probs [A], value)."""
         torch = self.torch
         F = torch.nn.functional
         with torch.no_grad():
-            x = torch.from_numpy(board.state()).permute(2, 0, 1)[None]
+            x = torch.from_numpy(np.ascontiguousarray(state, np.float32)).permute(2, 0, 1)[None]
             h = F.relu(F.conv2d(x, *self.stem, padding=1))
             for c1, c2, r in self.blocks:
                 a = F.relu(F.conv2d(h, *c1, padding=1))
@@ -340,3 +344,40 @@ def baseline_worker(args):
         games += 1
         expansions += r["expansions"]
     return games, expansions, time.perf_counter() - t0
+
+
+class _Budget(Exception):
+    pass
+
+
+def chess_baseline_worker(args):
+    """CPU baseline for chess (BASELINE configs[4]): the oracle's chess MCTS
+    (C tree, python-chess order, reference arithmetic) with the torch-CPU
+    network called at batch 1 on Board.full_state, one thread per worker.
+    The reference itself cannot run chess under MCTS and
+    its python-chess object tree would be slower than this C tree, so this is
+    a generous stand-in.  A game at 800 sims/move outlasts the budget, so the
+    worker reports expansions (network calls) and plies completed.
+    Returns (expansions, plies, seconds)."""
+    (sims, weights, depth, budget_s, seed) = args
+    import torch
+
+    import chess_oracle as C
+    torch.set_num_threads(1)
+    net = TorchCPUNet(weights, depth)
+    t0 = time.perf_counter()
+    calls = [0]
+
+    def cb(pos, initial):
+        if time.perf_counter() - t0 > budget_s:
+            raise _Budget()
+        calls[0] += 1
+        x = C.full_state(*C.reference_history(pos, bool(initial)), pos)
+        return net.forward_state(x)
+
+    try:
+        C.play_game(sims, seed, 512, callback=cb)
+    except _Budget:
+        pass
+    el = time.perf_counter() - t0
+    return calls[0], calls[0] / max(sims, 1), el

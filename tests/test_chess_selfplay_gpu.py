@@ -34,16 +34,17 @@ def _compare(r, g, ref, tag):
                               ref["policy_probs"][t, :n].view(np.uint64)), (tag, g, t)
 
 
-@pytest.mark.parametrize("sims,plies,slots,games,greedy", [
-    (24, 40, 3, 5, 8),      # slot refill, the reference's greedy threshold (never reached)
-    (16, 30, 4, 4, 1),      # greedy from the first move (one-hot policy, one draw consumed)
-    (8, 400, 4, 6, 8),      # long games: checkmate / stalemate / 75-move / cap terminations
-    (2, 60, 2, 2, 8),       # S=2: the root expansion plus one visit
+@pytest.mark.parametrize("sims,plies,slots,games,greedy,lanes", [
+    (24, 40, 3, 5, 8, 1),      # slot refill, the reference's greedy threshold (never reached)
+    (24, 40, 3, 5, 8, 3),      # same games on three streams: results do not depend on lanes
+    (16, 30, 4, 4, 1, 2),      # greedy from the first move (one-hot policy, one draw consumed)
+    (8, 400, 4, 6, 8, 2),      # long games: checkmate / stalemate / 75-move / cap terminations
+    (2, 60, 2, 2, 8, 1),       # S=2: the root expansion plus one visit
 ])
-def test_chess_selfplay_synthetic_matches_oracle(sims, plies, slots, games, greedy):
+def test_chess_selfplay_synthetic_matches_oracle(sims, plies, slots, games, greedy, lanes):
     from custom_alphazero import engine as az
     eng = _engine(mcts_iterations=sims, slots=slots, evaluator=az.EVAL_SYNTHETIC, max_plies=plies,
-                  index_move_greedy=greedy)
+                  index_move_greedy=greedy, lanes=lanes)
     st = eng.selfplay_run(0, games, 1000)
     r = eng.selfplay_results()
     assert st["errors"] == 0 and st["games_done"] == games
@@ -73,7 +74,7 @@ def chess_net():
             w[k] = rng.normal(0, 0.1, w[k].shape).astype(np.float32)
         elif k.endswith(".var"):
             w[k] = rng.uniform(0.5, 1.5, w[k].shape).astype(np.float32)
-    eng = _engine(mcts_iterations=16, slots=64, evaluator=az.EVAL_NETWORK, max_plies=12)
+    eng = _engine(mcts_iterations=16, slots=64, evaluator=az.EVAL_NETWORK, max_plies=12, lanes=2)
     eng.set_weights(w.items())
     yield eng, w
     eng.close()
