@@ -71,14 +71,21 @@ class PolicyValueModel:
     # ------------------------------------------------------------ forward
     def _eng(self):
         if self._engine is None:
-            H, W, _ = self.input_dim
-            c = ConfigConnectN
-            self._engine = az.Engine(H, W, min(c.n, H, W), c.gravity, 1,
-                                     slots=ConfigModel.forward_batch, evaluator=az.EVAL_NETWORK,
-                                     filters=ConfigModel.filters, depth=self.depth,
-                                     value_hidden=ConfigModel.value_hidden,
-                                     bn_epsilon=ConfigModel.bn_epsilon,
-                                     device=self.device.index or 0)
+            H, W, C = self.input_dim
+            if C == 118:  # chess planes (chess/board.py:55-73): the chess engine's forward
+                self._engine = az.ChessEngine(1, slots=ConfigModel.forward_batch,
+                                              evaluator=az.EVAL_NETWORK, filters=ConfigModel.filters,
+                                              depth=self.depth, value_hidden=ConfigModel.value_hidden,
+                                              bn_epsilon=ConfigModel.bn_epsilon,
+                                              device=self.device.index or 0)
+            else:
+                c = ConfigConnectN
+                self._engine = az.Engine(H, W, min(c.n, H, W), c.gravity, 1,
+                                         slots=ConfigModel.forward_batch, evaluator=az.EVAL_NETWORK,
+                                         filters=ConfigModel.filters, depth=self.depth,
+                                         value_hidden=ConfigModel.value_hidden,
+                                         bn_epsilon=ConfigModel.bn_epsilon,
+                                         device=self.device.index or 0)
         if self._engine_version != self._version:
             self._engine.set_weights(self.engine_weights())
             self._engine_version = self._version

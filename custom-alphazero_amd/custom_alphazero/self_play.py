@@ -42,6 +42,11 @@ def play_game(process_id: int, all_possible_moves: List[Move], mcts_iterations: 
     np.random.seed(int((process_id + 1) * time.time()) % (2 ** 32 - 1))
     if model is None:
         model = best_saved_model(run_id)
+    if ConfigGeneral.game == "chess":
+        # one game on the chess engine, seeded like the reference's process seed
+        seed = int(np.random.randint(0, 2 ** 31 - 1))
+        states, policies, rewards, records = play_chess(model, 1, seed, 0, mcts_iterations)
+        return states, policies, rewards, records[0]
     mcts = MCTS(board=Board(), all_possible_moves=all_possible_moves,
                 concurrency=ConfigGeneral.concurrency, plays_inferences=plays_inferences,
                 model=model, use_solver=ConfigMCTS.use_solver)
@@ -108,12 +113,74 @@ def _batched_engine(model, n_slots):
     return eng
 
 
+_CHESS_ENGINES = {}
+
+
+def _chess_engine(model, n_slots, sims):
+    synthetic = isinstance(model, SyntheticEvaluator)
+    key = (sims, n_slots, synthetic, ConfigMCTS.index_move_greedy, ConfigMCTS.exploration_constant,
+           ConfigModel.depth, ConfigSelfPlay.chess_max_plies)
+    eng = _CHESS_ENGINES.get(key)
+    if eng is None:
+        eng = az.ChessEngine(sims, slots=n_slots,
+                             evaluator=az.EVAL_SYNTHETIC if synthetic else az.EVAL_NETWORK,
+                             max_plies=ConfigSelfPlay.chess_max_plies,
+                             index_move_greedy=ConfigMCTS.index_move_greedy,
+                             exploration_constant=ConfigMCTS.exploration_constant,
+                             filters=ConfigModel.filters, depth=ConfigModel.depth,
+                             value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon)
+        eng.weights_key = None
+        _CHESS_ENGINES.clear()
+        _CHESS_ENGINES[key] = eng
+    if not synthetic:
+        wkey = model.hash if hasattr(model, "hash") else (id(model), getattr(model, "_version", None))
+        if eng.weights_key != wkey:
+            eng.set_weights(model.engine_weights())
+            eng.weights_key = wkey
+    return eng
+
+
+def play_chess(model, n_games: int, base_seed: int, first_game: int = 0, sims: Optional[int] = None):
+    """Batched chess self-play (BASELINE configs[4]).  Returns (states
+    [M,8,8,118] f32 -- Board.full_state of each MCTS.play parent board, exact
+    in f32 --, policies [M,1880] f64, rewards [M], records), in game order."""
+    from custom_alphazero.chess import kernels as K
+    from custom_alphazero.chess.board import Board as ChessBoard
+    sims = int(sims or ConfigSelfPlay.mcts_iterations)
+    eng = _chess_engine(model, min(n_games, ConfigSelfPlay.chess_concurrent_games), sims)
+    eng.selfplay_run(first_game, n_games, base_seed)
+    r = eng.selfplay_results()
+    start = ChessBoard()._pos  # host bookkeeping only: FEN -> az_chess_pos
+    states, policies, rewards, records = [], [], [], []
+    for g in range(n_games):
+        T = int(r["lengths"][g])
+        pos = r["positions"][g, :T]
+        # the reference's history deque: [0 x 7, state] on Board(), then
+        # [0 x 6, start state, state] (chess/board.py docstring)
+        hist = np.zeros((T, K.HISTORY), K.POS_DTYPE)
+        valid = np.zeros((T, K.HISTORY), np.uint8)
+        hist[:, 7], valid[:, 7] = pos, 1
+        hist[1:, 6], valid[1:, 6] = start, 1
+        states.append(K.encode(hist, valid) if T else np.zeros((0, 8, 8, K.PLANES), np.float32))
+        pol = np.zeros((T, K.ACTIONS), np.float64)
+        for t in range(T):
+            n = int(r["policy_n"][g, t])
+            pol[t, r["policy_actions"][g, t, :n]] = r["policy_probs"][g, t, :n]
+        policies.append(pol)
+        rewards.append(alternating_rewards(int(r["results"][g]), T))
+        records.append(GameRecord(first_game + g, (base_seed + first_game + g) % 2 ** 32, T,
+                                  int(r["results"][g]), int(r["expansions"][g]),
+                                  r["moves"][g, :T].astype(np.int32)))
+    return np.concatenate(states), np.vstack(policies), np.concatenate(rewards), records
+
+
 def play(run_id: str, plays_inferences: Optional[Dict[str, Tuple[np.ndarray, float]]] = None,
          model=None, n_games: Optional[int] = None, base_seed: Optional[int] = None,
          first_game: int = 0):
     """Batched self-play.  Returns (states [M,H,W,4] f32, policies [M,A] f64,
     rewards [M] int64, records) concatenated in game order like the reference
-    (self_play.py:112-118)."""
+    (self_play.py:112-118); with ConfigGeneral.game == "chess" the chess
+    engine's (play_chess)."""
     if model is None:
         model = best_saved_model(run_id)
     n_games = int(n_games or ConfigSelfPlay.games_per_call)
@@ -121,6 +188,8 @@ def play(run_id: str, plays_inferences: Optional[Dict[str, Tuple[np.ndarray, flo
         base_seed = ConfigSelfPlay.base_seed
     if base_seed is None:
         base_seed = int(time.time()) % (2 ** 32 - 1)
+    if ConfigGeneral.game == "chess":
+        return play_chess(model, n_games, base_seed, first_game)
     eng = _batched_engine(model, min(n_games, ConfigSelfPlay.concurrent_games))
     if ConfigSelfPlay.cache_log2 and (plays_inferences is None
                                       or plays_inferences is not _CACHE_OWNER["dict"]):

@@ -20,12 +20,23 @@ def reset_plays_inferences_dict() -> dict:
 
 
 def get_all_possible_moves():
+    if ConfigGeneral.game == "chess":  # utils.py:13-15
+        from custom_alphazero.chess.utils import get_all_possible_moves as chess_moves
+        return chess_moves()
     return Board.get_all_possible_moves()
+
+
+def input_dim():
+    """Board().full_state.shape of the configured game: (H, W, 4), or chess's
+    (8, 8, 118) (chess/board.py:55-73; static, no device call)."""
+    if ConfigGeneral.game == "chess":
+        return (8, 8, 118)
+    return Board().full_state.shape
 
 
 def init_model(path: Optional[str] = None, seed: Optional[int] = None):
     from custom_alphazero.model.policy_value import PolicyValueModel
-    model = PolicyValueModel(input_dim=Board().full_state.shape,
+    model = PolicyValueModel(input_dim=input_dim(),
                              action_space=len(get_all_possible_moves()), seed=seed)
     if path is not None:
         model.load_with_meta(path)

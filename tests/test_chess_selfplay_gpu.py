@@ -122,3 +122,40 @@ def test_chess_engine_errors():
     with pytest.raises(az.AzError, match="arena"):
         eng = _engine(mcts_iterations=64, slots=2, evaluator=az.EVAL_SYNTHETIC, arena_edges=300)
         eng.selfplay_run(0, 2, 0)
+
+
+def test_chess_play_api_matches_oracle():
+    """self_play.play with ConfigGeneral.game == "chess": states are the
+    reference's Board.full_state of each parent board, policies the dense
+    MCTS.play policy, rewards alternate from the final result."""
+    from custom_alphazero import self_play
+    from custom_alphazero.config import ConfigGeneral, ConfigSelfPlay
+    from custom_alphazero.mcts.mcts import SyntheticEvaluator
+    saved = (ConfigGeneral.game, ConfigSelfPlay.mcts_iterations, ConfigSelfPlay.chess_max_plies,
+             ConfigSelfPlay.chess_concurrent_games)
+    try:
+        ConfigGeneral.game = "chess"
+        ConfigSelfPlay.mcts_iterations, ConfigSelfPlay.chess_max_plies = 12, 24
+        ConfigSelfPlay.chess_concurrent_games = 2
+        states, policies, rewards, records = self_play.play("run", {}, model=SyntheticEvaluator(),
+                                                            n_games=3, base_seed=500)
+    finally:
+        (ConfigGeneral.game, ConfigSelfPlay.mcts_iterations, ConfigSelfPlay.chess_max_plies,
+         ConfigSelfPlay.chess_concurrent_games) = saved
+    off = 0
+    for g in range(3):
+        ref = C.play_game(12, 500 + g, 24)
+        T = ref["T"]
+        assert records[g].length == T and np.array_equal(records[g].moves, ref["moves"])
+        for t in range(T):
+            x = C.full_state(*C.reference_history(ref["positions"][t], t == 0), ref["positions"][t])
+            assert np.array_equal(states[off + t].astype(np.float64), x), (g, t)
+            dense = np.zeros(1880)
+            n = ref["policy_n"][t]
+            dense[ref["policy_actions"][t, :n]] = ref["policy_probs"][t, :n]
+            assert np.array_equal(policies[off + t], dense), (g, t)
+        exp = np.repeat(ref["result"], T)
+        exp[-2::-2] = -exp[-2::-2]
+        assert np.array_equal(rewards[off:off + T], exp)
+        off += T
+    assert off == len(states) == len(policies) == len(rewards)
