@@ -825,6 +825,13 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
   e->net.depth = c.depth;
   e->net.algo = c.conv_algo;
   e->net.hidden = c.value_hidden;
+  // 256 boards per launch leave one workgroup per CU: the two-chunk-group
+  // Winograd variant (az_wino.hip) for every chess forward; AZ_WINO_KSPLIT
+  // overrides it for A/B runs
+  {
+    const char* ks = getenv("AZ_WINO_KSPLIT");
+    e->net.wino_ksplit = ks ? atoi(ks) : 2;
+  }
   if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));
   // auto = 1: at 256 games a chess step is bound by its launch chain; extra
   // streams measured slower (375k expansions/s with 1 lane, 311k with 2,

@@ -14,6 +14,7 @@ namespace az {
 struct NetDev {
   int filters = 128, depth = 0, hidden = 256;
   int algo = 0;  // AZ_CONV_WINOGRAD / AZ_CONV_DIRECT
+  int wino_ksplit = 1;  // Winograd variant for every conv of this network (1, or 2 = chess)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c), in_ch == 4
   float* stem_u = nullptr;  // Winograd U of the zero-padded stem [3][3][F][F], in_ch > 4
@@ -104,9 +105,11 @@ struct HeadConv {
   const float* bvc;  // [1]
   float4* feat;      // null: write the block output instead
 };
+// ksplit = 2: the two-chunk-group variant (small batches; az_wino.hip)
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
-                      int n_max, int H, int W, hipStream_t s, const HeadConv* heads = nullptr);
+                      int n_max, int H, int W, hipStream_t s, const HeadConv* heads = nullptr,
+                      int ksplit = 1);
 // x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
 // boards (optional): one-hot input straight from the eval queue's boards
 // (bitwise the same outputs as encoding them into x first)

@@ -66,13 +66,21 @@ __device__ __forceinline__ int vswz(int j, int t) {
 // epilogue (feat, az_nn.h HeadConv) and never writes the block output.
 // (HIP's second launch-bounds argument is the minimum waves per SIMD: two,
 // i.e. two workgroups per CU, which the V buffer's LDS also allows.)
-template <bool RESIDUAL, int CK, bool HEADS>
-__global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
+// KSPLIT = 2 (small batches, the chess engine): two groups of 4 waves share
+// the workgroup's 32 tiles, group g takes input-channel chunks g, g+2 (each
+// group its own V buffer), and group 1's accumulators are added into group
+// 0's through LDS before the epilogue.  Each wave issues half the MFMAs, and
+// with one workgroup per CU the 8 waves overlap one group's transform with
+// the other's MFMAs.  The reduction order differs from KSPLIT = 1 (same
+// layer, within NET_TOL), so an engine uses one variant for every forward.
+template <bool RESIDUAL, int CK, bool HEADS, int KSPLIT>
+__global__ __launch_bounds__(kWinoThreads * KSPLIT, KSPLIT == 1 ? 2 : 1) void wino_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
     int n_static, int H, int W, HeadConv hc) {
   static_assert(CK == 16 || CK == 32, "chunk of 16 or 32 input channels");
+  static_assert(KSPLIT == 1 || KSPLIT == 2, "one or two chunk groups");
   constexpr int NX = RESIDUAL ? 20 : 16;   // 16 Winograd points (+4 residual pixel rows)
   constexpr int RC = CK / 4;               // float4 per V row
   constexpr int VB = NX * kWinoTiles * RC; // float4 in the V buffer
@@ -80,14 +88,17 @@ __global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
   constexpr int KS = CK / 2;               // MFMA k-steps per stage
   constexpr int QB = CK / 8;               // float4 of B (and of A) per lane per stage
   constexpr int IPT = 16 * CK / kWinoThreads;  // producer items per thread (tile, c4, half)
-  __shared__ float4 vbuf[VB];
+  __shared__ float4 vbuf_all[VB * KSPLIT];
 
   const int HW = H * W, TW = (W + 1) >> 1, TH = (H + 1) >> 1, TB = TH * TW;
   const int n_boards = count ? *count : n_static;
   const int tiles = n_boards * TB;
   const int t0 = blockIdx.x * kWinoTiles;
   if (t0 >= tiles) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // kg = chunk group; tid/wave below are within the group
+  const int kg = KSPLIT == 1 ? 0 : (int)(threadIdx.x >> 8);
+  const int tid = threadIdx.x & (kWinoThreads - 1), lane = tid & 63, wave = tid >> 6;
+  float4* vbuf = vbuf_all + kg * VB;
 
   // ---- producer geometry: item -> (tile pt, 4-channel group pc, half ph)
   int pt[IPT], pc[IPT], ph[IPT], pbase[IPT], pty[IPT], ptx[IPT];
@@ -249,15 +260,17 @@ __global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
   f32x16 M[2];
 
   Patch P;
-  produce_load(0, P);
+  produce_load(kg, P);
   produce_store(P);
-  load_b(0, 0, bq[0]);
+  load_b(kg, 0, bq[0]);
   __syncthreads();
 
   // the chunk loop stays rolled: one copy of the 16-20 unrolled stages is
   // already ~10 KB of code
 #pragma unroll 1
-  for (int c = 0; c < NCH; ++c) {
+  for (int ci = 0; ci < NCH / KSPLIT; ++ci) {
+    const int c = ci * KSPLIT + kg;
+    const bool more = ci + 1 < NCH / KSPLIT;
     load_a(0, aq[0]);
 #pragma unroll
     for (int xi = 0; xi < NX; ++xi) {
@@ -268,8 +281,8 @@ __global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
       if (xi + 1 < NX) {
         load_b(c, xi + 1, bq[(xi + 1) & 1]);
         load_a(xi + 1, aq[(xi + 1) & 1]);
-      } else if (c + 1 < NCH) {
-        load_b(c + 1, 0, bq[(xi + 1) & 1]);
+      } else if (more) {
+        load_b(c + KSPLIT, 0, bq[(xi + 1) & 1]);
       }
       float av[KS], bv[KS];
 #pragma unroll
@@ -298,14 +311,34 @@ __global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
     }
     __builtin_amdgcn_sched_barrier(0);
     if (NX == 16) scatter(15, M[1]);
-    if (c + 1 < NCH) {
+    if (more) {
       __syncthreads();  // every wave is done with chunk c's V
       if (AZ_WINO_DIAG != 2 && AZ_WINO_DIAG != 4) {
-        produce_load(c + 1, P);
+        produce_load(c + KSPLIT, P);
         produce_store(P);
       }
       __syncthreads();
     }
+  }
+  if constexpr (KSPLIT == 2) {
+    // group 1's accumulators into group 0's: [p*16 + i][wave*64 + lane]
+    // (consecutive lanes, consecutive words: conflict-free)
+    float* red = reinterpret_cast<float*>(vbuf_all);
+    __syncthreads();  // both groups are done with their V buffers
+    if (kg == 1) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(p * 16 + i) * kWinoThreads + tid] = Y[p][i];
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) Y[p][i] += red[(p * 16 + i) * kWinoThreads + tid];
+    }
+    __syncthreads();  // `red` (the V buffers) is free again for the epilogue
   }
 
   // ---- epilogue: bias (+ residual bias, folded on the host), ReLU, store
@@ -328,10 +361,11 @@ __global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
       for (int i = 8 * half; i < 8 * half + 8; ++i) {
         const int row = (i & 3) + 8 * (i >> 2) + 4 * h - 16 * half;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
+        for (int p = 0; p < 4; ++p)
+          if (kg == 0) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][i] + bcol, 0.0f);
       }
       __syncthreads();
-      if (tid < 64) {
+      if (kg == 0 && tid < 64) {
         const int tau = t0 + 16 * half + (tid >> 2), p = tid & 3;
         if (tau < tiles) {
           const int b = tau / TB, lt = tau - b * TB;
@@ -353,6 +387,7 @@ __global__ __launch_bounds__(kWinoThreads, 2) void wino_conv_kernel(
     }
     return;
   }
+  if (kg != 0) return;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int tau = t0 + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -379,7 +414,7 @@ size_t wino_pack_index(int xi, int cin, int cout) {
 
 void launch_wino_conv(const float* in, const float* res_in, const float* upack,
                       const float* rpack, const float* bias, float* out, const int* count,
-                      int n_max, int H, int W, hipStream_t s, const HeadConv* heads) {
+                      int n_max, int H, int W, hipStream_t s, const HeadConv* heads, int ksplit) {
   const int TB = ((H + 1) / 2) * ((W + 1) / 2);
   const int grid = (n_max * TB + kWinoTiles - 1) / kWinoTiles;
   if (grid <= 0) return;
@@ -387,17 +422,24 @@ void launch_wino_conv(const float* in, const float* res_in, const float* upack,
   const float4* rp = reinterpret_cast<const float4*>(rpack);
   constexpr int CK = kWinoCK;
   HeadConv hc{};
-  if (heads && heads->feat) {
-    hc = *heads;
-    wino_conv_kernel<true, CK, true><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count,
-                                                                  n_max, H, W, hc);
-  } else if (res_in) {
-    wino_conv_kernel<true, CK, false><<<grid, kWinoThreads, 0, s>>>(in, res_in, u, rp, bias, out, count,
-                                                                   n_max, H, W, hc);
+  const bool fuse = heads && heads->feat;
+  if (fuse) hc = *heads;
+#define AZ_WINO_LAUNCH(KS_)                                                                          \
+  if (fuse)                                                                                         \
+    wino_conv_kernel<true, CK, true, KS_><<<grid, kWinoThreads * KS_, 0, s>>>(in, res_in, u, rp, bias, \
+                                                                          out, count, n_max, H, W, hc); \
+  else if (res_in)                                                                                  \
+    wino_conv_kernel<true, CK, false, KS_><<<grid, kWinoThreads * KS_, 0, s>>>(                      \
+        in, res_in, u, rp, bias, out, count, n_max, H, W, hc);                                      \
+  else                                                                                              \
+    wino_conv_kernel<false, CK, false, KS_><<<grid, kWinoThreads * KS_, 0, s>>>(                     \
+        in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc);
+  if (ksplit == 2) {
+    AZ_WINO_LAUNCH(2)
   } else {
-    wino_conv_kernel<false, CK, false><<<grid, kWinoThreads, 0, s>>>(in, nullptr, u, nullptr, bias, out,
-                                                                    count, n_max, H, W, hc);
+    AZ_WINO_LAUNCH(1)
   }
+#undef AZ_WINO_LAUNCH
 }
 
 }  // namespace az
