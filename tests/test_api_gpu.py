@@ -168,3 +168,22 @@ def test_self_play_run_loop(tmp_path, golden, game_cfg, monkeypatch):
     saved = np.load(tmp_path / "connect_n" / "run-x" / ConfigPath.self_play_dir / "iteration_1" /
                     ConfigPath.samples_file)
     np.testing.assert_array_equal(saved["values"], z["reward"][keep])
+
+
+def test_mcts_visualizer_over_device_tree(game_cfg, golden, tmp_path):
+    """visualize_mcts.MctsVisualizer (reference visualize_mcts.py) walks the
+    device tree views: every visited edge becomes one DOT edge, the played
+    edge is red, visit proportions sum to 1 per expanded node."""
+    from custom_alphazero.visualize_mcts import MctsVisualizer
+    game_cfg(golden("mcts_c4_s25"))
+    m = MCTS(Board(), Board.get_all_possible_moves(), False, {}, model=SyntheticEvaluator())
+    m.search(25)
+    m.play(greedy=True)
+    vis = MctsVisualizer(m.root, mcts_name="c4")
+    visited = [e for e in vis.edges if e.visit_count > 0]
+    assert len(visited) > 1 and sum(e.visit_count for e in m.root.edges) == 24
+    dot = vis.graph_mcts.source
+    assert dot.count(" -> ") == len(visited) and 'color="red"' in dot and "penwidth=\"4\"" in dot
+    assert abs(sum(e.proportion_n for e in m.root.edges) - 1.0) < 1e-12
+    path = vis.graph_mcts.save(directory=str(tmp_path))
+    assert open(path).read() == dot
