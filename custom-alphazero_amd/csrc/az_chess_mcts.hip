@@ -831,6 +831,8 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
   {
     const char* ks = getenv("AZ_WINO_KSPLIT");
     e->net.wino_ksplit = ks ? atoi(ks) : 2;
+    const char* wt = getenv("AZ_WINO_TILES");
+    e->net.wino_tiles = wt ? atoi(wt) : 16;
   }
   if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));
   // auto = 1: at 256 games a chess step is bound by its launch chain; extra

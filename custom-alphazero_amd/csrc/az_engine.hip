@@ -244,7 +244,7 @@ int ready_to_search(az_engine* e) {
 // U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
 // in float64 from the folded Keras kernel, rounded once to float, in the
 // kernel's fragment order.
-[[maybe_unused]] std::vector<float> pack_wino(const std::vector<double>& w, int F) {
+[[maybe_unused]] std::vector<float> pack_wino(const std::vector<double>& w, int F, int tiles) {
   static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   std::vector<float> p((size_t)16 * F * F);
   std::vector<double> U((size_t)F * F);
@@ -259,20 +259,22 @@ int ready_to_search(az_engine* e) {
         for (size_t i = 0; i < (size_t)F * F; ++i) U[i] += gg * src[i];
       }
     for (int cin = 0; cin < F; ++cin)
-      for (int co = 0; co < F; ++co) p[az::wino_pack_index(xi, cin, co)] = (float)U[(size_t)cin * F + co];
+      for (int co = 0; co < F; ++co)
+        p[tiles == 16 ? az::wino16_pack_index(xi, cin, co) : az::wino_pack_index(xi, cin, co)] =
+            (float)U[(size_t)cin * F + co];
   }
   return p;
 }
 
 // 1x1 projection residual [cin][cout] in the same fragment order, as if it
 // were point 0 of a 16-point-per-chunk stream compacted to one point.
-[[maybe_unused]] std::vector<float> pack_wino_res(const std::vector<double>& wr, int F) {
+[[maybe_unused]] std::vector<float> pack_wino_res(const std::vector<double>& wr, int F, int tiles) {
   std::vector<float> p((size_t)F * F);
   const int CK = az::kWinoCK;
   for (int cin = 0; cin < F; ++cin)
     for (int co = 0; co < F; ++co) {
       // index within the chunk's 16-point block, then compact chunks to 1 point
-      const size_t i16 = az::wino_pack_index(0, cin, co);
+      const size_t i16 = tiles == 16 ? az::wino16_pack_index(0, cin, co) : az::wino_pack_index(0, cin, co);
       const size_t per_point = (size_t)4 * (CK / 8) * 64 * 4;  // floats per point per chunk
       const size_t c = (size_t)cin / CK;
       p[i16 - c * 16 * per_point + c * per_point] = (float)wr[(size_t)cin * F + co];
@@ -377,7 +379,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
         for (int c = 0; c < in_ch; ++c)
           for (int o = 0; o < F; ++o)
             wp[((size_t)tap * F + c) * F + o] = w[((size_t)tap * in_ch + c) * F + o];
-      if ((rc = upload(owned, &net.stem_u, pack_wino(wp, F)))) return rc;
+      if ((rc = upload(owned, &net.stem_u, pack_wino(wp, F, net.wino_tiles)))) return rc;
     }
     net.in_ch = in_ch;
   }
@@ -396,7 +398,8 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
     for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
     if ((rc = upload(owned, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
-        (rc = upload(owned, &net.u1_w[d], pack_wino(w, F))) || (rc = upload(owned, &net.c1_b[d], bt)))
+        (rc = upload(owned, &net.u1_w[d], pack_wino(w, F, net.wino_tiles))) ||
+        (rc = upload(owned, &net.c1_b[d], bt)))
       return rc;
     if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
     if ((rc = fold_unit(m, p + ".res", 1, F, F, eps, wr, br))) return rc;
@@ -407,8 +410,9 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     }
     for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
     if ((rc = upload(owned, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
-        (rc = upload(owned, &net.u2_w[d], pack_wino(w, F))) ||
-        (rc = upload(owned, &net.r2_w[d], pack_wino_res(wr, F))) || (rc = upload(owned, &net.c2_b[d], bt2)))
+        (rc = upload(owned, &net.u2_w[d], pack_wino(w, F, net.wino_tiles))) ||
+        (rc = upload(owned, &net.r2_w[d], pack_wino_res(wr, F, net.wino_tiles))) ||
+        (rc = upload(owned, &net.c2_b[d], bt2)))
       return rc;
   }
   // heads
@@ -569,6 +573,10 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   }
   e->net.depth = c.depth;
   e->net.algo = c.conv_algo;
+  {  // Winograd variant (az_wino.hip 32 tiles / az_wino16.hip 16 tiles); AZ_WINO_TILES for A/B runs
+    const char* wt = getenv("AZ_WINO_TILES");
+    e->net.wino_tiles = wt ? atoi(wt) : 16;
+  }
   // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
   int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);
   nl = std::min(nl, std::min(g.slots, 8));

@@ -591,8 +591,11 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   constexpr int F = 128;
   if (net.stem_u) {
     // chess: 118 input planes zero-padded to F, the stem is one more Winograd conv
-    launch_wino_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
-                     net.wino_ksplit);
+    if (net.wino_tiles == 16)
+      launch_wino16_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s);
+    else
+      launch_wino_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
+                       net.wino_ksplit);
   } else {
     const int total = n_max * HW * (F / 4);
     if (boards)
@@ -632,13 +635,19 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
     switch (variant) {
       case 0:  // Winograd F(2x2,3x3) (az_wino.hip)
       {
-        launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s, nullptr,
-                         net.wino_ksplit);
+        if (net.wino_tiles == 16)
+          launch_wino16_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s);
+        else
+          launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s,
+                           nullptr, net.wino_ksplit);
         // last block: the head 1x1 convs run in conv2's epilogue, features into nxt
         HeadConv hc{net.pc_w, net.pc_b, net.vc_w, net.vc_b,
                     d == net.depth - 1 && AZ_FUSE_HEADS ? reinterpret_cast<float4*>(nxt) : nullptr};
-        launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc,
-                         net.wino_ksplit);
+        if (net.wino_tiles == 16)
+          launch_wino16_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc);
+        else
+          launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc,
+                           net.wino_ksplit);
         fused_heads = hc.feat != nullptr;
         break;
       }

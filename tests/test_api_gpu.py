@@ -184,6 +184,6 @@ def test_mcts_visualizer_over_device_tree(game_cfg, golden, tmp_path):
     assert len(visited) > 1 and sum(e.visit_count for e in m.root.edges) == 24
     dot = vis.graph_mcts.source
     assert dot.count(" -> ") == len(visited) and 'color="red"' in dot and "penwidth=\"4\"" in dot
-    assert abs(sum(e.proportion_n for e in m.root.edges) - 1.0) < 1e-12
+    assert abs(sum(e.proportion_n for e in vis.mcts_root_node.edges) - 1.0) < 1e-12
     path = vis.graph_mcts.save(directory=str(tmp_path))
     assert open(path).read() == dot
