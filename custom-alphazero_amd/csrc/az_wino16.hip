@@ -30,6 +30,11 @@ constexpr int kW16Threads = 256;
 #ifndef AZ_W16_OCC
 #define AZ_W16_OCC 2
 #endif
+// stages of B (weight fragments) in flight ahead of the MFMAs that use them:
+// 2 measured best (chess 484k -> 585k expansions/s, C4 +2%; 3 = 2)
+#ifndef AZ_W16_PF
+#define AZ_W16_PF 2
+#endif
 
 __host__ __device__ constexpr int w16_sign(int a, int i) {
   return i == 0 ? (a == 3 ? 0 : 1) : (a == 0 ? 0 : (a == 1 ? 1 : -1));
@@ -187,12 +192,19 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
       }
     }
   };
-  float4 bq[2][QB], aq[2][2];
+  constexpr int PF = AZ_W16_PF;
+  constexpr int NB = PF == 1 ? 2 : 4;  // B register buffers (>= PF + 1, divides NX)
+  float4 bq[NB][QB], aq[2][2];
   f32x4 M[2][2];
+  // stage k of the flat (chunk, point) sequence -> its B fragments
+  auto load_b_flat = [&](int k, float4 (&dst)[QB]) {
+    if (k < NCH * NX) load_b(k / NX, k % NX, dst);
+  };
 
   produce_load(0);
   produce_store();
-  load_b(0, 0, bq[0]);
+#pragma unroll
+  for (int k = 0; k < PF; ++k) load_b_flat(k, bq[k]);
   __syncthreads();
 
 #pragma unroll 1
@@ -201,12 +213,10 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
 #pragma unroll
     for (int xi = 0; xi < NX; ++xi) {
       __builtin_amdgcn_sched_barrier(0);
-      if (xi + 1 < NX) {
-        load_b(c, xi + 1, bq[(xi + 1) & 1]);
-        load_a(xi + 1, aq[(xi + 1) & 1]);
-      } else if (c + 1 < NCH) {
-        load_b(c + 1, 0, bq[(xi + 1) & 1]);
-      }
+      // flat stage c*NX + xi uses buffer (c*NX + xi) % NB; NX % NB == 0 keeps it static
+      static_assert(NX % NB == 0, "buffer of a stage must not depend on the chunk");
+      load_b_flat(c * NX + xi + PF, bq[(xi + PF) % NB]);
+      if (xi + 1 < NX) load_a(xi + 1, aq[(xi + 1) & 1]);
       float av[KS], bv[2][KS];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -215,7 +225,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
       }
 #pragma unroll
       for (int q = 0; q < QB; ++q) {  // q = 2 nb + s / 4
-        const float4 b4 = bq[xi & 1][q];
+        const float4 b4 = bq[xi % NB][q];
         const int nb = q >> 1, s0 = (q & 1) * 4;
         bv[nb][s0] = b4.x, bv[nb][s0 + 1] = b4.y, bv[nb][s0 + 2] = b4.z, bv[nb][s0 + 3] = b4.w;
       }
