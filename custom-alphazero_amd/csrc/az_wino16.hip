@@ -46,6 +46,13 @@ __device__ __forceinline__ int w16_swz(int j, int t) {
   return j ^ ((t / RPB) & (RC - 1));
 }
 
+// V row (tile) that MFMA row m holds.  ds_read_b128 serves a wave in lane
+// groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): each group mixes k
+// quarters 0 and 1 (or 2 and 3) over complementary row sets, so rows 0-3 and
+// 12-15 go to tiles 0-7 and rows 4-11 to tiles 8-15 -- with the XOR swizzle
+// every group then reads 16 distinct bank slots (identity: 2-way conflicts).
+__device__ __forceinline__ int w16_tile(int m) { return m < 4 ? m : (m < 12 ? m + 4 : m - 8); }
+
 template <bool RESIDUAL, bool HEADS>
 __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
@@ -70,8 +77,9 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
   if (t0 >= tiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // ---- producer geometry: thread -> (tile pt, 4-channel group pc, half ph)
-  const int ph = tid & 1, pc = (tid >> 1) & (RC - 1), pt = tid / (2 * RC);
+  // ---- producer geometry: thread -> (4-channel group pc, half ph, tile pt);
+  // the 8 lanes of a ds_write_b128 group store 8 distinct 16-B slots of a row
+  const int pc = tid & (RC - 1), ph = (tid / RC) & 1, pt = tid / (2 * RC);
   const int tau_p = t0 + pt;
   const bool pvalid = tau_p < tiles;
   int pbase = pc * 4, pty = 0, ptx = 0;
@@ -169,10 +177,11 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
 #pragma unroll
     for (int q = 0; q < QB; ++q) dst[q] = base[o + q * 64];
   };
+  const int rt = w16_tile(r);  // this lane's A row (tile)
   auto load_a = [&](int xi, float4 (&dst)[2]) {
-    const float4* vrow = vbuf + (xi * kW16Tiles + r) * RC;
+    const float4* vrow = vbuf + (xi * kW16Tiles + rt) * RC;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) dst[q] = vrow[w16_swz<CK>(2 * g + q, r)];
+    for (int q = 0; q < 2; ++q) dst[q] = vrow[w16_swz<CK>(2 * g + q, rt)];
   };
   auto scatter = [&](int xi, const f32x4 (&m)[2]) {
     const int a = xi >> 2, bb = xi & 3;
@@ -263,7 +272,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     }
   }
 
-  // ---- epilogue: D row (tile) = 4g + v, column = 32 wave + 16 nb + (lane & 15)
+  // ---- epilogue: D row m = 4g + v (tile w16_tile(m)), column = 32 wave + 16 nb + (lane & 15)
   if constexpr (HEADS) {
     static_assert(RESIDUAL, "heads fuse into the block's second conv");
     static_assert(64 * 129 * 4 <= VB * 16, "the transpose fits the V buffer");
@@ -275,7 +284,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
       const float bcol = bias[col];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int row = 4 * g + v;
+        const int row = w16_tile(4 * g + v);
 #pragma unroll
         for (int p = 0; p < 4; ++p) tb[(row * 4 + p) * 129 + col] = fmaxf(Y[p][nb][v] + bcol, 0.0f);
       }
@@ -308,7 +317,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     const float bcol = bias[col];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int tau = t0 + 4 * g + v;
+      const int tau = t0 + w16_tile(4 * g + v);
       if (tau >= tiles) continue;
       const int b = tau / TB, lt = tau - b * TB;
       const int ty = lt / TW, tx = lt - ty * TW;
