@@ -235,7 +235,7 @@ def chess_main(args):
             "terminal_visits": d["terminal_visits"],
             "lanes": args.lanes or "auto",
             "roofline": {
-                "kernel": "wino_conv_kernel (residual tower, 8 launches per forward)",
+                "kernel": "wino16_conv_kernel (residual tower, 8 launches per forward)",
                 "bound": "mfma",
                 "achieved": round(achieved, 2),
                 "peak": FP32_MFMA_PEAK_TFLOPS,
@@ -437,8 +437,8 @@ def main():
                                     if args.cache_log2 else None),
             "cache_off": off,
             "roofline": {
-                "kernel": ("wino_conv_kernel (Winograd F(2x2,3x3) on fp32 MFMA, fused BN/ReLU and 1x1 "
-                           "projection residual)" if args.conv_algo == 0 else
+                "kernel": ("wino16_conv_kernel (Winograd F(2x2,3x3) on fp32 MFMA 16x16x4, 16 tiles per "
+                           "workgroup, fused BN/ReLU and 1x1 projection residual)" if args.conv_algo == 0 else
                            "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"),
                 "bound": "mfma",
                 "achieved": round(achieved, 2),

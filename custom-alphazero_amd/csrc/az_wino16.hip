@@ -35,6 +35,13 @@ constexpr int kW16Threads = 256;
 #ifndef AZ_W16_PF
 #define AZ_W16_PF 2
 #endif
+// 1: the next chunk's patch loads are issued at the start of the current
+// chunk's MFMA stages (latency hidden behind them; the patch stays in
+// registers until the chunk ends).  Measured slower: 188 VGPRs drop the
+// kernel to 2 waves/SIMD (B=4096 178 vs 185 TFLOP/s, C4 self-play -4%)
+#ifndef AZ_W16_EARLY
+#define AZ_W16_EARLY 0
+#endif
 
 __host__ __device__ constexpr int w16_sign(int a, int i) {
   return i == 0 ? (a == 3 ? 0 : 1) : (a == 0 ? 0 : (a == 1 ? 1 : -1));
@@ -226,6 +233,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
       static_assert(NX % NB == 0, "buffer of a stage must not depend on the chunk");
       load_b_flat(c * NX + xi + PF, bq[(xi + PF) % NB]);
       if (xi + 1 < NX) load_a(xi + 1, aq[(xi + 1) & 1]);
+      if (AZ_W16_EARLY && xi == 0 && c + 1 < NCH) produce_load(c + 1);
       float av[KS], bv[2][KS];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -266,7 +274,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     if (NX == 16) scatter(15, M[1]);
     if (c + 1 < NCH) {
       __syncthreads();
-      produce_load(c + 1);
+      if (!AZ_W16_EARLY) produce_load(c + 1);
       produce_store();
       __syncthreads();
     }
