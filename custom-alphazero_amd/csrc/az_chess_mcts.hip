@@ -289,8 +289,16 @@ __global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
 
 // the leaf's is_game_over() (mcts.py:173-179): terminal leaves back up the
 // canonical get_result (1 checkmate, 0 draw); others are queued for evaluation
-__global__ __launch_bounds__(128) void leaf_kernel(CCfg g, CTree t) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+// AZ_LEAF_SPW slots per wave: the move generator diverges per position, so a
+// wave costs about the union of its lanes' paths; fewer slots per wave spread
+// the serial work over more CUs (the step is latency-bound here): 1 measured
+// best (626k expansions/s vs 593k with 64, 614k with 4)
+#ifndef AZ_LEAF_SPW
+#define AZ_LEAF_SPW 1
+#endif
+__global__ __launch_bounds__(64) void leaf_kernel(CCfg g, CTree t) {
+  if (threadIdx.x >= AZ_LEAF_SPW) return;
+  const int s = blockIdx.x * AZ_LEAF_SPW + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
   const Pos q = load_pos(t.leaf[s]);
   bool check;
@@ -677,7 +685,7 @@ int simulate(az_chess_engine* e, CLane& L) {
   const int S = L.g.slots;
   select_kernel<<<S, 64, 0, s>>>(L.g, L.t);
   AZC_HIP(hipMemsetAsync(L.t.eval_count, 0, sizeof(int32_t), s));
-  leaf_kernel<<<(S + 63) / 64, 64, 0, s>>>(L.g, L.t);
+  leaf_kernel<<<(S + AZ_LEAF_SPW - 1) / AZ_LEAF_SPW, 64, 0, s>>>(L.g, L.t);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
     encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, reinterpret_cast<float4*>(L.x));
     az::launch_forward(e->net, L.x, L.t.eval_count, S, 8, 8, AZ_CHESS_ACTIONS, L.act[0], L.act[1],
