@@ -208,6 +208,12 @@ def chess_main(args):
     busy = st1["conv_busy_ms"]
     launches = st1["conv_launches"]
     achieved = local_evals * conv_flop_per_board / (busy * 1e-3) / 1e12 if busy else 0.0
+    boards_per_launch = local_evals / max(launches / (2 * args.depth), 1)
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "r1", "pmc_chess_traffic.json")
+    if os.path.exists(pmc):  # PMC bytes/board (FETCH_SIZE/WRITE_SIZE passes) x live batch
+        with open(pmc) as fp:
+            traffic = int(json.load(fp)["winograd"]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
     if rank == 0:
         line = {
             "metric": f"MCTS node-expansions/s (Chess, {args.sims} sims/move)",
@@ -241,13 +247,15 @@ def chess_main(args):
                 "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (PMC bytes/board, profiles/r1/pmc_chess_traffic.json, "
+                                "x live boards/launch)",
                 "achieved_basis": "algorithmic (direct-convolution) FLOP of the tower / conv-busy time (HIP events)",
                 "algorithmic_flop_per_board": conv_flop_per_board,
                 "mfma_flop_per_board": mfma_flop_per_board,
                 "mfma_frac": round(achieved * mfma_flop_per_board / conv_flop_per_board
                                    / FP32_MFMA_PEAK_TFLOPS, 4),
-                "boards_per_launch": round(local_evals / max(launches / (2 * args.depth), 1), 1),
+                "boards_per_launch": round(boards_per_launch, 1),
                 "avg_launch_ms": round(st1["conv_ms"] / max(launches, 1), 4),
                 "conv_busy_ms": round(busy, 2),
             },

@@ -43,6 +43,7 @@ constexpr int kW16Threads = 256;
 #define AZ_W16_EARLY 0
 #endif
 
+
 __host__ __device__ constexpr int w16_sign(int a, int i) {
   return i == 0 ? (a == 3 ? 0 : 1) : (a == 0 ? 0 : (a == 1 ? 1 : -1));
 }

@@ -8,6 +8,7 @@ import json
 import sys
 
 out, B = sys.argv[1], int(sys.argv[2])
+only = int(sys.argv[sys.argv.index("--only") + 1]) if "--only" in sys.argv else None
 
 
 def per_kernel(d, name):
@@ -25,6 +26,8 @@ def per_kernel(d, name):
 res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, az_forward at B={B} boards",
        "correction": "fetch bytes = 2 x FETCH_SIZE KiB (gfx950, 16 B/lane streams); write = WRITE_SIZE KiB"}
 for algo, key in ((0, "winograd"), (1, "direct")):
+    if only is not None and algo != only:
+        continue
     f = per_kernel(f"{out}/fetch_{algo}", "FETCH_SIZE")
     w = per_kernel(f"{out}/write_{algo}", "WRITE_SIZE")
     per = {k: (2 * f[k] + w.get(k, 0.0)) * 1024 / B for k in f}
