@@ -1,0 +1,183 @@
+"""Self-play at BASELINE.json's full single-GPU sizes, checked through
+size-independent properties plus bit-exact oracle replay of sampled games.
+
+configs[1]: Connect-4, 100 sims/move, 4096 concurrent games, random-init
+network (the bench workload, with and without its 2^25-entry transposition
+cache).  configs[2]: Connect-5 on 9x9, 200 sims/move, 8192 concurrent games.
+configs[3]: one GPU's shard of 32768 Connect-4 games at 400 sims/move (the
+last of 8 ranks: games 28672..32767, seeds base + game index).  configs[4]: chess, 800 sims/move, 256 concurrent games per GPU
+(2048 across 8), random-init network, games capped at 3 plies so the test
+finishes in seconds.  The small-size parity tests (test_engine_gpu.py,
+test_chess_selfplay_gpu.py) pin the arithmetic; these pin that nothing
+changes at the sizes the bench runs (arena sizing, queue chunking, cache
+pressure, slot counts past one workgroup grid).
+"""
+import numpy as np
+import pytest
+
+import chess_oracle as C
+import oracle
+from custom_alphazero import engine as az
+from test_chess_selfplay_gpu import _compare
+from test_engine_gpu import make_net_engine, selfplay_games
+
+pytestmark = pytest.mark.gpu
+
+C4 = dict(H=6, W=7, n=4, grav=True, S=100, slots=4096)
+C4_SEED = 4242
+GREEDY_PLY = 8  # ConfigSelfPlay.index_move_greedy (reference config.py)
+
+
+@pytest.fixture(scope="module")
+def c4_games():
+    out = {}
+    for cache_log2 in (0, 25):
+        eng, _ = make_net_engine(**C4, seed=11, cache_log2=cache_log2)
+        out[cache_log2] = (eng, selfplay_games(eng, 0, C4["slots"], base_seed=C4_SEED))
+    yield out
+    for eng, _ in out.values():
+        eng.close()
+
+
+def check_rules_and_policies(games, H, W, n):
+    """Every game replays legally on the oracle rules: board before each move,
+    terminal status only at the end, result = the last mover's outcome;
+    policies normalised, supported on legal columns, one-hot on the move from
+    ply 8."""
+    for g, got in enumerate(games):
+        T = got["T"]
+        assert 2 * n - 1 <= T <= H * W, (g, T)
+        boards, status, mask, _ = oracle.board_replay(H, W, n, True, got["moves"])
+        assert (status[:-1] == 0).all() and status[-1] in (1, 2), (g, status)
+        assert not got["boards"][0].any()  # every game starts on the empty board
+        np.testing.assert_array_equal(got["boards"][1:], boards[:-1])
+        assert got["rewards"][-1] == (1 if status[-1] == 1 else 0)
+        legal = np.vstack([np.ones((1, W), bool), mask[:-1]])
+        pol = got["policy"]
+        assert (pol >= 0).all() and np.allclose(pol.sum(axis=1), 1.0, rtol=0, atol=1e-12), g
+        assert not (pol[~legal] != 0).any(), g
+        assert (pol[np.arange(T), got["moves"]] > 0).all(), g
+        if T > GREEDY_PLY:
+            tail = pol[GREEDY_PLY:]
+            assert ((tail == 0) | (tail == 1)).all() and (tail.sum(axis=1) == 1).all(), g
+            np.testing.assert_array_equal(tail.argmax(axis=1), got["moves"][GREEDY_PLY:])
+
+
+def replay_on_oracle(eng, got, H, W, n, S, seed):
+    """One engine game == the oracle's MCTS (reference self_play.py:37-82)
+    driven by the engine's own batch-1 network outputs."""
+    cache = {}
+
+    def cb(board):
+        key = board.tobytes()
+        if key not in cache:
+            p, v = eng.forward(oracle.full_state(board[None]))
+            cache[key] = (p[0], float(v[0]))
+        return cache[key]
+
+    ref = oracle.play_game(H, W, n, True, S, seed, evaluator="callback", callback=cb)
+    assert got["T"] == ref["T"]
+    np.testing.assert_array_equal(got["moves"], ref["moves"])
+    np.testing.assert_array_equal(got["policy"].view(np.uint64), ref["policy"].view(np.uint64))
+    assert got["expansions"] == ref["expansions"]
+
+
+def test_c4_fullsize_rules_and_policies(c4_games):
+    check_rules_and_policies(c4_games[25][1], C4["H"], C4["W"], C4["n"])
+
+
+def test_c4_fullsize_cache_is_transparent(c4_games):
+    """The transposition cache at the bench size changes nothing: same moves,
+    policies (bitwise) and expansion counts for all 4096 games."""
+    a, b = c4_games[0][1], c4_games[25][1]
+    for g, (x, y) in enumerate(zip(a, b)):
+        assert x["T"] == y["T"] and x["expansions"] == y["expansions"], g
+        np.testing.assert_array_equal(x["moves"], y["moves"])
+        np.testing.assert_array_equal(x["policy"].view(np.uint64), y["policy"].view(np.uint64))
+
+
+@pytest.mark.parametrize("g", [0, 1777, 4095])
+def test_c4_fullsize_game_replays_on_oracle(c4_games, g):
+    """Sampled games of the 4096 replay bit for bit through the oracle's MCTS
+    (reference self_play.py:37-82) driven by the engine's own batch-1 network
+    outputs."""
+    eng, games = c4_games[25]
+    replay_on_oracle(eng, games[g], C4["H"], C4["W"], C4["n"], C4["S"], C4_SEED + g)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(H=9, W=9, n=5, S=200, slots=8192, first=0, replay=(8191,)),        # configs[2]
+    dict(H=6, W=7, n=4, S=400, slots=4096, first=7 * 4096, replay=(4095,)),  # configs[3], rank 7
+], ids=["c5_9x9_s200_8192", "c4_s400_shard7"])
+@pytest.mark.timeout(400)  # configs[2] plays ~80M expansions (about 90 s)
+def test_connect_n_fullsize_configs(cfg):
+    """BASELINE configs[2] and one rank's shard of configs[3] at full size:
+    rules and policies for every game, sampled games replayed on the oracle
+    (a shard's game i uses seed base + first + i, as bench.py's ranks do)."""
+    H, W, n, S = cfg["H"], cfg["W"], cfg["n"], cfg["S"]
+    eng, _ = make_net_engine(H, W, n, True, S=S, slots=cfg["slots"], seed=13, cache_log2=25)
+    try:
+        games = selfplay_games(eng, cfg["first"], cfg["slots"], base_seed=C4_SEED)
+        check_rules_and_policies(games, H, W, n)
+        for g in cfg["replay"]:
+            replay_on_oracle(eng, games[g], H, W, n, S, C4_SEED + cfg["first"] + g)
+    finally:
+        eng.close()
+
+
+CHESS = dict(sims=800, slots=256, plies=3)
+CHESS_SEED = 900
+
+
+@pytest.fixture(scope="module")
+def chess_games():
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    w = init_weights(weight_spec(8, 8, 1880, in_channels=118), seed=5)
+    eng = az.ChessEngine(mcts_iterations=CHESS["sims"], slots=CHESS["slots"],
+                         evaluator=az.EVAL_NETWORK, max_plies=CHESS["plies"])
+    eng.set_weights(w.items())
+    st = eng.selfplay_run(0, CHESS["slots"], CHESS_SEED)
+    assert st["errors"] == 0 and st["games_done"] == CHESS["slots"]
+    yield eng, eng.selfplay_results()
+    eng.close()
+
+
+def test_chess_fullsize_rules_and_policies(chess_games):
+    """All 256 games: positions chain through Board.play on the oracle rules,
+    each move is legal, each root policy covers exactly the legal moves (in
+    the 1880-action space) and is normalised; 800 sims expand every root."""
+    _, r = chess_games
+    all_mv = C.all_moves()
+    start = C.from_fen()
+    for g in range(CHESS["slots"]):
+        T = int(r["lengths"][g])
+        assert T == CHESS["plies"] and r["terminations"][g] == 5, g  # the ply cap
+        pos = start
+        for t in range(T):
+            assert r["positions"][g, t].tobytes() == pos.tobytes(), (g, t)
+            mv = int(r["moves"][g, t])
+            assert mv in set(C.legal_moves(pos).tolist()), (g, t)
+            legal = np.flatnonzero(C.legal_mask(pos, all_mv))
+            k = int(r["policy_n"][g, t])
+            acts = r["policy_actions"][g, t, :k]
+            np.testing.assert_array_equal(np.sort(acts), legal)
+            probs = r["policy_probs"][g, t, :k]
+            assert (probs >= 0).all() and abs(probs.sum() - 1.0) < 1e-12, (g, t)
+            assert probs[list(all_mv[acts]).index(mv)] > 0, (g, t)
+            pos = C.play_canonical(pos, mv)
+        assert r["expansions"][g] >= CHESS["plies"], g
+
+
+@pytest.mark.parametrize("g", [0, 255])
+def test_chess_fullsize_game_replays_on_oracle(chess_games, g):
+    """Games of the 256 replay bit for bit through the chess oracle's MCTS
+    with the engine's own batch-1 network outputs (800 sims/move)."""
+    eng, r = chess_games
+
+    def cb(pos, initial):
+        x = C.full_state(*C.reference_history(pos, bool(initial)), pos)[None].astype(np.float32)
+        p, v = eng.forward(x)
+        return p[0], float(v[0])
+
+    ref = C.play_game(CHESS["sims"], CHESS_SEED + g, CHESS["plies"], callback=cb)
+    _compare(r, g, ref, "fullsize")
