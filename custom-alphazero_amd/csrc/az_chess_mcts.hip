@@ -64,6 +64,7 @@ struct CTree {
   uint16_t* leaf_moves;    // [slots][AZ_CHESS_MAX_MOVES]
   int32_t* leaf_n;         // [slots]
   int32_t* slot_exp;       // [slots]
+  float* root_value;       // [slots] the root's evaluated_value (tree API views)
   uint32_t* mt;            // [625][mt_stride] word-major MT19937 (a lane view offsets it)
   int32_t mt_stride;       // slots of the whole engine
   int32_t* eval_slot;      // [slots]
@@ -86,6 +87,18 @@ struct CSamples {
   int32_t* result = nullptr;
   int32_t* term = nullptr;
   int32_t* expansions = nullptr;
+};
+
+// MCTS.play through the tree API (az_chess_tree_play); all null/-1 in self-play
+struct CPlayOut {
+  const double* uniforms = nullptr;  // [slots] host random_sample draws; null: per-slot MT19937
+  int greedy = -1;                   // -1: self_play.py:62's fullmove rule; 0/1: MCTS.play(greedy)
+  int deterministic = 0;             // edge = argmax(probabilities) (mcts.py:199)
+  int32_t* move = nullptr;           // [slots] move code, -1 idle
+  int32_t* status = nullptr;         // [slots] outcome of the new root
+  int32_t* pol_n = nullptr;          // [slots]
+  int16_t* pol_a = nullptr;          // [slots][AZ_CHESS_MAX_MOVES]
+  double* pol_p = nullptr;           // [slots][AZ_CHESS_MAX_MOVES]
 };
 
 constexpr int kMtN = 624;
@@ -230,6 +243,29 @@ __global__ void slot_init_kernel(CCfg g, CTree t, CSamples smp, int64_t n_first)
   else t.game_id[s] = -1;
 }
 
+// MCTS.__init__ (mcts.py:86-104) for the listed slots: a new root, no tree
+__global__ void tree_reset_kernel(CCfg g, CTree t, int n, const int32_t* slots, const az_chess_pos* roots) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = slots[i];
+  t.root[s] = roots[i];
+  t.root_first[s] = 0;
+  t.root_n[s] = 0;
+  t.root_value[s] = 0.f;
+  t.half[s] = 0;
+  t.top[s] = 0;
+  t.ply[s] = 0;
+  t.initial[s] = 1;
+  t.path_len[s] = 0;
+  t.slot_exp[s] = 0;
+  t.game_id[s] = s;
+}
+
+__global__ void tree_release_kernel(CTree t, int n, const int32_t* slots) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) t.game_id[slots[i]] = -1;
+}
+
 // MCTS.select (mcts.py:111-120): one wave per slot
 __global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
   const int s = blockIdx.x, lane = threadIdx.x;
@@ -322,8 +358,11 @@ __global__ __launch_bounds__(64) void leaf_kernel(CCfg g, CTree t) {
 
 // Board.full_state of the queued leaves into the network input [q][64][128]:
 // history [0 x 6, start position, board] (every board made by play(), see
-// chess/board.py docstring) or [0 x 7, board] for a game's first Board();
-// planes 118..127 are the zero padding of the stem.
+// chess/board.py docstring) or, for a root set by reset (the MCTS root is a
+// deepcopy, whose copy() re-runs __init__), [0 x 7, start-position state]
+// whatever the position -- the game's first Board() is the start position;
+// the castling/counter planes are the board's own.  Planes 118..127 are the
+// zero padding of the stem.
 __global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, float4* __restrict__ x) {
   __shared__ Pos sp[2];
   __shared__ float feat[6];
@@ -351,14 +390,15 @@ __global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, floa
     for (int e = threadIdx.x; e < 64 * 32; e += blockDim.x) {
       const int pix = e >> 5, k0 = (e & 31) * 4;
       const int sq = (7 - (pix >> 3)) * 8 + (pix & 7);
-      const int cur_idx = onehot_index(sp[1], sq), st_idx = onehot_index(sp[0], sq);
+      const int st_idx = onehot_index(sp[0], sq), cur_idx = initial ? st_idx : onehot_index(sp[1], sq);
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int k = k0 + i;
         float val = 0.f;
         if (k >= 112 && k < 118) val = feat[k - 112];
-        else if (k >= 98 && k < 112) val = k - 98 == 13 ? (float)sp[1].rep : (cur_idx == k - 98 ? 1.f : 0.f);
+        else if (k >= 98 && k < 112)
+          val = k - 98 == 13 ? (initial ? 0.f : (float)sp[1].rep) : (cur_idx == k - 98 ? 1.f : 0.f);
         else if (k >= 84 && k < 98 && !initial) val = k - 84 == 13 ? 0.f : (st_idx == k - 84 ? 1.f : 0.f);
         v[i] = val;
       }
@@ -456,6 +496,7 @@ __global__ __launch_bounds__(64) void expand_kernel(CCfg g, CTree t, const float
       if (depth == 0) {
         t.root_first[s] = first;
         t.root_n[s] = n;
+        t.root_value[s] = value;
       } else {
         Edge& pe = E[path[depth - 1]];
         pe.child = first;
@@ -472,7 +513,7 @@ __global__ __launch_bounds__(64) void expand_kernel(CCfg g, CTree t, const float
 
 // MCTS.play (mcts.py:182-222) for every active slot + the self-play loop's
 // bookkeeping (self_play.py:59-82); one wave per slot
-__global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp) {
+__global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp, CPlayOut po) {
   __shared__ double pi[AZ_CHESS_MAX_MOVES];
   __shared__ int chosen;
   __shared__ int done_code;
@@ -486,6 +527,7 @@ __global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp)
     if (lane == 0) flag(t, az::kErrNoRoot);
     return;
   }
+  const bool tree_api = po.move != nullptr;
   const Pos root = load_pos(t.root[s]);
   const int64_t gid = t.game_id[s];
   const int64_t gi = gid - smp.first_game;
@@ -493,7 +535,7 @@ __global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp)
   for (int j = lane; j < n; j += 64) pi[j] = (double)E[first + j].N;
   __syncthreads();
   if (lane == 0) {
-    const bool greedy = root.full >= g.greedy_ply;  // self_play.py:62
+    const bool greedy = po.greedy < 0 ? root.full >= g.greedy_ply : po.greedy != 0;  // self_play.py:62
     if (greedy) {
       int im = 0;
       for (int i = 1; i < n; ++i)
@@ -503,26 +545,43 @@ __global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp)
       const double sum = pairwise(pi, n);  // normalize_probabilities on float64 counts
       for (int i = 0; i < n; ++i) pi[i] = sum == 0.0 ? 1.0 / (double)n : pi[i] / sum;
     }
-    // np.random.choice(edges, 1, p): one random_sample, cumsum, normalise, searchsorted right
-    const double u = mt_uniform(t, s);
-    double cdf[1];
-    double acc = 0.0, last;
-    for (int i = 0; i < n; ++i) acc += pi[i];
-    last = acc;
-    acc = 0.0;
-    int idx = 0;
-    for (int i = 0; i < n; ++i) {
-      acc += pi[i];
-      cdf[0] = acc / last;
-      if (cdf[0] <= u) idx = i + 1;
+    if (po.deterministic) {
+      int im = 0;  // np.argmax(probabilities): first maximum
+      for (int i = 1; i < n; ++i)
+        if (pi[i] > pi[im]) im = i;
+      chosen = im;
+    } else {
+      // np.random.choice(edges, 1, p): one random_sample, cumsum, normalise, searchsorted right
+      const double u = po.uniforms ? po.uniforms[s] : mt_uniform(t, s);
+      double cdf[1];
+      double acc = 0.0, last;
+      for (int i = 0; i < n; ++i) acc += pi[i];
+      last = acc;
+      acc = 0.0;
+      int idx = 0;
+      for (int i = 0; i < n; ++i) {
+        acc += pi[i];
+        cdf[0] = acc / last;
+        if (cdf[0] <= u) idx = i + 1;
+      }
+      chosen = idx < n ? idx : n - 1;
     }
-    chosen = idx < n ? idx : n - 1;
   }
   __syncthreads();
   const int c_idx = chosen;
   const Edge c = E[first + c_idx];
   // sample record (MCTS.play return_details: parent state, policy, move)
-  if (gi >= 0 && gi < smp.n_games && ply < smp.plies) {
+  if (tree_api) {
+    const size_t r = (size_t)s;
+    for (int j = lane; j < n; j += 64) {
+      po.pol_a[r * AZ_CHESS_MAX_MOVES + j] = (int16_t)action_of(t.lut, (uint16_t)E[first + j].action);
+      po.pol_p[r * AZ_CHESS_MAX_MOVES + j] = pi[j];
+    }
+    if (lane == 0) {
+      po.move[s] = (uint16_t)c.action;
+      po.pol_n[s] = n;
+    }
+  } else if (gi >= 0 && gi < smp.n_games && ply < smp.plies) {
     const size_t r = (size_t)gi * smp.plies + ply;
     for (int j = lane; j < n; j += 64) {
       smp.pol_a[r * AZ_CHESS_MAX_MOVES + j] = (int16_t)action_of(t.lut, (uint16_t)E[first + j].action);
@@ -592,7 +651,12 @@ __global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp)
     bool check;
     const int nl = legal_moves(nr, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check);
     int oc = nl < 0 ? AZ_CHESS_ONGOING : outcome(nr, nl, check);
-    if (oc == AZ_CHESS_ONGOING && ply + 1 >= g.max_plies) oc = AZ_CHESS_MAX_PLIES;
+    if (tree_api) {
+      po.status[s] = oc;  // the MCTS object keeps its (possibly finished) board
+      oc = AZ_CHESS_ONGOING;
+    } else if (oc == AZ_CHESS_ONGOING && ply + 1 >= g.max_plies) {
+      oc = AZ_CHESS_MAX_PLIES;
+    }
     done_code = oc;
   }
   __syncthreads();
@@ -654,6 +718,12 @@ struct az_chess_engine {
   float* values = nullptr;
   std::vector<void*> owned, sample_bufs;
   int64_t sp_n = 0;
+  // tree API staging (allocated on first use)
+  double* tree_u = nullptr;
+  int32_t *tree_move = nullptr, *tree_status = nullptr, *tree_pol_n = nullptr, *tree_slots = nullptr;
+  int16_t* tree_pol_a = nullptr;
+  double* tree_pol_p = nullptr;
+  az_chess_pos* tree_roots = nullptr;
 
   template <typename T>
   int alloc(T** p, size_t count) {
@@ -727,6 +797,7 @@ int make_lane(az_chess_engine* e, CLane* L, int first, int n) {
   t.leaf_moves += f * AZ_CHESS_MAX_MOVES;
   t.leaf_n += f;
   t.slot_exp += f;
+  t.root_value += f;
   t.mt += f;
   t.eval_slot += f;
   int rc;
@@ -798,7 +869,8 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
       (rc = e->alloc(&t.game_id, S)) || (rc = e->alloc(&t.path, S * g.max_depth)) ||
       (rc = e->alloc(&t.path_len, S)) || (rc = e->alloc(&t.leaf, S)) ||
       (rc = e->alloc(&t.leaf_moves, S * AZ_CHESS_MAX_MOVES)) || (rc = e->alloc(&t.leaf_n, S)) ||
-      (rc = e->alloc(&t.slot_exp, S)) || (rc = e->alloc(&t.mt, S * (kMtN + 1))) ||
+      (rc = e->alloc(&t.slot_exp, S)) || (rc = e->alloc(&t.root_value, S)) ||
+      (rc = e->alloc(&t.mt, S * (kMtN + 1))) ||
       (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_count, 1)) ||
       (rc = e->alloc(&t.stats, az::kStatCount)))
     return cleanup(rc);
@@ -1002,7 +1074,7 @@ int az_chess_selfplay_step(az_chess_engine* e, int n_moves, az_stats* st) {
     for (int s = 0; s < e->g.sims; ++s)
       for (CLane* L : e->lanes)
         if ((rc = simulate(e, *L))) return rc;
-    for (CLane* L : e->lanes) play_kernel<<<L->g.slots, 64, 0, L->stream>>>(L->g, L->t, e->smp);
+    for (CLane* L : e->lanes) play_kernel<<<L->g.slots, 64, 0, L->stream>>>(L->g, L->t, e->smp, CPlayOut{});
     AZC_HIP(hipGetLastError());
   }
   if ((rc = sync_lanes(e))) return rc;
@@ -1044,6 +1116,160 @@ int az_chess_selfplay_results(az_chess_engine* e, int32_t* lengths, int32_t* res
   if (policy_actions)
     AZC_HIP(hipMemcpy(policy_actions, s.pol_a, G * P * M * sizeof(int16_t), hipMemcpyDeviceToHost));
   if (policy_probs) AZC_HIP(hipMemcpy(policy_probs, s.pol_p, G * P * M * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+namespace {
+int tree_buffers(az_chess_engine* e) {
+  if (e->tree_move) return 0;
+  const size_t S = (size_t)e->g.slots, M = AZ_CHESS_MAX_MOVES;
+  int rc;
+  if ((rc = e->alloc(&e->tree_u, S)) || (rc = e->alloc(&e->tree_status, S)) || (rc = e->alloc(&e->tree_pol_n, S)) ||
+      (rc = e->alloc(&e->tree_slots, S)) || (rc = e->alloc(&e->tree_pol_a, S * M)) ||
+      (rc = e->alloc(&e->tree_pol_p, S * M)) || (rc = e->alloc(&e->tree_roots, S)) ||
+      (rc = e->alloc(&e->tree_move, S)))
+    return rc;
+  return 0;
+}
+
+int tree_slot_list(az_chess_engine* e, int n, const int32_t* slots) {
+  if (n < 0 || n > e->g.slots || (n && !slots)) return az::fail_abi(AZ_E_INVALID, "bad slot list");
+  std::vector<char> seen(e->g.slots, 0);
+  for (int i = 0; i < n; ++i) {
+    if (slots[i] < 0 || slots[i] >= e->g.slots || seen[slots[i]])
+      return az::fail_abi(AZ_E_INVALID, "slot index out of range or repeated");
+    seen[slots[i]] = 1;
+  }
+  int rc;
+  if ((rc = tree_buffers(e))) return rc;
+  if (n) AZC_HIP(hipMemcpyAsync(e->tree_slots, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+  return 0;
+}
+}  // namespace
+
+int az_chess_tree_reset(az_chess_engine* e, int n, const int32_t* slots, const az_chess_pos* roots) {
+  if (!e || (n && !roots)) return az::fail_abi(AZ_E_INVALID, "null argument");
+  if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
+    return az::fail_abi(AZ_E_STATE, "network evaluator selected but az_chess_engine_set_weights was not called");
+  AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  if ((rc = sync_lanes(e)) || (rc = tree_slot_list(e, n, slots))) return rc;
+  if (!n) return 0;
+  // a root must be a position the device rules accept (legal move list fits)
+  std::vector<az_chess_pos> r(roots, roots + n);
+  for (const az_chess_pos& p : r)
+    if (p.turn > 1 || p.ep_square < -1 || p.ep_square > 63)
+      return az::fail_abi(AZ_E_INVALID, "malformed az_chess_pos");
+  AZC_HIP(hipMemcpyAsync(e->tree_roots, r.data(), n * sizeof(az_chess_pos), hipMemcpyHostToDevice, e->stream));
+  tree_reset_kernel<<<(n + 63) / 64, 64, 0, e->stream>>>(e->g, e->t, n, e->tree_slots, e->tree_roots);
+  AZC_HIP(hipGetLastError());
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int az_chess_tree_release(az_chess_engine* e, int n, const int32_t* slots) {
+  if (!e) return az::fail_abi(AZ_E_INVALID, "null engine");
+  AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  if ((rc = sync_lanes(e)) || (rc = tree_slot_list(e, n, slots))) return rc;
+  if (!n) return 0;
+  tree_release_kernel<<<(n + 63) / 64, 64, 0, e->stream>>>(e->t, n, e->tree_slots);
+  AZC_HIP(hipGetLastError());
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int az_chess_tree_search(az_chess_engine* e, int n_sims) {
+  if (!e || n_sims < 0) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
+    return az::fail_abi(AZ_E_STATE, "network evaluator selected but az_chess_engine_set_weights was not called");
+  AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  for (int s = 0; s < n_sims; ++s)
+    for (CLane* L : e->lanes)
+      if ((rc = simulate(e, *L))) return rc;
+  if ((rc = sync_lanes(e))) return rc;
+  return check_errors(e);
+}
+
+int az_chess_tree_play(az_chess_engine* e, const double* uniforms, int greedy, int deterministic, int32_t* moves,
+                       int32_t* status, int32_t* policy_n, int16_t* policy_actions, double* policy_probs) {
+  if (!e || (!deterministic && !uniforms)) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  if ((rc = sync_lanes(e)) || (rc = tree_buffers(e))) return rc;
+  const size_t S = (size_t)e->g.slots, M = AZ_CHESS_MAX_MOVES;
+  if (!deterministic) AZC_HIP(hipMemcpyAsync(e->tree_u, uniforms, S * sizeof(double), hipMemcpyHostToDevice, e->stream));
+  AZC_HIP(hipMemsetAsync(e->tree_move, 0xff, S * sizeof(int32_t), e->stream));
+  AZC_HIP(hipMemsetAsync(e->tree_status, 0, S * sizeof(int32_t), e->stream));
+  AZC_HIP(hipMemsetAsync(e->tree_pol_n, 0, S * sizeof(int32_t), e->stream));
+  AZC_HIP(hipStreamSynchronize(e->stream));
+  for (CLane* L : e->lanes) {
+    const size_t f = (size_t)L->first;
+    CPlayOut po;
+    po.uniforms = deterministic ? nullptr : e->tree_u + f;
+    po.greedy = greedy ? 1 : 0;
+    po.deterministic = deterministic ? 1 : 0;
+    po.move = e->tree_move + f;
+    po.status = e->tree_status + f;
+    po.pol_n = e->tree_pol_n + f;
+    po.pol_a = e->tree_pol_a + f * M;
+    po.pol_p = e->tree_pol_p + f * M;
+    play_kernel<<<L->g.slots, 64, 0, L->stream>>>(L->g, L->t, CSamples{}, po);
+  }
+  AZC_HIP(hipGetLastError());
+  if ((rc = sync_lanes(e)) || (rc = check_errors(e))) return rc;
+  if (moves) AZC_HIP(hipMemcpy(moves, e->tree_move, S * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (status) AZC_HIP(hipMemcpy(status, e->tree_status, S * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (policy_n) AZC_HIP(hipMemcpy(policy_n, e->tree_pol_n, S * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (policy_actions) AZC_HIP(hipMemcpy(policy_actions, e->tree_pol_a, S * M * sizeof(int16_t), hipMemcpyDeviceToHost));
+  if (policy_probs) AZC_HIP(hipMemcpy(policy_probs, e->tree_pol_p, S * M * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int az_chess_tree_info(az_chess_engine* e, int slot, int64_t* info, float* root_value) {
+  if (!e || !info || slot < 0 || slot >= e->g.slots) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  if ((rc = sync_lanes(e))) return rc;
+  int32_t top, first, cnt, ply;
+  int64_t gid;
+  AZC_HIP(hipMemcpy(&top, e->t.top + slot, 4, hipMemcpyDeviceToHost));
+  AZC_HIP(hipMemcpy(&first, e->t.root_first + slot, 4, hipMemcpyDeviceToHost));
+  AZC_HIP(hipMemcpy(&cnt, e->t.root_n + slot, 4, hipMemcpyDeviceToHost));
+  AZC_HIP(hipMemcpy(&ply, e->t.ply + slot, 4, hipMemcpyDeviceToHost));
+  AZC_HIP(hipMemcpy(&gid, e->t.game_id + slot, 8, hipMemcpyDeviceToHost));
+  if (root_value) AZC_HIP(hipMemcpy(root_value, e->t.root_value + slot, 4, hipMemcpyDeviceToHost));
+  info[0] = top;
+  info[1] = first;
+  info[2] = cnt;
+  info[3] = ply;
+  info[4] = gid >= 0;
+  return 0;
+}
+
+int az_chess_tree_export(az_chess_engine* e, int slot, double* prior, double* w, int32_t* n, int32_t* child,
+                         int32_t* child_n, int32_t* moves, float* child_value) {
+  if (!e || slot < 0 || slot >= e->g.slots) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  if ((rc = sync_lanes(e))) return rc;
+  int32_t top, half;
+  AZC_HIP(hipMemcpy(&top, e->t.top + slot, 4, hipMemcpyDeviceToHost));
+  AZC_HIP(hipMemcpy(&half, e->t.half + slot, 4, hipMemcpyDeviceToHost));
+  std::vector<az::Edge> h(top);
+  if (top)
+    AZC_HIP(hipMemcpy(h.data(), e->t.edges + ((size_t)slot * 2 + half) * e->g.half_cap, top * sizeof(az::Edge),
+                      hipMemcpyDeviceToHost));
+  for (int i = 0; i < top; ++i) {
+    if (prior) prior[i] = h[i].prior;
+    if (w) w[i] = h[i].W;
+    if (n) n[i] = h[i].N;
+    if (child) child[i] = h[i].child;
+    if (child_n) child_n[i] = h[i].child_n;
+    if (moves) moves[i] = (uint16_t)h[i].action;
+    if (child_value) child_value[i] = h[i].child_value;
+  }
   return 0;
 }
 

@@ -76,7 +76,9 @@ EXPORTED = (
     "az_chess_all_moves", "az_chess_legal", "az_chess_encode", "az_chess_play", "az_chess_perft",
     "az_chess_engine_create", "az_chess_engine_destroy", "az_chess_engine_set_weights",
     "az_chess_forward", "az_chess_selfplay_begin", "az_chess_selfplay_step", "az_chess_selfplay_run",
-    "az_chess_selfplay_results", "az_chess_stats", "az_chess_timer_enable",
+    "az_chess_selfplay_results", "az_chess_stats", "az_chess_timer_enable", "az_chess_tree_reset",
+    "az_chess_tree_release", "az_chess_tree_search", "az_chess_tree_play", "az_chess_tree_info",
+    "az_chess_tree_export",
 )
 
 _lib = None
@@ -139,6 +141,12 @@ def load_library():
         "az_chess_selfplay_results": (ctypes.c_int, [P] + [P] * 9),
         "az_chess_stats": (ctypes.c_int, [P, ctypes.POINTER(Stats)]),
         "az_chess_timer_enable": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_chess_tree_reset": (ctypes.c_int, [P, ctypes.c_int, P, P]),
+        "az_chess_tree_release": (ctypes.c_int, [P, ctypes.c_int, P]),
+        "az_chess_tree_search": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_chess_tree_play": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, P, P, P, P, P]),
+        "az_chess_tree_info": (ctypes.c_int, [P, ctypes.c_int, P, P]),
+        "az_chess_tree_export": (ctypes.c_int, [P, ctypes.c_int, P, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -422,3 +430,44 @@ class ChessEngine:
 
     def timer(self, on):
         _check(self._L.az_chess_timer_enable(self._h, int(bool(on))))
+
+    # ------------------------------------------------------------- tree API
+    def tree_reset(self, slots, roots):
+        from custom_alphazero.chess.kernels import POS_DTYPE
+        slots = np.ascontiguousarray(slots, np.int32)
+        roots = np.ascontiguousarray(roots, POS_DTYPE).reshape(len(slots))
+        _check(self._L.az_chess_tree_reset(self._h, len(slots), _ptr(slots), _ptr(roots)))
+
+    def tree_release(self, slots):
+        slots = np.ascontiguousarray(slots, np.int32)
+        _check(self._L.az_chess_tree_release(self._h, len(slots), _ptr(slots)))
+
+    def tree_search(self, n_sims):
+        _check(self._L.az_chess_tree_search(self._h, int(n_sims)))
+
+    def tree_play(self, uniforms=None, greedy=False, deterministic=False):
+        """-> moves [S] (move codes, -1 idle), status [S] (AZ_CHESS_* of the new
+        root), policy_n [S], policy_actions [S, 256], policy_probs [S, 256]."""
+        S, M = self.slots, self.MAX_MOVES
+        u = None if deterministic else np.ascontiguousarray(uniforms, np.float64).reshape(S)
+        out = dict(moves=np.zeros(S, np.int32), status=np.zeros(S, np.int32),
+                   policy_n=np.zeros(S, np.int32), policy_actions=np.zeros((S, M), np.int16),
+                   policy_probs=np.zeros((S, M), np.float64))
+        _check(self._L.az_chess_tree_play(self._h, _ptr(u), int(bool(greedy)), int(bool(deterministic)),
+                                          *(_ptr(out[k]) for k in ("moves", "status", "policy_n",
+                                                                   "policy_actions", "policy_probs"))))
+        return out
+
+    def tree_export(self, slot):
+        info = np.zeros(5, np.int64)
+        rv = np.zeros(1, np.float32)
+        _check(self._L.az_chess_tree_info(self._h, int(slot), _ptr(info), _ptr(rv)))
+        n = int(info[0])
+        out = dict(prior=np.zeros(n, np.float64), w=np.zeros(n, np.float64), n=np.zeros(n, np.int32),
+                   child=np.zeros(n, np.int32), child_n=np.zeros(n, np.int32),
+                   moves=np.zeros(n, np.int32), child_value=np.zeros(n, np.float32))
+        _check(self._L.az_chess_tree_export(self._h, int(slot), *(_ptr(out[k]) for k in (
+            "prior", "w", "n", "child", "child_n", "moves", "child_value"))))
+        out.update(arena_top=n, root_first=int(info[1]), root_n=int(info[2]), ply=int(info[3]),
+                   active=bool(info[4]), root_value=float(rv[0]))
+        return out

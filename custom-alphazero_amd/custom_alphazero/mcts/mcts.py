@@ -10,6 +10,11 @@ a caller seeding np.random gets the reference's move sequence bit for bit.
 `root` / `current_root` are read-only UCTNode/UCTEdge views exported from the
 device arena (the reference's objects, mcts.py:22-85, for visualisation and
 inspection; mutating them does not change the search).
+
+A chess Board (custom_alphazero.chess.board.Board) selects ChessMCTS: the
+same API over az_chess_tree_* (csrc/az_chess_mcts.hip).  The chess arena
+keeps only the live tree (play() compacts the chosen child's subtree into
+the other arena half), so there `root` is the tree under the current root.
 """
 from copy import deepcopy
 from typing import List, Optional, Tuple, Union
@@ -103,6 +108,11 @@ def _engine_for(model, all_possible_moves) -> az.Engine:
 
 
 class MCTS:
+    def __new__(cls, board=None, *args, **kwargs):
+        if cls is MCTS and _is_chess_board(board):
+            return super().__new__(ChessMCTS)
+        return super().__new__(cls)
+
     def __init__(self, board: Board, all_possible_moves: List[Move], concurrency: bool = False,
                  plays_inferences: Optional[dict] = None, model=None, use_solver: bool = False):
         if use_solver:
@@ -185,6 +195,121 @@ class MCTS:
     @property
     def root(self) -> UCTNode:
         return self._build(current=False)
+
+    @property
+    def current_root(self) -> UCTNode:
+        return self._build(current=True)
+
+
+# ---------------------------------------------------------------- chess
+def _is_chess_board(board) -> bool:
+    from custom_alphazero.chess.board import Board as ChessBoard
+    return isinstance(board, ChessBoard)
+
+
+def _chess_engine_for(model):
+    from custom_alphazero.config import ConfigSelfPlay as SP
+    if isinstance(model, SyntheticEvaluator):
+        evaluator = az.EVAL_SYNTHETIC
+    elif model is not None and hasattr(model, "engine_weights"):
+        evaluator = az.EVAL_NETWORK
+    else:
+        raise TypeError(
+            "MCTS on the MI355X engine needs a custom_alphazero PolicyValueModel (or "
+            "SyntheticEvaluator); HTTP inference and the exact solver are not on the device path")
+    sims = max(SP.mcts_iterations, 1)
+    max_plies = max(SP.chess_max_plies, 1)
+    # a tree holds at most the visits of its root: sims per search plus the
+    # reused subtree; 218 edges bound one expansion, ~40 is typical
+    eng = az.ChessEngine(mcts_iterations=sims, slots=1, evaluator=evaluator, max_plies=max_plies,
+                         index_move_greedy=ConfigMCTS.index_move_greedy,
+                         exploration_constant=ConfigMCTS.exploration_constant,
+                         filters=ConfigModel.filters, depth=ConfigModel.depth,
+                         value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon,
+                         arena_edges=160 * sims + 4096)
+    if evaluator == az.EVAL_NETWORK:
+        eng.set_weights(model.engine_weights())
+    return eng
+
+
+class ChessMCTS(MCTS):
+    """MCTS (mcts.py:86-222) with a chess board: search, expansion (network
+    on Board.full_state, priors zipped with python-chess's move order),
+    backup and play run on the device (az_chess_tree_*).  The root is
+    evaluated with the history of a deepcopied board, [0 x 7, start-position
+    state] (python-chess copy() re-runs the reference subclass's __init__),
+    every later board with [0 x 6, start state, board]."""
+
+    def __init__(self, board, all_possible_moves, concurrency: bool = False,
+                 plays_inferences: Optional[dict] = None, model=None, use_solver: bool = False):
+        from custom_alphazero.chess.utils import get_all_possible_moves
+        if use_solver:
+            raise NotImplementedError("the exact solver (c4solver) is not on the device path")
+        canonical = get_all_possible_moves()
+        if [m.uci for m in all_possible_moves] != [m.uci for m in canonical]:
+            raise ValueError("chess MCTS on the device uses get_all_possible_moves() (1880 moves, "
+                             "Move order) as the action space")
+        self.board = deepcopy(board)
+        self.all_possible_moves = all_possible_moves
+        self.concurrency = concurrency
+        self.plays_inferences = plays_inferences
+        self.model = model
+        self.use_solver = use_solver
+        self._engine = _chess_engine_for(model)
+        self._engine.tree_reset([0], self.board._pos[None])
+        self.path_cache = []
+
+    def search(self, iterations_number: int):
+        if self.board.is_game_over():
+            return
+        self._engine.tree_search(int(iterations_number))
+
+    def play(self, greedy: bool = False, return_details: bool = False, deterministic: bool = False):
+        if self.board.is_game_over():
+            raise RuntimeError("play() on a finished game")
+        u = None if deterministic else np.array([np.random.random_sample()])
+        out = self._engine.tree_play(u, greedy=greedy, deterministic=deterministic)
+        code = int(out["moves"][0])
+        if code < 0:
+            raise RuntimeError("play() on a finished game")
+        from custom_alphazero.chess.move import Move as ChessMove
+        move = ChessMove.from_code(code)
+        parent_state = self.board.full_state
+        self.board.play(move, keep_same_player=True)
+        child_state = self.board.full_state
+        if return_details:
+            policy = np.zeros(len(self.all_possible_moves))
+            k = int(out["policy_n"][0])
+            policy[out["policy_actions"][0, :k].astype(np.int64)] = out["policy_probs"][0, :k]
+            return parent_state, child_state, policy, move
+        return self.board
+
+    def _build(self, current=False):
+        from custom_alphazero.chess.move import Move as ChessMove
+        t = self._engine.tree_export(0)
+
+        def make_node(first, count, value, board_fn):
+            node = UCTNode(board_fn, evaluated_value=value)
+            for i in range(first, first + count):
+                mv = ChessMove.from_code(int(t["moves"][i]))
+                child_fn = (lambda parent=node, m=mv:
+                            parent.board.play(m, on_copy=True, keep_same_player=True))
+                if t["child"][i] >= 0:
+                    child = make_node(int(t["child"][i]), int(t["child_n"][i]),
+                                      float(t["child_value"][i]), child_fn)
+                else:
+                    child = UCTNode(child_fn)
+                node.edges.append(UCTEdge(node, child, mv, float(t["prior"][i]), int(t["n"][i]),
+                                          float(t["w"][i])))
+            return node
+
+        board = deepcopy(self.board)
+        value = t["root_value"] if t["root_n"] else None
+        return make_node(t["root_first"], t["root_n"], value, lambda: board)
+
+    @property
+    def root(self) -> UCTNode:
+        return self._build()
 
     @property
     def current_root(self) -> UCTNode:

@@ -145,6 +145,37 @@ int az_chess_selfplay_results(az_chess_engine* eng, int32_t* lengths, int32_t* r
                               uint16_t* moves, int32_t* policy_n, int16_t* policy_actions,
                               double* policy_probs);
 int az_chess_stats(az_chess_engine* eng, az_stats* st);
+
+/* MCTS tree API on chess boards (mcts/mcts.py:86-222 with a chess Board):
+ * replaces the per-object UCTNode/UCTEdge tree of one MCTS instance with a
+ * slot of the engine.  A reset root evaluates with the history of a board
+ * made by deepcopy (python-chess copy() re-runs the subclass __init__:
+ * [0 x 7, start-position state], whatever the position); every board after
+ * play() holds [0 x 6, start state, board].  Positions are canonical
+ * (Board.play(keep_same_player=True) form). */
+int az_chess_tree_reset(az_chess_engine* eng, int n, const int32_t* slots, const az_chess_pos* roots);
+/* Idle the given slots (search and play skip them) until the next reset. */
+int az_chess_tree_release(az_chess_engine* eng, int n, const int32_t* slots);
+/* MCTS.search(n_sims) on every active slot. */
+int az_chess_tree_search(az_chess_engine* eng, int n_sims);
+/* MCTS.play(greedy, deterministic) on every active slot: uniforms [slots] are
+ * the np.random.random_sample draws np.random.choice consumes (ignored when
+ * deterministic).  Per slot: moves (move code, -1 idle), status (AZ_CHESS_*
+ * outcome of the new root), the policy sparsely as in
+ * az_chess_selfplay_results (policy_n, policy_actions [slots][256], policy_probs
+ * [slots][256]).  The chosen child's subtree becomes the tree (mcts.py:212);
+ * siblings are dropped.  Any output pointer may be NULL. */
+int az_chess_tree_play(az_chess_engine* eng, const double* uniforms, int greedy, int deterministic,
+                       int32_t* moves, int32_t* status, int32_t* policy_n, int16_t* policy_actions,
+                       double* policy_probs);
+/* Tree snapshot of one slot: info = {edges, root_first, root_n, ply,
+ * active}, root_value = the root's evaluated_value (0 before expansion);
+ * then the edge arrays (length info[0]); moves are move codes, child the
+ * first edge of the child's expansion or -1. */
+int az_chess_tree_info(az_chess_engine* eng, int slot, int64_t* info, float* root_value);
+int az_chess_tree_export(az_chess_engine* eng, int slot, double* prior, double* w, int32_t* n,
+                         int32_t* child, int32_t* child_n, int32_t* moves, float* child_value);
+
 /* HIP-event timing of the residual-tower conv launches (bench.py roofline) */
 int az_chess_timer_enable(az_chess_engine* eng, int on);
 

@@ -889,6 +889,40 @@ static void ct_search(ctree* t, int root, int sims) {
     }
 }
 
+/* MCTS.play's probabilities (mcts.py:188-196) and edge choice: np.argmax
+ * when deterministic (mcts.py:198-199), else np.random.choice on the draw u
+ * (cumsum, normalise by the last element, searchsorted right) */
+static int ct_policy_choice(const ctree* t, const cnode* node, int greedy, int deterministic, double u,
+                            double* pi) {
+    int n = node->count;
+    double counts[256];
+    for (int i = 0; i < n; ++i) counts[i] = (double)t->edges[node->first + i].N;
+    if (greedy) {
+        int im = 0;
+        for (int i = 1; i < n; ++i)
+            if (counts[i] > counts[im]) im = i;
+        for (int i = 0; i < n; ++i) pi[i] = i == im ? 1.0 : 0.0;
+    } else {
+        orc_normalize_f64(counts, n, pi);
+    }
+    if (deterministic) {
+        int im = 0;
+        for (int i = 1; i < n; ++i)
+            if (pi[i] > pi[im]) im = i;
+        return im;
+    }
+    double acc = 0.0, cdf[256];
+    for (int i = 0; i < n; ++i) {
+        acc += pi[i];
+        cdf[i] = acc;
+    }
+    double last = cdf[n - 1];
+    int idx = 0;
+    for (int i = 0; i < n; ++i)
+        if (cdf[i] / last <= u) idx = i + 1;
+    return idx >= n ? n - 1 : idx;
+}
+
 typedef struct {
     int32_t T, result, termination;
     int64_t expansions, terminal_visits;
@@ -930,28 +964,9 @@ int orc_chess_play_game(int sims, uint32_t seed, int max_plies, int greedy_ply, 
             t.error = 1;
             break;
         }
-        double counts[256], pi[256];
-        for (int i = 0; i < n; ++i) counts[i] = (double)t.edges[node->first + i].N;
-        int greedy = node->pos.fullmove_number >= greedy_ply;
-        if (greedy) {
-            int im = 0;
-            for (int i = 1; i < n; ++i)
-                if (counts[i] > counts[im]) im = i;
-            for (int i = 0; i < n; ++i) pi[i] = i == im ? 1.0 : 0.0;
-        } else {
-            orc_normalize_f64(counts, n, pi);
-        }
-        double u = orc_mt_uniform(&rng);
-        double acc = 0.0, cdf[256];
-        for (int i = 0; i < n; ++i) {
-            acc += pi[i];
-            cdf[i] = acc;
-        }
-        double last = cdf[n - 1];
-        int idx = 0;
-        for (int i = 0; i < n; ++i)
-            if (cdf[i] / last <= u) idx = i + 1;
-        if (idx >= n) idx = n - 1;
+        double pi[256];
+        int idx = ct_policy_choice(&t, node, node->pos.fullmove_number >= greedy_ply, 0,
+                                   orc_mt_uniform(&rng), pi);
         positions[T] = node->pos;
         moves[T] = t.edges[node->first + idx].action;
         pol_n[T] = n;
@@ -972,4 +987,78 @@ int orc_chess_play_game(int sims, uint32_t seed, int max_plies, int greedy_ply, 
     free(t.nodes);
     free(t.edges);
     return err ? -1 : 0;
+}
+
+/* ---------------------------------------------------------------------
+ * One MCTS object (mcts.py:86-222) on a chess board, for the tree API
+ * parity tests: the root node is marked initial (its board is a deepcopy,
+ * history [0 x 7, start-position state]); play() moves the root to the
+ * chosen child (tree reuse) and returns the new root's outcome.
+ * ------------------------------------------------------------------- */
+typedef struct {
+    ctree t;
+    int root;
+} orc_chess_tree;
+
+void* orc_chess_tree_new(const cpos* root, double c_puct, int eval_kind,
+                         int (*cb)(void*, const cpos*, int, float*, float*), void* ctx) {
+    init_tables();
+    orc_chess_tree* h = (orc_chess_tree*)calloc(1, sizeof(orc_chess_tree));
+    h->t.c_puct = c_puct;
+    h->t.eval_kind = eval_kind;
+    h->t.cb = cb;
+    h->t.ctx = ctx;
+    h->root = ct_new_node(&h->t, root, 1);
+    return h;
+}
+
+void orc_chess_tree_search(void* hv, int sims) {
+    orc_chess_tree* h = (orc_chess_tree*)hv;
+    ct_search(&h->t, h->root, sims);
+}
+
+/* -> outcome of the new root (0 ongoing, 1..4), -1 when the root has no edges */
+int orc_chess_tree_play(void* hv, double u, int greedy, int deterministic, uint16_t* move, int32_t* pol_n,
+                        int16_t* pol_a, double* pol_p) {
+    orc_chess_tree* h = (orc_chess_tree*)hv;
+    cnode* node = h->t.nodes + h->root;
+    int n = node->count;
+    if (n == 0) return -1;
+    double pi[256];
+    int idx = ct_policy_choice(&h->t, node, greedy, deterministic, u, pi);
+    *move = h->t.edges[node->first + idx].action;
+    *pol_n = n;
+    for (int i = 0; i < n; ++i) {
+        pol_a[i] = (int16_t)action_index(h->t.edges[node->first + i].action);
+        pol_p[i] = pi[i];
+    }
+    h->root = h->t.edges[node->first + idx].child;
+    return orc_chess_outcome(&h->t.nodes[h->root].pos);
+}
+
+/* root edges in edge order: move, prior, N, W, and the child's edge count */
+int orc_chess_tree_root(void* hv, uint16_t* moves, double* prior, int64_t* N, double* W, int32_t* child_n) {
+    orc_chess_tree* h = (orc_chess_tree*)hv;
+    const cnode* node = h->t.nodes + h->root;
+    for (int i = 0; i < node->count; ++i) {
+        const cedge* e = h->t.edges + node->first + i;
+        moves[i] = e->action;
+        prior[i] = e->prior;
+        N[i] = e->N;
+        W[i] = e->W;
+        child_n[i] = h->t.nodes[e->child].count;
+    }
+    return node->count;
+}
+
+int64_t orc_chess_tree_expansions(void* hv) { return ((orc_chess_tree*)hv)->t.expansions; }
+
+int orc_chess_tree_error(void* hv) { return ((orc_chess_tree*)hv)->t.error; }
+
+void orc_chess_tree_free(void* hv) {
+    orc_chess_tree* h = (orc_chess_tree*)hv;
+    if (!h) return;
+    free(h->t.nodes);
+    free(h->t.edges);
+    free(h);
 }

@@ -124,15 +124,18 @@ def full_state(hist, valid, cur):
 
 
 def reference_history(pos, is_root):
-    """The history deque the reference's boards carry in MCTS use: a fresh
-    Board() holds [0 x 7, state]; every board made by play() comes out of
-    python-chess's copy(), which re-runs the subclass __init__ (start
-    position), so it holds [0 x 6, start-position state, state]."""
+    """The history deque the reference's boards carry in MCTS use.  The root
+    node's board is a deepcopy (mcts.py:96, 107), and python-chess's copy()
+    re-runs the subclass __init__ (start position), so it holds [0 x 7,
+    start-position state] whatever the position (for a game's first Board(),
+    the start position itself); every board made by play() holds [0 x 6,
+    start-position state, state]."""
     start = from_fen(START_FEN)
     hist = [start] * 8
     valid = [0] * 8
-    hist[7], valid[7] = pos, 1
+    valid[7] = 1
     if not is_root:
+        hist[7] = pos
         hist[6], valid[6] = start, 1
     return hist, valid
 
@@ -239,3 +242,83 @@ def synth(pos, initial):
     v = np.zeros(1, np.float32)
     L.orc_chess_synth(_p(_one(pos)), int(initial), _p(probs), _p(v))
     return probs, float(v[0])
+
+
+class Tree:
+    """One MCTS object (mcts.py:86-222) on a chess root, on the oracle
+    (orc_chess_tree_*): search(n), play(u, greedy, deterministic), root()."""
+
+    def __init__(self, root, c_puct=1.5, callback=None):
+        L = lib()
+        P = ctypes.c_void_p
+        L.orc_chess_tree_new.restype = P
+        L.orc_chess_tree_new.argtypes = [P, ctypes.c_double, ctypes.c_int, CHESS_CB, P]
+        L.orc_chess_tree_search.argtypes = [P, ctypes.c_int]
+        L.orc_chess_tree_play.argtypes = [P, ctypes.c_double, ctypes.c_int, ctypes.c_int, P, P, P, P]
+        L.orc_chess_tree_play.restype = ctypes.c_int
+        L.orc_chess_tree_root.argtypes = [P, P, P, P, P, P]
+        L.orc_chess_tree_root.restype = ctypes.c_int
+        L.orc_chess_tree_expansions.argtypes = [P]
+        L.orc_chess_tree_expansions.restype = ctypes.c_int64
+        L.orc_chess_tree_error.argtypes = [P]
+        L.orc_chess_tree_error.restype = ctypes.c_int
+        L.orc_chess_tree_free.argtypes = [P]
+        self._L, self._err, self._callback = L, [], callback
+
+        def _cb(ctx, pos_ptr, initial, probs_ptr, value_ptr):
+            try:
+                pos = np.frombuffer(ctypes.string_at(pos_ptr, POS_DTYPE.itemsize), POS_DTYPE)[0]
+                p, v = callback(pos, int(initial))
+                p = np.ascontiguousarray(p, np.float32)
+                ctypes.memmove(probs_ptr, p.ctypes.data, 4 * 1880)
+                value_ptr[0] = float(v)
+                return 0
+            except Exception as e:  # pragma: no cover - surfaced by _check
+                self._err.append(e)
+                return 1
+
+        self._cb = CHESS_CB(_cb) if callback is not None else CHESS_CB()
+        self._root = _one(root)
+        self._h = L.orc_chess_tree_new(_p(self._root), c_puct, 1 if callback else 0, self._cb, None)
+
+    def _check(self):
+        if self._err:
+            raise self._err[0]
+        assert self._L.orc_chess_tree_error(self._h) == 0
+
+    def search(self, n):
+        self._L.orc_chess_tree_search(self._h, int(n))
+        self._check()
+
+    def play(self, u=0.0, greedy=False, deterministic=False):
+        mv = np.zeros(1, np.uint16)
+        n = np.zeros(1, np.int32)
+        pa = np.zeros(256, np.int16)
+        pp = np.zeros(256, np.float64)
+        oc = self._L.orc_chess_tree_play(self._h, float(u), int(greedy), int(deterministic), _p(mv), _p(n),
+                                         _p(pa), _p(pp))
+        if oc < 0:
+            raise RuntimeError("play() before search")
+        k = int(n[0])
+        return int(mv[0]), oc, pa[:k].copy(), pp[:k].copy()
+
+    def root(self):
+        mv = np.zeros(256, np.uint16)
+        prior = np.zeros(256, np.float64)
+        N = np.zeros(256, np.int64)
+        W = np.zeros(256, np.float64)
+        cn = np.zeros(256, np.int32)
+        k = self._L.orc_chess_tree_root(self._h, _p(mv), _p(prior), _p(N), _p(W), _p(cn))
+        return dict(moves=mv[:k], prior=prior[:k], n=N[:k], w=W[:k], child_n=cn[:k])
+
+    @property
+    def expansions(self):
+        return int(self._L.orc_chess_tree_expansions(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.orc_chess_tree_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
