@@ -129,6 +129,23 @@ struct Pos {
   int half, full;
 
   AZC_HD bb occ() const { return co[0] | co[1]; }
+  // colour / piece-type accessors by select: indexing co[] or p[] with a
+  // runtime value put the whole Pos in scratch memory (104 B per lane)
+  AZC_HD bb C(int c) const { return c ? co[1] : co[0]; }
+  AZC_HD void C_or(int c, bb v) {
+    if (c) co[1] |= v;
+    else co[0] |= v;
+  }
+  AZC_HD void P_or(int type, bb v) {
+    switch (type) {
+      case 1: p[0] |= v; break;
+      case 2: p[1] |= v; break;
+      case 3: p[2] |= v; break;
+      case 4: p[3] |= v; break;
+      case 5: p[4] |= v; break;
+      default: p[5] |= v; break;
+    }
+  }
 };
 
 AZC_HD Pos load_pos(const az_chess_pos& a) {
@@ -171,13 +188,13 @@ AZC_HD bb attackers(const Pos& q, int color, int s, bb occ) {
   bb qr = q.p[QUEEN - 1] | q.p[ROOK - 1], qb = q.p[QUEEN - 1] | q.p[BISHOP - 1];
   bb a = (king_att(s) & q.p[KING - 1]) | (knight_att(s) & q.p[KNIGHT - 1]) |
          (pawn_att(!color, s) & q.p[PAWN - 1]);
-  if (qr & q.co[color]) a |= rook_att(s, occ) & qr;
-  if (qb & q.co[color]) a |= bishop_att(s, occ) & qb;
-  return a & q.co[color];
+  if (qr & q.C(color)) a |= rook_att(s, occ) & qr;
+  if (qb & q.C(color)) a |= bishop_att(s, occ) & qb;
+  return a & q.C(color);
 }
 
 AZC_HD int king_sq(const Pos& q, int color) {
-  bb k = q.p[KING - 1] & q.co[color];
+  bb k = q.p[KING - 1] & q.C(color);
   return k ? msb(k) : -1;
 }
 
@@ -232,7 +249,7 @@ AZC_HD bool attacked_for_king(const Pos& q, bb path, bb occ) {
 AZC_HD void gen_castling(const Pos& q, bb from_mask, bb to_mask, MoveOut& o) {
   int t = q.turn;
   bb back = t ? RANK_1 : RANK_8;
-  bb king = q.co[t] & q.p[KING - 1] & back & from_mask;
+  bb king = q.C(t) & q.p[KING - 1] & back & from_mask;
   king &= (~king + 1);
   if (!king) return;
   int ks = msb(king);
@@ -255,14 +272,14 @@ AZC_HD void gen_ep(const Pos& q, bb from_mask, bb to_mask, MoveOut& o) {
   int ep = q.ep;
   if (ep < 0 || !(sq_bb(ep) & to_mask) || (sq_bb(ep) & q.occ())) return;
   int t = q.turn;
-  bb cap = q.p[PAWN - 1] & q.co[t] & from_mask & pawn_att(!t, ep) & (0xFFull << (8 * (t ? 4 : 3)));
+  bb cap = q.p[PAWN - 1] & q.C(t) & from_mask & pawn_att(!t, ep) & (0xFFull << (8 * (t ? 4 : 3)));
   for (; cap; cap &= ~sq_bb(msb(cap))) o.add(msb(cap), ep, 0);
 }
 
 // python-chess generate_pseudo_legal_moves(from_mask, to_mask)
 AZC_HD void gen_pseudo(const Pos& q, bb from_mask, bb to_mask, MoveOut& o) {
   int t = q.turn;
-  bb own = q.co[t], occ = q.occ();
+  bb own = q.C(t), occ = q.occ();
   for (bb np = own & ~q.p[PAWN - 1] & from_mask; np; np &= ~sq_bb(msb(np))) {
     int f = msb(np);
     for (bb mv = piece_attacks(q, f, occ) & ~own & to_mask; mv; mv &= ~sq_bb(msb(mv))) o.add(f, msb(mv), 0);
@@ -272,7 +289,7 @@ AZC_HD void gen_pseudo(const Pos& q, bb from_mask, bb to_mask, MoveOut& o) {
   if (!pawns) return;
   for (bb c = pawns; c; c &= ~sq_bb(msb(c))) {
     int f = msb(c);
-    for (bb tg = pawn_att(t, f) & q.co[!t] & to_mask; tg; tg &= ~sq_bb(msb(tg))) o.add_pawn(f, msb(tg));
+    for (bb tg = pawn_att(t, f) & q.C(!t) & to_mask; tg; tg &= ~sq_bb(msb(tg))) o.add_pawn(f, msb(tg));
   }
   bb single, dbl;
   if (t) {
@@ -297,13 +314,13 @@ AZC_HD void gen_pseudo(const Pos& q, bb from_mask, bb to_mask, MoveOut& o) {
 
 AZC_HD bb slider_blockers(const Pos& q, int king) {
   bb rq = q.p[ROOK - 1] | q.p[QUEEN - 1], bq = q.p[BISHOP - 1] | q.p[QUEEN - 1];
-  bb snipers = ((rook_att(king, 0) & rq) | (bishop_att(king, 0) & bq)) & q.co[!q.turn];
+  bb snipers = ((rook_att(king, 0) & rq) | (bishop_att(king, 0) & bq)) & q.C(!q.turn);
   bb blockers = 0, occ = q.occ();
   for (; snipers; snipers &= ~sq_bb(msb(snipers))) {
     bb b = between(king, msb(snipers)) & occ;
     if (b && sq_bb(msb(b)) == b) blockers |= b;
   }
-  return blockers & q.co[q.turn];
+  return blockers & q.C(q.turn);
 }
 
 // python-chess pin_mask(color, square): file, rank, then diagonal rays
@@ -318,7 +335,7 @@ AZC_HD bb pin_mask(const Pos& q, int color, int s) {
   bb sl[3] = {rq, rq, bq};
   for (int i = 0; i < 3; ++i) {
     if (rays[i] & sm) {
-      for (bb sn = rays[i] & sl[i] & q.co[!color]; sn; sn &= ~sq_bb(msb(sn))) {
+      for (bb sn = rays[i] & sl[i] & q.C(!color); sn; sn &= ~sq_bb(msb(sn))) {
         int p = msb(sn);
         if ((between(p, king) & (occ | sm)) == sm) return line(king, p);
       }
@@ -332,9 +349,9 @@ AZC_HD bool ep_skewered(const Pos& q, int king, int capturer) {
   int t = q.turn;
   int last_double = q.ep + (t ? -8 : 8);
   bb occ = (q.occ() & ~sq_bb(last_double) & ~sq_bb(capturer)) | sq_bb(q.ep);
-  bb horiz = q.co[!t] & (q.p[ROOK - 1] | q.p[QUEEN - 1]);
+  bb horiz = q.C(!t) & (q.p[ROOK - 1] | q.p[QUEEN - 1]);
   if ((ray_attack(2, king, occ) | ray_attack(6, king, occ)) & horiz) return true;
-  bb diag = q.co[!t] & (q.p[BISHOP - 1] | q.p[QUEEN - 1]);
+  bb diag = q.C(!t) & (q.p[BISHOP - 1] | q.p[QUEEN - 1]);
   return (bishop_att(king, occ) & diag) != 0;
 }
 
@@ -370,7 +387,7 @@ AZC_HD int legal_moves(const Pos& q, uint16_t* out, bool* check) {
     bb sliders = checkers & (q.p[BISHOP - 1] | q.p[ROOK - 1] | q.p[QUEEN - 1]);
     bb attacked = 0;
     for (bb s = sliders; s; s &= ~sq_bb(msb(s))) attacked |= line(king, msb(s)) & ~sq_bb(msb(s));
-    for (bb mv = king_att(king) & ~q.co[q.turn] & ~attacked; mv; mv &= ~sq_bb(msb(mv))) o.add(king, msb(mv), 0);
+    for (bb mv = king_att(king) & ~q.C(q.turn) & ~attacked; mv; mv &= ~sq_bb(msb(mv))) o.add(king, msb(mv), 0);
     int checker = msb(checkers);
     if (sq_bb(checker) == checkers) {
       bb target = between(king, checker) | checkers;
@@ -397,8 +414,8 @@ AZC_HD void remove_piece(Pos& q, int s) {
 }
 AZC_HD void set_piece(Pos& q, int s, int type, int color) {
   remove_piece(q, s);
-  q.p[type - 1] |= sq_bb(s);
-  q.co[color] |= sq_bb(s);
+  q.P_or(type, sq_bb(s));
+  q.C_or(color, sq_bb(s));
 }
 
 // python-chess Board.push of a legal move (standard chess)
@@ -417,7 +434,7 @@ AZC_HD void push(Pos& q, uint16_t m) {
   if (!t) q.full++;
   bb from_bb = sq_bb(from), to_bb = sq_bb(to);
   bb touched = from_bb ^ to_bb;
-  if ((touched & q.p[PAWN - 1]) || (touched & q.co[!t])) q.half = 0;
+  if ((touched & q.p[PAWN - 1]) || (touched & q.C(!t))) q.half = 0;
   int piece = piece_at(q, from);
   remove_piece(q, from);
   int captured = piece_at(q, to);
@@ -431,7 +448,7 @@ AZC_HD void push(Pos& q, uint16_t m) {
       remove_piece(q, ep + (t ? -8 : 8));
   }
   if (promo) piece = promo;
-  if (piece == KING && (q.co[t] & to_bb)) {  // castling (king takes own rook)
+  if (piece == KING && (q.C(t) & to_bb)) {  // castling (king takes own rook)
     bool a_side = (to & 7) < (from & 7);
     remove_piece(q, from);
     remove_piece(q, to);
@@ -469,7 +486,7 @@ AZC_HD void play(Pos& q, uint16_t m, bool keep_same_player) {
 }
 
 AZC_HD bool insufficient_color(const Pos& q, int c) {
-  bb own = q.co[c], opp = q.co[!c];
+  bb own = q.C(c), opp = q.C(!c);
   if (own & (q.p[PAWN - 1] | q.p[ROOK - 1] | q.p[QUEEN - 1])) return false;
   if (own & q.p[KNIGHT - 1]) return popc(own) <= 2 && !(opp & ~q.p[KING - 1] & ~q.p[QUEEN - 1]);
   if (own & q.p[BISHOP - 1]) {

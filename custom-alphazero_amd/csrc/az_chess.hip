@@ -212,22 +212,23 @@ __global__ void play_kernel(az_chess_pos* pos, const uint16_t* __restrict__ move
   store_pos(q, pos[i]);
 }
 
-// perft: count the legal moves of every position of a level (and their sum)
+// perft: the legal moves of every position of a level into a global move
+// table [n][AZ_CHESS_MAX_MOVES] (no per-lane scratch array), their counts and
+// sum
 __global__ void __launch_bounds__(128) perft_count_kernel(const az_chess_pos* __restrict__ pos, int n,
-                                                          int32_t* counts,
+                                                          uint16_t* __restrict__ moves, int32_t* counts,
                                                           unsigned long long* total, int* err) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   int k = 0;
   if (i < n) {
-    uint16_t buf[AZ_CHESS_MAX_MOVES];
     bool check;
     Pos q = load_pos(pos[i]);
-    k = legal_moves(q, buf, &check);
+    k = legal_moves(q, moves + (size_t)i * AZ_CHESS_MAX_MOVES, &check);
     if (k < 0) {
       atomicOr(err, 1);
       k = 0;
     }
-    if (counts) counts[i] = k;
+    counts[i] = k;
   }
   // wave-level sum before the one atomic per wave
   unsigned long long s = (unsigned long long)k;
@@ -237,18 +238,18 @@ __global__ void __launch_bounds__(128) perft_count_kernel(const az_chess_pos* __
 
 // perft: expand a level into the next (children at the exclusive-scan offsets)
 __global__ void __launch_bounds__(128) perft_expand_kernel(const az_chess_pos* __restrict__ pos, int n,
+                                                           const uint16_t* __restrict__ moves,
+                                                           const int32_t* __restrict__ counts,
                                                            const long long* __restrict__ offs,
                                                            az_chess_pos* __restrict__ next) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint16_t buf[AZ_CHESS_MAX_MOVES];
-  bool check;
-  Pos q = load_pos(pos[i]);
-  int k = legal_moves(q, buf, &check);
-  long long o = offs[i];
+  const Pos q = load_pos(pos[i]);
+  const int k = counts[i];
+  const long long o = offs[i];
   for (int j = 0; j < k; ++j) {
     Pos c = q;
-    push(c, buf[j]);
+    push(c, moves[(size_t)i * AZ_CHESS_MAX_MOVES + j]);
     store_pos(c, next[o + j]);
   }
 }
@@ -360,13 +361,15 @@ extern "C" int az_chess_perft(int device, const az_chess_pos* pos, int depth, ui
   AZC_HIP(dtot.alloc(1));
   AZC_HIP(derr.alloc(1));
   AZC_HIP(hipMemsetAsync(derr.p, 0, sizeof(int), c->stream));
-  const long long kMaxLevel = 1ll << 26;  // 5.4 GB of positions
+  const long long kMaxLevel = 1ll << 26;  // 5.4 GB of positions (+ 34 GB of move lists)
   for (int d = 1; d <= depth; ++d) {
     DBuf<int32_t> cnt;
+    DBuf<uint16_t> mv;
     AZC_HIP(cnt.alloc(n));
+    AZC_HIP(mv.alloc((size_t)n * AZ_CHESS_MAX_MOVES));
     AZC_HIP(hipMemsetAsync(dtot.p, 0, sizeof(unsigned long long), c->stream));
     int blocks = (int)((n + 127) / 128);
-    perft_count_kernel<<<blocks, 128, 0, c->stream>>>(level.p, (int)n, cnt.p, dtot.p, derr.p);
+    perft_count_kernel<<<blocks, 128, 0, c->stream>>>(level.p, (int)n, mv.p, cnt.p, dtot.p, derr.p);
     AZC_HIP(hipGetLastError());
     unsigned long long tot = 0;
     int err = 0;
@@ -393,7 +396,7 @@ extern "C" int az_chess_perft(int device, const az_chess_pos* pos, int depth, ui
     AZC_HIP(doff.alloc(n));
     AZC_HIP(next.alloc(run));
     AZC_HIP(hipMemcpy(doff.p, ho.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
-    perft_expand_kernel<<<blocks, 128, 0, c->stream>>>(level.p, (int)n, doff.p, next.p);
+    perft_expand_kernel<<<blocks, 128, 0, c->stream>>>(level.p, (int)n, mv.p, cnt.p, doff.p, next.p);
     AZC_HIP(hipGetLastError());
     AZC_HIP(hipStreamSynchronize(c->stream));
     std::swap(level.p, next.p);

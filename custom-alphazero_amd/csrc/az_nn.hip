@@ -128,14 +128,19 @@ __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict
   for (int r = blockIdx.x * PPB + threadIdx.x / G4; r < npix; r += gridDim.x * PPB) {
     const int b = r / HW, p = r - b * HW;
     const int y = p / W, xx = p - y * W;
+    // the board's words as scalars: indexing own[q >> 6] put the Board in
+    // scratch (40 B per lane, 51 us per launch at 1940 boards)
     const Board bd = boards[b];
+    const uint64_t own0 = bd.own[0], own1 = bd.own[1], opp0 = bd.opp[0], opp1 = bd.opp[1];
     float4 acc = b4;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ny = y + tap / 3 - 1, nx = xx + tap % 3 - 1;
       if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
       const int q = ny * W + nx;
-      const int st = bit(bd.own, q) ? 1 : (bit(bd.opp, q) ? 2 : 0);
+      const uint64_t ow = q < 64 ? own0 : own1, op = q < 64 ? opp0 : opp1;
+      const int sh = q & 63;
+      const int st = ((ow >> sh) & 1ull) ? 1 : (((op >> sh) & 1ull) ? 2 : 0);
       const float4 w1 = wsh[(tap * 4 + st) * G4 + cg];
       const float4 w3 = wsh[(tap * 4 + 3) * G4 + cg];
       acc.x = fmaf(1.0f, w1.x, acc.x);
