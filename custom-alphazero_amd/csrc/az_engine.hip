@@ -439,6 +439,13 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     if ((rc = fetch(m, std::string(ds.name) + ".bias", ds.out, b))) return rc;
     std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
     if ((rc = upload(owned, ds.w, a)) || (rc = upload(owned, ds.b, c))) return rc;
+    if (ds.w == &net.pd_w && A > kMaxActions) {
+      const int K = ds.in, tiles = (A + 63) / 64;
+      std::vector<float> t((size_t)tiles * K * 64, 0.f);
+      for (int k = 0; k < K; ++k)
+        for (int o = 0; o < A; ++o) t[((size_t)(o / 64) * K + k) * 64 + (o % 64)] = a[(size_t)k * A + o];
+      if ((rc = upload(owned, &net.pd_wt, t))) return rc;
+    }
   }
   net.ready = true;
   return 0;

@@ -28,6 +28,8 @@ struct NetDev {
   float *pc_w = nullptr, *pc_b = nullptr;  // policy conv [F][2], [2]
   float *vc_w = nullptr, *vc_b = nullptr;  // value conv [F], [1]
   float *pd_w = nullptr, *pd_b = nullptr;  // policy dense [2HW][A], [A]
+  float* pd_wt = nullptr;  // A > kMaxActions (chess): [ceil(A/64)][2HW][64], one contiguous slab per
+                           // policy_dense_kernel column tile, zero past A
   float *v1_w = nullptr, *v1_b = nullptr;  // value dense1 [HW][hidden], [hidden]
   float *v2_w = nullptr, *v2_b = nullptr;  // value dense2 [hidden], [1]
   bool ready = false;

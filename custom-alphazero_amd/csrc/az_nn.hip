@@ -501,16 +501,27 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
                                                            const float* __restrict__ bpd,
                                                            const int* __restrict__ count, int n_static,
                                                            int HW, int A, float* __restrict__ logits) {
-  __shared__ float ws[K][64];
-  __shared__ float ps[32][K];
+  __shared__ __attribute__((aligned(16))) float ws[K][64];
+  __shared__ __attribute__((aligned(16))) float ps[32][K];
   const int n = count ? *count : n_static;
   const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 32;
   if (b0 >= n) return;  // block-uniform
   const int t = threadIdx.x;
-  for (int idx = t; idx < K * 64; idx += 256) {
-    const int i = idx >> 6, a = idx & 63;
-    ws[i][a] = a0 + a < A ? wpd[(size_t)i * A + a0 + a] : 0.f;
+  // the tile's weight slab is contiguous (NetDev::pd_wt): 8 float4 loads per
+  // thread, all in flight together (scalar loads from the [K][A] matrix, each
+  // awaited before its LDS store, took 13 of the kernel's 17.7 us)
+  {
+    const float4* src = reinterpret_cast<const float4*>(wpd) + (size_t)blockIdx.x * K * 16;
+    float4 v[K * 16 / 256];
+#pragma unroll
+    for (int k = 0; k < K * 16 / 256; ++k) v[k] = src[t + 256 * k];
+#pragma unroll
+    for (int k = 0; k < K * 16 / 256; ++k) {
+      const int idx = t + 256 * k;
+      *reinterpret_cast<float4*>(&ws[idx >> 4][(idx & 15) * 4]) = v[k];
+    }
   }
+#pragma unroll 8
   for (int idx = t; idx < 32 * HW; idx += 256) {
     const int b = idx / HW, p = idx - b * HW;
     const float4 f = b0 + b < n ? feat[(size_t)(b0 + b) * HW + p] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -524,10 +535,18 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = bias;
-  for (int i = 0; i < 2 * HW; ++i) {
-    const float w = ws[i][a];
+  // the 8 boards' features as float4 over i (wave-uniform rows: LDS
+  // broadcasts), 12 LDS reads per 32 FMAs instead of 36; same FMA order
+  for (int i = 0; i < 2 * HW; i += 4) {
+    const float w0 = ws[i][a], w1 = ws[i + 1][a], w2 = ws[i + 2][a], w3 = ws[i + 3][a];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = fmaf(ps[bg + j][i], w, acc[j]);
+    for (int j = 0; j < 8; ++j) {
+      const float4 f = *reinterpret_cast<const float4*>(&ps[bg + j][i]);
+      acc[j] = fmaf(f.x, w0, acc[j]);
+      acc[j] = fmaf(f.y, w1, acc[j]);
+      acc[j] = fmaf(f.z, w2, acc[j]);
+      acc[j] = fmaf(f.w, w3, acc[j]);
+    }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j)
@@ -535,40 +554,71 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
 }
 
 // softmax over the logits in place + the value head (Dense(hidden) ReLU ->
-// Dense(1) tanh), one wave per board, heads_kernel's arithmetic; the value
-// layer's weights [HW][hidden] are staged in LDS once per workgroup.
-__global__ __launch_bounds__(256) void heads_tail_kernel(const float4* __restrict__ feat, HeadWeights hw,
-                                                         const int* __restrict__ count, int n_static, int HW,
-                                                         int A, int hidden, float* __restrict__ probs,
-                                                         float* __restrict__ values) {
-  __shared__ float vflat[4][kMaxCells];
-  extern __shared__ float wv1[];
-  const int n = count ? *count : n_static;
-  if ((int)blockIdx.x * 4 >= n) return;  // block-uniform
-  for (int i = threadIdx.x; i < HW * hidden; i += 256) wv1[i] = hw.wv1[i];
-  __syncthreads();
+// Dense(1) tanh), one board per 256-thread workgroup: a thread holds 8 of
+// the board's logits in registers (one read, one exp, one write per logit)
+// and owns hidden unit j of the value layer, whose weights it reads straight
+// from L2 (each p a coalesced 1 KB row across the workgroup).  Block
+// reductions: wave shuffles, then the 4 waves' partials through LDS.
+// (4 boards per workgroup with the value weights staged in LDS: 29.6 us per
+// launch at 256 boards -- 64 workgroups, 64 KB staged by each.)
+constexpr int kTailThreads = 256, kTailPer = 8;  // A <= 2048
+
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int b = blockIdx.x * 4 + wave; b < n; b += gridDim.x * 4) {  // wave-uniform
-    for (int p = lane; p < HW; p += 64) vflat[wave][p] = feat[(size_t)b * HW + p].z;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __syncthreads();  // red is reused by consecutive reductions
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int w = 1; w < kTailThreads / 64; ++w) r = is_max ? fmaxf(r, red[w]) : r + red[w];
+  return r;
+}
+
+__global__ __launch_bounds__(kTailThreads) void heads_tail_kernel(const float4* __restrict__ feat, HeadWeights hw,
+                                                                  const int* __restrict__ count, int n_static,
+                                                                  int HW, int A, int hidden,
+                                                                  float* __restrict__ probs,
+                                                                  float* __restrict__ values) {
+  __shared__ float vflat[kMaxCells];
+  __shared__ float red[kTailThreads / 64];
+  const int n = count ? *count : n_static;
+  const int t = threadIdx.x;
+  for (int b = blockIdx.x; b < n; b += gridDim.x) {  // block-uniform
+    __syncthreads();  // vflat of the previous board is no longer read
+    for (int p = t; p < HW; p += kTailThreads) vflat[p] = feat[(size_t)b * HW + p].z;
     float* row = probs + (size_t)b * A;
+    float x[kTailPer];
     float m = -INFINITY;
-    for (int a = lane; a < A; a += 64) m = fmaxf(m, row[a]);
-    m = wave_max(m);
-    float z = 0.f;
-    for (int a = lane; a < A; a += 64) z += expf(row[a] - m);
-    z = wave_sum(z);
-    for (int a = lane; a < A; a += 64) row[a] = expf(row[a] - m) / z;
-    float part = 0.f;
-    for (int j = lane; j < hidden; j += 64) {
-      float s = hw.bv1[j];
-      for (int p = 0; p < HW; ++p) s += vflat[wave][p] * wv1[p * hidden + j];
-      part += fmaxf(s, 0.f) * hw.wv2[j];
+#pragma unroll
+    for (int k = 0; k < kTailPer; ++k) {
+      const int a = t + k * kTailThreads;
+      x[k] = a < A ? row[a] : -INFINITY;
+      m = fmaxf(m, x[k]);
     }
-    part = wave_sum(part);
-    if (lane == 0) values[b] = tanhf(part + hw.bv2[0]);
-    __builtin_amdgcn_wave_barrier();
+    m = block_reduce(m, red, true);
+    float z = 0.f;
+#pragma unroll
+    for (int k = 0; k < kTailPer; ++k) {
+      const int a = t + k * kTailThreads;
+      x[k] = a < A ? expf(x[k] - m) : 0.f;
+      z += x[k];
+    }
+    z = block_reduce(z, red, false);  // its barriers also publish vflat
+#pragma unroll
+    for (int k = 0; k < kTailPer; ++k) {
+      const int a = t + k * kTailThreads;
+      if (a < A) row[a] = x[k] / z;
+    }
+    float part = 0.f;
+    for (int j = t; j < hidden; j += kTailThreads) {
+      float sv = hw.bv1[j];
+#pragma unroll 16
+      for (int p = 0; p < HW; ++p) sv += vflat[p] * hw.wv1[p * hidden + j];
+      part += fmaxf(sv, 0.f) * hw.wv2[j];
+    }
+    part = block_reduce(part, red, false);
+    if (t == 0) values[b] = tanhf(part + hw.bv2[0]);
   }
 }
 
@@ -678,14 +728,12 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   heads_kernel<F, FEAT_, STAGE_, kMaxActions><<<hblocks, 256, STAGE_ ? wbytes : 0, s>>>(           \
       cur, hw, count, n_max, HW, A, net.hidden, probs, values)
   if (A > kMaxActions) {  // chess: 1880 actions
-    if (fused_heads && HW == 64) {
+    if (fused_heads && HW == 64 && A <= kTailThreads * kTailPer && net.pd_wt) {
       const float4* feat = reinterpret_cast<const float4*>(cur);
       policy_dense_kernel<128><<<dim3((A + 63) / 64, (n_max + 31) / 32), 256, 0, s>>>(
-          feat, net.pd_w, net.pd_b, count, n_max, HW, A, probs);
-      // (one board per 64-thread block with the weights read through L2 measured
-      // slower: 561k vs 626k chess expansions/s)
-      heads_tail_kernel<<<std::min((n_max + 3) / 4, 256), 256, (size_t)HW * net.hidden * sizeof(float), s>>>(
-          feat, hw, count, n_max, HW, A, net.hidden, probs, values);
+          feat, net.pd_wt, net.pd_b, count, n_max, HW, A, probs);
+      heads_tail_kernel<<<std::min(n_max, 2048), kTailThreads, 0, s>>>(feat, hw, count, n_max, HW, A,
+                                                                       net.hidden, probs, values);
     } else
       heads_kernel<F, false, false, 2048><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A,
                                                                           net.hidden, probs, values);
