@@ -107,6 +107,41 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
 // Blocks loop over pixels (8 per pass: lane group = 32 channel quads) with
 // the 18 KB of stem weights staged once per block in LDS (read per pixel
 // through L1 the kernel was L1-bandwidth bound).
+// Copy n floats from global memory into LDS with the whole workgroup (256
+// threads), 8 loads per thread in flight per batch (float4 when both sides
+// are 16-byte aligned).  A rolled one-float-per-iteration loop waits for each
+// load before its LDS store: the Connect-4 heads kernel staged its 45 KB of
+// dense weights in 45 serialized L2 round trips.
+__device__ __forceinline__ void stage_lds(float* dst, const float* __restrict__ src, int n) {
+  const int t = threadIdx.x;
+  if ((n & 3) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const int n4 = n >> 2;
+    for (int base = 0; base < n4; base += 8 * 256) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = s4[min(base + t + k * 256, n4 - 1)];  // clamped: no guard
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = base + t + k * 256;
+        if (j < n4) d4[j] = v[k];
+      }
+    }
+  } else {
+    for (int base = 0; base < n; base += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = src[min(base + t + k * 256, n - 1)];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = base + t + k * 256;
+        if (j < n) dst[j] = v[k];
+      }
+    }
+  }
+}
+
 template <int F>
 __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict__ boards,
                                                          const float* __restrict__ ws,
@@ -121,7 +156,7 @@ __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict
   const int HW = H * W;
   const int npix = n * HW;
   if ((int)blockIdx.x * PPB >= npix) return;  // block-uniform
-  for (int i = threadIdx.x; i < 36 * G4; i += 256) wsh[i] = reinterpret_cast<const float4*>(ws)[i];
+  stage_lds(reinterpret_cast<float*>(wsh), ws, 36 * G4 * 4);
   __syncthreads();
   const int cg = threadIdx.x % G4;
   const float4 b4 = reinterpret_cast<const float4*>(bias)[cg];
@@ -420,8 +455,8 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
   if constexpr (STAGE) {
     if ((int)blockIdx.x * 4 >= n) return;  // block-uniform
     const int npd = 2 * HW * A, nv1 = HW * hidden;
-    for (int i = threadIdx.x; i < npd; i += 256) wsm[i] = hw.wpd[i];
-    for (int i = threadIdx.x; i < nv1; i += 256) wsm[npd + i] = hw.wv1[i];
+    stage_lds(wsm, hw.wpd, npd);
+    stage_lds(wsm + npd, hw.wv1, nv1);
     __syncthreads();
     wpd = wsm;
     wv1 = wsm + npd;
@@ -521,10 +556,12 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
       *reinterpret_cast<float4*>(&ws[idx >> 4][(idx & 15) * 4]) = v[k];
     }
   }
-#pragma unroll 8
-  for (int idx = t; idx < 32 * HW; idx += 256) {
-    const int b = idx / HW, p = idx - b * HW;
-    const float4 f = b0 + b < n ? feat[(size_t)(b0 + b) * HW + p] : make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int HWK = K / 2;  // the launcher passes K = 2 * HW
+#pragma unroll
+  for (int k = 0; k < 32 * HWK / 256; ++k) {
+    const int idx = t + 256 * k;
+    const int b = idx / HWK, p = idx - b * HWK;
+    const float4 f = feat[(size_t)min(b0 + b, n - 1) * HWK + p];  // clamped (rows past n unused)
     ps[b][2 * p] = f.x;
     ps[b][2 * p + 1] = f.y;
   }
