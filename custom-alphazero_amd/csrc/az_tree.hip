@@ -228,18 +228,35 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
   Board b = t.root_board[s];
   int first = t.root_first[s], cnt = t.root_n[s];
   int depth = 0, status = kOngoing;
+  // below the root, the children's visits sum to the parent edge's N - 1 (the
+  // first visit expanded the node), so sqrt(sum) is fetched before the
+  // children's edges arrive instead of after them: one dependent load per
+  // level instead of two
+  int sum_next = -1;
   while (cnt > 0) {
     const bool mine = j < cnt;
+    double sq;
+    int sum;
+    if (sum_next >= 0) {
+      sum = sum_next;
+      if (sum >= g.pow_len) {
+        if (j == 0) flag_error(t, kErrPow);
+        return;
+      }
+      sq = t.powtab[sum];
+    }
     Edge e;
     if (mine) e = E[first + j];
-    int sum = mine ? e.N : 0;
+    if (sum_next < 0) {
+      sum = mine ? e.N : 0;
 #pragma unroll
-    for (int off = L / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off, L);
-    if (sum >= g.pow_len) {
-      if (j == 0) flag_error(t, kErrPow);
-      return;
+      for (int off = L / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off, L);
+      if (sum >= g.pow_len) {
+        if (j == 0) flag_error(t, kErrPow);
+        return;
+      }
+      sq = t.powtab[sum];
     }
-    const double sq = t.powtab[sum];
     double best_v = -INFINITY;
     int best = L;
     if (mine) {
@@ -264,6 +281,7 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
     const int action = __shfl(mine ? (int)e.action : 0, best, L);
     const int child = __shfl(mine ? e.child : 0, best, L);
     const int child_n = __shfl(mine ? (int)e.child_n : 0, best, L);
+    sum_next = __shfl(mine ? e.N : 0, best, L) - 1;
     if (j == 0) path[depth] = first + best;
     ++depth;
     status = play(g, b, action);
