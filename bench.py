@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.join(REPO, "custom-alphazero_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
-HBM_PEAK_GBS = 8000.0
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
 def parse():
@@ -308,7 +308,8 @@ def main():
                     evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index,
                     cache_log2=args.cache_log2, lanes=args.lanes, conv_algo=args.conv_algo)
     eng.set_weights(named)
-    budget = args.slots * (2 + (args.warmup + 2 * args.steps) // 5)
+    tree_steps = 3
+    budget = args.slots * (2 + (args.warmup + 2 * args.steps + tree_steps) // 5)
     eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)
 
     eng.selfplay_step(args.warmup)
@@ -325,6 +326,33 @@ def main():
     elapsed = time.perf_counter() - t0
     st1 = eng.stats()
     eng.timer(False)
+
+    # tree kernels (select + expand: latency/HBM-bound) timed with HIP events
+    # in a short window of their own (4 more events per simulation), priced
+    # with SURVEY.md 8d's algorithmic bytes per simulation
+    eng.timer(True, tree=True)
+    sa = eng.stats()
+    eng.selfplay_step(tree_steps)
+    sb = eng.stats()
+    eng.timer(False)
+    sims_t = max(sb["simulations"] - sa["simulations"], 1)
+    depth = (sb["path_edges"] - sa["path_edges"]) / sims_t
+    f_exp = (sb["expansions"] - sa["expansions"]) / sims_t
+    A = args.width
+    bytes_per_sim = 16 * A * depth + 24 * depth + f_exp * (16 * A + 672 + 672 + 64)
+    tree_gbs = bytes_per_sim * sims_t / (sb["tree_ms"] * 1e-3) / 1e9 if sb["tree_ms"] else 0.0
+    roofline_tree = {
+        "kernels": "select_group_kernel + expand_kernel (PUCT descent, backup, prior normalisation)",
+        "bound": "hbm", "achieved": round(tree_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(tree_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+        "bytes_per_simulation": round(bytes_per_sim, 1), "mean_depth": round(depth, 3),
+        "expand_fraction": round(f_exp, 4),
+        "avg_launch_ms": round(sb["tree_ms"] / max(sb["tree_launches"], 1), 4),
+        "simulations_per_launch": round(sims_t / max(sb["tree_launches"] / 2, 1), 1),
+        "basis": "16*A*d + 24*d + f_exp*(16*A + 672 + 672 + 64) bytes per simulation (SURVEY.md 8d) x "
+                 "simulations / summed select+expand event time; latency-bound (dependent loads down "
+                 "each path), not bandwidth-bound",
+    }
 
     # second window, same slots continuing, cache bypassed: the rate without
     # the reference's plays_inferences semantics (every leaf evaluated)
@@ -456,6 +484,7 @@ def main():
                                                   "weights change; bit-identical results"}
                                     if args.cache_log2 else None),
             "cache_off": off,
+            "roofline_tree": roofline_tree,
             "roofline": {
                 "kernel": ("wino16_conv_kernel (Winograd F(2x2,3x3) on fp32 MFMA 16x16x4, 16 tiles per "
                            "workgroup, fused BN/ReLU and 1x1 projection residual)" if args.conv_algo == 0 else

@@ -59,6 +59,7 @@ struct Lane {
   float* probs = nullptr;
   float* values = nullptr;
   az::ConvTimer timer;
+  az::ConvTimer tree_timer;  // select and expand launches (bench.py roofline_tree)
 };
 
 struct az_engine {
@@ -135,7 +136,9 @@ int simulate(az_engine* e, Lane& L) {
   // eval_count, miss_count, nn_count, dup_count are one contiguous block
   AZ_HIP(hipMemsetAsync(L.t.eval_count, 0, 4 * sizeof(int32_t), s));
   L.t.epoch += 1;  // fresh per-simulation dedup table (tags of older epochs read as empty)
+  if (L.tree_timer.enabled) L.tree_timer.begin(s);
   az::launch_select(L.g, L.t, e->cache, s);
+  if (L.tree_timer.enabled) L.tree_timer.end(s, 1);
   const az::Board* rows = L.t.eval_board;
   const int32_t* n_rows = L.t.eval_count;
   if (e->cache.enabled) {
@@ -155,7 +158,9 @@ int simulate(az_engine* e, Lane& L) {
   } else {
     az::launch_synth_eval(L.g, rows, n_rows, L.probs, L.values, s);
   }
+  if (L.tree_timer.enabled) L.tree_timer.begin(s);
   az::launch_expand(L.g, L.t, e->cache, L.probs, L.values, s);
+  if (L.tree_timer.enabled) L.tree_timer.end(s, 1);
   if (e->cache.enabled) az::launch_cache_insert(L.g, L.t, e->cache, L.probs, L.values, s);
   AZ_HIP(hipGetLastError());
   return 0;
@@ -722,6 +727,15 @@ int az_stats_get(az_engine* e, az_stats* st) {
   }
   if (hi > lo) busy += hi - lo;
   st->conv_busy_ms = busy;
+  std::vector<az::ConvTimer*> ttimers = {&e->whole.tree_timer};
+  for (Lane* L : e->lanes)
+    if (L != &e->whole) ttimers.push_back(&L->tree_timer);
+  for (az::ConvTimer* tm : ttimers) {
+    tm->flush();
+    st->tree_ms += tm->total_ms;
+    st->tree_launches += tm->launches;
+  }
+  st->path_edges = (int64_t)h[az::kStatPathEdges];
   st->cache_hits = (int64_t)h[az::kStatCacheHits];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
   return 0;
@@ -749,14 +763,25 @@ int az_timer_enable(az_engine* e, int on) {
   if (!e->timer_ref) AZ_HIP(hipEventCreate(&e->timer_ref));
   AZ_HIP(hipEventRecord(e->timer_ref, e->stream));
   AZ_HIP(hipStreamSynchronize(e->stream));
-  std::vector<az::ConvTimer*> timers = {&e->timer, &e->whole.timer};
+  // on: 1 = conv launches, 2 = conv + select/expand launches (more events per
+  // simulation: bench.py times the tree kernels in a window of their own)
+  std::vector<az::ConvTimer*> timers = {&e->timer, &e->whole.timer}, ttimers = {&e->whole.tree_timer};
   for (Lane* L : e->lanes)
-    if (L != &e->whole) timers.push_back(&L->timer);
+    if (L != &e->whole) {
+      timers.push_back(&L->timer);
+      ttimers.push_back(&L->tree_timer);
+    }
   for (az::ConvTimer* tm : timers) {
     tm->flush();
     tm->reset();
     tm->ref = &e->timer_ref;
     tm->enabled = on != 0;
+  }
+  for (az::ConvTimer* tm : ttimers) {
+    tm->flush();
+    tm->reset();
+    tm->ref = &e->timer_ref;
+    tm->enabled = on >= 2;
   }
   return 0;
 }

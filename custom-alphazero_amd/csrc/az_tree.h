@@ -31,6 +31,7 @@ enum : int {
   kStatCacheHits = 7,    // expansions served by the transposition cache
   kStatNNEvals = 8,      // boards the evaluator actually computed
   kStatCacheInserts = 9,
+  kStatPathEdges = 10,   // edges on the selected paths (sum of select depths)
   kStatCount = 12
 };
 enum : unsigned long long {

@@ -103,6 +103,7 @@ __device__ __forceinline__ bool same_board(const Board& a, const Board& b) {
 __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c, int s, Edge* E,
                           const int32_t* path, int depth, int status, const Board& b) {
   stat_add(t, kStatSims, 1);
+  if (depth) stat_add(t, kStatPathEdges, (unsigned long long)depth);
   if (depth > 0 && status != kOngoing) {
     // get_result(keep_same_player=True): 1 for the player who just moved, 0 draw
     backup(E, path, depth, status == kWin ? 1.0 : 0.0);

@@ -59,7 +59,8 @@ class Stats(ctypes.Structure):
         ("plies", ctypes.c_int64), ("active_slots", ctypes.c_int64), ("errors", ctypes.c_int64),
         ("conv_launches", ctypes.c_int64), ("conv_ms", ctypes.c_double),
         ("cache_hits", ctypes.c_int64), ("evaluations", ctypes.c_int64),
-        ("conv_busy_ms", ctypes.c_double), ("reserved", ctypes.c_int64 * 4),
+        ("conv_busy_ms", ctypes.c_double), ("tree_launches", ctypes.c_int64), ("tree_ms", ctypes.c_double),
+        ("path_edges", ctypes.c_int64), ("reserved", ctypes.c_int64 * 1),
     ]
 
     def as_dict(self):
@@ -334,8 +335,8 @@ class Engine:
     def cache_enable(self, on=True):
         _check(self._L.az_cache_enable(self._h, int(bool(on))))
 
-    def timer(self, on):
-        _check(self._L.az_timer_enable(self._h, int(bool(on))))
+    def timer(self, on, tree=False):
+        _check(self._L.az_timer_enable(self._h, (2 if tree else 1) if on else 0))
 
     def pow_table(self, n):
         out = np.zeros(int(n), np.float64)

@@ -89,7 +89,10 @@ typedef struct az_stats {
     int64_t evaluations;      /* boards the evaluator computed (network or synthetic) */
     double conv_busy_ms;      /* union of the timed conv intervals over all lanes (device
                                  time in which at least one lane's conv kernels ran) */
-    int64_t reserved[4];
+    int64_t tree_launches;    /* timed select + expand kernels (az_timer_enable) */
+    double tree_ms;           /* their summed device time */
+    int64_t path_edges;       /* edges on the selected paths (sum of select depths) */
+    int64_t reserved[1];
 } az_stats;
 
 int az_abi_version(void);
@@ -155,6 +158,8 @@ int az_stats_get(az_engine* eng, az_stats* st);
 int az_cache_clear(az_engine* eng);
 /* Bypass (0) or use (1) an allocated cache; results are identical either way. */
 int az_cache_enable(az_engine* eng, int on);
+/* HIP-event timing for bench.py: on = 1 the conv launches, 2 also the
+ * select and expand launches (az_stats conv_* / tree_*), 0 off. */
 int az_timer_enable(az_engine* eng, int on);
 /* The host-built libm pow(k, 0.5) table the kernels use (tests). */
 int az_pow_table(az_engine* eng, double* out, int64_t n);
