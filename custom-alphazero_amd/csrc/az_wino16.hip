@@ -61,7 +61,13 @@ __device__ __forceinline__ int w16_swz(int j, int t) {
 // every group then reads 16 distinct bank slots (identity: 2-way conflicts).
 __device__ __forceinline__ int w16_tile(int m) { return m < 4 ? m : (m < 12 ? m + 4 : m - 8); }
 
-template <bool RESIDUAL, bool HEADS>
+// NS = 2 splits the 128 output channels over two workgroups (blockIdx.y):
+// wave w of half h owns the 16 channels 64h + 16w .. +15 (one N block), so a
+// launch has twice the workgroups and each wave half the MFMA chain, at the
+// cost of both halves building the same V.  For launches too small to fill
+// the CUs (a chess step's 256 boards = 256 workgroups); the same reduction
+// order per output, so both splits give identical results.
+template <bool RESIDUAL, bool HEADS, int NS>
 __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
@@ -73,7 +79,9 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
   constexpr int VB = NX * kW16Tiles * RC;    // float4 in the V buffer
   constexpr int NCH = 128 / CK;
   constexpr int KS = CK / 4;                 // k-steps per stage (lane quarter: 8 channels)
-  constexpr int QB = 4;                      // float4 of B per lane per stage (2 N blocks x 8)
+  static_assert(NS == 1 || (NS == 2 && !HEADS), "the fused heads need all 128 channels");
+  constexpr int NBW = 2 / NS;                // N blocks (16 channels) per wave
+  constexpr int QB = 2 * NBW;                // float4 of B per lane per stage (NBW N blocks x 8)
   constexpr int IPT = 2 * kW16Tiles * RC / kW16Threads;  // producer items per thread (1)
   static_assert(IPT == 1, "one producer item per thread");
   __shared__ float4 vbuf[VB];
@@ -171,17 +179,23 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
 
   // ---- consumer geometry: lane -> tile row r, k quarter g
   const int r = lane & 15, g = lane >> 4;
-  f32x4 Y[4][2];
+  f32x4 Y[4][NBW];
 #pragma unroll
   for (int p = 0; p < 4; ++p)
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) Y[p][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = 0; nb < NBW; ++nb) Y[p][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const unsigned blane = (unsigned)(wave * 64 * QB + lane);
+  // the packed U keeps the 2-block-per-wave order (wino16_pack_index): a
+  // split wave reads its N block's two float4 (q = 2 nb + s/4) from the
+  // owning unsplit wave's fragment
+  const int wsrc = NS == 1 ? wave : 2 * blockIdx.y + (wave >> 1);
+  const int qoff = NS == 1 ? 0 : 2 * (wave & 1);
+  const unsigned blane = (unsigned)((wsrc * 4 + qoff) * 64 + lane);
+  const int colbase = NS == 1 ? 32 * wave : 64 * blockIdx.y + 16 * wave;
   auto load_b = [&](int c, int xi, float4 (&dst)[QB]) {
     const bool res = RESIDUAL && xi >= 16;
     const float4* base = res ? rpack : upack;
-    const unsigned o = blane + (unsigned)(res ? c * 4 * 64 * QB : (c * 16 + xi) * 4 * 64 * QB);
+    const unsigned o = blane + (unsigned)(res ? c * 4 * 64 * 4 : (c * 16 + xi) * 4 * 64 * 4);
 #pragma unroll
     for (int q = 0; q < QB; ++q) dst[q] = base[o + q * 64];
   };
@@ -191,7 +205,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
 #pragma unroll
     for (int q = 0; q < 2; ++q) dst[q] = vrow[w16_swz<CK>(2 * g + q, rt)];
   };
-  auto scatter = [&](int xi, const f32x4 (&m)[2]) {
+  auto scatter = [&](int xi, const f32x4 (&m)[NBW]) {
     const int a = xi >> 2, bb = xi & 3;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -202,7 +216,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
         const int sj = w16_sign(bb, j);
         if (sj == 0) continue;
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
+        for (int nb = 0; nb < NBW; ++nb) {
           if (si * sj > 0) Y[2 * i + j][nb] += m[nb];
           else Y[2 * i + j][nb] -= m[nb];
         }
@@ -212,7 +226,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
   constexpr int PF = AZ_W16_PF;
   constexpr int NB = PF == 1 ? 2 : 4;  // B register buffers (>= PF + 1, divides NX)
   float4 bq[NB][QB], aq[2][2];
-  f32x4 M[2][2];
+  f32x4 M[2][NBW];
   // stage k of the flat (chunk, point) sequence -> its B fragments
   auto load_b_flat = [&](int k, float4 (&dst)[QB]) {
     if (k < NCH * NX) load_b(k / NX, k % NX, dst);
@@ -235,7 +249,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
       load_b_flat(c * NX + xi + PF, bq[(xi + PF) % NB]);
       if (xi + 1 < NX) load_a(xi + 1, aq[(xi + 1) & 1]);
       if (AZ_W16_EARLY && xi == 0 && c + 1 < NCH) produce_load(c + 1);
-      float av[KS], bv[2][KS];
+      float av[KS], bv[NBW][KS];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const float4 a4 = aq[xi & 1][q];
@@ -252,23 +266,26 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
 #pragma unroll
         for (int s = 0; s < KS; ++s)
 #pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
+          for (int nb = 0; nb < NBW; ++nb)
             Y[p][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[nb][s], Y[p][nb], 0, 0, 0);
       } else {
-        f32x4(&m)[2] = M[xi & 1];
+        f32x4(&m)[NBW] = M[xi & 1];
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < NBW; ++nb)
           m[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[nb][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
         for (int s = 1; s < KS; ++s)
 #pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
+          for (int nb = 0; nb < NBW; ++nb)
             m[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[nb][s], m[nb], 0, 0, 0);
       }
       if (xi >= 1 && xi - 1 < 16) {
         scatter(xi - 1, M[(xi - 1) & 1]);
-        asm volatile("" ::"v"(Y[0][0]), "v"(Y[0][1]), "v"(Y[1][0]), "v"(Y[1][1]), "v"(Y[2][0]), "v"(Y[2][1]),
-                     "v"(Y[3][0]), "v"(Y[3][1]));
+        if constexpr (NBW == 2)
+          asm volatile("" ::"v"(Y[0][0]), "v"(Y[0][1]), "v"(Y[1][0]), "v"(Y[1][1]), "v"(Y[2][0]), "v"(Y[2][1]),
+                       "v"(Y[3][0]), "v"(Y[3][1]));
+        else
+          asm volatile("" ::"v"(Y[0][0]), "v"(Y[1][0]), "v"(Y[2][0]), "v"(Y[3][0]));
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -321,8 +338,8 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     return;
   }
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
-    const int col = wave * 32 + nb * 16 + r;
+  for (int nb = 0; nb < NBW; ++nb) {
+    const int col = colbase + nb * 16 + r;
     const float bcol = bias[col];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -357,17 +374,33 @@ void launch_wino16_conv(const float* in, const float* res_in, const float* upack
   if (grid <= 0) return;
   const float4* u = reinterpret_cast<const float4*>(upack);
   const float4* rp = reinterpret_cast<const float4*>(rpack);
+  // split the output channels over two workgroups when a launch has fewer
+  // workgroups than AZ_W16_SPLIT_BELOW (default 640: C4 at ~700 boards +5%,
+  // chess at 256 +3%, C4 at 1000 boards -5% if split; profiles/ab_split.sh); 0 = never
+  static const int split_below = [] {
+    const char* v = getenv("AZ_W16_SPLIT_BELOW");
+    return v ? atoi(v) : 640;
+  }();
+  const bool split = grid < split_below;
   HeadConv hc{};
   if (heads && heads->feat) {
     hc = *heads;
-    wino16_conv_kernel<true, true><<<grid, kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max, H,
-                                                                W, hc);
+    wino16_conv_kernel<true, true, 1><<<grid, kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max,
+                                                                   H, W, hc);
   } else if (res_in) {
-    wino16_conv_kernel<true, false><<<grid, kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max,
-                                                                 H, W, hc);
+    if (split)
+      wino16_conv_kernel<true, false, 2><<<dim3(grid, 2), kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out,
+                                                                              count, n_max, H, W, hc);
+    else
+      wino16_conv_kernel<true, false, 1><<<grid, kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out, count,
+                                                                      n_max, H, W, hc);
   } else {
-    wino16_conv_kernel<false, false><<<grid, kW16Threads, 0, s>>>(in, nullptr, u, nullptr, bias, out, count,
-                                                                  n_max, H, W, hc);
+    if (split)
+      wino16_conv_kernel<false, false, 2><<<dim3(grid, 2), kW16Threads, 0, s>>>(in, nullptr, u, nullptr, bias,
+                                                                               out, count, n_max, H, W, hc);
+    else
+      wino16_conv_kernel<false, false, 1><<<grid, kW16Threads, 0, s>>>(in, nullptr, u, nullptr, bias, out,
+                                                                       count, n_max, H, W, hc);
   }
 }
 
