@@ -269,6 +269,9 @@ __global__ void tree_release_kernel(CTree t, int n, const int32_t* slots) {
 // MCTS.select (mcts.py:111-120): one wave per slot
 __global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
   const int s = blockIdx.x, lane = threadIdx.x;
+  // the eval queue is filled by leaf_kernel, after this launch (a memset
+  // launch per simulation cost 5 us)
+  if (s == 0 && lane == 0) *t.eval_count = 0;
   if (t.game_id[s] < 0) return;
   const Edge* E = arena(g, t, s, t.half[s]);
   int32_t* path = t.path + (size_t)s * g.max_depth;
@@ -754,7 +757,6 @@ int simulate(az_chess_engine* e, CLane& L) {
   hipStream_t s = L.stream;
   const int S = L.g.slots;
   select_kernel<<<S, 64, 0, s>>>(L.g, L.t);
-  AZC_HIP(hipMemsetAsync(L.t.eval_count, 0, sizeof(int32_t), s));
   leaf_kernel<<<(S + AZ_LEAF_SPW - 1) / AZ_LEAF_SPW, 64, 0, s>>>(L.g, L.t);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
     encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, reinterpret_cast<float4*>(L.x));
