@@ -213,3 +213,47 @@ def test_chess_mcts_api_matches_oracle():
     x = fresh.board.full_state
     ref = C.full_state(*C.reference_history(board._pos, True), board._pos)
     np.testing.assert_array_equal(x, ref)
+
+
+def test_chess_mcts_api_with_model_matches_oracle():
+    """mcts.MCTS on a chess Board with a chess PolicyValueModel (input
+    (8, 8, 118), 1880 actions): the oracle's MCTS object, fed the model's own
+    outputs on the reference's full_state, gives the same root edges and
+    moves (a non-start root: history [0 x 7, start state])."""
+    from custom_alphazero.chess.board import Board
+    from custom_alphazero.chess.utils import get_all_possible_moves
+    from custom_alphazero.config import ConfigSelfPlay
+    from custom_alphazero.mcts.mcts import MCTS
+    from custom_alphazero.model.policy_value import PolicyValueModel
+    model = PolicyValueModel(input_dim=(8, 8, 118), action_space=1880, seed=4)
+    moves = get_all_possible_moves()
+    board = Board(board_fen=ROOTS[1].split()[0])
+    saved = ConfigSelfPlay.mcts_iterations
+    try:
+        ConfigSelfPlay.mcts_iterations = 20
+        m = MCTS(board=board, all_possible_moves=moves, concurrency=False, plays_inferences={}, model=model)
+    finally:
+        ConfigSelfPlay.mcts_iterations = saved
+
+    def cb(pos, initial):
+        x = C.full_state(*C.reference_history(pos, bool(initial)), pos)[None].astype(np.float32)
+        p, v = model(x)
+        return p.numpy()[0], float(v.numpy()[0, 0])
+
+    tr = C.Tree(board._pos, callback=cb)
+    np.random.seed(7)
+    rng = np.random.RandomState(7)
+    for step in range(3):
+        m.search(20)
+        tr.search(20)
+        want = tr.root()
+        root = m.current_root
+        assert [e.action.code for e in root.edges] == want["moves"].tolist()
+        assert [e.visit_count for e in root.edges] == want["n"].tolist()
+        assert np.array_equal(np.array([e.prior for e in root.edges]).view(np.uint64),
+                              want["prior"].view(np.uint64))
+        _, _, policy, move = m.play(return_details=True)
+        mv, oc, pa, pp = tr.play(rng.random_sample())
+        assert move.code == mv
+        if oc:
+            break
