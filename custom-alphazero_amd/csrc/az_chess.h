@@ -405,6 +405,152 @@ AZC_HD int legal_moves(const Pos& q, uint16_t* out, bool* check) {
   return n;
 }
 
+// ---- wave-parallel generation: the 64 lanes of one wave (all active and
+// converged) produce legal_moves' list in the same order, lane L owning
+// square 63 - L (python-chess walks squares from the highest): per-lane
+// counts, an exclusive prefix across the wave, then each lane writes its
+// moves at its offset.  Candidates go to LDS (`cand`), the _is_safe filter
+// runs one candidate per lane and compacts in order with a ballot.
+AZC_HD int wave_offset(int v, int lane, int* total) {
+  int incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  *total = __shfl(incl, 63, 64);
+  return incl - v;
+}
+AZC_HD void wave_put(uint16_t* out, int k, int from, int to, int promo) {
+  if (k < AZ_CHESS_MAX_MOVES) out[k] = (uint16_t)(from | (to << 6) | (promo << 12));
+}
+AZC_HD int wave_put_pawn(uint16_t* out, int k, int from, int to) {
+  const int r = to >> 3;
+  if (r == 0 || r == 7) {
+    wave_put(out, k, from, to, QUEEN);
+    wave_put(out, k + 1, from, to, ROOK);
+    wave_put(out, k + 2, from, to, BISHOP);
+    wave_put(out, k + 3, from, to, KNIGHT);
+    return k + 4;
+  }
+  wave_put(out, k, from, to, 0);
+  return k + 1;
+}
+// a lane-0-only generator step (castling, en passant: at most two moves)
+template <typename F>
+AZC_HD int wave_serial(uint16_t* out, int n, int lane, F&& gen) {
+  int nn = n;
+  if (lane == 0) {
+    MoveOut o{out, n};
+    gen(o);
+    nn = o.n;
+  }
+  return __shfl(nn, 0, 64);
+}
+
+// gen_pseudo(from_mask, to_mask) appended at out[n..]; returns the new count
+AZC_HD int gen_pseudo_wave(const Pos& q, bb from_mask, bb to_mask, uint16_t* out, int n, int lane) {
+  const int t = q.turn, sq = 63 - lane;
+  const bb own = q.C(t), occ = q.occ();
+  int total;
+  {  // pieces other than pawns, from-square descending, targets descending
+    const bb np = own & ~q.p[PAWN - 1] & from_mask;
+    bb tg = ((np >> sq) & 1) ? piece_attacks(q, sq, occ) & ~own & to_mask : 0;
+    int k = n + wave_offset(popc(tg), lane, &total);
+    for (; tg; tg &= ~sq_bb(msb(tg))) wave_put(out, k++, sq, msb(tg), 0);
+    n += total;
+  }
+  if (from_mask & q.p[KING - 1])
+    n = wave_serial(out, n, lane, [&](MoveOut& o) { gen_castling(q, from_mask, to_mask, o); });
+  const bb pawns = q.p[PAWN - 1] & own & from_mask;
+  if (!pawns) return n;
+  const bb promo = RANK_1 | RANK_8;
+  {  // pawn captures, from-square descending (promotions Q, R, B, N)
+    bb tg = ((pawns >> sq) & 1) ? pawn_att(t, sq) & q.C(!t) & to_mask : 0;
+    int k = n + wave_offset(popc(tg & ~promo) + 4 * popc(tg & promo), lane, &total);
+    for (; tg; tg &= ~sq_bb(msb(tg))) k = wave_put_pawn(out, k, sq, msb(tg));
+    n += total;
+  }
+  bb single, dbl;
+  if (t) {
+    single = (pawns << 8) & ~occ;
+    dbl = (single << 8) & ~occ & (0xFFull << 16 | 0xFFull << 24);
+  } else {
+    single = (pawns >> 8) & ~occ;
+    dbl = (single >> 8) & ~occ & (0xFFull << 40 | 0xFFull << 32);
+  }
+  single &= to_mask;
+  dbl &= to_mask;
+  {  // single pushes, to-square descending
+    const bool on = (single >> sq) & 1;
+    const int k = n + wave_offset(on ? ((sq_bb(sq) & promo) ? 4 : 1) : 0, lane, &total);
+    if (on) wave_put_pawn(out, k, sq + (t ? -8 : 8), sq);
+    n += total;
+  }
+  {  // double pushes, to-square descending
+    const bool on = (dbl >> sq) & 1;
+    const int k = n + wave_offset(on ? 1 : 0, lane, &total);
+    if (on) wave_put(out, k, sq + (t ? -16 : 16), sq, 0);
+    n += total;
+  }
+  if (q.ep >= 0) n = wave_serial(out, n, lane, [&](MoveOut& o) { gen_ep(q, from_mask, to_mask, o); });
+  return n;
+}
+
+// legal_moves with the wave: candidates in `cand` (LDS, AZ_CHESS_MAX_MOVES),
+// the legal list in `out`; same return value and *check as legal_moves
+AZC_HD int legal_moves_wave(const Pos& q, uint16_t* cand, uint16_t* out, bool* check, int lane) {
+  const int king = king_sq(q, q.turn);
+  *check = false;
+  int n = 0;
+  if (king < 0) {
+    n = gen_pseudo_wave(q, ~0ull, ~0ull, cand, 0, lane);
+    if (n > AZ_CHESS_MAX_MOVES) return -1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int j = lane; j < n; j += 64) out[j] = cand[j];
+    return n;
+  }
+  const bb blockers = slider_blockers(q, king);
+  const bb checkers = attackers(q, !q.turn, king, q.occ());
+  if (checkers) {
+    *check = true;
+    const bb sliders = checkers & (q.p[BISHOP - 1] | q.p[ROOK - 1] | q.p[QUEEN - 1]);
+    bb attacked = 0;
+    for (bb s = sliders; s; s &= ~sq_bb(msb(s))) attacked |= line(king, msb(s)) & ~sq_bb(msb(s));
+    const bb kt = king_att(king) & ~q.C(q.turn) & ~attacked;  // king moves, targets descending
+    const bool on = (kt >> (63 - lane)) & 1;
+    int total;
+    const int k = wave_offset(on ? 1 : 0, lane, &total);
+    if (on) wave_put(cand, k, king, 63 - lane, 0);
+    n = total;
+    const int checker = msb(checkers);
+    if (sq_bb(checker) == checkers) {
+      const bb target = between(king, checker) | checkers;
+      n = gen_pseudo_wave(q, ~q.p[KING - 1], target, cand, n, lane);
+      if (q.ep >= 0 && !(sq_bb(q.ep) & target) && q.ep + (q.turn ? -8 : 8) == checker)
+        n = wave_serial(cand, n, lane, [&](MoveOut& o) { gen_ep(q, ~0ull, ~0ull, o); });
+    }
+  } else {
+    n = gen_pseudo_wave(q, ~0ull, ~0ull, cand, 0, lane);
+  }
+  if (n > AZ_CHESS_MAX_MOVES) return -1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  int kept = 0;
+  for (int base = 0; base < n; base += 64) {  // _is_safe, order kept
+    const int j = base + lane;
+    const uint16_t m = j < n ? cand[j] : 0;
+    const bool keep = j < n && is_safe(q, king, blockers, m);
+    const unsigned long long mask = __ballot(keep);
+    if (keep) out[kept + __popcll(mask & ((1ull << lane) - 1ull))] = m;
+    kept += __popcll(mask);
+  }
+  return kept;
+}
+
 AZC_HD void remove_piece(Pos& q, int s) {
   bb m = ~sq_bb(s);
 #pragma unroll

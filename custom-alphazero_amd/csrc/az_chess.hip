@@ -136,26 +136,33 @@ struct DBuf {
 // Board.moves / legal_moves_mask / outcome, one thread per position.  The
 // move list is generated straight into the position's output row (pseudo-
 // legal first, then compacted in place by the _is_safe filter).
-__global__ void __launch_bounds__(128) legal_kernel(const az_chess_pos* __restrict__ pos, int n,
-                                                    uint16_t* __restrict__ moves, int32_t* counts,
-                                                    uint8_t* __restrict__ mask, int32_t* outcome_out,
-                                                    const int16_t* __restrict__ lut) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(64) legal_kernel(const az_chess_pos* __restrict__ pos, int n,
+                                                   uint16_t* __restrict__ moves, int32_t* counts,
+                                                   uint8_t* __restrict__ mask, int32_t* outcome_out,
+                                                   const int16_t* __restrict__ lut) {
+  // one wave per position with the self-play leaves' generator
+  // (legal_moves_wave), so the Board API and its tests exercise it; the
+  // perft kernels keep the one-thread legal_moves: both are pinned
+  __shared__ uint16_t cand[AZ_CHESS_MAX_MOVES];
+  const int i = blockIdx.x, lane = threadIdx.x;
   if (i >= n) return;
-  Pos q = load_pos(pos[i]);
+  const Pos q = load_pos(pos[i]);
   uint16_t* row = moves + (size_t)i * AZ_CHESS_MAX_MOVES;
   bool check;
-  int k = legal_moves(q, row, &check);
-  counts[i] = k;
+  const int k = legal_moves_wave(q, cand, row, &check, lane);
+  if (lane == 0) counts[i] = k;
   if (k < 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (mask) {
     uint8_t* mrow = mask + (size_t)i * AZ_CHESS_ACTIONS;
-    for (int j = 0; j < k; ++j) {
-      int a = action_of(lut, row[j]);
+    for (int j = lane; j < k; j += 64) {
+      const int a = action_of(lut, row[j]);
       if (a >= 0) mrow[a] = 1;
     }
   }
-  if (outcome_out) outcome_out[i] = outcome(q, k, check);
+  if (outcome_out && lane == 0) outcome_out[i] = outcome(q, k, check);
 }
 
 // Board.full_state for n boards: one workgroup per board, its 8 history
@@ -285,7 +292,7 @@ extern "C" int az_chess_legal(int device, const az_chess_pos* pos, int n, uint16
     AZC_HIP(hipMemsetAsync(dmask.p, 0, (size_t)n * AZ_CHESS_ACTIONS, c->stream));
   }
   AZC_HIP(hipMemcpyAsync(dpos.p, pos, sizeof(az_chess_pos) * n, hipMemcpyHostToDevice, c->stream));
-  legal_kernel<<<(n + 127) / 128, 128, 0, c->stream>>>(dpos.p, n, dmv.p, dcnt.p, mask ? dmask.p : nullptr,
+  legal_kernel<<<n, 64, 0, c->stream>>>(dpos.p, n, dmv.p, dcnt.p, mask ? dmask.p : nullptr,
                                                       outcome_out ? dout.p : nullptr, c->lut);
   AZC_HIP(hipGetLastError());
   AZC_HIP(hipMemcpyAsync(counts, dcnt.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));

@@ -327,21 +327,18 @@ __global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
 }
 
 // the leaf's is_game_over() (mcts.py:173-179): terminal leaves back up the
-// canonical get_result (1 checkmate, 0 draw); others are queued for evaluation
-// AZ_LEAF_SPW slots per wave: the move generator diverges per position, so a
-// wave costs about the union of its lanes' paths; fewer slots per wave spread
-// the serial work over more CUs (the step is latency-bound here): 1 measured
-// best (626k expansions/s vs 593k with 64, 614k with 4)
-#ifndef AZ_LEAF_SPW
-#define AZ_LEAF_SPW 1
-#endif
+// canonical get_result (1 checkmate, 0 draw); others are queued for evaluation.
+// One wave per slot: the wave generates the legal moves (legal_moves_wave,
+// one square per lane; a single lane per slot took 19 us per launch), lane 0
+// does the rest.
 __global__ __launch_bounds__(64) void leaf_kernel(CCfg g, CTree t) {
-  if (threadIdx.x >= AZ_LEAF_SPW) return;
-  const int s = blockIdx.x * AZ_LEAF_SPW + threadIdx.x;
-  if (s >= g.slots || t.game_id[s] < 0) return;
+  __shared__ uint16_t cand[AZ_CHESS_MAX_MOVES];
+  const int s = blockIdx.x, lane = threadIdx.x;
+  if (s >= g.slots || t.game_id[s] < 0) return;  // block-uniform
   const Pos q = load_pos(t.leaf[s]);
   bool check;
-  const int n = legal_moves(q, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check);
+  const int n = legal_moves_wave(q, cand, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check, lane);
+  if (lane != 0) return;
   if (n < 0) {
     flag(t, az::kErrIllegal);
     return;
@@ -757,7 +754,7 @@ int simulate(az_chess_engine* e, CLane& L) {
   hipStream_t s = L.stream;
   const int S = L.g.slots;
   select_kernel<<<S, 64, 0, s>>>(L.g, L.t);
-  leaf_kernel<<<(S + AZ_LEAF_SPW - 1) / AZ_LEAF_SPW, 64, 0, s>>>(L.g, L.t);
+  leaf_kernel<<<S, 64, 0, s>>>(L.g, L.t);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
     encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, reinterpret_cast<float4*>(L.x));
     az::launch_forward(e->net, L.x, L.t.eval_count, S, 8, 8, AZ_CHESS_ACTIONS, L.act[0], L.act[1],
