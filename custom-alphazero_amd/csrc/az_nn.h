@@ -53,7 +53,9 @@ struct ConvTimer {
     if (used + 2 > pool.size()) {
       for (int i = 0; i < 256; ++i) {
         hipEvent_t e;
-        (void)hipEventCreate(&e);
+        // timing only: no system-scope fence (a default event's cache
+        // writeback/invalidate cost ~12 us between the kernels it sits between)
+        (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
         pool.push_back(e);
       }
     }
