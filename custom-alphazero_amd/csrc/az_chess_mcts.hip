@@ -8,8 +8,9 @@
 //   select   one wave per slot: PUCT over the node's edges (4 per lane),
 //            ΣN and first-max argmax by wave shuffles, the position replayed
 //            along the path with push + mirror (no boards stored per node)
-//   leaf     one thread per slot: legal moves + outcome of the leaf; terminal
-//            leaves back up get_result's value, the rest join the eval queue
+//   leaf     one wave per slot: legal moves (one square per lane) + outcome of
+//            the leaf; terminal leaves back up get_result's value, the rest
+//            join the eval queue
 //   encode   one workgroup per queued board: Board.full_state planes straight
 //            into the network input (padded to 128 channels)
 //   expand   one wave per queued board: priors = probs[mask] renormalised in
