@@ -748,6 +748,9 @@ int check_errors(az_chess_engine* e) {
   if (err & az::kErrPath) m += " path-overflow";
   if (err & az::kErrIllegal) m += " illegal-move";
   if (err & az::kErrNoRoot) m += " play-before-search";
+  // play on a slot without a searched root changes nothing: that flag is
+  // cleared once reported (the others mean a broken tree and stay)
+  if (err == az::kErrNoRoot) AZC_HIP(hipMemset(e->t.stats + az::kStatErrors, 0, sizeof(err)));
   return az::fail_abi(AZ_E_DEVICE, m);
 }
 

@@ -109,6 +109,9 @@ int check_device_errors(az_engine* e) {
     if (err & az::kErrPath) m += " path-overflow";
     if (err & az::kErrIllegal) m += " illegal-move";
     if (err & az::kErrNoRoot) m += " play-before-search";
+    // play on a slot without a searched root changes nothing: that flag is
+    // cleared once reported (the others mean a broken tree and stay)
+    if (err == az::kErrNoRoot) AZ_HIP(hipMemset(e->t.stats + az::kStatErrors, 0, sizeof(err)));
     return fail(AZ_E_DEVICE, m);
   }
   return 0;

@@ -134,6 +134,11 @@ def test_chess_tree_terminal_root_and_mate_in_one():
     assert _root_edges(eng, 0)["moves"].size == 0
     with pytest.raises(az.AzError, match="play-before-search"):
         eng.tree_play(np.array([0.1]))
+    # that error leaves the engine usable: a new root searches and plays
+    root = C.from_fen(ROOTS[2])
+    eng.tree_reset([0], np.array([root], C.POS_DTYPE))
+    tr = C.Tree(root)
+    _run(eng, [tr], [(12, False, False)], seed=3)
     eng.close()
 
 

@@ -266,4 +266,8 @@ def test_abi_error_behaviour():
     eng.tree_reset([0], np.zeros((1, 6, 7), np.int8))
     with pytest.raises(az.AzError, match="play-before-search"):
         eng.tree_play([0.5])
+    # ... which leaves the engine usable
+    eng.tree_search(10)
+    moves, status, _ = eng.tree_play([0.5])
+    assert 0 <= moves[0] < 7 and status[0] == 0
     eng.close()
