@@ -103,6 +103,7 @@ struct CPlayOut {
 };
 
 constexpr int kMtN = 624;
+constexpr int kStemFirstChunk = 2;  // input chunks of 32 planes the self-play stem skips
 
 __device__ __forceinline__ Edge* arena(const CCfg& g, const CTree& t, int s, int h) {
   return t.edges + ((size_t)s * 2 + h) * g.half_cap;
@@ -388,8 +389,9 @@ __global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, floa
     }
     __syncthreads();
     float4* o = x + (size_t)b * 64 * 32;
-    for (int e = threadIdx.x; e < 64 * 32; e += blockDim.x) {
-      const int pix = e >> 5, k0 = (e & 31) * 4;
+    for (int e2 = threadIdx.x; e2 < 64 * (32 - 8 * kStemFirstChunk); e2 += blockDim.x) {
+      const int per = 32 - 8 * kStemFirstChunk;  // float4 per pixel written
+      const int pix = e2 / per, e = pix * 32 + 8 * kStemFirstChunk + e2 % per, k0 = (e & 31) * 4;
       const int sq = (7 - (pix >> 3)) * 8 + (pix & 7);
       const int st_idx = onehot_index(sp[0], sq), cur_idx = initial ? st_idx : onehot_index(sp[1], sq);
       float v[4];
@@ -761,8 +763,13 @@ int simulate(az_chess_engine* e, CLane& L) {
   leaf_kernel<<<S, 64, 0, s>>>(L.g, L.t);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
     encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, reinterpret_cast<float4*>(L.x));
+    // history slots 0-5 (planes 0-83) are always empty in self-play (every
+    // board's history is [0 x 6, start, board] or [0 x 7, start]): the stem
+    // skips input chunks 0-1 (planes 0-63; they would add exact zeros) and
+    // encode_queue_kernel writes planes 64-127 only
     az::launch_forward(e->net, L.x, L.t.eval_count, S, 8, 8, AZ_CHESS_ACTIONS, L.act[0], L.act[1],
-                       L.act[2], L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr);
+                       L.act[2], L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr, nullptr,
+                       kStemFirstChunk);
   } else {
     synth_kernel<<<(S + 255) / 256, 256, 0, s>>>(L.g, L.t, L.probs, L.values);
   }

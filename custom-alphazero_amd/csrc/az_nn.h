@@ -105,7 +105,7 @@ size_t wino16_pack_index(int xi, int cin, int cout);  // az_wino16.hip
 struct HeadConv;
 void launch_wino16_conv(const float* in, const float* res_in, const float* upack, const float* rpack,
                         const float* bias, float* out, const int* count, int n_max, int H, int W,
-                        hipStream_t s, const HeadConv* heads = nullptr);
+                        hipStream_t s, const HeadConv* heads = nullptr, int first_chunk = 0);
 // The heads' 1x1 convolutions (policy F->2, value F->1, each + folded BN +
 // ReLU, model.py:68-149), fused into the last block's conv2 epilogue: feat =
 // [boards][HW] float4 (policy ch 0, policy ch 1, value, 0); the block output
@@ -132,6 +132,7 @@ int load_network(NetDev& net, const ::az_tensor* tensors, int n, int in_ch, int 
 // x: [n][HW][4] (in_ch == 4) or [n][HW][F] zero-padded planes (in_ch > 4)
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
-                    hipStream_t s, ConvTimer* timer, const Board* boards = nullptr);
+                    hipStream_t s, ConvTimer* timer, const Board* boards = nullptr,
+                    int stem_first_chunk = 0);
 
 }  // namespace az

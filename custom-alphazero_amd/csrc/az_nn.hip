@@ -677,14 +677,17 @@ void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* ma
 
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
-                    hipStream_t s, ConvTimer* timer, const Board* boards) {
+                    hipStream_t s, ConvTimer* timer, const Board* boards, int stem_first_chunk) {
   if (n_max <= 0) return;
   const int HW = H * W;
   constexpr int F = 128;
   if (net.stem_u) {
     // chess: 118 input planes zero-padded to F, the stem is one more Winograd conv
+    // stem_first_chunk: input chunks (32 planes) before it are known zero and
+    // skipped -- they would add exact zeros (chess self-play: planes 0-83)
     if (net.wino_tiles == 16)
-      launch_wino16_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s);
+      launch_wino16_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
+                         stem_first_chunk);
     else
       launch_wino_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
                        net.wino_ksplit);

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ upack, const float4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
-    int n_static, int H, int W, HeadConv hc) {
+    int n_static, int H, int W, HeadConv hc, int c0) {
   constexpr int CK = 32;
   constexpr int NX = RESIDUAL ? 20 : 16;
   constexpr int RC = CK / 4;                 // float4 per V row
@@ -232,14 +232,16 @@ __global__ __launch_bounds__(kW16Threads, AZ_W16_OCC) void wino16_conv_kernel(
     if (k < NCH * NX) load_b(k / NX, k % NX, dst);
   };
 
-  produce_load(0);
+  // c0 > 0: the input's first c0 chunks are zero (they would only add exact
+  // zeros); flat stage c*NX + xi keeps its B buffer for any c0 (NX % NB == 0)
+  produce_load(c0);
   produce_store();
 #pragma unroll
-  for (int k = 0; k < PF; ++k) load_b_flat(k, bq[k]);
+  for (int k = 0; k < PF; ++k) load_b_flat(c0 * NX + k, bq[k]);
   __syncthreads();
 
 #pragma unroll 1
-  for (int c = 0; c < NCH; ++c) {
+  for (int c = c0; c < NCH; ++c) {
     load_a(0, aq[0]);
 #pragma unroll
     for (int xi = 0; xi < NX; ++xi) {
@@ -368,7 +370,7 @@ size_t wino16_pack_index(int xi, int cin, int cout) {
 
 void launch_wino16_conv(const float* in, const float* res_in, const float* upack, const float* rpack,
                         const float* bias, float* out, const int* count, int n_max, int H, int W,
-                        hipStream_t s, const HeadConv* heads) {
+                        hipStream_t s, const HeadConv* heads, int first_chunk) {
   const int TB = ((H + 1) / 2) * ((W + 1) / 2);
   const int grid = (n_max * TB + kW16Tiles - 1) / kW16Tiles;
   if (grid <= 0) return;
@@ -386,21 +388,21 @@ void launch_wino16_conv(const float* in, const float* res_in, const float* upack
   if (heads && heads->feat) {
     hc = *heads;
     wino16_conv_kernel<true, true, 1><<<grid, kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out, count, n_max,
-                                                                   H, W, hc);
+                                                                   H, W, hc, 0);
   } else if (res_in) {
     if (split)
       wino16_conv_kernel<true, false, 2><<<dim3(grid, 2), kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out,
-                                                                              count, n_max, H, W, hc);
+                                                                              count, n_max, H, W, hc, 0);
     else
       wino16_conv_kernel<true, false, 1><<<grid, kW16Threads, 0, s>>>(in, res_in, u, rp, bias, out, count,
-                                                                      n_max, H, W, hc);
+                                                                      n_max, H, W, hc, 0);
   } else {
     if (split)
-      wino16_conv_kernel<false, false, 2><<<dim3(grid, 2), kW16Threads, 0, s>>>(in, nullptr, u, nullptr, bias,
-                                                                               out, count, n_max, H, W, hc);
+      wino16_conv_kernel<false, false, 2><<<dim3(grid, 2), kW16Threads, 0, s>>>(
+          in, nullptr, u, nullptr, bias, out, count, n_max, H, W, hc, first_chunk);
     else
       wino16_conv_kernel<false, false, 1><<<grid, kW16Threads, 0, s>>>(in, nullptr, u, nullptr, bias, out,
-                                                                       count, n_max, H, W, hc);
+                                                                       count, n_max, H, W, hc, first_chunk);
   }
 }
 
