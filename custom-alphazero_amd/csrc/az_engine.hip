@@ -252,9 +252,38 @@ int ready_to_search(az_engine* e) {
 // U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
 // in float64 from the folded Keras kernel, rounded once to float, in the
 // kernel's fragment order.
-[[maybe_unused]] std::vector<float> pack_wino(const std::vector<double>& w, int F, int tiles) {
+// bf16 round-to-nearest-even bits of a float (finite), as the device's bf16_rne
+[[maybe_unused]] uint16_t bf16_bits(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+[[maybe_unused]] float bf16_value(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+// x (float) = t0 + t1 + t2, bf16 each (az_wino16x.hip)
+[[maybe_unused]] void split3_host(float x, uint16_t t[3]) {
+  t[0] = bf16_bits(x);
+  const float r1 = x - bf16_value(t[0]);
+  t[1] = bf16_bits(r1);
+  const float r2 = r1 - bf16_value(t[1]);
+  t[2] = bf16_bits(r2);
+}
+// bf16x3 terms packed as floats' storage (two bf16 per float slot) for upload
+[[maybe_unused]] std::vector<float> as_float_storage(const std::vector<uint16_t>& h) {
+  std::vector<float> f((h.size() + 1) / 2);
+  memcpy(f.data(), h.data(), h.size() * sizeof(uint16_t));
+  return f;
+}
+
+[[maybe_unused]] std::vector<float> pack_wino(const std::vector<double>& w, int F, int tiles, bool x3 = false) {
   static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   std::vector<float> p((size_t)16 * F * F);
+  std::vector<uint16_t> h(x3 ? (size_t)16 * F * F * 3 : 0);
   std::vector<double> U((size_t)F * F);
   for (int xi = 0; xi < 16; ++xi) {
     const int a = xi >> 2, b = xi & 3;
@@ -267,16 +296,34 @@ int ready_to_search(az_engine* e) {
         for (size_t i = 0; i < (size_t)F * F; ++i) U[i] += gg * src[i];
       }
     for (int cin = 0; cin < F; ++cin)
-      for (int co = 0; co < F; ++co)
+      for (int co = 0; co < F; ++co) {
+        if (x3) {  // az_wino16x.hip: three bf16 terms per weight
+          uint16_t t[3];
+          split3_host((float)U[(size_t)cin * F + co], t);
+          for (int k = 0; k < 3; ++k) h[az::wino16x_pack_index(xi, cin, co, k)] = t[k];
+          continue;
+        }
         p[tiles == 16 ? az::wino16_pack_index(xi, cin, co) : az::wino_pack_index(xi, cin, co)] =
             (float)U[(size_t)cin * F + co];
+      }
   }
-  return p;
+  return x3 ? as_float_storage(h) : p;
 }
 
 // 1x1 projection residual [cin][cout] in the same fragment order, as if it
 // were point 0 of a 16-point-per-chunk stream compacted to one point.
-[[maybe_unused]] std::vector<float> pack_wino_res(const std::vector<double>& wr, int F, int tiles) {
+[[maybe_unused]] std::vector<float> pack_wino_res(const std::vector<double>& wr, int F, int tiles,
+                                                 bool x3 = false) {
+  if (x3) {
+    std::vector<uint16_t> h((size_t)F * F * 3);
+    for (int cin = 0; cin < F; ++cin)
+      for (int co = 0; co < F; ++co) {
+        uint16_t t[3];
+        split3_host((float)wr[(size_t)cin * F + co], t);
+        for (int k = 0; k < 3; ++k) h[az::wino16x_res_index(cin, co, k)] = t[k];
+      }
+    return as_float_storage(h);
+  }
   std::vector<float> p((size_t)F * F);
   const int CK = az::kWinoCK;
   for (int cin = 0; cin < F; ++cin)
@@ -387,7 +434,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
         for (int c = 0; c < in_ch; ++c)
           for (int o = 0; o < F; ++o)
             wp[((size_t)tap * F + c) * F + o] = w[((size_t)tap * in_ch + c) * F + o];
-      if ((rc = upload(owned, &net.stem_u, pack_wino(wp, F, net.wino_tiles)))) return rc;
+      if ((rc = upload(owned, &net.stem_u, pack_wino(wp, F, net.wino_tiles, net.wino_x3 != 0)))) return rc;
     }
     net.in_ch = in_ch;
   }
@@ -406,7 +453,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
     for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
     if ((rc = upload(owned, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
-        (rc = upload(owned, &net.u1_w[d], pack_wino(w, F, net.wino_tiles))) ||
+        (rc = upload(owned, &net.u1_w[d], pack_wino(w, F, net.wino_tiles, net.wino_x3 != 0))) ||
         (rc = upload(owned, &net.c1_b[d], bt)))
       return rc;
     if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
@@ -418,8 +465,8 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     }
     for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
     if ((rc = upload(owned, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
-        (rc = upload(owned, &net.u2_w[d], pack_wino(w, F, net.wino_tiles))) ||
-        (rc = upload(owned, &net.r2_w[d], pack_wino_res(wr, F, net.wino_tiles))) ||
+        (rc = upload(owned, &net.u2_w[d], pack_wino(w, F, net.wino_tiles, net.wino_x3 != 0))) ||
+        (rc = upload(owned, &net.r2_w[d], pack_wino_res(wr, F, net.wino_tiles, net.wino_x3 != 0))) ||
         (rc = upload(owned, &net.c2_b[d], bt2)))
       return rc;
   }
@@ -591,6 +638,8 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   {  // Winograd variant (az_wino.hip 32 tiles / az_wino16.hip 16 tiles); AZ_WINO_TILES for A/B runs
     const char* wt = getenv("AZ_WINO_TILES");
     e->net.wino_tiles = wt ? atoi(wt) : 16;
+    const char* x3 = getenv("AZ_WINO_X3");  // fp32 products from bf16 terms (az_wino16x.hip)
+    e->net.wino_x3 = x3 ? atoi(x3) : 1;
   }
   // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
   int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);

@@ -17,6 +17,7 @@ struct NetDev {
   int wino_ksplit = 1;  // 32-tile Winograd kernel: 1, or 2 = two chunk groups per workgroup
   int wino_tiles = 32;  // tiles per workgroup: 32 (wino_conv_kernel) or 16 (wino16_conv_kernel);
                         // one variant for every conv of a network (set before load_network)
+  int wino_x3 = 0;      // 16 tiles: 1 = wino16x_conv_kernel (fp32 products from three bf16 terms)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c), in_ch == 4
   float* stem_u = nullptr;  // Winograd U of the zero-padded stem [3][3][F][F], in_ch > 4
@@ -101,11 +102,16 @@ void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* ma
 constexpr int kWinoCK = AZ_WINO_CK;
 size_t wino_pack_index(int xi, int cin, int cout);
 size_t wino16_pack_index(int xi, int cin, int cout);  // az_wino16.hip
+size_t wino16x_pack_index(int xi, int cin, int cout, int k);  // az_wino16x.hip (bf16 units)
+size_t wino16x_res_index(int cin, int cout, int k);
 // 16-tile variant on v_mfma_f32_16x16x4_f32 (small launches; az_wino16.hip)
 struct HeadConv;
 void launch_wino16_conv(const float* in, const float* res_in, const float* upack, const float* rpack,
                         const float* bias, float* out, const int* count, int n_max, int H, int W,
                         hipStream_t s, const HeadConv* heads = nullptr, int first_chunk = 0);
+void launch_wino16x_conv(const float* in, const float* res_in, const float* upack, const float* rpack,
+                         const float* bias, float* out, const int* count, int n_max, int H, int W,
+                         hipStream_t s, const HeadConv* heads = nullptr, int first_chunk = 0);
 // The heads' 1x1 convolutions (policy F->2, value F->1, each + folded BN +
 // ReLU, model.py:68-149), fused into the last block's conv2 epilogue: feat =
 // [boards][HW] float4 (policy ch 0, policy ch 1, value, 0); the block output

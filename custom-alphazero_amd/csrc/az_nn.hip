@@ -675,6 +675,17 @@ void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* ma
   legal_mask_kernel<<<(total + 255) / 256, 256, 0, s>>>(boards, n, g, mask);
 }
 
+// the network's 16-tile variant: fp32 MFMA (az_wino16.hip) or bf16x3 terms
+// (az_wino16x.hip); one variant for every forward of an engine
+static void launch_w16(const NetDev& net, const float* in, const float* res_in, const float* upack,
+                       const float* rpack, const float* bias, float* out, const int* count, int n_max, int H,
+                       int W, hipStream_t s, const HeadConv* heads = nullptr, int first_chunk = 0) {
+  if (net.wino_x3)
+    launch_wino16x_conv(in, res_in, upack, rpack, bias, out, count, n_max, H, W, s, heads, first_chunk);
+  else
+    launch_wino16_conv(in, res_in, upack, rpack, bias, out, count, n_max, H, W, s, heads, first_chunk);
+}
+
 void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
                     int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
                     hipStream_t s, ConvTimer* timer, const Board* boards, int stem_first_chunk) {
@@ -686,7 +697,7 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
     // stem_first_chunk: input chunks (32 planes) before it are known zero and
     // skipped -- they would add exact zeros (chess self-play: planes 0-83)
     if (net.wino_tiles == 16)
-      launch_wino16_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
+      launch_w16(net, x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
                          stem_first_chunk);
     else
       launch_wino_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
@@ -731,7 +742,7 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
       case 0:  // Winograd F(2x2,3x3) (az_wino.hip)
       {
         if (net.wino_tiles == 16)
-          launch_wino16_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s);
+          launch_w16(net, cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s);
         else
           launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s,
                            nullptr, net.wino_ksplit);
@@ -739,7 +750,7 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
         HeadConv hc{net.pc_w, net.pc_b, net.vc_w, net.vc_b,
                     d == net.depth - 1 && AZ_FUSE_HEADS ? reinterpret_cast<float4*>(nxt) : nullptr};
         if (net.wino_tiles == 16)
-          launch_wino16_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc);
+          launch_w16(net, mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc);
         else
           launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc,
                            net.wino_ksplit);
