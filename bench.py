@@ -33,6 +33,37 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 sparsity)
+
+
+def wino_x3():
+    """The engines' Winograd kernel: 1 (default) = fp32 products from three bf16
+    terms per operand (csrc/az_wino16x.hip), 0 = fp32 MFMA (az_wino16.hip)."""
+    v = os.environ.get("AZ_WINO_X3")
+    return int(v) if v is not None else 1
+
+
+def issued_mfma(achieved, conv_flop_per_board, mfma_flop_per_board, conv_algo):
+    """The MFMA work the conv kernel issues for `achieved` algorithmic TFLOP/s:
+    the Winograd FLOP (2.25x below the direct count at 2x2 tiles) as fp32
+    16x16x4 MFMAs, or as six bf16 16x16x32 products per fp32 product."""
+    wino = achieved * mfma_flop_per_board / conv_flop_per_board
+    if conv_algo == 0 and wino_x3():
+        a = 6 * wino
+        return {"dtype": "bf16 (3 terms per fp32 operand, 6 products)", "flop_per_board": 6 * mfma_flop_per_board,
+                "achieved": round(a, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "frac": round(a / BF16_MFMA_PEAK_TFLOPS, 4)}
+    return {"dtype": "fp32", "flop_per_board": mfma_flop_per_board, "achieved": round(wino, 2),
+            "peak": FP32_MFMA_PEAK_TFLOPS, "frac": round(wino / FP32_MFMA_PEAK_TFLOPS, 4)}
+
+
+def conv_kernel_name(conv_algo, chess=False):
+    if conv_algo != 0:
+        return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"
+    k = ("wino16x_conv_kernel (Winograd F(2x2,3x3), fp32 products from three bf16 terms per operand on "
+         "the 16x16x32 bf16 MFMA" if wino_x3() else
+         "wino16_conv_kernel (Winograd F(2x2,3x3) on the fp32 16x16x4 MFMA")
+    return k + (", residual tower, 8 launches per forward)" if chess else
+                ", 16 tiles per workgroup, fused BN/ReLU and 1x1 projection residual)")
 
 
 def parse():
@@ -244,7 +275,7 @@ def chess_main(args):
             "terminal_visits": d["terminal_visits"],
             "lanes": args.lanes or "auto",
             "roofline": {
-                "kernel": "wino16_conv_kernel (residual tower, 8 launches per forward)",
+                "kernel": conv_kernel_name(args.conv_algo, chess=True),
                 "bound": "mfma",
                 "achieved": round(achieved, 2),
                 "peak": FP32_MFMA_PEAK_TFLOPS,
@@ -258,8 +289,7 @@ def chess_main(args):
                 "busy_union": {"achieved": round(union, 2), "frac": round(union / FP32_MFMA_PEAK_TFLOPS, 4)},
                 "algorithmic_flop_per_board": conv_flop_per_board,
                 "mfma_flop_per_board": mfma_flop_per_board,
-                "mfma_frac": round(achieved * mfma_flop_per_board / conv_flop_per_board
-                                   / FP32_MFMA_PEAK_TFLOPS, 4),
+                "issued": issued_mfma(achieved, conv_flop_per_board, mfma_flop_per_board, args.conv_algo),
                 "boards_per_launch": round(boards_per_launch, 1),
                 "avg_launch_ms": round(avg_ms, 4),
                 "conv_busy_ms": round(busy, 2),
@@ -414,7 +444,6 @@ def main():
     # other lane's kernels, so the union-of-busy-time rate is given beside it
     per_launch_flop = boards_per_launch * conv_flop_per_board / (2 * args.depth)
     achieved = per_launch_flop / (conv_avg_ms * 1e-3) / 1e12 if conv_avg_ms else 0.0
-    mfma_achieved = achieved * mfma_flop_per_board / conv_flop_per_board
     union = (local_exp * conv_flop_per_board) / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
     traffic = None
     pmc = os.path.join(REPO, "profiles", "r1", "pmc_conv_traffic.json")
@@ -443,8 +472,7 @@ def main():
         iso = nb * conv_flop_per_board / (2 * args.depth) / (iso_ms * 1e-3) / 1e12
         isolated = {"boards": nb, "avg_launch_ms": round(iso_ms, 4),
                     "achieved": round(iso, 2), "frac": round(iso / FP32_MFMA_PEAK_TFLOPS, 4),
-                    "mfma_frac": round(iso * mfma_flop_per_board / conv_flop_per_board
-                                       / FP32_MFMA_PEAK_TFLOPS, 4)}
+                    "issued": issued_mfma(iso, conv_flop_per_board, mfma_flop_per_board, args.conv_algo)}
 
     game_name = "Connect-4 6x7" if (args.height, args.width, args.n) == (6, 7, 4) else \
         f"Connect-{args.n} {args.height}x{args.width}"
@@ -486,9 +514,7 @@ def main():
             "cache_off": off,
             "roofline_tree": roofline_tree,
             "roofline": {
-                "kernel": ("wino16_conv_kernel (Winograd F(2x2,3x3) on fp32 MFMA 16x16x4, 16 tiles per "
-                           "workgroup, fused BN/ReLU and 1x1 projection residual)" if args.conv_algo == 0 else
-                           "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"),
+                "kernel": conv_kernel_name(args.conv_algo),
                 "bound": "mfma",
                 "achieved": round(achieved, 2),
                 "peak": FP32_MFMA_PEAK_TFLOPS,
@@ -505,8 +531,7 @@ def main():
                                         "both lanes (launches of the two lanes overlap)"},
                 "algorithmic_flop_per_board": conv_flop_per_board,
                 "mfma_flop_per_board": mfma_flop_per_board,
-                "mfma_achieved": round(mfma_achieved, 2),
-                "mfma_frac": round(mfma_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "issued": issued_mfma(achieved, conv_flop_per_board, mfma_flop_per_board, args.conv_algo),
                 "boards_per_launch": round(boards_per_launch, 1),
                 "avg_launch_ms": round(conv_avg_ms, 4),
                 "conv_busy_ms": round(busy_ms, 2),

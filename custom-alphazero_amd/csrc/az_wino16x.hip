@@ -26,6 +26,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kXTiles = 16;
 constexpr int kXThreads = 256;
+#ifndef AZ_W16X_PF
+#define AZ_W16X_PF 2  // stages of B fragments in flight ahead of their MFMAs
+#endif
+#ifndef AZ_W16X_OCC
+#define AZ_W16X_OCC 2  // minimum waves per SIMD for the register allocator
+#endif
 
 __host__ __device__ constexpr int x_sign(int a, int i) {
   return i == 0 ? (a == 3 ? 0 : 1) : (a == 0 ? 0 : (a == 1 ? 1 : -1));
@@ -61,7 +67,7 @@ __device__ __forceinline__ void split3(const float4 v, uint2 (&t)[3]) {
 }
 
 template <bool RESIDUAL, bool HEADS, int NS>
-__global__ __launch_bounds__(kXThreads, 2) void wino16x_conv_kernel(
+__global__ __launch_bounds__(kXThreads, AZ_W16X_OCC) void wino16x_conv_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const uint4* __restrict__ upack, const uint4* __restrict__ rpack,
     const float* __restrict__ bias, float* __restrict__ out, const int* __restrict__ count,
@@ -229,8 +235,8 @@ __global__ __launch_bounds__(kXThreads, 2) void wino16x_conv_kernel(
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
     return acc;
   };
-  constexpr int PF = 2;
-  constexpr int NB = 4;  // B register buffers (>= PF + 1, divides NX)
+  constexpr int PF = AZ_W16X_PF;
+  constexpr int NB = PF == 1 ? 2 : 4;  // B register buffers (>= PF + 1, divides NX)
   static_assert(NX % NB == 0, "buffer of a stage must not depend on the chunk");
   uint4 bq[NB][QB], aq[2][3];
   f32x4 M[2][NBW];

@@ -44,7 +44,7 @@ def main():
         rf = b["roofline"]
         print(f"same run, bench.py HIP events: avg_launch_ms {rf['avg_launch_ms']} "
               f"({rf['avg_launch_ms'] * 1e3:.1f} us), boards/launch {rf['boards_per_launch']}, "
-              f"achieved {rf['achieved']} TFLOP/s algorithmic, {rf['mfma_achieved']} MFMA-executed; "
+              f"achieved {rf['achieved']} TFLOP/s algorithmic, {rf['issued']['achieved']} issued ({rf['issued']['dtype']}); "
               f"value {b['value']} games/s under the profiler")
     except Exception as ex:  # noqa: BLE001
         print(f"(bench_trace.json unreadable: {ex})")
