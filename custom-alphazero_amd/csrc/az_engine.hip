@@ -252,7 +252,7 @@ int ready_to_search(az_engine* e) {
 // U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
 // in float64 from the folded Keras kernel, rounded once to float, in the
 // kernel's fragment order.
-// bf16 round-to-nearest-even bits of a float (finite), as the device's bf16_rne
+// bf16 round-to-nearest-even bits of a float (finite), as the device's v_cvt_pk_bf16_f32 (split3)
 [[maybe_unused]] uint16_t bf16_bits(float f) {
   uint32_t u;
   memcpy(&u, &f, 4);

@@ -42,28 +42,26 @@ __host__ __device__ constexpr int x_sign(int a, int i) {
 // tiles 4-11 of the next; g ^ f(t / 4), f = (0, 2, 3, 1), separates them
 __device__ __forceinline__ int x16_swz(int g, int t) { return g ^ ((0x78 >> (2 * (t >> 2))) & 3); }
 
-// bf16 bits, round to nearest even (finite inputs)
-__device__ __forceinline__ uint32_t bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// two fp32 -> packed bf16 (lo, hi), round to nearest even: one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t bf16_pk(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{lo, hi}), bf16x2));
 }
 // the three bf16 terms of four channels, as three pairs of packed words
 __device__ __forceinline__ void split3(const float4 v, uint2 (&t)[3]) {
-  const float x[4] = {v.x, v.y, v.z, v.w};
-  uint32_t h[3][4];
+  float x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const uint32_t a = bf16_rne(x[e]);
-    const float r1 = x[e] - __uint_as_float(a << 16);
-    const uint32_t b = bf16_rne(r1);
-    const float r2 = r1 - __uint_as_float(b << 16);
-    h[0][e] = a;
-    h[1][e] = b;
-    h[2][e] = bf16_rne(r2);
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t p0 = bf16_pk(x[0], x[1]), p1 = bf16_pk(x[2], x[3]);
+    t[k] = make_uint2(p0, p1);
+    if (k < 2) {
+      x[0] -= __uint_as_float(p0 << 16);
+      x[1] -= __uint_as_float(p0 & 0xffff0000u);
+      x[2] -= __uint_as_float(p1 << 16);
+      x[3] -= __uint_as_float(p1 & 0xffff0000u);
+    }
   }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) t[k] = make_uint2(h[k][0] | (h[k][1] << 16), h[k][2] | (h[k][3] << 16));
 }
 
 template <bool RESIDUAL, bool HEADS, int NS>
