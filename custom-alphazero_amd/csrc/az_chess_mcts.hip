@@ -924,7 +924,8 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
     const char* wt = getenv("AZ_WINO_TILES");
     e->net.wino_tiles = wt ? atoi(wt) : 16;
     const char* x3 = getenv("AZ_WINO_X3");  // fp32 products from bf16 terms (az_wino16x.hip)
-    e->net.wino_x3 = x3 ? atoi(x3) : 1;
+    // (its buffer loads address activations with 31-bit byte offsets)
+    e->net.wino_x3 = (x3 ? atoi(x3) : 1) && (size_t)S * 64 * 128 * 4 < ((size_t)1 << 31);
   }
   if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));
   // auto = 1: at 256 games a chess step is bound by its launch chain; extra

@@ -639,7 +639,8 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
     const char* wt = getenv("AZ_WINO_TILES");
     e->net.wino_tiles = wt ? atoi(wt) : 16;
     const char* x3 = getenv("AZ_WINO_X3");  // fp32 products from bf16 terms (az_wino16x.hip)
-    e->net.wino_x3 = x3 ? atoi(x3) : 1;
+    // (its buffer loads address activations with 31-bit byte offsets)
+    e->net.wino_x3 = (x3 ? atoi(x3) : 1) && (size_t)S * g.HW * 128 * 4 < ((size_t)1 << 31);
   }
   // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
   int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);

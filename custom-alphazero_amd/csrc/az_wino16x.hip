@@ -98,34 +98,44 @@ __global__ __launch_bounds__(kXThreads, AZ_W16X_OCC) void wino16x_conv_kernel(
     ptx = lt - pty * TW;
     pbase += b * HW * 128;
   }
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 d[3][4], rr[2];
-  uint32_t ok = 0;
-  auto produce_load = [&](int c) {
-    const int cb = c * CK;
-    ok = 0;
+  // buffer loads: the byte offset of each input pixel is chunk invariant
+  // (voffset, computed once), the chunk goes in soffset; an off-board or
+  // past-the-end pixel gets kOOB, which the descriptor's range check reads as 0
+  const int in_bytes = n_static * HW * 128 * 4;  // < 2^31 (launcher)
+  const auto in_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, in_bytes, 0x00020000);
+  const auto res_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(RESIDUAL ? res_in : in), (short)0, in_bytes, 0x00020000);
+  constexpr unsigned kOOB = 0x80000000u;
+  unsigned voff[3][4], roff[2];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int y = 2 * pty - 1 + ph + r;
+  for (int r = 0; r < 3; ++r) {
+    const int y = 2 * pty - 1 + ph + r;
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int xx = 2 * ptx - 1 + x;
-        const bool o = pvalid && y >= 0 && y < H && xx >= 0 && xx < W;
-        const unsigned off = o ? (unsigned)(pbase + (y * W + xx) * 128 + cb) : 0u;
-        d[r][x] = *reinterpret_cast<const float4*>(in + off);
-        ok |= (uint32_t)o << (r * 4 + x);
-      }
+    for (int x = 0; x < 4; ++x) {
+      const int xx = 2 * ptx - 1 + x;
+      const bool o = pvalid && y >= 0 && y < H && xx >= 0 && xx < W;
+      voff[r][x] = o ? (unsigned)(pbase + (y * W + xx) * 128) * 4u : kOOB;
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = 2 * ph + k;
+    const int y = 2 * pty + (p >> 1), xx = 2 * ptx + (p & 1);
+    const bool o = RESIDUAL && pvalid && y < H && xx < W;
+    roff[k] = o ? (unsigned)(pbase + (y * W + xx) * 128) * 4u : kOOB;
+  }
+  float4 d[3][4], rr[2];
+  auto produce_load = [&](int c) {
+    const int sb = c * CK * 4;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        d[r][x] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, voff[r][x], sb, 0));
     if constexpr (RESIDUAL) {
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int p = 2 * ph + k;
-        const int y = 2 * pty + (p >> 1), xx = 2 * ptx + (p & 1);
-        const bool o = pvalid && y < H && xx < W;
-        const unsigned off = o ? (unsigned)(pbase + (y * W + xx) * 128 + cb) : 0u;
-        rr[k] = *reinterpret_cast<const float4*>(res_in + off);
-        ok |= (uint32_t)o << (12 + k);
-      }
+      for (int k = 0; k < 2; ++k)
+        rr[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(res_rsrc, roff[k], sb, 0));
     }
   };
   // 8-byte unit of (plane, point xi, tile pt, channel group pc)
@@ -138,16 +148,6 @@ __global__ __launch_bounds__(kXThreads, AZ_W16X_OCC) void wino16x_conv_kernel(
     for (int k = 0; k < 3; ++k) v2[(k * PLANE + (xi * kXTiles + pt) * ROW) * 2 + wslot] = t[k];
   };
   auto produce_store = [&]() {
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        if (!((ok >> (r * 4 + x)) & 1)) d[r][x] = z4;
-    if constexpr (RESIDUAL) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (!((ok >> (12 + k)) & 1)) rr[k] = z4;
-    }
     // T = B^T d (rows), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
     float4 T[2][4];
 #pragma unroll
@@ -188,13 +188,19 @@ __global__ __launch_bounds__(kXThreads, AZ_W16X_OCC) void wino16x_conv_kernel(
   // a split wave reads its N block's three terms from the owning wave's fragment
   const int wsrc = NS == 1 ? wave : 2 * blockIdx.y + (wave >> 1);
   const int nb0 = NS == 1 ? 0 : (wave & 1);
-  const unsigned blane = (unsigned)((wsrc * 2 + nb0) * 3 * 64 + lane);
+  // (buffer loads: lane part in voffset, chunk and point in soffset)
+  const unsigned blane = (unsigned)((wsrc * 2 + nb0) * 3 * 64 + lane) * 16u;
+  const auto u_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)upack, (short)0, NCH * 16 * 4 * 2 * 3 * 64 * 16,
+                                                        0x00020000);
+  const auto r_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(RESIDUAL ? rpack : upack), (short)0,
+                                                        NCH * 4 * 2 * 3 * 64 * 16, 0x00020000);
   auto load_b = [&](int c, int xi, uint4 (&dst)[QB]) {
     const bool res = RESIDUAL && xi >= 16;
-    const uint4* base = res ? rpack : upack;
-    const unsigned o = blane + (unsigned)(res ? c * 4 * 2 * 3 * 64 : (c * 16 + xi) * 4 * 2 * 3 * 64);
+    const int so = (res ? c * 4 * 2 * 3 * 64 : (c * 16 + xi) * 4 * 2 * 3 * 64) * 16;
 #pragma unroll
-    for (int q = 0; q < QB; ++q) dst[q] = base[o + q * 64];
+    for (int q = 0; q < QB; ++q)
+      dst[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(res ? r_rsrc : u_rsrc, blane,
+                                                                              so + q * 64 * 16, 0));
   };
   const int aslot = x16_swz(g, r);
   auto load_a = [&](int xi, uint4 (&dst)[3]) {
