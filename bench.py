@@ -5,19 +5,34 @@ Workload (BASELINE.json configs[1]): Connect-4 6x7, n=4, gravity, 100
 simulations per move, 4096 concurrent games per GPU, random-init
 128-filter x 4-block policy/value network (Keras defaults, torch seed 0).
 A "step" is one move for every game slot: `sims` lockstep simulations
-(select -> batched network forward -> expand/backup) then a move commit;
-finished games are replaced by new ones (game g seeded MT19937(g)), so the
-timed window is steady-state.  value = games completed in the K timed steps,
-summed over ranks, / max-over-ranks wall time.
+(select -> batched network forward -> expand/backup), a move commit, and
+the D2H copy of the games that finished (az_selfplay_drain: a game counts
+when its samples are on the host).  Finished games are
+replaced by new ones (game g seeded MT19937(g)).
+
+Steady state, whatever --warmup says: all slots start at ply 0 together
+and the shared transposition cache (the reference's plays_inferences)
+starts empty, so the first moves are not representative.  Untimed moves
+run until at least --warmup moves have passed AND the cache has turned over
+three eviction generations (az_tree.h: its hit rate is then stationary) --
+every one of them real work.  The line states the cache's capacity,
+generation, live fill, age in moves and the window's hit rate.
+value = games drained in the K timed steps, summed over ranks / max-over-
+ranks wall time.
 
 Multi-GPU (torchrun, one rank per GPU): games are sharded by global game id
 (independent, no data-path collective: scaling "weak"); rank 0's weights
-reach the other ranks by one RCCL broadcast over xGMI before timing.
+reach the other ranks by one RCCL broadcast over xGMI before timing, and
+the games each rank finished in the window are gathered to rank 0 (compact
+int8 boards + f64 policies, RCCL) right after it.
 
-The CPU baseline (rank 0, N=1 only) is oracle/refport.py -- the reference's
-self-play structure, pinned to the reference by tests/test_refport.py -- run
-as one game per worker process with a 1-thread torch-CPU network, like the
-reference's joblib fan-out; it runs before the GPU is touched.
+The CPU baselines (rank 0, N=1 only) are oracle/refport.py -- the
+reference's self-play structure, pinned to the reference by
+tests/test_refport.py -- run before the GPU is touched: the reference's
+joblib fan-out (one game per worker process, 1-thread torch-CPU network,
+plays_inferences shared through a Manager dict, self_play.py:98,
+utils.py:38-39) at the benchmark's sims, and BASELINE configs[0] (25
+sims/move, one worker, mono-process dict).
 """
 import argparse
 import json
@@ -34,36 +49,10 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 sparsity)
-
-
-def wino_x3():
-    """The engines' Winograd kernel: 1 (default) = fp32 products from three bf16
-    terms per operand (csrc/az_wino16x.hip), 0 = fp32 MFMA (az_wino16.hip)."""
-    v = os.environ.get("AZ_WINO_X3")
-    return int(v) if v is not None else 1
-
-
-def issued_mfma(achieved, conv_flop_per_board, mfma_flop_per_board, conv_algo):
-    """The MFMA work the conv kernel issues for `achieved` algorithmic TFLOP/s:
-    the Winograd FLOP (2.25x below the direct count at 2x2 tiles) as fp32
-    16x16x4 MFMAs, or as six bf16 16x16x32 products per fp32 product."""
-    wino = achieved * mfma_flop_per_board / conv_flop_per_board
-    if conv_algo == 0 and wino_x3():
-        a = 6 * wino
-        return {"dtype": "bf16 (3 terms per fp32 operand, 6 products)", "flop_per_board": 6 * mfma_flop_per_board,
-                "achieved": round(a, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "frac": round(a / BF16_MFMA_PEAK_TFLOPS, 4)}
-    return {"dtype": "fp32", "flop_per_board": mfma_flop_per_board, "achieved": round(wino, 2),
-            "peak": FP32_MFMA_PEAK_TFLOPS, "frac": round(wino / FP32_MFMA_PEAK_TFLOPS, 4)}
-
-
-def conv_kernel_name(conv_algo, chess=False):
-    if conv_algo != 0:
-        return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"
-    k = ("wino16x_conv_kernel (Winograd F(2x2,3x3), fp32 products from three bf16 terms per operand on "
-         "the 16x16x32 bf16 MFMA" if wino_x3() else
-         "wino16_conv_kernel (Winograd F(2x2,3x3) on the fp32 16x16x4 MFMA")
-    return k + (", residual tower, 8 launches per forward)" if chess else
-                ", 16 tiles per workgroup, fused BN/ReLU and 1x1 projection residual)")
+BOX_CPU_SHARE = 16              # CPUs one GPU's box grants a job (gpurun); workers stay inside it
+MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
+MAX_PREROLL = 800
+CACHE_TURNOVER_GENS = 3         # cache generations before the window (hit rate stationary)
 
 
 def parse():
@@ -72,7 +61,7 @@ def parse():
     ap.add_argument("--game", choices=("connect_n", "chess"), default="connect_n",
                     help="chess: BASELINE configs[4] per-GPU shard (256 games, 800 sims/move)")
     ap.add_argument("--steps", type=int, default=None, help="timed moves (30; chess 3)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed moves first (60; chess 2)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed moves at least (5; chess 2)")
     ap.add_argument("--slots", type=int, default=None, help="concurrent games per GPU (4096; chess 256)")
     ap.add_argument("--sims", type=int, default=None, help="sims per move (100; chess 800)")
     ap.add_argument("--height", type=int, default=6)
@@ -80,7 +69,10 @@ def parse():
     ap.add_argument("--n", type=int, default=4)
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
-    ap.add_argument("--cpu-workers", type=int, default=0, help="0 = min(15, cores-1)")
+    ap.add_argument("--cpu-configs0-seconds", type=float, default=10.0,
+                    help="BASELINE configs[0] line (C4, 25 sims/move, 1 worker)")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="0 = os.cpu_count() - 1 (self_play.py:98), inside the box's CPU share")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="slot groups on separate HIP streams (0 = auto)")
     ap.add_argument("--conv-algo", type=int, default=0, help="0 Winograd, 1 direct")
@@ -91,45 +83,84 @@ def parse():
                     help="skip the second timed window with the cache bypassed")
     args = ap.parse_args()
     chess = args.game == "chess"
-    for k, c4, ch in (("steps", 30, 3), ("warmup", 60, 2), ("slots", 4096, 256), ("sims", 100, 800)):
+    for k, c4, ch in (("steps", 30, 3), ("warmup", 5, 2), ("slots", 4096, 256), ("sims", 100, 800)):
         if getattr(args, k) is None:
             setattr(args, k, ch if chess else c4)
     return args
 
 
-def cpu_baseline(args, weights):
-    """Reference-structured CPU self-play, bounded sample (about budget seconds)."""
-    import multiprocessing as mp
-    import platform
-
-    import refport
-    cores = len(os.sched_getaffinity(0))
-    workers = args.cpu_workers or max(1, min(15, cores - 1))
-    job = (args.height, args.width, args.n, True, args.sims, weights, args.depth,
-           args.cpu_baseline_seconds)
-    ctx = mp.get_context("fork")  # no GPU initialised yet in this process
-    t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
-        res = pool.map(refport.baseline_worker, [job + (10_000_000 + 1000 * i,) for i in range(workers)])
-    wall = time.perf_counter() - t0
-    games = sum(r[0] for r in res)
-    exps = sum(r[1] for r in res)
-    cpu_model = ""
+def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
-        cpu_model = platform.processor()
+        pass
+    import platform
+    return platform.processor()
+
+
+def cpu_workers(args):
+    """The reference's fan-out is os.cpu_count() - 1 worker processes
+    (self_play.py:98); on a GPU box os.cpu_count() is the whole machine while
+    a job's share is BOX_CPU_SHARE CPUs, so the pool stays inside that share."""
+    total = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0))
+    ref = max(1, total - 1)
+    w = args.cpu_workers or max(1, min(ref, aff - 1, BOX_CPU_SHARE - 1))
+    why = (f"reference n_jobs = os.cpu_count() - 1 = {ref}; this host: os.cpu_count() {total}, "
+           f"affinity {aff}; capped at the box's {BOX_CPU_SHARE}-CPU share - 1" if w < ref else
+           f"reference n_jobs = os.cpu_count() - 1 = {ref}")
+    return w, why
+
+
+def cpu_baseline(args, weights):
+    """Reference-structured CPU self-play, bounded sample (about budget seconds)."""
+    import multiprocessing as mp
+
+    import refport
+    workers, why = cpu_workers(args)
+    job = (args.height, args.width, args.n, True, args.sims, weights, args.depth,
+           args.cpu_baseline_seconds)
+    ctx = mp.get_context("fork")  # no GPU initialised yet in this process
+    with ctx.Manager() as manager:
+        shared = manager.dict()  # plays_inferences = Manager().dict() (utils.py:38-39)
+        t0 = time.perf_counter()
+        with ctx.Pool(workers) as pool:
+            res = pool.map(refport.baseline_worker,
+                           [job + (10_000_000 + 1000 * i, shared) for i in range(workers)])
+        wall = time.perf_counter() - t0
+        entries = len(shared)
+    games = sum(r[0] for r in res)
+    exps = sum(r[1] for r in res)
     return {
         "value": round(games / wall, 4), "unit": "games/s", "cores": workers,
         "kind": "port", "expansions_per_s": round(exps / wall, 1),
+        "cores_reason": why,
         "sample": (f"oracle/refport.py self-play, C4 {args.sims} sims/move, {workers} worker processes "
-                   f"x 1 torch-CPU thread, batch-1 forward, plays_inferences dict kept across each "
-                   f"worker's games; {games} games in "
-                   f"{wall:.1f}s ({cpu_model})"),
+                   f"x 1 torch-CPU thread, batch-1 forward, one plays_inferences Manager dict shared by "
+                   f"all workers ({entries} entries at the end); {games} games in {wall:.1f}s "
+                   f"({_cpu_model()})"),
     }
+
+
+def cpu_configs0(args, weights):
+    """BASELINE configs[0]: C4 via self_play.py, 25 sims/move, 1 CPU worker
+    (mono-process: plays_inferences is a plain dict)."""
+    import multiprocessing as mp
+
+    import refport
+    ctx = mp.get_context("fork")
+    job = (args.height, args.width, args.n, True, 25, weights, args.depth, args.cpu_configs0_seconds,
+           30_000_000, None)
+    t0 = time.perf_counter()
+    with ctx.Pool(1) as pool:
+        games, exps, _ = pool.map(refport.baseline_worker, [job])[0]
+    wall = time.perf_counter() - t0
+    return {"config": "BASELINE.json configs[0]: Connect-4 6x7, 25 sims/move, 1 CPU worker",
+            "value": round(games / wall, 4), "unit": "games/s", "expansions_per_s": round(exps / wall, 1),
+            "cores": 1, "kind": "port",
+            "sample": f"oracle/refport.py, {games} games in {wall:.1f}s ({_cpu_model()})"}
 
 
 def _device_weights(spec, host_w, rank, world, args, dev):
@@ -154,12 +185,83 @@ def _device_weights(spec, host_w, rank, world, args, dev):
     return named, flat
 
 
+def _reduce(values, op, world, args, dev):
+    """All-reduce a list of numbers (float64) over the ranks."""
+    if world == 1:
+        return list(values)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64,
+                     device="cpu" if args.dist_backend == "gloo" else dev)
+    dist.all_reduce(t, op=op)
+    return t.tolist()
+
+
+def conv_kernel_name(conv_algo, chess=False):
+    if conv_algo != 0:
+        return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"
+    k = ("wino16x_conv_kernel (Winograd F(2x2,3x3), fp32 products from three bf16 terms per operand on "
+         "the 16x16x32 bf16 MFMA")
+    return k + (", residual tower, 8 launches per forward)" if chess else
+                ", 16 tiles per workgroup, fused BN/ReLU and 1x1 projection residual)")
+
+
+def conv_roofline(args, conv_algo, boards_per_launch, avg_ms, busy_ms, boards_total, launches,
+                  direct_flop_per_board, issued_per_board, pmc_file, chess=False):
+    """roofline for the residual tower's 3x3 convs (the dominant kernel).
+    achieved = FLOP the kernel issues per launch (boards per launch x issued
+    FLOP per board / 8 launches per forward) / the launch's mean duration
+    (HIP events on its lane's stream); frac against the peak of the pipe it
+    issues on.  The direct-convolution FLOP at the fp32 peak is given beside
+    it as the algorithmic equivalent (SURVEY.md 8d's count)."""
+    n_conv = 2 * args.depth
+    flop, peak, dtype = issued_per_board, (BF16_MFMA_PEAK_TFLOPS if conv_algo == 0 else FP32_MFMA_PEAK_TFLOPS), \
+        ("bf16 (3 terms per fp32 operand, 6 products)" if conv_algo == 0 else "fp32")
+    achieved = boards_per_launch * flop / n_conv / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
+    alg = boards_per_launch * direct_flop_per_board / n_conv / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
+    union = boards_total * flop / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
+    traffic = None
+    if os.path.exists(pmc_file):  # PMC bytes/board (rocprofv3 FETCH_SIZE/WRITE_SIZE) x live batch
+        with open(pmc_file) as fp:
+            tj = json.load(fp)
+        key = "winograd" if conv_algo == 0 else "direct"
+        if key in tj:
+            traffic = int(tj[key]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+    return {
+        "kernel": conv_kernel_name(conv_algo, chess),
+        "bound": "mfma",
+        "achieved": round(achieved, 2),
+        "peak": peak,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / peak, 4),
+        "traffic": traffic,
+        "traffic_unit": f"HBM bytes per launch (PMC bytes/board, {os.path.relpath(pmc_file, REPO)}, "
+                        f"x live boards/launch)",
+        "dtype": dtype,
+        "achieved_basis": "issued MFMA FLOP per launch (boards_per_launch x issued_flop_per_board / "
+                          f"{n_conv} launches) / avg_launch_ms (HIP events on each lane's stream, timed region)",
+        "issued_flop_per_board": int(flop),
+        "algorithmic_equivalent": {
+            "achieved": round(alg, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+            "frac": round(alg / FP32_MFMA_PEAK_TFLOPS, 4),
+            "flop_per_board": int(direct_flop_per_board),
+            "basis": "direct-convolution FLOP (SURVEY.md 8d) per launch / avg_launch_ms, priced at the fp32 "
+                     "MFMA peak: what the layer would need from an fp32 direct convolution (Winograd "
+                     "issues fewer multiplies, so this can exceed 1)"},
+        "busy_union": {"achieved": round(union, 2), "frac": round(union / peak, 4),
+                       "basis": "all timed boards' issued FLOP / union of the conv intervals of all lanes"},
+        "boards_per_launch": round(boards_per_launch, 1),
+        "avg_launch_ms": round(avg_ms, 4),
+        "conv_busy_ms": round(busy_ms, 2),
+        "launches_timed": launches,
+    }
+
+
 def chess_cpu_baseline(args, weights):
     import multiprocessing as mp
 
     import refport
-    cores = len(os.sched_getaffinity(0))
-    workers = args.cpu_workers or max(1, min(15, cores - 1))
+    workers, why = cpu_workers(args)
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
@@ -169,11 +271,22 @@ def chess_cpu_baseline(args, weights):
     wall = time.perf_counter() - t0
     exps = sum(r[0] for r in res)
     return {"value": round(exps / wall, 2), "unit": "expansions/s", "cores": workers, "kind": "port",
+            "cores_reason": why,
             "plies_per_s_est": round(sum(r[1] for r in res) / wall, 4),
             "sample": (f"oracle chess MCTS (C tree, reference arithmetic) + torch-CPU network at batch 1 "
                        f"on Board.full_state, {workers} worker processes x 1 thread, {args.sims} sims/move, "
                        f"{exps} expansions in {wall:.1f}s; the reference's own chess path cannot run "
                        f"under MCTS (chess/board.py:178 vs mcts.py:179)")}
+
+
+def _init_dist(args, world, local_rank):
+    import torch
+    import torch.distributed as dist
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    if world > 1:
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(args.dist_backend)
+    return dev_index, torch.device("cuda", dev_index)
 
 
 def chess_main(args):
@@ -194,11 +307,7 @@ def chess_main(args):
     import torch
     import torch.distributed as dist
     from custom_alphazero import engine as az
-    dev_index = local_rank % max(torch.cuda.device_count(), 1)
-    if world > 1:
-        torch.cuda.set_device(dev_index)
-        dist.init_process_group(args.dist_backend)
-    dev = torch.device("cuda", dev_index)
+    dev_index, dev = _init_dist(args, world, local_rank)
     named, _flat = _device_weights(spec, host_w, rank, world, args, dev)
     eng = az.ChessEngine(mcts_iterations=args.sims, slots=args.slots, evaluator=az.EVAL_NETWORK,
                          max_plies=512, depth=args.depth, device=dev_index, conv_algo=args.conv_algo,
@@ -223,35 +332,23 @@ def chess_main(args):
     d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
                                       "terminal_visits", "evaluations")}
     local_evals = d["evaluations"]
-    if world > 1:
-        red_dev = "cpu" if args.dist_backend == "gloo" else dev
-        t = torch.tensor([d["games_done"], d["expansions"], d["simulations"], d["plies"]],
-                         dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        d["games_done"], d["expansions"], d["simulations"], d["plies"] = (int(v) for v in t.tolist())
-        elapsed = float(tmax.item())
+    g, e, s, p, ev = _reduce([d["games_done"], d["expansions"], d["simulations"], d["plies"],
+                              d["evaluations"]], dist.ReduceOp.SUM if world > 1 else None, world, args, dev)
+    (elapsed,) = _reduce([elapsed], dist.ReduceOp.MAX if world > 1 else None, world, args, dev)
     F, HW, TB = 128, 64, 16
-    conv_flop_per_board = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
-    mfma_flop_per_board = (TB * 36 * 2 * F * F * args.depth if args.conv_algo == 0
-                           else conv_flop_per_board)
-    busy = st1["conv_busy_ms"]
+    direct_flop = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
+    wino_flop = TB * 36 * 2 * F * F * args.depth         # 16 points per 2x2 tile (+4 residual rows / conv2)
+    issued = 6 * wino_flop if args.conv_algo == 0 else direct_flop
     launches = st1["conv_launches"]
     boards_per_launch = local_evals / max(launches / (2 * args.depth), 1)
     avg_ms = st1["conv_ms"] / max(launches, 1)
-    # per launch: algorithmic FLOP of one tower conv / its mean duration (HIP events)
-    achieved = boards_per_launch * conv_flop_per_board / (2 * args.depth) / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
-    union = local_evals * conv_flop_per_board / (busy * 1e-3) / 1e12 if busy else 0.0
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "r1", "pmc_chess_traffic.json")
-    if os.path.exists(pmc):  # PMC bytes/board (FETCH_SIZE/WRITE_SIZE passes) x live batch
-        with open(pmc) as fp:
-            traffic = int(json.load(fp)["winograd"]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+    roof = conv_roofline(args, args.conv_algo, boards_per_launch, avg_ms, st1["conv_busy_ms"], local_evals,
+                         launches, direct_flop, issued,
+                         os.path.join(REPO, "profiles", "r1", "pmc_chess_traffic.json"), chess=True)
     if rank == 0:
         line = {
             "metric": f"MCTS node-expansions/s (Chess, {args.sims} sims/move)",
-            "value": round(d["expansions"] / elapsed, 1),
+            "value": round(e / elapsed, 1),
             "unit": "expansions/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -260,7 +357,7 @@ def chess_main(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32 network / f64 PUCT",
+            "dtype": "fp32-accurate network (fp32 products from 3 bf16 terms on the bf16 MFMA) / f64 PUCT",
             "data": "synthetic (self-generated games, random-init Keras-default weights, torch seed 0)",
             "config": {
                 "workload": (f"Chess (custom_alphazero/chess), {args.sims} sims/move, {args.slots} concurrent "
@@ -269,31 +366,12 @@ def chess_main(args):
                 "global_batch": args.slots * world,
                 "parallelism": f"games sharded over {world} GPU(s)",
             },
-            "plies_per_s": round(d["plies"] / elapsed, 2),
-            "simulations_per_s": round(d["simulations"] / elapsed, 1),
-            "games_timed": d["games_done"],
-            "terminal_visits": d["terminal_visits"],
+            "plies_per_s": round(p / elapsed, 2),
+            "simulations_per_s": round(s / elapsed, 1),
+            "network_evaluations_per_s": round(ev / elapsed, 1),
+            "games_timed": int(g),
             "lanes": args.lanes or "auto",
-            "roofline": {
-                "kernel": conv_kernel_name(args.conv_algo, chess=True),
-                "bound": "mfma",
-                "achieved": round(achieved, 2),
-                "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (PMC bytes/board, profiles/r1/pmc_chess_traffic.json, "
-                                "x live boards/launch)",
-                "achieved_basis": "algorithmic (direct-convolution) FLOP per launch (boards_per_launch x "
-                                  "algorithmic_flop_per_board / 8 tower launches) / avg_launch_ms (HIP events)",
-                "busy_union": {"achieved": round(union, 2), "frac": round(union / FP32_MFMA_PEAK_TFLOPS, 4)},
-                "algorithmic_flop_per_board": conv_flop_per_board,
-                "mfma_flop_per_board": mfma_flop_per_board,
-                "issued": issued_mfma(achieved, conv_flop_per_board, mfma_flop_per_board, args.conv_algo),
-                "boards_per_launch": round(boards_per_launch, 1),
-                "avg_launch_ms": round(avg_ms, 4),
-                "conv_busy_ms": round(busy, 2),
-            },
+            "roofline": roof,
             "cpu_baseline": base,
         }
         if base:
@@ -301,6 +379,33 @@ def chess_main(args):
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+class WindowGames:
+    """The games drained in the timed window (this rank), kept compact for
+    the N>1 replay-buffer gather."""
+
+    def __init__(self):
+        self.parts = []
+
+    def add(self, d):
+        if len(d["lengths"]):
+            self.parts.append(d)
+
+    def results(self):
+        if not self.parts:
+            return None
+        return {k: np.concatenate([p[k] for p in self.parts]) for k in
+                ("lengths", "results", "expansions", "boards", "policies", "moves")}
+
+
+def step_and_drain(eng, sink=None):
+    """One move for every slot, then the D2H copy of the games it finished."""
+    st = eng.selfplay_step(1)
+    d = eng.selfplay_drain()
+    if sink is not None:
+        sink.add(d)
+    return st, len(d["lengths"])
 
 
 def main():
@@ -316,21 +421,20 @@ def main():
     spec = weight_spec(args.height, args.width, A, depth=args.depth)
     host_w = init_weights(spec, seed=0)
 
-    base = None
+    base = base0 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline(args, host_w)
+        if (args.height, args.width, args.n) == (6, 7, 4) and args.cpu_configs0_seconds > 0:
+            base0 = cpu_configs0(args, host_w)
 
     import torch
     import torch.distributed as dist
+    from custom_alphazero import distributed as D
     from custom_alphazero import engine as az
 
-    # one rank per GPU; the modulo only matters when rehearsing several ranks
-    # on a one-GPU box
-    dev_index = local_rank % max(torch.cuda.device_count(), 1)
-    if world > 1:
-        torch.cuda.set_device(dev_index)
-        dist.init_process_group(args.dist_backend)
-    dev = torch.device("cuda", dev_index)
+    SUM = dist.ReduceOp.SUM if world > 1 else None
+    MAX = dist.ReduceOp.MAX if world > 1 else None
+    dev_index, dev = _init_dist(args, world, local_rank)
     # weights: rank 0's init, one flat RCCL broadcast (~5 MB) to every rank
     named, _flat = _device_weights(spec, host_w, rank, world, args, dev)
 
@@ -339,36 +443,79 @@ def main():
                     cache_log2=args.cache_log2, lanes=args.lanes, conv_algo=args.conv_algo)
     eng.set_weights(named)
     tree_steps = 3
-    budget = args.slots * (2 + (args.warmup + 2 * args.steps + tree_steps) // 5)
+    total_moves = MAX_PREROLL + 2 * args.steps + tree_steps + args.warmup
+    budget = args.slots * (2 + total_moves // 7)   # a C4 game lasts >= 7 plies
     eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)
 
-    eng.selfplay_step(args.warmup)
+    # ---- untimed: at least --warmup moves, until the cache is stationary
+    pre = 0
+    while True:
+        st, _ = step_and_drain(eng)
+        pre += 1
+        gen_ok = (not args.cache_log2 or not st["cache_gen_size"]
+                  or st["cache_generation"] >= CACHE_TURNOVER_GENS)
+        done = pre >= max(args.warmup, MIN_PREROLL) and gen_ok
+        if world > 1:  # every rank runs the same number of untimed moves
+            (done,) = _reduce([0.0 if done else 1.0], SUM, world, args, dev)
+            done = done == 0.0
+        if done or pre >= MAX_PREROLL:
+            break
+
+    # ---- timed window: K steps, each drained to the host
+    window = WindowGames()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     eng.timer(True)
     st0 = eng.stats()
     t0 = time.perf_counter()
-    eng.selfplay_step(args.steps)
+    drained = 0
+    for _ in range(args.steps):
+        _, k = step_and_drain(eng, window)
+        drained += k
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st1 = eng.stats()
     eng.timer(False)
+    d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
+                                      "terminal_visits", "cache_hits", "evaluations", "cache_inserts")}
+    local_evals = d["evaluations"]
+    conv_ms, conv_launches, busy_ms = st1["conv_ms"], st1["conv_launches"], st1["conv_busy_ms"]
 
-    # tree kernels (select + expand: latency/HBM-bound) timed with HIP events
-    # in a short window of their own (4 more events per simulation), priced
-    # with SURVEY.md 8d's algorithmic bytes per simulation
+    # ---- N>1: the window's games to rank 0 (replay-buffer gather, RCCL)
+    gather = None
+    if world > 1:
+        t_g = time.perf_counter()
+        res = window.results()
+        if res is None:
+            res = {"lengths": np.zeros(0, np.int32), "results": np.zeros(0, np.int32),
+                   "expansions": np.zeros(0, np.int32),
+                   "boards": np.zeros((0, args.height * args.width, args.height, args.width), np.int8),
+                   "policies": np.zeros((0, args.height * args.width, A)),
+                   "moves": np.zeros((0, args.height * args.width), np.int32)}
+        g = D.gather_games(res, device=None if args.dist_backend == "gloo" else dev)
+        gt = time.perf_counter() - t_g
+        if rank == 0:
+            gather = {"games": int(len(g["lengths"])), "samples": int(len(g["moves"])),
+                      "bytes": int(g["boards"].nbytes + g["policies"].nbytes + g["moves"].nbytes),
+                      "seconds": round(gt, 4),
+                      "how": f"compact int8 boards + f64 policies + int16 moves, all_gather over "
+                             f"{args.dist_backend} after the timed window (distributed.gather_games)"}
+
+    # ---- tree kernels (select + expand: latency/HBM-bound) timed with HIP
+    # events in a short window of their own (4 more events per simulation),
+    # priced with SURVEY.md 8d's algorithmic bytes per simulation
     eng.timer(True, tree=True)
     sa = eng.stats()
-    eng.selfplay_step(tree_steps)
+    for _ in range(tree_steps):
+        step_and_drain(eng)
     sb = eng.stats()
     eng.timer(False)
     sims_t = max(sb["simulations"] - sa["simulations"], 1)
     depth = (sb["path_edges"] - sa["path_edges"]) / sims_t
     f_exp = (sb["expansions"] - sa["expansions"]) / sims_t
-    A = args.width
     bytes_per_sim = 16 * A * depth + 24 * depth + f_exp * (16 * A + 672 + 672 + 64)
     tree_gbs = bytes_per_sim * sims_t / (sb["tree_ms"] * 1e-3) / 1e9 if sb["tree_ms"] else 0.0
     roofline_tree = {
@@ -384,79 +531,55 @@ def main():
                  "each path), not bandwidth-bound",
     }
 
-    # second window, same slots continuing, cache bypassed: the rate without
-    # the reference's plays_inferences semantics (every leaf evaluated)
+    # ---- second window, same slots continuing, cache bypassed: the rate
+    # without the reference's plays_inferences semantics (every leaf evaluated)
     off = None
     if args.cache_log2 and not args.no_cache_window:
         eng.cache_enable(False)
         if world > 1:
             dist.barrier()
+        torch.cuda.synchronize()
         s0 = eng.stats()
-        t0 = time.perf_counter()
-        eng.selfplay_step(args.steps)
+        t2 = time.perf_counter()
+        g2 = 0
+        for _ in range(args.steps):
+            g2 += step_and_drain(eng)[1]
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        el2 = time.perf_counter() - t0
+        el2 = time.perf_counter() - t2
         s1 = eng.stats()
-        g2 = s1["games_done"] - s0["games_done"]
-        if world > 1:
-            t2 = torch.tensor([g2, el2], dtype=torch.float64,
-                              device="cpu" if args.dist_backend == "gloo" else dev)
-            dist.all_reduce(t2[:1], op=dist.ReduceOp.SUM)
-            tm = t2[1:].clone()
-            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-            g2, el2 = int(t2[0].item()), float(tm.item())
+        g2, e2 = _reduce([g2, s1["expansions"] - s0["expansions"]], SUM, world, args, dev)
+        (el2,) = _reduce([el2], MAX, world, args, dev)
         off = {"value": round(g2 / el2, 3), "unit": "games/s", "ms_per_step": round(1e3 * el2 / args.steps, 3),
-               "expansions_per_s": round((s1["expansions"] - s0["expansions"]) / el2 * world, 1)}
+               "expansions_per_s": round(e2 / el2, 1)}
 
-    d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
-                                      "terminal_visits", "cache_hits", "evaluations")}
-    conv_ms, conv_launches = st1["conv_ms"], st1["conv_launches"]
-    if world > 1:
-        red_dev = "cpu" if args.dist_backend == "gloo" else dev
-        t = torch.tensor([d["games_done"], d["expansions"], d["simulations"], d["plies"]],
-                         dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        d["games_done"], d["expansions"], d["simulations"], d["plies"] = (int(v) for v in t.tolist())
-        elapsed = float(tmax.item())
+    tot = _reduce([drained, d["games_done"], d["expansions"], d["simulations"], d["plies"], d["cache_hits"],
+                   d["evaluations"]], SUM, world, args, dev)
+    drained_all, games_all, exp_all, sims_all, plies_all, hits_all, evals_all = tot
+    (elapsed,) = _reduce([elapsed], MAX, world, args, dev)
     if st1["active_slots"] < args.slots:
         print(f"warning: rank {rank} ran out of game budget", file=sys.stderr)
 
     # dominant kernel: the residual tower's 3x3 convs (8 launches per forward at
-    # depth 4).  Algorithmic FLOP = the direct convolution (SURVEY.md 8d, 19 F*F
-    # MACs per pixel per block: 9F + 9F + the 1x1 F); the Winograd kernel issues
-    # fewer MFMA FLOP (16 points per 2x2 tile + 4 residual rows per conv2).
+    # depth 4).  Direct FLOP = SURVEY.md 8d's count (19 F*F MACs per pixel per
+    # block: 9F + 9F + the 1x1 F); the Winograd kernel issues 16 points per
+    # 2x2 tile (+ 4 residual pixel rows in conv2), each as six bf16 products.
     HW, F = args.height * args.width, 128
     TB = ((args.height + 1) // 2) * ((args.width + 1) // 2)
-    conv_flop_per_board = HW * 2 * F * F * 19 * args.depth
-    mfma_flop_per_board = (TB * 36 * 2 * F * F * args.depth if args.conv_algo == 0
-                           else conv_flop_per_board)
-    local_exp = st1["evaluations"] - st0["evaluations"]  # boards the network computed
+    direct_flop = HW * 2 * F * F * 19 * args.depth
+    wino_flop = TB * 36 * 2 * F * F * args.depth
+    issued = 6 * wino_flop if args.conv_algo == 0 else direct_flop
     conv_avg_ms = conv_ms / max(conv_launches, 1)
-    busy_ms = st1["conv_busy_ms"]
-    boards_per_launch = local_exp / max(conv_launches / (2 * args.depth), 1)
-    # roofline.achieved: algorithmic FLOP of one launch (a conv of the tower,
-    # the mean of conv1 and conv2) / the launch's mean duration (HIP events
-    # on its lane's stream); with two lanes a launch shares the CUs with the
-    # other lane's kernels, so the union-of-busy-time rate is given beside it
-    per_launch_flop = boards_per_launch * conv_flop_per_board / (2 * args.depth)
-    achieved = per_launch_flop / (conv_avg_ms * 1e-3) / 1e12 if conv_avg_ms else 0.0
-    union = (local_exp * conv_flop_per_board) / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "r1", "pmc_conv_traffic.json")
-    if os.path.exists(pmc):  # PMC bytes/board (rocprofv3 FETCH_SIZE/WRITE_SIZE) x live batch
-        with open(pmc) as fp:
-            tj = json.load(fp)
-        key = "winograd" if args.conv_algo == 0 else "direct"
-        if key in tj:
-            traffic = int(tj[key]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+    boards_per_launch = local_evals / max(conv_launches / (2 * args.depth), 1)
+    pmc = os.path.join(REPO, "profiles", "r2", "pmc_conv_traffic.json")
+    if not os.path.exists(pmc):
+        pmc = os.path.join(REPO, "profiles", "r1", "pmc_conv_traffic.json")
+    roof = conv_roofline(args, args.conv_algo, boards_per_launch, conv_avg_ms, busy_ms, local_evals,
+                         conv_launches, direct_flop, issued, pmc)
 
     # the same kernels alone on one stream at the live per-lane batch (what a
     # launch costs without the other lane's kernels sharing the CUs)
-    isolated = None
     if rank == 0:
         nb = max(1, int(round(boards_per_launch)))
         rng = np.random.RandomState(1)
@@ -469,11 +592,15 @@ def main():
         si = eng.stats()
         eng.timer(False)
         iso_ms = si["conv_ms"] / max(si["conv_launches"], 1)
-        iso = nb * conv_flop_per_board / (2 * args.depth) / (iso_ms * 1e-3) / 1e12
-        isolated = {"boards": nb, "avg_launch_ms": round(iso_ms, 4),
-                    "achieved": round(iso, 2), "frac": round(iso / FP32_MFMA_PEAK_TFLOPS, 4),
-                    "issued": issued_mfma(iso, conv_flop_per_board, mfma_flop_per_board, args.conv_algo)}
+        iso = nb * issued / (2 * args.depth) / (iso_ms * 1e-3) / 1e12
+        roof["isolated"] = {"boards": nb, "avg_launch_ms": round(iso_ms, 4), "achieved": round(iso, 2),
+                            "frac": round(iso / roof["peak"], 4)}
 
+    cap = st1["cache_capacity"]
+    gen_size = st1["cache_gen_size"]
+    gen = st1["cache_generation"]
+    live = (st1["cache_inserts"] - gen * gen_size + (gen_size if gen >= 1 else 0)) if gen_size else \
+        st1["cache_inserts"]
     game_name = "Connect-4 6x7" if (args.height, args.width, args.n) == (6, 7, 4) else \
         f"Connect-{args.n} {args.height}x{args.width}"
     cfg_ref = {(6, 7, 4, 100): "BASELINE.json configs[1]", (9, 9, 5, 200): "BASELINE.json configs[2]",
@@ -482,7 +609,7 @@ def main():
     if rank == 0:
         line = {
             "metric": f"self-play games/s ({game_name}, {args.sims} sims/move)",
-            "value": round(d["games_done"] / elapsed, 3),
+            "value": round(drained_all / elapsed, 3),
             "unit": "games/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -491,7 +618,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32 network / f64 PUCT",
+            "dtype": "fp32-accurate network (fp32 products from 3 bf16 terms on the bf16 MFMA) / f64 PUCT",
             "data": "synthetic (self-generated games, random-init Keras-default weights, torch seed 0)",
             "config": {
                 "workload": (f"{game_name} n={args.n} gravity, {args.sims} sims/move, "
@@ -500,45 +627,37 @@ def main():
                 "global_batch": args.slots * world,
                 "parallelism": f"games sharded over {world} GPU(s)",
             },
-            "expansions_per_s": round(d["expansions"] / elapsed, 1),
-            "simulations_per_s": round(d["simulations"] / elapsed, 1),
-            "plies_per_s": round(d["plies"] / elapsed, 1),
-            "games_timed": d["games_done"],
-            "network_evaluations_per_s": round(d["evaluations"] / elapsed, 1),
-            "transposition_cache": ({"entries": 2 ** args.cache_log2,
-                                     "hit_rate": round(d["cache_hits"] / max(d["expansions"], 1), 4),
-                                     "semantics": "reference plays_inferences (mcts.py:122-143): board -> "
-                                                  "network output, shared by all games, emptied when "
-                                                  "weights change; bit-identical results"}
-                                    if args.cache_log2 else None),
+            "untimed_moves": pre,
+            "untimed_rule": (f"max(--warmup, {MIN_PREROLL}) moves and until the transposition cache has "
+                             f"turned over {CACHE_TURNOVER_GENS} eviction generations (stationary hit rate)"),
+            "games_timed": int(drained_all),
+            "games_timed_basis": "games whose samples reached the host in the window (az_selfplay_drain "
+                                 "after every step, D2H inside the timed region)",
+            "games_finished_on_device": int(games_all),
+            "expansions_per_s": round(exp_all / elapsed, 1),
+            "simulations_per_s": round(sims_all / elapsed, 1),
+            "plies_per_s": round(plies_all / elapsed, 1),
+            "network_evaluations_per_s": round(evals_all / elapsed, 1),
+            "transposition_cache": ({
+                "capacity": cap,
+                "hit_rate": round(hits_all / max(exp_all, 1), 4),
+                "eviction": ({"inserts_per_generation": gen_size, "live_generations": 2,
+                              "rule": "lookups use the current and previous generation; inserts reuse "
+                                      "entries 3+ generations old (az_tree.h)"} if gen_size else None),
+                "generation_at_window_end": gen,
+                "live_entries": int(live),
+                "fill": round(live / cap, 4) if cap else None,
+                "age_moves_at_window_start": pre,
+                "inserts_in_window": d["cache_inserts"],
+                "semantics": "reference plays_inferences (mcts.py:122-143): board -> network output, shared "
+                             "by all games on the GPU, emptied when weights change; bit-identical results",
+            } if args.cache_log2 else None),
             "cache_off": off,
             "roofline_tree": roofline_tree,
-            "roofline": {
-                "kernel": conv_kernel_name(args.conv_algo),
-                "bound": "mfma",
-                "achieved": round(achieved, 2),
-                "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (PMC bytes/board, profiles/r1/pmc_conv_traffic.json, "
-                                "x live boards/launch)",
-                "achieved_basis": "algorithmic (direct-convolution) FLOP per launch (boards_per_launch x "
-                                  "algorithmic_flop_per_board / 8 launches) / avg_launch_ms (HIP events on "
-                                  "each lane's stream, timed region)",
-                "busy_union": {"achieved": round(union, 2), "frac": round(union / FP32_MFMA_PEAK_TFLOPS, 4),
-                               "basis": "all timed boards' algorithmic FLOP / union of the conv intervals of "
-                                        "both lanes (launches of the two lanes overlap)"},
-                "algorithmic_flop_per_board": conv_flop_per_board,
-                "mfma_flop_per_board": mfma_flop_per_board,
-                "issued": issued_mfma(achieved, conv_flop_per_board, mfma_flop_per_board, args.conv_algo),
-                "boards_per_launch": round(boards_per_launch, 1),
-                "avg_launch_ms": round(conv_avg_ms, 4),
-                "conv_busy_ms": round(busy_ms, 2),
-                "launches_timed": conv_launches,
-                "isolated": isolated,
-            },
+            "roofline": roof,
+            "replay_buffer_gather": gather,
             "cpu_baseline": base,
+            "cpu_baseline_configs0": base0,
         }
         if base:
             line["gpu_over_cpu"] = round(line["value"] / base["value"], 1) if base["value"] else None

@@ -60,6 +60,7 @@ struct Lane {
   float* values = nullptr;
   az::ConvTimer timer;
   az::ConvTimer tree_timer;  // select and expand launches (bench.py roofline_tree)
+  hipEvent_t move_done[3] = {nullptr, nullptr, nullptr};  // end of move m on this lane, m mod 3
 };
 
 struct az_engine {
@@ -86,6 +87,11 @@ struct az_engine {
   std::vector<hipStream_t> lane_streams;
   hipEvent_t timer_ref = nullptr;  // common origin of every ConvTimer's intervals
   int64_t sp_first = 0, sp_n = 0;
+  int64_t moves_issued = 0;        // self-play moves enqueued (lane drift bound, az_tree.h)
+  int64_t drained = 0;             // finished games az_selfplay_drain has returned
+  uint8_t* drain_dev = nullptr;    // packed records (device) and their pinned host copy
+  uint8_t* drain_host = nullptr;
+  size_t drain_cap = 0;            // records the two buffers hold
 
   template <typename T>
   int alloc(T** p, size_t count) {
@@ -180,6 +186,7 @@ int cache_clear(az_engine* e) {
   int rc;
   if ((rc = sync_all(e))) return rc;
   AZ_HIP(hipMemsetAsync(e->cache.state, 0, ((size_t)e->cache.mask + 1) * sizeof(uint32_t), e->stream));
+  AZ_HIP(hipMemsetAsync(e->cache.ctl, 0, 2 * sizeof(unsigned long long), e->stream));
   AZ_HIP(hipStreamSynchronize(e->stream));
   return 0;
 }
@@ -612,11 +619,17 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
     const size_t cap = (size_t)1 << c.cache_log2;
     az::CacheDev& cd = e->cache;
     if ((rc = e->alloc(&cd.keys, cap)) || (rc = e->alloc(&cd.state, cap)) ||
-        (rc = e->alloc(&cd.pay, cap * (A + 1))))
+        (rc = e->alloc(&cd.pay, cap * (A + 1))) || (rc = e->alloc(&cd.ctl, 2)))
       return cleanup(rc);
     cd.mask = (uint32_t)(cap - 1);
     cd.enabled = 1;
-    if (hipMemset(cd.state, 0, cap * sizeof(uint32_t)) != hipSuccess)
+    // eviction by generations of cap/8 inserts, when a generation outlasts
+    // three moves of every slot's inserts (the lane-drift bound, az_tree.h);
+    // otherwise the table only fills (entries are never overwritten)
+    const unsigned long long gen = cap / 8;
+    cd.gen_size = gen > 3ull * (unsigned long long)g.slots * (unsigned long long)g.sims ? gen : 0;
+    if (hipMemset(cd.state, 0, cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(cd.ctl, 0, 2 * sizeof(unsigned long long)) != hipSuccess)
       return cleanup(fail(AZ_E_HIP, "cache memset failed"));
   }
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
@@ -660,6 +673,9 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
         return cleanup(fail(AZ_E_HIP, "hipStreamCreate failed"));
       e->lane_streams.push_back(st);
       L->stream = st;
+      for (hipEvent_t& ev : L->move_done)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+          return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
     }
   }
   e->net.hidden = c.value_hidden;
@@ -675,8 +691,13 @@ int az_engine_destroy(az_engine* eng) {
     (void)hipStreamSynchronize(s);
     (void)hipStreamDestroy(s);
   }
-  for (Lane* L : eng->lanes)
+  for (Lane* L : eng->lanes) {
+    for (hipEvent_t ev : L->move_done)
+      if (ev) (void)hipEventDestroy(ev);
     if (L != &eng->whole) delete L;
+  }
+  if (eng->drain_dev) (void)hipFree(eng->drain_dev);
+  if (eng->drain_host) (void)hipHostFree(eng->drain_host);
   for (void* p : eng->sample_bufs) (void)hipFree(p);
   for (void* p : eng->owned) (void)hipFree(p);
   if (eng->timer_ref) (void)hipEventDestroy(eng->timer_ref);
@@ -791,6 +812,15 @@ int az_stats_get(az_engine* e, az_stats* st) {
   st->path_edges = (int64_t)h[az::kStatPathEdges];
   st->cache_hits = (int64_t)h[az::kStatCacheHits];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
+  if (e->cache.ctl) {
+    unsigned long long ctl[2];
+    AZ_HIP(hipMemcpy(ctl, e->cache.ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+    st->cache_generation = (int64_t)ctl[0];
+    st->cache_inserts = (int64_t)ctl[1];
+    st->cache_gen_size = (int64_t)e->cache.gen_size;
+    st->cache_capacity = (int64_t)e->cache.mask + 1;
+  }
+  st->games_drained = e->drained;
   return 0;
 }
 
@@ -871,8 +901,11 @@ int az_selfplay_begin(az_engine* e, int64_t first_game, int64_t n_games, uint32_
       (rc = get((void**)&smp.moves, G * P * sizeof(int16_t))) ||
       (rc = get((void**)&smp.length, G * sizeof(int32_t))) ||
       (rc = get((void**)&smp.result, G * sizeof(int32_t))) ||
-      (rc = get((void**)&smp.expansions, G * sizeof(int32_t))))
+      (rc = get((void**)&smp.expansions, G * sizeof(int32_t))) ||
+      (rc = get((void**)&smp.done_ids, G * sizeof(int64_t))) ||
+      (rc = get((void**)&smp.done_count, sizeof(unsigned long long))))
     return rc;
+  e->drained = 0;
   unsigned long long st[az::kStatCount] = {0};
   const int64_t first_wave = std::min<int64_t>(n_games, e->g.slots);
   st[az::kStatNextGame] = (unsigned long long)(first_game + first_wave);
@@ -890,12 +923,23 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
   int rc;
   if ((rc = ready_to_search(e))) return rc;
   AZ_HIP(hipSetDevice(e->device));
+  const bool multi = e->lanes.size() > 1;
   for (int mv = 0; mv < n_moves; ++mv) {
+    const int64_t m = e->moves_issued++;
+    // a lane starts move m once every other lane has finished move m - 2:
+    // lanes drift at most two moves apart (the cache eviction bound, az_tree.h)
+    if (multi && m >= 2)
+      for (Lane* L : e->lanes)
+        for (Lane* O : e->lanes)
+          if (O != L) AZ_HIP(hipStreamWaitEvent(L->stream, O->move_done[(m - 2) % 3], 0));
     // lanes interleaved per simulation so every stream always has work queued
     for (int s = 0; s < e->g.sims; ++s)
       for (Lane* L : e->lanes)
         if ((rc = simulate(e, *L))) return rc;
-    for (Lane* L : e->lanes) az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
+    for (Lane* L : e->lanes) {
+      az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
+      if (multi) AZ_HIP(hipEventRecord(L->move_done[m % 3], L->stream));
+    }
     AZ_HIP(hipGetLastError());
   }
   if ((rc = sync_all(e))) return rc;
@@ -939,6 +983,54 @@ int az_selfplay_results(az_engine* e, int32_t* lengths, int32_t* results, int32_
     AZ_HIP(hipMemcpy(hm.data(), smp.moves, hm.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < hm.size(); ++i) moves[i] = hm[i];
   }
+  return 0;
+}
+
+int az_selfplay_drain(az_engine* e, int64_t max_games, int64_t* n_out, int64_t* game_ids, int32_t* lengths,
+                      int32_t* results, int32_t* expansions, int8_t* boards, double* policies,
+                      int32_t* moves) {
+  if (!e || !n_out || max_games < 0) return fail(AZ_E_INVALID, "bad arguments");
+  *n_out = 0;
+  if (!e->smp.done_count) return 0;  // no self-play batch begun
+  AZ_HIP(hipSetDevice(e->device));
+  int rc;
+  if ((rc = sync_all(e))) return rc;
+  unsigned long long done = 0;
+  AZ_HIP(hipMemcpy(&done, e->smp.done_count, sizeof(done), hipMemcpyDeviceToHost));
+  const int64_t n = std::min<int64_t>((int64_t)done - e->drained, max_games);
+  if (n <= 0) return 0;
+  const size_t rec = az::drain_record_bytes(e->g);
+  if ((size_t)n > e->drain_cap) {
+    if (e->drain_dev) AZ_HIP(hipFree(e->drain_dev));
+    if (e->drain_host) AZ_HIP(hipHostFree(e->drain_host));
+    e->drain_dev = nullptr;
+    e->drain_host = nullptr;
+    e->drain_cap = 0;
+    const size_t cap = std::max<size_t>((size_t)n, 1024);
+    AZ_HIP(hipMalloc(&e->drain_dev, cap * rec));
+    AZ_HIP(hipHostMalloc(&e->drain_host, cap * rec, hipHostMallocDefault));
+    e->drain_cap = cap;
+  }
+  az::launch_drain_pack(e->g, e->smp, e->drained, (int)n, e->drain_dev, e->stream);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipMemcpyAsync(e->drain_host, e->drain_dev, (size_t)n * rec, hipMemcpyDeviceToHost, e->stream));
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  const size_t HW = (size_t)e->g.HW, A = (size_t)e->g.A;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint8_t* r = e->drain_host + (size_t)i * rec;
+    const int32_t* h = reinterpret_cast<const int32_t*>(r + 8);
+    if (game_ids) memcpy(game_ids + i, r, sizeof(int64_t));
+    if (lengths) lengths[i] = h[0];
+    if (results) results[i] = h[1];
+    if (expansions) expansions[i] = h[2];
+    if (policies) memcpy(policies + i * HW * A, r + 24, HW * A * sizeof(double));
+    const int16_t* mv = reinterpret_cast<const int16_t*>(r + 24 + 8 * HW * A);
+    if (moves)
+      for (size_t p = 0; p < HW; ++p) moves[i * HW + p] = mv[p];
+    if (boards) memcpy(boards + i * HW * HW, mv + HW, HW * HW);
+  }
+  e->drained += n;
+  *n_out = n;
   return 0;
 }
 

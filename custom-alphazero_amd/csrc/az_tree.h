@@ -32,7 +32,7 @@ enum : int {
   kStatNNEvals = 8,      // boards the evaluator actually computed
   kStatCacheInserts = 9,
   kStatPathEdges = 10,   // edges on the selected paths (sum of select depths)
-  kStatCount = 12
+  kStatCount = 12        // (kStatCacheInserts counts since engine creation; CacheDev::ctl since a clear)
 };
 enum : unsigned long long {
   kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16
@@ -79,7 +79,31 @@ struct TreeDev {
 // utils.py:38-39): board -> (probs[A], value), shared by every game on the
 // device, cleared when the weights change.  Open addressing, linear probing.
 // The evaluator is deterministic per board, so hits never change a search.
+//
+// Eviction by generations (the reference's dict grows without bound until
+// the next model; a fixed table would fill up and every miss would then
+// probe to max_probe).  Each `gen_size` inserts start a new generation;
+// lookups use entries of the current and previous generation only, and an
+// insert may overwrite an entry at least kCacheReuseAge generations old.  A
+// reader checks liveness in select and reads the payload in expand, one
+// simulation later; an overwrite in between needs kCacheReuseAge - 1 = 2
+// generation turns inside that window, i.e. 2 * gen_size inserts.  The engine
+// bounds the drift between lanes to two moves (move events, az_engine.hip)
+// and enables eviction only when 2 * gen_size > lanes' inserts in three moves
+// (slots * sims * 3), so a payload is never overwritten while a reader holds
+// its index.
+//
+// State word: [31:16] 16-bit fingerprint (hash bits 48-63, so most probes
+// need no key read), [15:2] generation mod 2^14, [1:0] status.
 enum : uint32_t { kCacheEmpty = 0, kCacheClaimed = 1, kCacheReady = 2 };
+constexpr uint32_t kCacheGenMask = 0x3fff;
+constexpr uint32_t kCacheLiveGens = 2;  // age 0 (current) and 1 are looked up
+constexpr uint32_t kCacheReuseAge = 3;  // age >= 3 may be overwritten
+AZ_HD uint32_t cache_fp(uint64_t h) { return (uint32_t)(h >> 48); }
+AZ_HD uint32_t cache_age(uint32_t st, uint32_t gen) { return (gen - (st >> 2)) & kCacheGenMask; }
+AZ_HD uint32_t cache_word(uint32_t fp, uint32_t gen, uint32_t status) {
+  return (fp << 16) | ((gen & kCacheGenMask) << 2) | status;
+}
 struct CacheDev {
   Board* keys = nullptr;       // [cap]
   uint32_t* state = nullptr;   // [cap]
@@ -87,6 +111,8 @@ struct CacheDev {
   uint32_t mask = 0;           // cap - 1
   int enabled = 0;
   int max_probe = 32;
+  unsigned long long* ctl = nullptr;  // device [0] generation, [1] inserts since the last clear
+  unsigned long long gen_size = 0;    // inserts per generation; 0 = no eviction
 };
 
 // Self-play sample sink, indexed by game id - first_game.
@@ -99,7 +125,17 @@ struct SampleDev {
   int32_t* length = nullptr;   // [n_games]
   int32_t* result = nullptr;   // [n_games]: get_result(keep_same_player=True)
   int32_t* expansions = nullptr;  // [n_games]
+  int64_t* done_ids = nullptr;    // [n_games] game ids in the order they finished
+  unsigned long long* done_count = nullptr;  // [1]
 };
+
+// Finished games [from, from + n) of smp.done_ids packed for one D2H copy
+// (az_selfplay_drain): ids, lengths, results, expansions, then per game
+// HW plies of int8 cells (row-major, canonical), f64 policies [HW][A] and
+// int16 moves.  Layout of one record: drain_record_bytes().
+size_t drain_record_bytes(const GameCfg& g);
+void launch_drain_pack(const GameCfg& g, const SampleDev& smp, int64_t from, int n, uint8_t* out,
+                       hipStream_t s);
 
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s);
 // cache on: misses are deduplicated inside select (step tag table); this

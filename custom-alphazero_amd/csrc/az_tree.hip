@@ -123,23 +123,31 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   // concurrently by another lane's insert kernel: the acquire load pairs with
   // its release exchange, so a Ready entry's key and payload are complete
   // (a Claimed one reads as absent: the leaf is evaluated here, same result).
-  uint32_t idx = (uint32_t)board_hash(b) & c.mask;
-  for (int p = 0; p < c.max_probe; ++p) {
-    const uint32_t st = __hip_atomic_load(c.state + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (st == kCacheEmpty) break;
-    if (st == kCacheReady && same_board(c.keys[idx], b)) {
-      t.eval_src[q] = (int32_t)idx;
-      stat_add(t, kStatCacheHits, 1);
-      return;
+  // Only live generations count (az_tree.h); older entries are skipped, not
+  // treated as the end of the probe chain.
+  const uint64_t h = board_hash(b);
+  {
+    const uint32_t gen =
+        (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t fp = cache_fp(h);
+    uint32_t idx = (uint32_t)h & c.mask;
+    for (int p = 0; p < c.max_probe; ++p) {
+      const uint32_t st = __hip_atomic_load(c.state + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (st == kCacheEmpty) break;
+      if ((st & 3u) == kCacheReady && (st >> 16) == fp && cache_age(st, gen) < kCacheLiveGens &&
+          same_board(c.keys[idx], b)) {
+        t.eval_src[q] = (int32_t)idx;
+        stat_add(t, kStatCacheHits, 1);
+        return;
+      }
+      idx = (idx + 1) & c.mask;
     }
-    idx = (idx + 1) & c.mask;
   }
   // miss: one evaluator row per distinct board in this simulation.  Tag =
   // (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
   // empty, so the table needs no clearing.  A tag match is only a candidate:
   // dedup_resolve compares the full boards after this kernel.
   atomicAdd(t.miss_count, 1);
-  const uint64_t h = board_hash(b);
   const uint64_t tag = ((uint64_t)t.epoch << 32) | (uint32_t)(h >> 32);
   uint32_t slot = (uint32_t)h & t.step_mask;
   for (uint32_t p = 0; p <= t.step_mask; ++p) {
@@ -319,23 +327,32 @@ __global__ __launch_bounds__(256) void dedup_resolve_kernel(GameCfg g, TreeDev t
 
 // ------------------------------------------------------------ cache insert
 // plays_inferences[repr(board)] = probabilities, value (mcts.py:142): one
-// writer per distinct board (dedup), racing only for empty slots.
+// writer per distinct board (dedup), racing only for empty slots or slots
+// whose entry is kCacheReuseAge generations old (az_tree.h).
 __global__ __launch_bounds__(256) void cache_insert_kernel(GameCfg g, TreeDev t, CacheDev c,
                                                            const float* __restrict__ probs,
                                                            const float* __restrict__ values) {
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= *t.nn_count) return;
   const Board b = t.nn_board[u];
-  uint32_t idx = (uint32_t)board_hash(b) & c.mask;
+  const uint64_t h = board_hash(b);
+  const uint32_t gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t fp = cache_fp(h);
+  uint32_t idx = (uint32_t)h & c.mask;
   for (int p = 0; p < c.max_probe; ++p) {
-    if (atomicCAS(c.state + idx, kCacheEmpty, kCacheClaimed) == kCacheEmpty) {
+    const uint32_t st = __hip_atomic_load(c.state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool reusable = st == kCacheEmpty || (c.gen_size && cache_age(st, gen) >= kCacheReuseAge);
+    if (reusable && atomicCAS(c.state + idx, st, cache_word(fp, gen, kCacheClaimed)) == st) {
       c.keys[idx] = b;
       float* dst = c.pay + (size_t)idx * (g.A + 1);
       for (int a = 0; a < g.A; ++a) dst[a] = probs[(size_t)u * g.A + a];
       dst[g.A] = values[u];
       __threadfence();
-      atomicExch(c.state + idx, kCacheReady);
+      atomicExch(c.state + idx, cache_word(fp, gen, kCacheReady));
       stat_add(t, kStatCacheInserts, 1);
+      // every gen_size-th insert since the clear opens a new generation
+      const unsigned long long n = atomicAdd(c.ctl + 1, 1ull) + 1;
+      if (c.gen_size && n % c.gen_size == 0) atomicAdd(c.ctl, 1ull);
       return;
     }
     idx = (idx + 1) & c.mask;
@@ -498,6 +515,7 @@ __global__ __launch_bounds__(64) void play_kernel(GameCfg g, TreeDev t, SampleDe
     smp.length[gi] = ply + 1;
     smp.result[gi] = status == kWin ? 1 : 0;
     smp.expansions[gi] = t.slot_expansions[s];
+    if (smp.done_ids) smp.done_ids[atomicAdd(smp.done_count, 1ull)] = gid;
   }
   stat_add(t, kStatGamesDone, 1);
   if (!refill) {
@@ -537,6 +555,52 @@ __global__ void slot_set_root_kernel(GameCfg g, TreeDev t, const int32_t* slots,
 __global__ void slot_release_kernel(TreeDev t, const int32_t* slots, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) t.game_id[slots[i]] = -1;
+}
+
+// ------------------------------------------------------------ sample drain
+// One workgroup per finished game: the game's record (drain_record_bytes)
+// with its boards as int8 cells (+1 side to move, -1 opponent), the layout
+// az_selfplay_results returns, so the host does no per-ply work.
+size_t drain_record_bytes(const GameCfg& g) {
+  const size_t b = 24 + (size_t)8 * g.HW * g.A + (size_t)2 * g.HW + (size_t)g.HW * g.HW;
+  return (b + 15) & ~(size_t)15;
+}
+
+__global__ __launch_bounds__(256) void drain_pack_kernel(GameCfg g, SampleDev smp, int64_t from,
+                                                         uint8_t* __restrict__ out, size_t rec) {
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int64_t gid = smp.done_ids[from + i];
+  const size_t gi = (size_t)(gid - smp.first_game);
+  uint8_t* r = out + (size_t)i * rec;
+  const int T = smp.length[gi];
+  if (tid == 0) {
+    *reinterpret_cast<int64_t*>(r) = gid;
+    int32_t* h = reinterpret_cast<int32_t*>(r + 8);
+    h[0] = T;
+    h[1] = smp.result[gi];
+    h[2] = smp.expansions[gi];
+    h[3] = 0;
+  }
+  double* pol = reinterpret_cast<double*>(r + 24);
+  const double* src = smp.policy + gi * g.HW * g.A;
+  for (int k = tid; k < g.HW * g.A; k += blockDim.x) pol[k] = k < T * g.A ? src[k] : 0.0;
+  int16_t* mv = reinterpret_cast<int16_t*>(r + 24 + (size_t)8 * g.HW * g.A);
+  for (int k = tid; k < g.HW; k += blockDim.x) mv[k] = k < T ? smp.moves[gi * g.HW + k] : (int16_t)0;
+  int8_t* cells = reinterpret_cast<int8_t*>(mv + g.HW);
+  for (int k = tid; k < g.HW * g.HW; k += blockDim.x) {
+    const int p = k / g.HW, c = k - p * g.HW;
+    int8_t v = 0;
+    if (p < T) {
+      const Board& b = smp.boards[gi * g.HW + p];
+      v = bit(b.own, c) ? 1 : (bit(b.opp, c) ? -1 : 0);
+    }
+    cells[k] = v;
+  }
+}
+
+void launch_drain_pack(const GameCfg& g, const SampleDev& smp, int64_t from, int n, uint8_t* out,
+                       hipStream_t s) {
+  if (n > 0) drain_pack_kernel<<<n, 256, 0, s>>>(g, smp, from, out, drain_record_bytes(g));
 }
 
 // ---------------------------------------------------------------- launchers

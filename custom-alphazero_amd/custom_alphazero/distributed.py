@@ -22,6 +22,19 @@ from typing import Callable, Dict, List, Sequence, Tuple
 import numpy as np
 
 
+def collective_device(device=None):
+    """Where collective buffers must live: the caller's device, else this
+    rank's current GPU under nccl (RCCL moves device memory only), else the
+    CPU (gloo)."""
+    import torch
+    import torch.distributed as dist
+    if device is not None:
+        return torch.device(device)
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def shard(n_games: int, world: int, rank: int) -> Tuple[int, int]:
     """Contiguous block of global game ids owned by `rank`: (first, count)."""
     base, extra = divmod(int(n_games), int(world))
@@ -42,8 +55,7 @@ def broadcast_weights(named: Sequence[Tuple[str, "object"]], device=None, src: i
     else:
         total = sum(int(np.prod(s)) for _, s in shapes)
         flat = torch.zeros(total, dtype=torch.float32)
-    if device is not None:
-        flat = flat.to(device)
+    flat = flat.to(collective_device(device))
     dist.broadcast(flat, src=src)
     out, off = [], 0
     for name, shape in shapes:
@@ -79,6 +91,7 @@ def gather_games(results: Dict[str, np.ndarray], device=None, dst: int = 0):
     blob = b"".join(np.ascontiguousarray(packed[k]).tobytes() for k in order)
     header = np.array([len(packed["lengths"]), len(packed["moves"])], np.int64)
     world = dist.get_world_size()
+    device = collective_device(device)
     sizes = torch.tensor([len(blob), *header.tolist()], dtype=torch.int64, device=device)
     all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
     dist.all_gather(all_sizes, sizes)
@@ -86,8 +99,7 @@ def gather_games(results: Dict[str, np.ndarray], device=None, dst: int = 0):
     buf = torch.zeros(max(max_len, 1), dtype=torch.uint8)
     if blob:
         buf[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-    if device is not None:
-        buf = buf.to(device)
+    buf = buf.to(device)
     bufs = [torch.zeros_like(buf) for _ in range(world)]
     dist.all_gather(bufs, buf)
     if dist.get_rank() != dst:
@@ -135,7 +147,7 @@ def selfplay_sharded(runner: Callable[[int, int, int], Dict[str, np.ndarray]], n
     engine's selfplay_run + selfplay_results) and gather to rank 0."""
     import torch.distributed as dist
 
-    first, count = shard(n_games, dist.get_world_size(), dist.get_rank())
+    first, count = shard(n_games, dist.get_world_size(), dist.get_rank())  # device: collective_device
     results = runner(first, count, base_seed)
     return gather_games(results, device=device)
 

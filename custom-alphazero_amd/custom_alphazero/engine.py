@@ -60,7 +60,10 @@ class Stats(ctypes.Structure):
         ("conv_launches", ctypes.c_int64), ("conv_ms", ctypes.c_double),
         ("cache_hits", ctypes.c_int64), ("evaluations", ctypes.c_int64),
         ("conv_busy_ms", ctypes.c_double), ("tree_launches", ctypes.c_int64), ("tree_ms", ctypes.c_double),
-        ("path_edges", ctypes.c_int64), ("reserved", ctypes.c_int64 * 1),
+        ("path_edges", ctypes.c_int64), ("cache_inserts", ctypes.c_int64),
+        ("cache_generation", ctypes.c_int64), ("cache_gen_size", ctypes.c_int64),
+        ("cache_capacity", ctypes.c_int64), ("games_drained", ctypes.c_int64),
+        ("reserved", ctypes.c_int64 * 3),
     ]
 
     def as_dict(self):
@@ -70,7 +73,7 @@ class Stats(ctypes.Structure):
 EXPORTED = (
     "az_abi_version", "az_last_error", "az_engine_create", "az_engine_destroy",
     "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
-    "az_selfplay_run", "az_selfplay_results", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_play",
+    "az_selfplay_run", "az_selfplay_results", "az_selfplay_drain", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
     "az_cache_clear", "az_cache_enable",
     # include/az_chess.h
@@ -115,6 +118,7 @@ def load_library():
         "az_selfplay_step": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(Stats)]),
         "az_selfplay_run": (ctypes.c_int, [P, I64, I64, ctypes.c_uint32, ctypes.POINTER(Stats)]),
         "az_selfplay_results": (ctypes.c_int, [P, P, P, P, P, P, P]),
+        "az_selfplay_drain": (ctypes.c_int, [P, I64, P, P, P, P, P, P, P, P]),
         "az_tree_reset": (ctypes.c_int, [P, ctypes.c_int, P, P]),
         "az_tree_release": (ctypes.c_int, [P, ctypes.c_int, P]),
         "az_tree_search": (ctypes.c_int, [P, ctypes.c_int]),
@@ -281,6 +285,22 @@ class Engine:
                                            _ptr(boards), _ptr(policies), _ptr(moves)))
         return dict(lengths=lengths, results=results, expansions=expansions, boards=boards,
                     policies=policies, moves=moves)
+
+    def selfplay_drain(self, max_games=None):
+        """Games finished since the previous drain, copied to the host (the
+        samples of a running batch, az_selfplay_drain): dict of arrays with
+        a leading game axis plus `game_ids` (finish order)."""
+        G = int(max_games if max_games is not None else max(self._n_games, 1))
+        P, A = self.height * self.width, self.action_space
+        n = ctypes.c_int64(0)
+        out = dict(game_ids=np.zeros(G, np.int64), lengths=np.zeros(G, np.int32),
+                   results=np.zeros(G, np.int32), expansions=np.zeros(G, np.int32),
+                   boards=np.zeros((G, P, self.height, self.width), np.int8),
+                   policies=np.zeros((G, P, A), np.float64), moves=np.zeros((G, P), np.int32))
+        _check(self._L.az_selfplay_drain(self._h, G, ctypes.byref(n), *(_ptr(out[k]) for k in (
+            "game_ids", "lengths", "results", "expansions", "boards", "policies", "moves"))))
+        k = int(n.value)
+        return {key: v[:k] for key, v in out.items()}
 
     # ------------------------------------------------------------- tree API
     def tree_reset(self, slots, boards):

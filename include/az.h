@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 1
+#define AZ_ABI_VERSION 2
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
@@ -34,7 +34,8 @@ extern "C" {
 #define AZ_EVAL_SYNTHETIC 1  /* oracle/synth.py's exact evaluator (parity runs) */
 
 /* az_config.conv_algo */
-#define AZ_CONV_WINOGRAD 0   /* Winograd F(2x2,3x3) on fp32 MFMA (default) */
+#define AZ_CONV_WINOGRAD 0   /* Winograd F(2x2,3x3); fp32 products formed from three bf16
+                                terms per operand on the bf16 MFMA (default) */
 #define AZ_CONV_DIRECT 1     /* direct implicit GEMM on fp32 MFMA */
 
 typedef struct az_engine az_engine;
@@ -92,7 +93,12 @@ typedef struct az_stats {
     int64_t tree_launches;    /* timed select + expand kernels (az_timer_enable) */
     double tree_ms;           /* their summed device time */
     int64_t path_edges;       /* edges on the selected paths (sum of select depths) */
-    int64_t reserved[1];
+    int64_t cache_inserts;    /* transposition-cache inserts since the last clear */
+    int64_t cache_generation; /* eviction generations since the last clear (az_tree.h) */
+    int64_t cache_gen_size;   /* inserts per generation (0 = no eviction: the table only fills) */
+    int64_t cache_capacity;   /* cache entries (2^cache_log2; 0 = no cache) */
+    int64_t games_drained;    /* finished games az_selfplay_drain has returned this batch */
+    int64_t reserved[3];
 } az_stats;
 
 int az_abi_version(void);
@@ -131,6 +137,16 @@ int az_selfplay_run(az_engine* eng, int64_t first_game, int64_t n_games, uint32_
  * policies [g][H*W][A] f64 (MCTS.play return_details policy); moves [g][H*W]. */
 int az_selfplay_results(az_engine* eng, int32_t* lengths, int32_t* results, int32_t* expansions,
                         int8_t* boards, double* policies, int32_t* moves);
+/* The games that finished since the previous drain (at most max_games, in the
+ * order they finished), copied to the caller's buffers: the batch's samples
+ * reach the host while self-play continues (play()'s results return,
+ * self_play.py:112-118, one step at a time).  *n_out = games copied; per game
+ * i: game_ids[i], lengths/results/expansions[i] as az_selfplay_results,
+ * boards [i][H*W][H][W] int8, policies [i][H*W][A] f64, moves [i][H*W]
+ * (rows past the game's length are zero).  Any output but n_out may be NULL. */
+int az_selfplay_drain(az_engine* eng, int64_t max_games, int64_t* n_out, int64_t* game_ids,
+                      int32_t* lengths, int32_t* results, int32_t* expansions, int8_t* boards,
+                      double* policies, int32_t* moves);
 
 /* MCTS tree API (mcts/mcts.py:88-222) over the engine's slots. */
 int az_tree_reset(az_engine* eng, int n, const int32_t* slots, const int8_t* boards);

@@ -331,14 +331,19 @@ class TorchCPUNet:
 
 def baseline_worker(args):
     """One CPU worker: plays games until `budget_s` elapses (a game in progress
-    finishes).  Returns (games, expansions, seconds)."""
-    (height, width, n, gravity, sims, weights, depth, budget_s, seed) = args
+    finishes).  `cache` is the plays_inferences the reference hands every
+    worker (utils.py:38-39): a multiprocessing Manager dict shared by all
+    workers when it fans out, or None for the mono-process path (a plain
+    dict kept across this worker's games).  Returns (games, expansions,
+    seconds)."""
+    (height, width, n, gravity, sims, weights, depth, budget_s, seed, cache) = args
     import torch
     torch.set_num_threads(1)
     net = TorchCPUNet(weights, depth)
     t0 = time.perf_counter()
     games = expansions = 0
-    cache = {}  # plays_inferences: kept across this worker's games (utils.py:38-39)
+    if cache is None:
+        cache = {}
     while time.perf_counter() - t0 < budget_s:
         r = play_game(height, width, n, gravity, sims, seed + games, net, cache=cache)
         games += 1

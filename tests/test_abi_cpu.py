@@ -33,14 +33,14 @@ def test_library_exports_every_declared_symbol():
     for name in header_functions():
         assert hasattr(lib, name), name
     L = az.load_library()
-    assert L.az_abi_version() == 1
+    assert L.az_abi_version() == 2
 
 
 def test_struct_sizes_match_header():
     # az_config: 8 int32 + double + 4 int32 ... computed by hand from az.h
     assert ctypes.sizeof(az.Config) == 4 * 6 + 8 + 4 * 5 + 4 + 8 + 8 + 8 + 32
     assert ctypes.sizeof(az.Tensor) == 8 + 8 + 8 + 4 + 4
-    assert ctypes.sizeof(az.Stats) == 8 * 8 + 8 + 8 * 7
+    assert ctypes.sizeof(az.Stats) == 8 * 8 + 8 + 8 * 7 + 8 * 7
     # az_chess_config: 2 int32, double, 6 int32, double, int64, int32 + 7 reserved
     assert ctypes.sizeof(az.ChessConfig) == 8 + 8 + 24 + 8 + 8 + 4 + 28
 

@@ -124,6 +124,59 @@ def test_selfplay_synthetic_many_games_vs_oracle(cache_log2, lanes):
         assert st["evaluations"] == st["expansions"] and st["cache_hits"] == 0
 
 
+@pytest.mark.parametrize("lanes", [1, 2, 3])
+def test_cache_eviction_generations_are_transparent(lanes):
+    """A cache small enough to turn over many eviction generations (az_tree.h:
+    entries 3+ generations old are overwritten while other lanes read the
+    table) leaves every game bitwise equal to the oracle."""
+    eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC, cache_log2=17, lanes=lanes)
+    games = selfplay_games(eng, 3000, 256, base_seed=9)
+    st = eng.stats()
+    assert st["cache_gen_size"] == 2 ** 17 // 8
+    assert st["cache_generation"] >= 4, st["cache_generation"]
+    assert st["cache_hits"] > 0 and st["errors"] == 0
+    for g, got in enumerate(games):
+        ref = oracle.play_game(6, 7, 4, True, 50, 9 + 3000 + g)
+        assert got["T"] == ref["T"]
+        np.testing.assert_array_equal(got["moves"], ref["moves"])
+        np.testing.assert_array_equal(got["policy"].view(np.uint64), ref["policy"].view(np.uint64))
+        assert got["expansions"] == ref["expansions"]
+    # too small for the lane-drift bound: eviction stays off (the table only fills)
+    small = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC, cache_log2=14, lanes=lanes)
+    assert small.stats()["cache_gen_size"] == 0
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_drain_returns_every_game_once(lanes):
+    """az_selfplay_drain after each move hands every finished game to the host
+    exactly once, with the same records az_selfplay_results returns."""
+    eng = az.Engine(6, 7, 4, True, 20, slots=40, evaluator=az.EVAL_SYNTHETIC, cache_log2=12, lanes=lanes)
+    n_games = 150
+    eng.selfplay_begin(500, n_games, 3)
+    parts, steps = [], 0
+    while True:
+        st = eng.selfplay_step(1)
+        parts.append(eng.selfplay_drain(max_games=64 if steps % 2 else None))
+        steps += 1
+        if st["active_slots"] == 0:
+            break
+    while True:  # a capped drain may leave games behind
+        d = eng.selfplay_drain()
+        if not len(d["lengths"]):
+            break
+        parts.append(d)
+    got = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    assert sorted(got["game_ids"].tolist()) == list(range(500, 500 + n_games))
+    assert eng.stats()["games_drained"] == n_games
+    ref = eng.selfplay_results()
+    order = np.argsort(got["game_ids"])
+    gi = got["game_ids"][order] - 500
+    for k in ("lengths", "results", "expansions", "moves", "boards"):
+        np.testing.assert_array_equal(got[k][order], ref[k][gi], err_msg=k)
+    np.testing.assert_array_equal(got["policies"][order].view(np.uint64), ref["policies"][gi].view(np.uint64))
+    assert len(eng.selfplay_drain()["lengths"]) == 0
+
+
 def test_pow_table_is_python_pow(golden):
     z = golden("numerics")
     eng = az.Engine(6, 7, 4, True, 100, slots=1, evaluator=az.EVAL_SYNTHETIC,
