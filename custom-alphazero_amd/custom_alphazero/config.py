@@ -93,3 +93,16 @@ class ConfigPath:
     model_prefix = "model"
     model_meta = "meta.json"
     model_success = "MODEL_SAVED_SUCCESSFULLY"
+
+
+def check_mcts_config():
+    """Refuse MCTS settings this engine does not implement instead of
+    silently ignoring them: Dirichlet root noise (mcts.py:70-85, used by
+    select at :113-116) is disabled in the reference (config.py:52) and not
+    built here (its numpy gamma/log/pow draws are outside the
+    parity scope)."""
+    if ConfigMCTS.enable_dirichlet_noise:
+        raise NotImplementedError(
+            "ConfigMCTS.enable_dirichlet_noise=True is not supported by the MI355X engine "
+            "(root Dirichlet noise, reference mcts.py:70-85, is disabled in the reference's config)")
+

@@ -19,7 +19,7 @@ import numpy as np
 
 from custom_alphazero import engine as az
 from custom_alphazero.config import (ConfigConnectN, ConfigMCTS, ConfigModel, ConfigSelfPlay,
-                                     ConfigServing)
+                                     ConfigServing, check_mcts_config)
 from custom_alphazero.connect_n.board import Board
 from custom_alphazero.connect_n.move import Move
 from custom_alphazero.mcts.mcts import MCTS
@@ -104,6 +104,7 @@ def evaluate_two_models(model, other_model, evaluate_with_mcts: bool = False,
 
 
 def _arena_engine(model, n_slots: int) -> az.Engine:
+    check_mcts_config()
     c = ConfigConnectN
     eng = az.Engine(c.board_height, c.board_width, c.n, c.gravity,
                     max(ConfigSelfPlay.mcts_iterations, 1), slots=n_slots,

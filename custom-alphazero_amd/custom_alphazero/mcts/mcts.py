@@ -22,7 +22,8 @@ from typing import List, Optional, Tuple, Union
 import numpy as np
 
 from custom_alphazero import engine as az
-from custom_alphazero.config import ConfigConnectN, ConfigMCTS, ConfigModel, ConfigSelfPlay
+from custom_alphazero.config import (ConfigConnectN, ConfigMCTS, ConfigModel, ConfigSelfPlay,
+                                     check_mcts_config)
 from custom_alphazero.connect_n.board import Board
 from custom_alphazero.connect_n.move import Move
 
@@ -134,6 +135,7 @@ class MCTS:
 
     # ------------------------------------------------------------ search
     def search(self, iterations_number: int):
+        check_mcts_config()
         if self.board.is_game_over():
             return
         self._engine.tree_search(int(iterations_number))
@@ -260,6 +262,7 @@ class ChessMCTS(MCTS):
         self.path_cache = []
 
     def search(self, iterations_number: int):
+        check_mcts_config()
         if self.board.is_game_over():
             return
         self._engine.tree_search(int(iterations_number))

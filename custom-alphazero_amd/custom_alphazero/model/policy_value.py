@@ -7,7 +7,6 @@ layout, names from model/weights.py); the forward runs in libaz
 model returns (probabilities [B, A], value [B, 1]) as torch CPU tensors, so
 the reference's `.numpy()` idiom (mcts.py:134-137) works unchanged.
 """
-import hashlib
 import json
 import os
 
@@ -15,7 +14,8 @@ import numpy as np
 
 from custom_alphazero import engine as az
 from custom_alphazero.config import ConfigConnectN, ConfigModel, ConfigPath
-from custom_alphazero.model.weights import init_weights, weight_spec
+from custom_alphazero.model.weights import (content_hash, init_weights, keras_order, reference_hash,
+                                            weight_spec)
 
 
 class PolicyValueModel:
@@ -43,27 +43,40 @@ class PolicyValueModel:
     def engine_weights(self):
         return [(name, self.weights[name]) for name, _ in self.spec]
 
+    @property
+    def weight_names(self):
+        """get_weights()/set_weights() order: tf.keras's for the reference
+        model (weights.keras_order)."""
+        return keras_order(self.spec)
+
     def get_weights(self):
-        return [self.weights[name].detach().cpu().numpy().reshape(shape) for name, shape in self.spec]
+        shapes = dict(self.spec)
+        return [self.weights[n].detach().cpu().numpy().reshape(shapes[n]) for n in self.weight_names]
 
     def set_weights(self, arrays):
         import torch
         arrays = list(arrays)
         if len(arrays) != len(self.spec):
             raise ValueError(f"expected {len(self.spec)} arrays, got {len(arrays)}")
-        for (name, shape), a in zip(self.spec, arrays):
+        shapes = dict(self.spec)
+        for name, a in zip(self.weight_names, arrays):
             a = np.asarray(a, np.float32)
-            if a.shape != tuple(shape):
-                raise ValueError(f"{name}: shape {a.shape} != {shape}")
+            if a.shape != tuple(shapes[name]):
+                raise ValueError(f"{name}: shape {a.shape} != {shapes[name]}")
             self.weights[name] = torch.from_numpy(a.copy()).to(self.device)
         self._version += 1
 
     @property
     def hash(self) -> int:
-        # The reference sums md5(str(weight)) over Keras' get_weights()
-        # (model.py:172-177); that string form is numpy-print dependent, so
-        # this hash is over the raw float32 bytes instead.
-        return sum(int(hashlib.md5(w.tobytes()).hexdigest(), 16) for w in self.get_weights())
+        """The reference's hash, sum of md5(str(weight)) over get_weights()
+        (model.py:172-177): a meta.json the reference wrote validates here."""
+        return reference_hash(self.get_weights())
+
+    @property
+    def content_hash(self) -> str:
+        """md5 of the raw float32 weights: changes whenever any weight does
+        (the reference hash only sees the corners of large arrays)."""
+        return content_hash(self.get_weights())
 
     def is_equal(self, other: "PolicyValueModel"):
         return self.hash == other.hash

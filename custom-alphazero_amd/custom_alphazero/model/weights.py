@@ -50,6 +50,47 @@ def weight_spec(height, width, action_space, filters=128, depth=4, hidden=256, i
     return spec
 
 
+def keras_order(spec):
+    """Names of `spec` in the order tf.keras `Model.get_weights()` returns
+    them for the reference's PolicyValueModel (model/tensorflow/model.py:
+    152-170; un-vendored TF 2.7.1, parity unpinned): per top-level layer
+    (residual tower, policy head, value head, in attribute order), that
+    layer's trainable weights depth-first (conv kernel, bias, BN gamma, beta
+    per InnerConvBlock; Dense kernel, bias), then its non-trainable ones (BN
+    moving mean, variance) depth-first."""
+    names = [n for n, _ in spec]
+
+    def split(prefixes):
+        own = [n for n in names if n.split(".")[0] in prefixes]
+        train = [n for n in own if n.rsplit(".", 1)[1] not in ("mean", "var")]
+        return train + [n for n in own if n.rsplit(".", 1)[1] in ("mean", "var")]
+
+    tower = {"stem"} | {n.split(".")[0] for n in names if n.startswith("block")}
+    out = split(tower) + split({"policy"}) + split({"value"})
+    assert sorted(out) == sorted(names)
+    return out
+
+
+def reference_hash(arrays):
+    """The reference's weight hash (model/tensorflow/model.py:172-177): the
+    sum over get_weights() of md5(str(weight)).  str() is numpy's summarised
+    print form (arrays over 1000 elements show only their corners), so two
+    weight sets that differ only inside large arrays hash the same; use
+    content_hash to detect a change of weights."""
+    import hashlib
+    return sum(int(hashlib.md5(str(np.asarray(w, np.float32)).encode("utf-8")).hexdigest(), 16)
+               for w in arrays)
+
+
+def content_hash(arrays):
+    """md5 over the raw float32 bytes of every array (order-sensitive)."""
+    import hashlib
+    h = hashlib.md5()
+    for w in arrays:
+        h.update(np.ascontiguousarray(w, np.float32).tobytes())
+    return h.hexdigest()
+
+
 def glorot_limit(shape):
     if len(shape) == 4:
         rf = shape[0] * shape[1]

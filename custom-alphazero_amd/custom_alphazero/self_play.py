@@ -19,7 +19,7 @@ import numpy as np
 
 from custom_alphazero import engine as az
 from custom_alphazero.config import (ConfigConnectN, ConfigGeneral, ConfigMCTS, ConfigModel,
-                                     ConfigPath, ConfigSelfPlay)
+                                     ConfigPath, ConfigSelfPlay, check_mcts_config)
 from custom_alphazero.connect_n.board import Board
 from custom_alphazero.connect_n.move import Move
 from custom_alphazero.mcts.mcts import MCTS, SyntheticEvaluator
@@ -84,6 +84,7 @@ _CACHE_OWNER = {"dict": None}
 
 
 def _batched_engine(model, n_slots):
+    check_mcts_config()
     c = ConfigConnectN
     synthetic = isinstance(model, SyntheticEvaluator)
     key = (c.board_height, c.board_width, c.n, c.gravity, ConfigSelfPlay.mcts_iterations, n_slots,
@@ -106,7 +107,7 @@ def _batched_engine(model, n_slots):
     if not synthetic:
         # content hash: play() reloads the best model from disk every call like
         # the reference (utils.py:42-48); unchanged weights keep the cache
-        wkey = model.hash if hasattr(model, "hash") else (id(model), getattr(model, "_version", None))
+        wkey = model.content_hash if hasattr(model, "content_hash") else (id(model), getattr(model, "_version", None))
         if eng.weights_key != wkey:  # new best model: upload (clears the cache)
             eng.set_weights(model.engine_weights())
             eng.weights_key = wkey
@@ -117,6 +118,7 @@ _CHESS_ENGINES = {}
 
 
 def _chess_engine(model, n_slots, sims):
+    check_mcts_config()
     synthetic = isinstance(model, SyntheticEvaluator)
     key = (sims, n_slots, synthetic, ConfigMCTS.index_move_greedy, ConfigMCTS.exploration_constant,
            ConfigModel.depth, ConfigSelfPlay.chess_max_plies)
@@ -133,7 +135,7 @@ def _chess_engine(model, n_slots, sims):
         _CHESS_ENGINES.clear()
         _CHESS_ENGINES[key] = eng
     if not synthetic:
-        wkey = model.hash if hasattr(model, "hash") else (id(model), getattr(model, "_version", None))
+        wkey = model.content_hash if hasattr(model, "content_hash") else (id(model), getattr(model, "_version", None))
         if eng.weights_key != wkey:
             eng.set_weights(model.engine_weights())
             eng.weights_key = wkey

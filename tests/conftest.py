@@ -25,3 +25,8 @@ def load_golden(name):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

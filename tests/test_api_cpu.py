@@ -88,3 +88,39 @@ def test_queue_payload_matches_append_queue_schema(tmp_path):
     np.testing.assert_array_equal(np.asarray(back["states"], np.float32), states)
     np.testing.assert_array_equal(np.asarray(back["policies"]), policies)
     np.testing.assert_array_equal(np.asarray(back["values"]), values)
+
+
+def test_reference_weight_hash_matches_legacy_numpy(golden_dir):
+    """PolicyValueModel.hash is the reference's sum of md5(str(weight)) over
+    Keras get_weights() (model/tensorflow/model.py:172-177); the digests were
+    taken under numpy 1.26 (tests/golden/make_weight_hash.py)."""
+    import json
+    import os
+
+    from custom_alphazero.model.weights import (content_hash, init_weights, keras_order, reference_hash,
+                                                weight_spec)
+    cases = json.load(open(os.path.join(golden_dir, "weight_hash.json")))
+    for case in cases.values():
+        H, W, A, C = case["shape"]
+        spec = weight_spec(H, W, A, in_channels=C)
+        w = init_weights(spec, seed=case["seed"], randomize_bn=case["randomize_bn"])
+        names = keras_order(spec)
+        assert names == case["names"]
+        assert str(reference_hash([w[n] for n in names])) == case["hash"]
+    # the reference hash sees only the corners of arrays over 1000 elements
+    k = w["block0.conv1.kernel"].copy()
+    k[1, 1, 64, 64] += 1.0
+    w2 = dict(w, **{"block0.conv1.kernel": k})
+    assert reference_hash([w2[n] for n in names]) == reference_hash([w[n] for n in names])
+    assert content_hash([w2[n] for n in names]) != content_hash([w[n] for n in names])
+
+
+def test_dirichlet_noise_is_refused():
+    from custom_alphazero.config import ConfigMCTS, check_mcts_config
+    check_mcts_config()
+    ConfigMCTS.enable_dirichlet_noise = True
+    try:
+        with pytest.raises(NotImplementedError):
+            check_mcts_config()
+    finally:
+        ConfigMCTS.enable_dirichlet_noise = False

@@ -113,8 +113,7 @@ def test_policy_value_model_matches_keras(game_cfg, golden):
     probs, value = model(x)
     p, v = probs.numpy(), value.numpy()
     assert p.shape == (9, 7) and v.shape == (9, 1)
-    w = dict(zip([n for n, _ in model.spec], model.get_weights()))
-    w = {n: a for n, a in w.items()}
+    w = dict(zip(model.weight_names, model.get_weights()))
     rp, rv = keras_ref.forward(w, x, depth=4)
     assert np.abs(p - rp).max() < 1e-5 and np.abs(v[:, 0] - rv).max() < 1e-5
     # the reference's batch-1 idiom (mcts.py:131-137)
@@ -187,3 +186,27 @@ def test_mcts_visualizer_over_device_tree(game_cfg, golden, tmp_path):
     assert abs(sum(e.proportion_n for e in vis.mcts_root_node.edges) - 1.0) < 1e-12
     path = vis.graph_mcts.save(directory=str(tmp_path))
     assert open(path).read() == dot
+
+
+def test_load_with_meta_accepts_reference_hash(tmp_path, game_cfg, golden):
+    """A meta.json whose hash the reference computed (sum of md5(str(w)),
+    model.py:172-177, digests taken under legacy numpy) validates; a wrong
+    hash is refused like the reference's assertion (model.py:199-201)."""
+    import json
+    import os
+
+    from custom_alphazero.config import ConfigPath
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    game_cfg(golden("mcts_c4_s25"))
+    case = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "weight_hash.json")))["c4_seed0"]
+    w = init_weights(weight_spec(6, 7, 7), seed=0)
+    np.savez(tmp_path / (ConfigPath.model_prefix + ".npz"), **w)
+    (tmp_path / ConfigPath.model_meta).write_text(json.dumps({"steps": 3, "learning_rate": 0.01,
+                                                             "hash": int(case["hash"])}))
+    (tmp_path / ConfigPath.model_success).write_bytes(b"")
+    m = PolicyValueModel((6, 7, 4), 7, seed=5)
+    m.load_with_meta(str(tmp_path))
+    assert m.hash == int(case["hash"]) and m.steps == 3
+    (tmp_path / ConfigPath.model_meta).write_text(json.dumps({"steps": 3, "hash": int(case["hash"]) + 1}))
+    with pytest.raises(AssertionError):
+        m.load_with_meta(str(tmp_path))
