@@ -48,7 +48,7 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no 2:1 sparsity)
+F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16/fp16 MFMA (no 2:1 sparsity)
 BOX_CPU_SHARE = 16              # CPUs one GPU's box grants a job (gpurun); workers stay inside it
 MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
 MAX_PREROLL = 800
@@ -75,7 +75,7 @@ def parse():
                     help="0 = os.cpu_count() - 1 (self_play.py:98), inside the box's CPU share")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="slot groups on separate HIP streams (0 = auto)")
-    ap.add_argument("--conv-algo", type=int, default=0, help="0 Winograd, 1 direct")
+    ap.add_argument("--conv-algo", type=int, default=0, help="0 fp16x2 direct (default), 1 fp32 direct")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
     ap.add_argument("--cache-log2", type=int, default=25,
                     help="transposition cache (the reference's plays_inferences) entries = 2^N; 0 = off")
@@ -200,10 +200,9 @@ def _reduce(values, op, world, args, dev):
 def conv_kernel_name(conv_algo, chess=False):
     if conv_algo != 0:
         return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"
-    k = ("wino16x_conv_kernel (Winograd F(2x2,3x3), fp32 products from three bf16 terms per operand on "
-         "the 16x16x32 bf16 MFMA")
-    return k + (", residual tower, 8 launches per forward)" if chess else
-                ", 16 tiles per workgroup, fused BN/ReLU and 1x1 projection residual)")
+    return ("conv16_kernel (direct 3x3 implicit GEMM on the 16x16x32 fp16 MFMA; fp32-accurate: both operands as "
+            "two fp16 terms, 3 products per k-step; fused BN/ReLU, 1x1 projection residual and head 1x1 convs"
+            + (", residual tower, 8 launches per forward)" if chess else ")"))
 
 
 def conv_roofline(args, conv_algo, boards_per_launch, avg_ms, busy_ms, boards_total, launches,
@@ -215,8 +214,8 @@ def conv_roofline(args, conv_algo, boards_per_launch, avg_ms, busy_ms, boards_to
     issues on.  The direct-convolution FLOP at the fp32 peak is given beside
     it as the algorithmic equivalent (SURVEY.md 8d's count)."""
     n_conv = 2 * args.depth
-    flop, peak, dtype = issued_per_board, (BF16_MFMA_PEAK_TFLOPS if conv_algo == 0 else FP32_MFMA_PEAK_TFLOPS), \
-        ("bf16 (3 terms per fp32 operand, 6 products)" if conv_algo == 0 else "fp32")
+    flop, peak, dtype = issued_per_board, (F16_MFMA_PEAK_TFLOPS if conv_algo == 0 else FP32_MFMA_PEAK_TFLOPS), \
+        ("fp16 (2 terms per fp32 operand, 3 products)" if conv_algo == 0 else "fp32")
     achieved = boards_per_launch * flop / n_conv / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
     alg = boards_per_launch * direct_flop_per_board / n_conv / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
     union = boards_total * flop / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
@@ -224,7 +223,7 @@ def conv_roofline(args, conv_algo, boards_per_launch, avg_ms, busy_ms, boards_to
     if os.path.exists(pmc_file):  # PMC bytes/board (rocprofv3 FETCH_SIZE/WRITE_SIZE) x live batch
         with open(pmc_file) as fp:
             tj = json.load(fp)
-        key = "winograd" if conv_algo == 0 else "direct"
+        key = "f16x2" if conv_algo == 0 else "direct"
         if key in tj:
             traffic = int(tj[key]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
     return {
@@ -246,8 +245,8 @@ def conv_roofline(args, conv_algo, boards_per_launch, avg_ms, busy_ms, boards_to
             "frac": round(alg / FP32_MFMA_PEAK_TFLOPS, 4),
             "flop_per_board": int(direct_flop_per_board),
             "basis": "direct-convolution FLOP (SURVEY.md 8d) per launch / avg_launch_ms, priced at the fp32 "
-                     "MFMA peak: what the layer would need from an fp32 direct convolution (Winograd "
-                     "issues fewer multiplies, so this can exceed 1)"},
+                     "MFMA peak: the rate an exact fp32 MFMA kernel would need for the same layer time (the "
+                     "fp16 two-term products run at 16x the fp32 rate, so this can exceed 1)"},
         "busy_union": {"achieved": round(union, 2), "frac": round(union / peak, 4),
                        "basis": "all timed boards' issued FLOP / union of the conv intervals of all lanes"},
         "boards_per_launch": round(boards_per_launch, 1),
@@ -335,10 +334,9 @@ def chess_main(args):
     g, e, s, p, ev = _reduce([d["games_done"], d["expansions"], d["simulations"], d["plies"],
                               d["evaluations"]], dist.ReduceOp.SUM if world > 1 else None, world, args, dev)
     (elapsed,) = _reduce([elapsed], dist.ReduceOp.MAX if world > 1 else None, world, args, dev)
-    F, HW, TB = 128, 64, 16
+    F, HW = 128, 64
     direct_flop = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
-    wino_flop = TB * 36 * 2 * F * F * args.depth         # 16 points per 2x2 tile (+4 residual rows / conv2)
-    issued = 6 * wino_flop if args.conv_algo == 0 else direct_flop
+    issued = 3 * direct_flop if args.conv_algo == 0 else direct_flop  # fp16x2: 3 products per MAC
     launches = st1["conv_launches"]
     boards_per_launch = local_evals / max(launches / (2 * args.depth), 1)
     avg_ms = st1["conv_ms"] / max(launches, 1)
@@ -357,7 +355,7 @@ def chess_main(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32-accurate network (fp32 products from 3 bf16 terms on the bf16 MFMA) / f64 PUCT",
+            "dtype": "fp32-accurate network (fp16 MFMA, two-term split operands, 3 products) / f64 PUCT",
             "data": "synthetic (self-generated games, random-init Keras-default weights, torch seed 0)",
             "config": {
                 "workload": (f"Chess (custom_alphazero/chess), {args.sims} sims/move, {args.slots} concurrent "
@@ -563,13 +561,11 @@ def main():
 
     # dominant kernel: the residual tower's 3x3 convs (8 launches per forward at
     # depth 4).  Direct FLOP = SURVEY.md 8d's count (19 F*F MACs per pixel per
-    # block: 9F + 9F + the 1x1 F); the Winograd kernel issues 16 points per
-    # 2x2 tile (+ 4 residual pixel rows in conv2), each as six bf16 products.
+    # block: 9F + 9F + the 1x1 F); conv16_kernel issues each MAC as three fp16
+    # MFMA products.
     HW, F = args.height * args.width, 128
-    TB = ((args.height + 1) // 2) * ((args.width + 1) // 2)
     direct_flop = HW * 2 * F * F * 19 * args.depth
-    wino_flop = TB * 36 * 2 * F * F * args.depth
-    issued = 6 * wino_flop if args.conv_algo == 0 else direct_flop
+    issued = 3 * direct_flop if args.conv_algo == 0 else direct_flop  # fp16x2: 3 products per MAC
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     boards_per_launch = local_evals / max(conv_launches / (2 * args.depth), 1)
     pmc = os.path.join(REPO, "profiles", "r2", "pmc_conv_traffic.json")
@@ -618,7 +614,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32-accurate network (fp32 products from 3 bf16 terms on the bf16 MFMA) / f64 PUCT",
+            "dtype": "fp32-accurate network (fp16 MFMA, two-term split operands, 3 products) / f64 PUCT",
             "data": "synthetic (self-generated games, random-init Keras-default weights, torch seed 0)",
             "config": {
                 "workload": (f"{game_name} n={args.n} gravity, {args.sims} sims/move, "

@@ -364,8 +364,10 @@ __global__ __launch_bounds__(64) void leaf_kernel(CCfg g, CTree t) {
 // deepcopy, whose copy() re-runs __init__), [0 x 7, start-position state]
 // whatever the position -- the game's first Board() is the start position;
 // the castling/counter planes are the board's own.  Planes 118..127 are the
-// zero padding of the stem.
-__global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, float4* __restrict__ x) {
+// zero padding of the stem.  Written as split16 rows (AZ_CONV_F16X2; the
+// plane values are small integers, exact in the first term) or fp32.
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, void* __restrict__ x) {
   __shared__ Pos sp[2];
   __shared__ float feat[6];
   __shared__ int initial;
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, floa
       feat[5] = (float)cur.half;
     }
     __syncthreads();
-    float4* o = x + (size_t)b * 64 * 32;
+    const size_t row0 = (size_t)b * 64;
     for (int e2 = threadIdx.x; e2 < 64 * (32 - 8 * kStemFirstChunk); e2 += blockDim.x) {
       const int per = 32 - 8 * kStemFirstChunk;  // float4 per pixel written
       const int pix = e2 / per, e = pix * 32 + 8 * kStemFirstChunk + e2 % per, k0 = (e & 31) * 4;
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, floa
         else if (k >= 84 && k < 98 && !initial) val = k - 84 == 13 ? 0.f : (st_idx == k - 84 ? 1.f : 0.f);
         v[i] = val;
       }
-      o[e] = make_float4(v[0], v[1], v[2], v[3]);
+      az::store_act4<SPLIT>(x, row0 + pix, e & 31, make_float4(v[0], v[1], v[2], v[3]));
     }
   }
 }
@@ -762,7 +764,10 @@ int simulate(az_chess_engine* e, CLane& L) {
   select_kernel<<<S, 64, 0, s>>>(L.g, L.t);
   leaf_kernel<<<S, 64, 0, s>>>(L.g, L.t);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
-    encode_queue_kernel<<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, reinterpret_cast<float4*>(L.x));
+    if (e->net.algo == AZ_CONV_F16X2)
+      encode_queue_kernel<true><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
+    else
+      encode_queue_kernel<false><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
     // history slots 0-5 (planes 0-83) are always empty in self-play (every
     // board's history is [0 x 6, start, board] or [0 x 7, start]): the stem
     // skips input chunks 0-1 (planes 0-63; they would add exact zeros) and
@@ -834,11 +839,11 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
     return az::fail_abi(AZ_E_INVALID, "unknown evaluator");
   if (c.evaluator == AZ_EVAL_NETWORK && c.filters != 128)
     return az::fail_abi(AZ_E_INVALID, "network evaluator supports filters == 128 (ConfigModel.filters)");
-  if (c.conv_algo != AZ_CONV_WINOGRAD && c.conv_algo != AZ_CONV_DIRECT)
-    return az::fail_abi(AZ_E_INVALID, "conv_algo must be AZ_CONV_WINOGRAD or AZ_CONV_DIRECT");
+  if (c.conv_algo != AZ_CONV_F16X2 && c.conv_algo != AZ_CONV_DIRECT)
+    return az::fail_abi(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2 or AZ_CONV_DIRECT");
   if (c.max_plies < 0 || c.arena_edges < 0) return az::fail_abi(AZ_E_INVALID, "negative bound");
-  if ((int64_t)c.slots * 64 * 128 >= (1ll << 31))
-    return az::fail_abi(AZ_E_INVALID, "slots * 64 * 128 must stay below 2^31 (32-bit activation offsets)");
+  if ((int64_t)c.slots * 64 * 512 >= (1ll << 31))
+    return az::fail_abi(AZ_E_INVALID, "slots * 64 * 512 must stay below 2^31 (32-bit activation byte offsets)");
   int dev_count = 0;
   if (hipGetDeviceCount(&dev_count) != hipSuccess || dev_count == 0)
     return az::fail_abi(AZ_E_HIP, "no HIP device visible: libaz has no CPU fallback");
@@ -915,18 +920,7 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
   e->net.depth = c.depth;
   e->net.algo = c.conv_algo;
   e->net.hidden = c.value_hidden;
-  // 256 boards per launch leave one workgroup per CU: the two-chunk-group
-  // Winograd variant (az_wino.hip) for every chess forward; AZ_WINO_KSPLIT
-  // overrides it for A/B runs
-  {
-    const char* ks = getenv("AZ_WINO_KSPLIT");
-    e->net.wino_ksplit = ks ? atoi(ks) : 2;
-    const char* wt = getenv("AZ_WINO_TILES");
-    e->net.wino_tiles = wt ? atoi(wt) : 16;
-    const char* x3 = getenv("AZ_WINO_X3");  // fp32 products from bf16 terms (az_wino16x.hip)
-    // (its buffer loads address activations with 31-bit byte offsets)
-    e->net.wino_x3 = (x3 ? atoi(x3) : 1) && (size_t)S * 64 * 128 * 4 < ((size_t)1 << 31);
-  }
+  e->net.err = t.stats + az::kStatErrors;
   if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));
   // auto = 1: at 256 games a chess step is bound by its launch chain; extra
   // streams measured slower (375k expansions/s with 1 lane, 311k with 2,
@@ -978,10 +972,12 @@ int az_chess_forward(az_chess_engine* e, const float* x, int n, float* probs, fl
   const int chunk = e->g.slots;
   for (int off = 0; off < n; off += chunk) {
     const int m = std::min(chunk, n - off);
-    // [m][64][118] -> [m][64][128] (planes 118..127 stay zero)
-    AZC_HIP(hipMemcpy2DAsync(e->x, 128 * sizeof(float), x + (size_t)off * 64 * AZ_CHESS_PLANES,
-                             AZ_CHESS_PLANES * sizeof(float), AZ_CHESS_PLANES * sizeof(float), (size_t)m * 64,
-                             hipMemcpyHostToDevice, e->stream));
+    // [m][64][118] -> the network input [m][64][128] (planes 118..127 zero), split16 for the
+    // fp16x2 convs; act[2] stages the host floats (the forward writes it only after the stem)
+    float* staging = static_cast<float*>(e->act[2]);
+    AZC_HIP(hipMemcpyAsync(staging, x + (size_t)off * 64 * AZ_CHESS_PLANES,
+                           (size_t)m * 64 * AZ_CHESS_PLANES * sizeof(float), hipMemcpyHostToDevice, e->stream));
+    az::launch_pad_rows(staging, m * 64, AZ_CHESS_PLANES, e->x, e->net.algo == AZ_CONV_F16X2, e->stream);
     az::launch_forward(e->net, e->x, nullptr, m, 8, 8, AZ_CHESS_ACTIONS, e->act[0], e->act[1], e->act[2],
                        e->probs, e->values, e->stream, e->timer.enabled ? &e->timer : nullptr);
     AZC_HIP(hipGetLastError());

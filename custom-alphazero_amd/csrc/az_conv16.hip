@@ -1,0 +1,360 @@
+// az_conv16.hip -- the residual tower's 3x3 convolutions as a direct implicit
+// GEMM on v_mfma_f32_16x16x32_f16, fp32-accurate through a two-term fp16
+// split of both operands.
+//
+// Numbers (split16 format, shared with the stem/heads kernels):
+//   x ~= t0 + t1 * 2^-12,  t0 = fp16_rn(x),  t1 = fp16_rn((x - t0) * 2^12)
+// (the subtraction is exact; x is represented to ~2^-22 relative, and for
+// |x| below fp16's normal range t1 still carries the remainder).  A weight
+// w, prescaled per conv by a power of two to |w'| <= 8, is b0 + b1 * 2^-12
+// the same way; the host stores B0 = 2^12 * b0 (exact, |B0| <= 32768) and
+// b1.  Then
+//   2^12 * a * w' ~= t0 * B0 + t0 * b1 + t1 * b0      (b0 = B0 * 2^-12)
+// -- three fp16 MFMAs per k-step into ONE fp32 accumulator; the dropped
+// t1*b1 term is 2^-24 relative.  The epilogue multiplies by 2^(e-12) (exact)
+// and adds the folded BN bias.  Against the bf16x3 Winograd kernel this is
+// half the MFMA work per product and no transforms; against fp32 MFMA it is
+// 5.3x the issue rate.  Network error vs float64 stays ~1e-7.
+//
+// Activation rows (one pixel = 512 B): term 0 of channels 0..127 (fp16),
+// then term 1.  Rows are pixels b*HW + y*W + x; a workgroup's TR rows cross
+// board boundaries freely.
+//
+// Workgroup = WM x 4 waves; wave (mh, nq) owns output rows mh*64 .. +64 (four
+// 16-row M blocks) and columns 32nq .. +32 (two 16-column N blocks).
+//  * A: the tile's input rows plus a halo of W+1 rows each side are copied
+//    ONCE into LDS by buffer_load ... lds (no VGPRs, no VALU; rows outside
+//    the batch come back as zeros from the buffer range check), 16-B slots
+//    rotated by twice the slab row (c16_phys) so every ds_read_b128 lane
+//    group hits 16 distinct bank quads.  A tap (dy, dx) reads the slab shifted by
+//    dy*W + dx rows; off-board neighbours read the zero row.
+//  * B: host-packed fragments ([k-step][n-block][term][lane] uint4) streamed
+//    into registers two k-steps ahead; no LDS, no barrier in the K loop.
+//  * conv2 fuses the block's 1x1 projection residual: four more k-steps on
+//    the block input's rows (prefetched into registers during the taps,
+//    written over the slab after them); with HEADS the policy/value 1x1
+//    convs run in the epilogue (feat = [rows] float4) instead of a store.
+// Every output element is summed in a fixed order (k-step, then term), so a
+// board's outputs do not depend on what else is in the batch.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "az_nn.h"
+#include "az_tree.h"
+
+namespace az {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef AZ_C16_PF
+#define AZ_C16_PF 2  // k-steps of B fragments in flight ahead of their MFMAs
+#endif
+#ifndef AZ_C16_APF
+#define AZ_C16_APF 0  // A fragments read one M block ahead (1) or just before their MFMAs (0)
+#endif
+constexpr int kC16Tile = 64;       // output rows per wave (4 M blocks)
+constexpr int kC16Pitch = 132;     // epilogue tile row pitch (floats)
+constexpr float kOverflow = 32752.f;  // |x| above this cannot be split (fp16 range)
+
+// LDS image of a row x (32 slots of 16 B): logical slot j (term j >> 4,
+// channels 8 (j & 15) ..) sits at (j & 16) | ((j + 2x) & 15).  A ds_read_b128
+// lane group reads 8 consecutive rows at chunk slot g and 8 at g + 1 (or g,
+// g + 1 swapped): 2x spreads one set over the even bank quads and the other
+// over the odd ones, whatever the tap's row shift (an XOR by the row's low
+// bits collides for odd shifts).
+__device__ __forceinline__ int c16_phys(int x, int j) { return (j & 16) | ((j + 2 * x) & 15); }
+__device__ __forceinline__ int c16_logical(int x, int s) { return (s & 16) | ((s - 2 * x) & 15); }
+
+// b0 = B0 * 2^-12 (exact: B0 was 2^12 * an fp16 value)
+__device__ __forceinline__ h8 unscale_b0(const uint4 v) {
+  const h8 b = __builtin_bit_cast(h8, v);
+  return b * (_Float16)0.000244140625f;
+}
+
+template <int WM, bool RES, bool HEADS, int C0>
+__global__ __launch_bounds__(256 * WM) void conv16_kernel(
+    const uint4* __restrict__ in, const uint4* __restrict__ res_in, const uint4* __restrict__ wpack,
+    const float* __restrict__ bias, float oscale, uint4* __restrict__ out, Conv16Heads hc,
+    const int* __restrict__ count, int n_static, int H, int W, unsigned long long* __restrict__ err) {
+  static_assert(!HEADS || RES, "the heads fuse into a block's second conv");
+  constexpr int TR = kC16Tile * WM;
+  constexpr int NT = 256 * WM;
+  constexpr int CPT = 4 - C0;          // 32-channel chunks per tap
+  constexpr int NK = 9 * CPT;          // tap k-steps
+  constexpr int NKR = NK + (RES ? 4 : 0);
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+
+  const int HW = H * W, halo = W + 1;
+  const int n_boards = count ? *count : n_static;
+  const int rows = n_boards * HW;
+  const int row0 = blockIdx.x * TR;
+  if (row0 >= rows) return;  // block-uniform
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slab_rows = TR + 2 * halo;  // + the zero row at index slab_rows
+  const int zrow = slab_rows;
+
+  // ---- B stream: k-step s of the executed sequence -> packed k-step
+  const uint4* wl = wpack + (size_t)((wave & 3) * 2) * 2 * 64 + lane;
+  auto pk_of = [&](int s) { return s < NK ? (s / CPT) * 4 + C0 + s % CPT : 36 + (s - NK); };
+  constexpr int PF = AZ_C16_PF, NB = PF + 1;
+  uint4 bq[NB][4];
+  auto load_b = [&](int s, uint4 (&dst)[4]) {
+    if (s >= NKR) return;
+    const uint4* p = wl + (size_t)pk_of(s) * 8 * 2 * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = p[q * 64];
+  };
+#pragma unroll
+  for (int k = 0; k < PF; ++k) load_b(k, bq[k]);
+
+  // ---- the slab (+ zero row) by LDS-DMA: one wave instruction = two rows;
+  // with RES the block input's TR rows go to a second region after it
+  const int slab_u4 = (((slab_rows + 2) >> 1) << 1) * 32;
+  {
+    const int in_bytes = n_static * HW * 512;  // < 2^31 (checked by the engine)
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, in_bytes, 0x00020000);
+    const int pairs = (slab_rows + 2) >> 1;
+    for (int pr = wave; pr < pairs; pr += NT / 64) {  // wave-uniform
+      const int r = 2 * pr + (lane >> 5), slot = lane & 31;
+      const int g = row0 - halo + r;
+      const bool ok = r < slab_rows && g >= 0 && g < rows;
+      const unsigned voff = ok ? (unsigned)(g * 512 + (c16_logical(r, slot) << 4)) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void*)(lds + 2 * pr * 32), 16, voff, 0, 0, 0);
+    }
+    if constexpr (RES) {
+      const auto xsrc = __builtin_amdgcn_make_buffer_rsrc((void*)res_in, (short)0, in_bytes, 0x00020000);
+      for (int pr = wave; pr < TR / 2; pr += NT / 64) {
+        const int r = 2 * pr + (lane >> 5), slot = lane & 31;
+        const int g = row0 + r;
+        const unsigned voff = g < rows ? (unsigned)(g * 512 + (c16_logical(r, slot) << 4)) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xsrc, (__attribute__((address_space(3))) void*)(lds + slab_u4 + 2 * pr * 32), 16, voff, 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // (its fence waits for the DMA)
+
+  // ---- per lane: the four M blocks' pixels
+  const int mh = wave >> 2, nq = wave & 3;
+  const int r16 = lane & 15, gq = lane >> 4;
+  int lr[4], py[4], px[4];
+  bool valid[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    lr[mb] = mh * 64 + mb * 16 + r16;
+    const int g = row0 + lr[mb];
+    valid[mb] = g < rows;
+    const int p = g % HW;
+    py[mb] = p / W;
+    px[mb] = p - py[mb] * W;
+  }
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int abase[4], akey[4];  // slab row (uint4 units) and swizzle key of each M block's tap row
+  auto set_tap = [&](int t) {
+    if (t >= 9) {  // the fused residual: the block input's own row, second region
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        abase[mb] = valid[mb] ? slab_u4 + lr[mb] * 32 : zrow * 32;
+        akey[mb] = lr[mb];
+      }
+      return;
+    }
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const bool ok = valid[mb] && py[mb] + dy >= 0 && py[mb] + dy < H && px[mb] + dx >= 0 && px[mb] + dx < W;
+      const int sr = lr[mb] + halo + dy * W + dx;
+      abase[mb] = (ok ? sr : zrow) * 32;
+      akey[mb] = sr;  // also for the zero row: the lane keeps its bank quad
+    }
+  };
+  // executed k-step s -> (tap, 32-channel chunk)
+  auto tap_of = [&](int s) { return s < NK ? s / CPT : 9; };
+  auto chunk_of = [&](int s) { return s < NK ? C0 + s % CPT : s - NK; };
+  uint4 aq[2][2];
+  auto load_a = [&](int i) {  // flat index i = s * 4 + mb
+    const int s = i >> 2, mb = i & 3;
+    if (s >= NKR) return;
+    if (mb == 0 && (s == 0 || tap_of(s) != tap_of(s - 1))) set_tap(tap_of(s));
+    const int sl = c16_phys(akey[mb], 4 * chunk_of(s) + gq);
+    aq[i & 1][0] = lds[abase[mb] + sl];
+    aq[i & 1][1] = lds[abase[mb] + 16 + sl];
+  };
+  if (AZ_C16_APF) load_a(0);
+#pragma unroll
+  for (int s = 0; s < NKR; ++s) {
+    // k-steps stay in program order: without this the scheduler sinks the
+    // B prefetch next to its use and waits vmcnt(0) every few k-steps
+    __builtin_amdgcn_sched_barrier(0);
+    load_b(s + PF, bq[(s + PF) % NB]);
+    const uint4(&b)[4] = bq[s % NB];
+    const h8 B00 = __builtin_bit_cast(h8, b[0]), B01 = __builtin_bit_cast(h8, b[1]);
+    const h8 B10 = __builtin_bit_cast(h8, b[2]), B11 = __builtin_bit_cast(h8, b[3]);
+    const h8 b00 = unscale_b0(b[0]), b10 = unscale_b0(b[2]);
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const int i = s * 4 + mb;
+      load_a(i + AZ_C16_APF);  // 1: the next M block's fragments are in flight during these MFMAs
+      const h8 a0 = __builtin_bit_cast(h8, aq[i & 1][0]);
+      const h8 a1 = __builtin_bit_cast(h8, aq[i & 1][1]);
+      acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b00, acc[mb][0], 0, 0, 0);
+      acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B01, acc[mb][0], 0, 0, 0);
+      acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B00, acc[mb][0], 0, 0, 0);
+      acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b10, acc[mb][1], 0, 0, 0);
+      acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B11, acc[mb][1], 0, 0, 0);
+      acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B10, acc[mb][1], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: BN bias (+ residual's) + ReLU into an fp32 tile in LDS
+  __syncthreads();  // slab no longer read
+  float* tile = reinterpret_cast<float*>(lds);
+  float vmax = 0.f;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int col = 32 * nq + 16 * nb + r16;
+    const float bc = bias[col];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float y = fmaxf(fmaf(acc[mb][nb][v], oscale, bc), 0.f);
+        vmax = fmaxf(vmax, y);
+        tile[(mh * 64 + mb * 16 + 4 * gq + v) * kC16Pitch + col] = y;
+      }
+  }
+  if (!HEADS && vmax > kOverflow && err) atomicOr(err, kErrActRange);
+  __syncthreads();
+
+  // 16 threads per row, 8 channels each
+  for (int idx = tid; idx < TR * 16; idx += NT) {
+    const int r = idx >> 4, q = idx & 15;
+    const int g = row0 + r;
+    if (g >= rows) continue;
+    const float4 u = *reinterpret_cast<const float4*>(tile + r * kC16Pitch + 8 * q);
+    const float4 w = *reinterpret_cast<const float4*>(tile + r * kC16Pitch + 8 * q + 4);
+    const float x[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+    if constexpr (HEADS) {
+      // policy conv F->2, value conv F->1 (+ folded BN, ReLU; model.py:68-149):
+      // 8 channels per thread in order, then a fixed xor tree over the 16
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 8 * q + e;
+        s0 = fmaf(x[e], hc.wpc[2 * c], s0);
+        s1 = fmaf(x[e], hc.wpc[2 * c + 1], s1);
+        s2 = fmaf(x[e], hc.wvc[c], s2);
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o, 16);
+        s1 += __shfl_xor(s1, o, 16);
+        s2 += __shfl_xor(s2, o, 16);
+      }
+      if (q == 0)
+        hc.feat[g] = make_float4(fmaxf(s0 + hc.bpc[0], 0.f), fmaxf(s1 + hc.bpc[1], 0.f),
+                                 fmaxf(s2 + hc.bvc[0], 0.f), 0.f);
+    } else {
+      uint4 t0, t1;
+      split16x8(x, t0, t1);
+      out[(size_t)g * 32 + q] = t0;
+      out[(size_t)g * 32 + 16 + q] = t1;
+    }
+  }
+}
+
+size_t conv16_lds_bytes(int WM, int W, bool res) {
+  const int TR = kC16Tile * WM;
+  const size_t slab = (size_t)(((TR + 2 * (W + 1) + 2) >> 1) << 1) * 512;
+  const size_t tile = (size_t)TR * kC16Pitch * 4;
+  return std::max(slab + (res ? (size_t)TR * 512 : 0), tile);
+}
+
+template <int WM, bool RES, bool HEADS, int C0>
+static void launch_one(const Conv16Args& a, hipStream_t s) {
+  const int TR = kC16Tile * WM;
+  const int grid = (a.n_max * a.H * a.W + TR - 1) / TR;
+  if (grid <= 0) return;
+  const size_t bytes = conv16_lds_bytes(WM, a.W, RES);
+  static bool attr = false;  // one instantiation per call site: set the LDS cap once
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv16_kernel<WM, RES, HEADS, C0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  conv16_kernel<WM, RES, HEADS, C0><<<grid, 256 * WM, bytes, s>>>(
+      reinterpret_cast<const uint4*>(a.in), reinterpret_cast<const uint4*>(a.res_in),
+      reinterpret_cast<const uint4*>(a.wpack), a.bias, a.oscale, reinterpret_cast<uint4*>(a.out), a.heads,
+      a.count, a.n_max, a.H, a.W, a.err);
+}
+
+void launch_conv16(const Conv16Args& a, hipStream_t s) {
+  const bool heads = a.heads.feat != nullptr;
+  if (a.wm == 2) {
+    if (heads) launch_one<2, true, true, 0>(a, s);
+    else if (a.res_in) launch_one<2, true, false, 0>(a, s);
+    else if (a.first_chunk == 2) launch_one<2, false, false, 2>(a, s);
+    else launch_one<2, false, false, 0>(a, s);
+  } else {
+    if (heads) launch_one<1, true, true, 0>(a, s);
+    else if (a.res_in) launch_one<1, true, false, 0>(a, s);
+    else if (a.first_chunk == 2) launch_one<1, false, false, 2>(a, s);
+    else launch_one<1, false, false, 0>(a, s);
+  }
+}
+
+// ---------------------------------------------------------------- host side
+static uint16_t f16_bits(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+static float f16_value(uint16_t u) {
+  _Float16 h;
+  memcpy(&h, &u, 2);
+  return (float)h;
+}
+
+int conv16_prescale(const double* w, size_t n, const double* w2, size_t n2) {
+  double m = 0.0;
+  for (size_t i = 0; i < n; ++i) m = std::max(m, std::fabs(w[i]));
+  for (size_t i = 0; i < n2; ++i) m = std::max(m, std::fabs(w2[i]));
+  if (m == 0.0) return 0;
+  return (int)std::floor(std::log2(m / 8.0)) + 1;  // max |w * 2^-e| in (4, 8]
+}
+
+void conv16_pack(const double* w3, int cin_n, const double* wr, int e, std::vector<uint16_t>& out) {
+  const int F = 128;
+  const int nks = wr ? 40 : 36;
+  out.assign((size_t)nks * 8 * 2 * 64 * 8, 0);
+  const double sc = std::ldexp(1.0, -e);
+  auto put = [&](int ks, int cin, int co, double v) {
+    const float ws = (float)(v * sc);
+    const uint16_t b0 = f16_bits(ws);
+    const uint16_t b1 = f16_bits((ws - f16_value(b0)) * 4096.f);
+    const uint16_t B0 = f16_bits(f16_value(b0) * 4096.f);  // exact
+    const int kk = cin % 32, nb = co / 16;
+    const int ln = (kk / 8) * 16 + (co % 16), j = kk % 8;
+    const size_t base = ((((size_t)ks * 8 + nb) * 2) * 64 + ln) * 8 + j;
+    out[base] = B0;
+    out[base + 64 * 8] = b1;
+  };
+  for (int tap = 0; tap < 9; ++tap)
+    for (int cin = 0; cin < cin_n; ++cin)
+      for (int co = 0; co < F; ++co) put(tap * 4 + cin / 32, cin, co, w3[((size_t)tap * cin_n + cin) * F + co]);
+  if (wr)
+    for (int cin = 0; cin < F; ++cin)
+      for (int co = 0; co < F; ++co) put(36 + cin / 32, cin, co, wr[(size_t)cin * F + co]);
+}
+
+}  // namespace az

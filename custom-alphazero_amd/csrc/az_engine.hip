@@ -115,6 +115,8 @@ int check_device_errors(az_engine* e) {
     if (err & az::kErrPath) m += " path-overflow";
     if (err & az::kErrIllegal) m += " illegal-move";
     if (err & az::kErrNoRoot) m += " play-before-search";
+    if (err & az::kErrActRange)
+      m += " activation-range(|x| > 32752 for the fp16x2 convs: use conv_algo=AZ_CONV_DIRECT)";
     // play on a slot without a searched root changes nothing: that flag is
     // cleared once reported (the others mean a broken tree and stay)
     if (err == az::kErrNoRoot) AZ_HIP(hipMemset(e->t.stats + az::kStatErrors, 0, sizeof(err)));
@@ -156,14 +158,9 @@ int simulate(az_engine* e, Lane& L) {
     n_rows = L.t.nn_count;
   }
   if (e->cfg.evaluator == AZ_EVAL_NETWORK) {
-    static const bool stem_boards = [] {  // AZ_STEM_BOARDS=0: encode + float stem (A/B)
-      const char* v = getenv("AZ_STEM_BOARDS");
-      return !v || atoi(v) != 0;
-    }();
-    if (!stem_boards) az::launch_encode(rows, n_rows, L.n, L.g.HW, L.x, s);
+    // the stem reads the queued boards straight (no encode pass; bitwise the same outputs)
     az::launch_forward(e->net, L.x, n_rows, L.n, L.g.H, L.g.W, L.g.A, L.act[0], L.act[1], L.act[2],
-                       L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr,
-                       stem_boards ? rows : nullptr);
+                       L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr, rows);
   } else {
     az::launch_synth_eval(L.g, rows, n_rows, L.probs, L.values, s);
   }
@@ -255,93 +252,20 @@ int ready_to_search(az_engine* e) {
   return p;
 }
 
-// Winograd F(2x2,3x3) weights for wino_conv_kernel (az_wino.hip):
-// U[xi = 4a + b][cin][cout] = sum_{ky,kx} G[a][ky] G[b][kx] w[ky][kx][cin][cout]
-// in float64 from the folded Keras kernel, rounded once to float, in the
-// kernel's fragment order.
-// bf16 round-to-nearest-even bits of a float (finite), as the device's v_cvt_pk_bf16_f32 (split3)
-[[maybe_unused]] uint16_t bf16_bits(float f) {
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-[[maybe_unused]] float bf16_value(uint16_t h) {
-  const uint32_t u = (uint32_t)h << 16;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
-}
-// x (float) = t0 + t1 + t2, bf16 each (az_wino16x.hip)
-[[maybe_unused]] void split3_host(float x, uint16_t t[3]) {
-  t[0] = bf16_bits(x);
-  const float r1 = x - bf16_value(t[0]);
-  t[1] = bf16_bits(r1);
-  const float r2 = r1 - bf16_value(t[1]);
-  t[2] = bf16_bits(r2);
-}
-// bf16x3 terms packed as floats' storage (two bf16 per float slot) for upload
-[[maybe_unused]] std::vector<float> as_float_storage(const std::vector<uint16_t>& h) {
-  std::vector<float> f((h.size() + 1) / 2);
-  memcpy(f.data(), h.data(), h.size() * sizeof(uint16_t));
-  return f;
-}
-
-[[maybe_unused]] std::vector<float> pack_wino(const std::vector<double>& w, int F, int tiles, bool x3 = false) {
-  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
-  std::vector<float> p((size_t)16 * F * F);
-  std::vector<uint16_t> h(x3 ? (size_t)16 * F * F * 3 : 0);
-  std::vector<double> U((size_t)F * F);
-  for (int xi = 0; xi < 16; ++xi) {
-    const int a = xi >> 2, b = xi & 3;
-    std::fill(U.begin(), U.end(), 0.0);
-    for (int ky = 0; ky < 3; ++ky)
-      for (int kx = 0; kx < 3; ++kx) {
-        const double gg = G[a][ky] * G[b][kx];
-        if (gg == 0.0) continue;
-        const double* src = w.data() + (size_t)(ky * 3 + kx) * F * F;
-        for (size_t i = 0; i < (size_t)F * F; ++i) U[i] += gg * src[i];
-      }
-    for (int cin = 0; cin < F; ++cin)
-      for (int co = 0; co < F; ++co) {
-        if (x3) {  // az_wino16x.hip: three bf16 terms per weight
-          uint16_t t[3];
-          split3_host((float)U[(size_t)cin * F + co], t);
-          for (int k = 0; k < 3; ++k) h[az::wino16x_pack_index(xi, cin, co, k)] = t[k];
-          continue;
-        }
-        p[tiles == 16 ? az::wino16_pack_index(xi, cin, co) : az::wino_pack_index(xi, cin, co)] =
-            (float)U[(size_t)cin * F + co];
-      }
-  }
-  return x3 ? as_float_storage(h) : p;
-}
-
-// 1x1 projection residual [cin][cout] in the same fragment order, as if it
-// were point 0 of a 16-point-per-chunk stream compacted to one point.
-[[maybe_unused]] std::vector<float> pack_wino_res(const std::vector<double>& wr, int F, int tiles,
-                                                 bool x3 = false) {
-  if (x3) {
-    std::vector<uint16_t> h((size_t)F * F * 3);
-    for (int cin = 0; cin < F; ++cin)
-      for (int co = 0; co < F; ++co) {
-        uint16_t t[3];
-        split3_host((float)wr[(size_t)cin * F + co], t);
-        for (int k = 0; k < 3; ++k) h[az::wino16x_res_index(cin, co, k)] = t[k];
-      }
-    return as_float_storage(h);
-  }
-  std::vector<float> p((size_t)F * F);
-  const int CK = az::kWinoCK;
-  for (int cin = 0; cin < F; ++cin)
-    for (int co = 0; co < F; ++co) {
-      // index within the chunk's 16-point block, then compact chunks to 1 point
-      const size_t i16 = tiles == 16 ? az::wino16_pack_index(0, cin, co) : az::wino_pack_index(0, cin, co);
-      const size_t per_point = (size_t)4 * (CK / 8) * 64 * 4;  // floats per point per chunk
-      const size_t c = (size_t)cin / CK;
-      p[i16 - c * 16 * per_point + c * per_point] = (float)wr[(size_t)cin * F + co];
-    }
-  return p;
+// conv16_kernel pack (az_conv16.hip) of a folded 3x3 conv [3][3][cin][F] (+ the
+// 1x1 residual [F][F]): fp16 bits, uploaded as raw storage; *scale = 2^(e-12)
+[[maybe_unused]] int upload_conv16(std::vector<void*>& owned, uint16_t** dst, float* scale,
+                                   const std::vector<double>& w3, int cin, const std::vector<double>* wr) {
+  const int e = az::conv16_prescale(w3.data(), w3.size(), wr ? wr->data() : nullptr, wr ? wr->size() : 0);
+  std::vector<uint16_t> pack;
+  az::conv16_pack(w3.data(), cin, wr ? wr->data() : nullptr, e, pack);
+  *scale = std::ldexp(1.f, e - 12);
+  void* q = nullptr;
+  AZ_HIP(hipMalloc(&q, pack.size() * sizeof(uint16_t)));
+  owned.push_back(q);
+  *dst = reinterpret_cast<uint16_t*>(q);
+  AZ_HIP(hipMemcpy(q, pack.data(), pack.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  return 0;
 }
 
 [[maybe_unused]] int upload(std::vector<void*>& owned, float** dst, const std::vector<float>& src) {
@@ -435,23 +359,24 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       std::vector<float> ws(36 * F);
       for (int i = 0; i < 36 * F; ++i) ws[i] = (float)w[i];  // Keras order == (tap, c, n)
       if ((rc = upload(owned, &net.stem_w, ws))) return rc;
-    } else {  // [3][3][in_ch][F] zero-padded to [3][3][F][F]
-      std::vector<double> wp((size_t)9 * F * F, 0.0);
+    } else {  // [3][3][in_ch][F]: the conv16 pack pads the channels; direct: [3][3][F][F] zero-padded
+      if ((rc = upload_conv16(owned, &net.stem_k, &net.stem_scale, w, in_ch, nullptr))) return rc;
+      std::vector<float> wt((size_t)F * 9 * F, 0.f);
       for (int tap = 0; tap < 9; ++tap)
         for (int c = 0; c < in_ch; ++c)
-          for (int o = 0; o < F; ++o)
-            wp[((size_t)tap * F + c) * F + o] = w[((size_t)tap * in_ch + c) * F + o];
-      if ((rc = upload(owned, &net.stem_u, pack_wino(wp, F, net.wino_tiles, net.wino_x3 != 0)))) return rc;
+          for (int o = 0; o < F; ++o) wt[(size_t)o * 9 * F + tap * F + c] = (float)w[((size_t)tap * in_ch + c) * F + o];
+      if ((rc = upload(owned, &net.stem_d, pack_fragments(wt, F, 9 * F)))) return rc;
     }
     net.in_ch = in_ch;
   }
-  net.c1_w.resize(net.depth, nullptr);
-  net.c1_b.resize(net.depth, nullptr);
-  net.c2_w.resize(net.depth, nullptr);
-  net.c2_b.resize(net.depth, nullptr);
-  net.u1_w.resize(net.depth, nullptr);
-  net.u2_w.resize(net.depth, nullptr);
-  net.r2_w.resize(net.depth, nullptr);
+  net.c1_w.assign(net.depth, nullptr);
+  net.c1_b.assign(net.depth, nullptr);
+  net.c2_w.assign(net.depth, nullptr);
+  net.c2_b.assign(net.depth, nullptr);
+  net.k1.assign(net.depth, nullptr);
+  net.k2.assign(net.depth, nullptr);
+  net.k1_scale.assign(net.depth, 1.f);
+  net.k2_scale.assign(net.depth, 1.f);
   for (int d = 0; d < net.depth; ++d) {
     const std::string p = "block" + std::to_string(d);
     if ((rc = fold_unit(m, p + ".conv1", 3, F, F, eps, w, b))) return rc;
@@ -460,7 +385,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
     for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
     if ((rc = upload(owned, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
-        (rc = upload(owned, &net.u1_w[d], pack_wino(w, F, net.wino_tiles, net.wino_x3 != 0))) ||
+        (rc = upload_conv16(owned, &net.k1[d], &net.k1_scale[d], w, F, nullptr)) ||
         (rc = upload(owned, &net.c1_b[d], bt)))
       return rc;
     if ((rc = fold_unit(m, p + ".conv2", 3, F, F, eps, w, b))) return rc;
@@ -472,8 +397,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     }
     for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
     if ((rc = upload(owned, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
-        (rc = upload(owned, &net.u2_w[d], pack_wino(w, F, net.wino_tiles, net.wino_x3 != 0))) ||
-        (rc = upload(owned, &net.r2_w[d], pack_wino_res(wr, F, net.wino_tiles, net.wino_x3 != 0))) ||
+        (rc = upload_conv16(owned, &net.k2[d], &net.k2_scale[d], w, F, &wr)) ||
         (rc = upload(owned, &net.c2_b[d], bt2)))
       return rc;
   }
@@ -529,10 +453,12 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   const int A = c.gravity ? c.board_width : c.board_width * c.board_height;
   if (A > az::kMaxActions) return fail(AZ_E_INVALID, "action space too large");
   if (c.slots < 1 || c.mcts_iterations < 1) return fail(AZ_E_INVALID, "slots and mcts_iterations must be >= 1");
-  if (c.conv_algo != AZ_CONV_WINOGRAD && c.conv_algo != AZ_CONV_DIRECT)
-    return fail(AZ_E_INVALID, "conv_algo must be AZ_CONV_WINOGRAD or AZ_CONV_DIRECT");
-  if (c.evaluator == AZ_EVAL_NETWORK && (int64_t)c.slots * c.board_height * c.board_width * 128 >= (1ll << 31))
-    return fail(AZ_E_INVALID, "slots * H * W * 128 must stay below 2^31 (32-bit activation offsets)");
+  if (c.conv_algo != AZ_CONV_F16X2 && c.conv_algo != AZ_CONV_DIRECT)
+    return fail(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2 or AZ_CONV_DIRECT");
+  if (c.evaluator == AZ_EVAL_NETWORK && c.conv_algo == AZ_CONV_F16X2 && c.board_width > 16)
+    return fail(AZ_E_INVALID, "AZ_CONV_F16X2 supports boards up to 16 columns (use AZ_CONV_DIRECT)");
+  if (c.evaluator == AZ_EVAL_NETWORK && (int64_t)c.slots * c.board_height * c.board_width * 512 >= (1ll << 31))
+    return fail(AZ_E_INVALID, "slots * H * W * 512 must stay below 2^31 (32-bit activation byte offsets)");
   if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC)
     return fail(AZ_E_INVALID, "unknown evaluator");
   if (c.evaluator == AZ_EVAL_NETWORK && c.filters != 128)
@@ -648,13 +574,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   }
   e->net.depth = c.depth;
   e->net.algo = c.conv_algo;
-  {  // Winograd variant (az_wino.hip 32 tiles / az_wino16.hip 16 tiles); AZ_WINO_TILES for A/B runs
-    const char* wt = getenv("AZ_WINO_TILES");
-    e->net.wino_tiles = wt ? atoi(wt) : 16;
-    const char* x3 = getenv("AZ_WINO_X3");  // fp32 products from bf16 terms (az_wino16x.hip)
-    // (its buffer loads address activations with 31-bit byte offsets)
-    e->net.wino_x3 = (x3 ? atoi(x3) : 1) && (size_t)S * g.HW * 128 * 4 < ((size_t)1 << 31);
-  }
+  e->net.err = e->t.stats + az::kStatErrors;
   // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
   int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);
   nl = std::min(nl, std::min(g.slots, 8));

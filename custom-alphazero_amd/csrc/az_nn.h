@@ -7,25 +7,24 @@
 
 namespace az {
 
-// Folded (BatchNorm-in) fp32 weights resident in HBM.  Layouts are chosen for
-// the kernels, not copied from Keras: conv weights are [Cout][K] with K
-// contiguous (K = tap*Cin + c), so a 32-wide K chunk of 128 output channels is
-// a [128][32] tile loaded with 16-byte reads.
+// Folded (BatchNorm-in) weights resident in HBM, packed for the kernels (not
+// Keras layouts).  AZ_CONV_F16X2 (default): conv16_kernel packs (fp16 term
+// pairs, az_conv16.hip) and split16 activations; AZ_CONV_DIRECT: fp32 MFMA
+// fragment packs ([chunk][tile][q][lane] float4) and fp32 activations.
 struct NetDev {
   int filters = 128, depth = 0, hidden = 256;
-  int algo = 0;  // AZ_CONV_WINOGRAD / AZ_CONV_DIRECT
-  int wino_ksplit = 1;  // 32-tile Winograd kernel: 1, or 2 = two chunk groups per workgroup
-  int wino_tiles = 32;  // tiles per workgroup: 32 (wino_conv_kernel) or 16 (wino16_conv_kernel);
-                        // one variant for every conv of a network (set before load_network)
-  int wino_x3 = 0;      // 16 tiles: 1 = wino16x_conv_kernel (fp32 products from three bf16 terms)
+  int algo = 0;             // AZ_CONV_F16X2 / AZ_CONV_DIRECT (one algorithm for every forward)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
-  float* stem_w = nullptr;  // [36][F]  (k = tap*4 + c), in_ch == 4
-  float* stem_u = nullptr;  // Winograd U of the zero-padded stem [3][3][F][F], in_ch > 4
+  float* stem_w = nullptr;  // in_ch == 4: [36][F] (k = tap*4 + c), VALU stem kernels
   float* stem_b = nullptr;  // [F]
-  std::vector<float*> c1_w, c1_b;  // fragment-packed [9F x F], [F]
-  std::vector<float*> c2_w, c2_b;  // fragment-packed [10F x F] (conv2 taps, then 1x1 residual), [F]
-  std::vector<float*> u1_w, u2_w;  // Winograd U[16][F][F], packed (az_engine.hip pack_wino)
-  std::vector<float*> r2_w;        // 1x1 projection residual [F][F], Winograd fragment order
+  // in_ch > 4 (chess): the stem is one more 3x3 conv over the zero-padded planes
+  uint16_t* stem_k = nullptr;  // conv16 pack (36 k-steps)
+  float stem_scale = 1.f;      // its 2^(e-12)
+  float* stem_d = nullptr;     // direct-kernel fragments [9F x F]
+  std::vector<uint16_t*> k1, k2;  // conv16 packs: conv1 (36 k-steps), conv2 + 1x1 residual (40)
+  std::vector<float> k1_scale, k2_scale;
+  std::vector<float*> c1_w, c1_b;  // direct: fragment-packed [9F x F]; folded bias [F]
+  std::vector<float*> c2_w, c2_b;  // direct: [10F x F] (conv2 taps, then the 1x1 residual); bias conv2 + res
   float *pc_w = nullptr, *pc_b = nullptr;  // policy conv [F][2], [2]
   float *vc_w = nullptr, *vc_b = nullptr;  // value conv [F], [1]
   float *pd_w = nullptr, *pd_b = nullptr;  // policy dense [2HW][A], [A]
@@ -33,6 +32,7 @@ struct NetDev {
                            // policy_dense_kernel column tile, zero past A
   float *v1_w = nullptr, *v1_b = nullptr;  // value dense1 [HW][hidden], [hidden]
   float *v2_w = nullptr, *v2_b = nullptr;  // value dense2 [hidden], [1]
+  unsigned long long* err = nullptr;       // the engine's device error word (kErrActRange)
   bool ready = false;
 };
 
@@ -94,51 +94,94 @@ void launch_encode(const Board* boards, const int* count, int n_max, int HW, flo
                    hipStream_t s);
 void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* mask,
                        hipStream_t s);
-// Winograd conv: input channels per LDS chunk (16 or 32; the host packing
-// follows it) and the packing index of a weight in the kernel's B stream
-#ifndef AZ_WINO_CK
-#define AZ_WINO_CK 32
-#endif
-constexpr int kWinoCK = AZ_WINO_CK;
-size_t wino_pack_index(int xi, int cin, int cout);
-size_t wino16_pack_index(int xi, int cin, int cout);  // az_wino16.hip
-size_t wino16x_pack_index(int xi, int cin, int cout, int k);  // az_wino16x.hip (bf16 units)
-size_t wino16x_res_index(int cin, int cout, int k);
-// 16-tile variant on v_mfma_f32_16x16x4_f32 (small launches; az_wino16.hip)
-struct HeadConv;
-void launch_wino16_conv(const float* in, const float* res_in, const float* upack, const float* rpack,
-                        const float* bias, float* out, const int* count, int n_max, int H, int W,
-                        hipStream_t s, const HeadConv* heads = nullptr, int first_chunk = 0);
-void launch_wino16x_conv(const float* in, const float* res_in, const float* upack, const float* rpack,
-                         const float* bias, float* out, const int* count, int n_max, int H, int W,
-                         hipStream_t s, const HeadConv* heads = nullptr, int first_chunk = 0);
-// The heads' 1x1 convolutions (policy F->2, value F->1, each + folded BN +
-// ReLU, model.py:68-149), fused into the last block's conv2 epilogue: feat =
-// [boards][HW] float4 (policy ch 0, policy ch 1, value, 0); the block output
-// itself is then never written.
-struct HeadConv {
+// conv16_kernel (az_conv16.hip): direct 3x3 conv on the fp16 MFMA with
+// split16 activations (x ~= t0 + t1 * 2^-12, per pixel 512 B: t0 of the 128
+// channels, then t1) and host-packed two-term weights (conv16_pack)
+struct Conv16Heads {
   const float* wpc;  // [F][2]
   const float* bpc;  // [2]
   const float* wvc;  // [F]
   const float* bvc;  // [1]
-  float4* feat;      // null: write the block output instead
+  float4* feat;      // non-null: the heads' 1x1 convs instead of storing the block output
 };
-// ksplit = 2: the two-chunk-group variant (small batches; az_wino.hip)
-void launch_wino_conv(const float* in, const float* res_in, const float* upack,
-                      const float* rpack, const float* bias, float* out, const int* count,
-                      int n_max, int H, int W, hipStream_t s, const HeadConv* heads = nullptr,
-                      int ksplit = 1);
-// x: [n][HW][4]; count (device int, may be null -> n_max) is the live batch.
-// boards (optional): one-hot input straight from the eval queue's boards
-// (bitwise the same outputs as encoding them into x first)
+struct Conv16Args {
+  const void* in = nullptr;      // split16 rows [n_max*H*W]
+  const void* res_in = nullptr;  // block input (fused 1x1 projection residual), or null
+  const void* wpack = nullptr;   // conv16_pack layout (36 or 40 k-steps)
+  const float* bias = nullptr;   // folded BN bias (+ the residual's)
+  float oscale = 1.f;            // 2^(e - 12) for the weights' prescale e
+  void* out = nullptr;           // split16 rows
+  Conv16Heads heads{};
+  const int* count = nullptr;    // live boards (device), or null -> n_max
+  int n_max = 0, H = 0, W = 0;
+  int wm = 2;                    // 1: 64-row tiles (4 waves), 2: 128-row tiles (8 waves)
+  int first_chunk = 0;           // 2: input channels 0..63 are known zero (chess self-play stem)
+  unsigned long long* err = nullptr;  // device error word: kErrActRange if an output leaves the split16 range
+};
+void launch_conv16(const Conv16Args& a, hipStream_t s);
+size_t conv16_lds_bytes(int WM, int W, bool res);
+// power-of-two prescale e of a conv's weights (max |w * 2^-e| in (4, 8])
+int conv16_prescale(const double* w, size_t n, const double* w2, size_t n2);
+// weights [3][3][cin_n][128] (+ 1x1 residual [128][128]) -> uint16 fp16 bits
+void conv16_pack(const double* w3, int cin_n, const double* wr, int e, std::vector<uint16_t>& out);
 // Folds and uploads the network weights (Keras names, model/weights.py);
 // device buffers are appended to `owned` (az_engine.hip)
 int load_network(NetDev& net, const ::az_tensor* tensors, int n, int in_ch, int HW, int A,
                  double eps, std::vector<void*>& owned);
-// x: [n][HW][4] (in_ch == 4) or [n][HW][F] zero-padded planes (in_ch > 4)
-void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
-                    int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
+// x: [n][HW][4] fp32 (in_ch == 4), or the zero-padded planes [n][HW][F] (in_ch > 4) as split16 rows
+// (AZ_CONV_F16X2) or fp32 (AZ_CONV_DIRECT); count (device int, may be null -> n_max) is the live
+// batch; boards (optional): one-hot input straight from the eval queue's boards (bitwise the same
+// outputs as encoding them into x first); stem_first_chunk: input planes below 32 * it are known zero
+void launch_forward(const NetDev& net, const void* x, const int* count, int n_max, int H, int W,
+                    int A, void* act_a, void* act_b, void* act_c, float* probs, float* values,
                     hipStream_t s, ConvTimer* timer, const Board* boards = nullptr,
                     int stem_first_chunk = 0);
+// fp32 rows [n][c_src] -> the network's input layout for in_ch > 4: [n][F] zero-padded, as split16
+// rows (split = true) or fp32
+void launch_pad_rows(const float* src, int n, int c_src, void* dst, bool split, hipStream_t s);
+
+// split16 of 8 floats: x ~= t0 + t1 * 2^-12 (t0 = fp16_rn(x), t1 = fp16_rn((x - t0) * 2^12), the
+// subtraction exact), 8 fp16 each -- the layout every kernel writing conv16 input uses
+typedef _Float16 az_h2 __attribute__((ext_vector_type(2)));
+typedef float az_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((az_f2{a, b}), az_h2));
+}
+__device__ __forceinline__ void split16x8(const float (&x)[8], uint4& t0, uint4& t1) {
+  uint32_t p[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[i] = pk_f16(x[2 * i], x[2 * i + 1]);
+    const az_h2 h = __builtin_bit_cast(az_h2, p[i]);
+    q[i] = pk_f16((x[2 * i] - (float)h[0]) * 4096.f, (x[2 * i + 1] - (float)h[1]) * 4096.f);
+  }
+  t0 = make_uint4(p[0], p[1], p[2], p[3]);
+  t1 = make_uint4(q[0], q[1], q[2], q[3]);
+}
+__device__ __forceinline__ void split16x4(const float4 v, uint2& t0, uint2& t1) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t p[2], q[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    p[i] = pk_f16(x[2 * i], x[2 * i + 1]);
+    const az_h2 h = __builtin_bit_cast(az_h2, p[i]);
+    q[i] = pk_f16((x[2 * i] - (float)h[0]) * 4096.f, (x[2 * i + 1] - (float)h[1]) * 4096.f);
+  }
+  t0 = make_uint2(p[0], p[1]);
+  t1 = make_uint2(q[0], q[1]);
+}
+// store 4 channels (c4 = channel / 4) of an activation row: fp32 or split16
+template <bool SPLIT>
+__device__ __forceinline__ void store_act4(void* act, size_t row, int c4, const float4 v) {
+  if constexpr (SPLIT) {
+    uint2 t0, t1;
+    split16x4(v, t0, t1);
+    uint2* r = reinterpret_cast<uint2*>(reinterpret_cast<char*>(act) + row * 512);
+    r[c4] = t0;
+    r[32 + c4] = t1;
+  } else {
+    reinterpret_cast<float4*>(act)[row * 32 + c4] = v;
+  }
+}
 
 }  // namespace az

@@ -12,10 +12,11 @@
 //
 // Kernels (each one's roofline in DESIGN.md):
 //   encode_boards    Board.full_state for the eval queue (HBM/latency bound)
-//   stem_conv        K = 36, VALU
-//   conv3x3_mfma     implicit GEMM on v_mfma_f32_32x32x2_f32 (exact f32 FMA
-//                    chains): M = boards*HW rows, N = F, K = 9F (+F for the
-//                    fused 1x1 projection residual).  MFMA bound.
+//   stem_conv        K = 36, VALU; writes split16 rows (AZ_CONV_F16X2) or fp32
+//   conv16_kernel    the tower's 3x3 convs, default (az_conv16.hip)
+//   conv3x3_mfma     AZ_CONV_DIRECT: implicit GEMM on v_mfma_f32_32x32x2_f32
+//                    (exact f32 FMA chains): M = boards*HW rows, N = F, K = 9F
+//                    (+F for the fused 1x1 projection residual).  MFMA bound.
 //   heads            one wave per board
 // Reduction order is fixed per output element and independent of the batch,
 // so a board's outputs do not depend on what else is in the batch.
@@ -24,10 +25,6 @@
 #include <algorithm>
 
 #include "az_nn.h"
-
-#ifndef AZ_FUSE_HEADS
-#define AZ_FUSE_HEADS 1
-#endif
 
 namespace az {
 
@@ -59,12 +56,12 @@ __global__ void legal_mask_kernel(const Board* __restrict__ boards, int n, GameC
 // -------------------------------------------------------------------- stem
 // conv3x3 4 -> F with 'same' zero padding, folded BN, ReLU.  One thread per
 // (row, 4 output channels).  ws: [36][F] with k = tap*4 + c, tap = ky*3+kx.
-template <int F>
+template <int F, bool SPLIT>
 __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict__ x,
                                                         const float* __restrict__ ws,
                                                         const float* __restrict__ bias,
                                                         const int* __restrict__ count, int n_static,
-                                                        int H, int W, float* __restrict__ out) {
+                                                        int H, int W, void* __restrict__ out) {
   // weights (18 KB) are read through L1 by every thread: no per-block LDS
   // staging (which cost ~18 KB of L2 traffic per 256 outputs)
   constexpr int G4 = F / 4;
@@ -95,7 +92,7 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
   acc.y = fmaxf(acc.y, 0.0f);
   acc.z = fmaxf(acc.z, 0.0f);
   acc.w = fmaxf(acc.w, 0.0f);
-  *reinterpret_cast<float4*>(out + (size_t)r * F + cg * 4) = acc;
+  store_act4<SPLIT>(out, (size_t)r, cg, acc);
 }
 
 // Same layer straight from the boards (self-play): the input is one-hot, so
@@ -142,12 +139,12 @@ __device__ __forceinline__ void stage_lds(float* dst, const float* __restrict__ 
   }
 }
 
-template <int F>
+template <int F, bool SPLIT>
 __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict__ boards,
                                                          const float* __restrict__ ws,
                                                          const float* __restrict__ bias,
                                                          const int* __restrict__ count, int n_static,
-                                                         int H, int W, float* __restrict__ out) {
+                                                         int H, int W, void* __restrict__ out) {
   constexpr int G4 = F / 4;
   static_assert(256 % G4 == 0, "a pass covers whole pixels");
   constexpr int PPB = 256 / G4;  // pixels per pass
@@ -191,7 +188,7 @@ __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict
     acc.y = fmaxf(acc.y, 0.0f);
     acc.z = fmaxf(acc.z, 0.0f);
     acc.w = fmaxf(acc.w, 0.0f);
-    *reinterpret_cast<float4*>(out + (size_t)r * F + cg * 4) = acc;
+    store_act4<SPLIT>(out, (size_t)r, cg, acc);
   }
 }
 
@@ -200,12 +197,12 @@ __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict
 //   k in [0, 9F): A = in[neighbour(r, tap)][c], tap = k / F, c = k % F
 //   k in [9F, 10F) (RESIDUAL): A = res_in[r][c]  (fused 1x1 projection)
 //
-// Workgroup = 4 waves = a 64-row x 128-column output tile.  Wave w owns rows
-// [32*(w>>1), +32) and the two 32-column MFMA tiles 2*(w&1), 2*(w&1)+1.
+// Workgroup = 4 waves = a 32-row x 128-column output tile; wave w owns
+// columns [32w, +32).
 //   * A: the tile's input rows plus a halo of W+1 rows on each side are staged
 //     ONCE into LDS (the "slab"); every tap reads its shifted view of it, and
-//     off-board neighbours read a zero row (the fused residual's 4 chunks read
-//     the lane's own block-input row from global instead).  Rows are 128 floats = 32 16-byte
+//     off-board neighbours read a zero row (the fused residual's block-input
+//     rows are staged beside it).  Rows are 128 floats = 32 16-byte
 //     chunks, chunk j of slab row r stored at j ^ (r & 15): the 16 distinct
 //     rows a ds_read_b128 lane group touches land on 16 distinct bank quads.
 //   * B: weights are pre-packed on the host in MFMA fragment order
@@ -223,31 +220,23 @@ __device__ __forceinline__ int slab_swz(int chunk, int key) {
   return (chunk & 16) | ((chunk ^ key) & 15);
 }
 
-// Variant flags (A/B-tested in profiles/conv_bench.py via AZ_CONV_VARIANT):
-//   PREA  : read the next chunk's A fragments from LDS one chunk ahead
-//   XSLAB : stage the fused residual's block-input rows in LDS (else: global)
-//   OCC   : __launch_bounds__ waves per SIMD (register cap)
-size_t conv_lds_bytes(int TR, int W, bool residual, bool xslab) {
+size_t conv_lds_bytes(int TR, int W, bool residual) {
   const int slab_rows = TR + 2 * (W + 1);
-  return (size_t)(slab_rows + 1 + (residual && xslab ? TR : 0)) * 512;
+  return (size_t)(slab_rows + 1 + (residual ? TR : 0)) * 512;
 }
 
-// DIAG (timing experiments only, wrong outputs): 1 = no B loads after the
-// first two chunks, 2 = no A LDS reads after the first chunk.
-// Tile shape: each wave owns RPW x TPW 32x32 MFMA tiles (RPW row tiles that
-// share every B fragment, TPW column tiles that share every A fragment); the
-// four waves of a workgroup are CG = 4/TPW column groups x RG = 4/CG row
-// groups, so a workgroup covers TR = 32*RPW*RG rows x 128 columns.
-template <int F, bool RESIDUAL, bool PREA, bool XSLAB, int OCC, int DIAG, int TPW, int RPW>
-__global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
+// One 32x32 MFMA tile per wave: the four waves take 32-column slices of a
+// 32-row x 128-column output tile.  (Round-1 A/B, DESIGN.md: wider tiles,
+// A read one chunk ahead, the residual rows from global and 3-4 waves/SIMD
+// all measured slower and were removed.)
+template <int F, bool RESIDUAL>
+__global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     const float* __restrict__ in, const float* __restrict__ res_in,
     const float4* __restrict__ wpack, const float* __restrict__ bias, float* __restrict__ out,
     const int* __restrict__ count, int n_static, int H, int W) {
   static_assert(F == 128, "tile assumes F = 128 channels (32 16-byte chunks per row)");
   constexpr int NCH = (RESIDUAL ? 10 : 9) * (F / kChunkK);
-  constexpr int CG = 4 / TPW;   // column groups
-  constexpr int RG = 4 / CG;    // row groups
-  constexpr int TR = 32 * RPW * RG;
+  constexpr int TR = 32;
   extern __shared__ __attribute__((aligned(16))) float4 lds4[];
 
   const int HW = H * W, halo = W + 1;
@@ -261,7 +250,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
   float4* zero_row = lds4 + slab_rows * 32;
   float4* xslab = zero_row + 32;
 
-  // ---- stage the slab (and, with XSLAB, the residual rows) once
+  // ---- stage the slab (and the residual rows) once
   const float4* in4 = reinterpret_cast<const float4*>(in);
   for (int i = tid; i < slab_rows * 32; i += 256) {
     const int r = i >> 5, j = i & 31, g = row0 - halo + r;
@@ -269,7 +258,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
     slab[r * 32 + slab_swz(j, r)] = v;
   }
   if (tid < 32) zero_row[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (RESIDUAL && XSLAB) {
+  if constexpr (RESIDUAL) {
     const float4* x4 = reinterpret_cast<const float4*>(res_in);
     for (int i = tid; i < TR * 32; i += 256) {
       const int r = i >> 5, j = i & 31, g = row0 + r;
@@ -281,126 +270,75 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_mfma_kernel(
 
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, r32 = lane & 31;
-  const int rg = wave / CG, cg = wave % CG;
-  int rl[RPW], grow[RPW], py[RPW], px[RPW];
-  bool row_ok[RPW];
-#pragma unroll
-  for (int rt = 0; rt < RPW; ++rt) {
-    rl[rt] = (rg * RPW + rt) * 32 + r32;  // local row of this lane's A operand
-    grow[rt] = row0 + rl[rt];
-    const int pos = grow[rt] % HW;
-    py[rt] = pos / W;
-    px[rt] = pos - (pos / W) * W;
-    row_ok[rt] = grow[rt] < rows;
-  }
+  const int rl = r32;  // local row of this lane's A operand
+  const int grow = row0 + rl;
+  const int pos = grow % HW;
+  const int py = pos / W, px = pos - (pos / W) * W;
+  const bool row_ok = grow < rows;
 
-  f32x16 acc[RPW][TPW];
+  f32x16 acc;
 #pragma unroll
-  for (int rt = 0; rt < RPW; ++rt)
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[rt][t][i] = 0.0f;
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
 
   // B fragment stream: float4 index ((c*4 + tile)*4 + q)*64 + lane.  Two
   // register buffers in ping-pong (the loop is unrolled by two, so no copy):
   // chunk c+1's loads are first consumed a whole chunk of MFMAs later.
-  const float4* wl = wpack + (size_t)(TPW * cg) * 256 + lane;
-  float4 b0[TPW][4], b1[TPW][4];
-  auto load_b = [&](int c, float4 (&dst)[TPW][4]) {
-    if (DIAG == 1 && c >= 2) return;
+  const float4* wl = wpack + (size_t)wave * 256 + lane;
+  float4 b0[4], b1[4];
+  auto load_b = [&](int c, float4 (&dst)[4]) {
     const float4* wn = wl + (size_t)c * 1024;
 #pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dst[t][q] = wn[t * 256 + q * 64];
+    for (int q = 0; q < 4; ++q) dst[q] = wn[q * 64];
   };
-  auto load_a = [&](int c, float4 (&dst)[RPW][4]) {
-    if (DIAG == 2 && c >= 2) return;
+  auto load_a = [&](int c, float4 (&dst)[4]) {
     const int tap = c >> 2;
-#pragma unroll
-    for (int rt = 0; rt < RPW; ++rt) {
-      const float4* base;
-      int key;
-      if (!RESIDUAL || tap < 9) {
-        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        const bool ok = row_ok[rt] && py[rt] + dy >= 0 && py[rt] + dy < H && px[rt] + dx >= 0 &&
-                        px[rt] + dx < W;
-        const int sr = rl[rt] + halo + dy * W + dx;
-        base = ok ? slab + sr * 32 : zero_row;
-        key = ok ? (sr & 15) : 0;
-      } else if constexpr (XSLAB) {
-        base = xslab + rl[rt] * 32;
-        key = rl[rt] & 15;
-      } else {
-        // fused 1x1 residual (4 of 40 chunks): this lane's own block-input
-        // row, straight from global
-        const float4* xr = reinterpret_cast<const float4*>(res_in) + (size_t)grow[rt] * 32 +
-                           (c & 3) * 8 + h * 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          dst[rt][q] = row_ok[rt] ? xr[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        continue;
-      }
-      const int cbase = (c & 3) * 8 + h * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dst[rt][q] = base[slab_swz(cbase + q, key)];
+    const float4* base;
+    int key;
+    if (!RESIDUAL || tap < 9) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const bool ok = row_ok && py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
+      const int sr = rl + halo + dy * W + dx;
+      base = ok ? slab + sr * 32 : zero_row;
+      key = ok ? (sr & 15) : 0;
+    } else {
+      base = xslab + rl * 32;
+      key = rl & 15;
     }
+    const int cbase = (c & 3) * 8 + h * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = base[slab_swz(cbase + q, key)];
   };
-  auto compute = [&](const float4 (&a4)[RPW][4], const float4 (&bc)[TPW][4]) {
+  auto compute = [&](const float4 (&a4)[4], const float4 (&bc)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int rt = 0; rt < RPW; ++rt) {
-          const float av = e == 0 ? a4[rt][q].x : e == 1 ? a4[rt][q].y : e == 2 ? a4[rt][q].z : a4[rt][q].w;
-#pragma unroll
-          for (int t = 0; t < TPW; ++t) {
-            const float bv = e == 0 ? bc[t][q].x : e == 1 ? bc[t][q].y : e == 2 ? bc[t][q].z : bc[t][q].w;
-            acc[rt][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[rt][t], 0, 0, 0);
-          }
-        }
-      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].x, bc[q].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].y, bc[q].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].z, bc[q].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[q].w, bc[q].w, acc, 0, 0, 0);
     }
   };
   static_assert(NCH % 2 == 0, "ping-pong loop needs an even chunk count");
-  float4 a0[RPW][4], a1[RPW][4];
+  float4 a0[4], a1[4];
   load_b(0, b0);
-  if constexpr (PREA) load_a(0, a0);
   // fully unrolled: no loop back-edge, so the waitcnt pass sees exactly which
-  // loads each MFMA needs (a rolled loop merged the pending state and waited
-  // on the chunk just issued); tap geometry folds to constants per chunk
+  // loads each MFMA needs; tap geometry folds to constants per chunk
 #pragma unroll
   for (int c = 0; c < NCH; c += 2) {
     load_b(c + 1, b1);
-    if constexpr (PREA) {
-      load_a(c + 1, a1);
-    } else {
-      load_a(c, a0);
-    }
+    load_a(c, a0);
     compute(a0, b0);
-    if (c + 2 < NCH) {
-      load_b(c + 2, b0);
-      if constexpr (PREA) load_a(c + 2, a0);
-    }
-    if constexpr (!PREA) load_a(c + 1, a1);
+    if (c + 2 < NCH) load_b(c + 2, b0);
+    load_a(c + 1, a1);
     compute(a1, b1);
   }
 
   // epilogue: C/D map col = lane&31, row = (i&3) + 8*(i>>2) + 4*h
+  const int col = wave * 32 + r32;
+  const float bcol = bias[col];
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const int col = (TPW * cg + t) * 32 + r32;
-    const float bcol = bias[col];
-#pragma unroll
-    for (int rt = 0; rt < RPW; ++rt) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = row0 + (rg * RPW + rt) * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (row < rows) out[(size_t)row * F + col] = fmaxf(acc[rt][t][i] + bcol, 0.0f);
-      }
-    }
+  for (int i = 0; i < 16; ++i) {
+    const int row = row0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (row < rows) out[(size_t)row * F + col] = fmaxf(acc[i] + bcol, 0.0f);
   }
 }
 
@@ -675,101 +613,123 @@ void launch_legal_mask(const Board* boards, int n, const GameCfg& g, uint8_t* ma
   legal_mask_kernel<<<(total + 255) / 256, 256, 0, s>>>(boards, n, g, mask);
 }
 
-// the network's 16-tile variant: fp32 MFMA (az_wino16.hip) or bf16x3 terms
-// (az_wino16x.hip); one variant for every forward of an engine
-static void launch_w16(const NetDev& net, const float* in, const float* res_in, const float* upack,
-                       const float* rpack, const float* bias, float* out, const int* count, int n_max, int H,
-                       int W, hipStream_t s, const HeadConv* heads = nullptr, int first_chunk = 0) {
-  if (net.wino_x3)
-    launch_wino16x_conv(in, res_in, upack, rpack, bias, out, count, n_max, H, W, s, heads, first_chunk);
-  else
-    launch_wino16_conv(in, res_in, upack, rpack, bias, out, count, n_max, H, W, s, heads, first_chunk);
+// fp32 rows [n][c_src] -> [n][F] zero-padded: split16 (AZ_CONV_F16X2) or fp32 (AZ_CONV_DIRECT)
+__global__ void pad_rows_kernel(const float* __restrict__ src, int n, int c_src, void* __restrict__ dst,
+                                bool split) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * 32) return;
+  const int r = idx >> 5, c4 = idx & 31;
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * c4 + i;
+    v[i] = c < c_src ? src[(size_t)r * c_src + c] : 0.f;
+  }
+  const float4 q = make_float4(v[0], v[1], v[2], v[3]);
+  if (split) store_act4<true>(dst, (size_t)r, c4, q);
+  else store_act4<false>(dst, (size_t)r, c4, q);
 }
 
-void launch_forward(const NetDev& net, const float* x, const int* count, int n_max, int H, int W,
-                    int A, float* act_a, float* act_b, float* act_c, float* probs, float* values,
+void launch_pad_rows(const float* src, int n, int c_src, void* dst, bool split, hipStream_t s) {
+  if (n <= 0) return;
+  pad_rows_kernel<<<(n * 32 + 255) / 256, 256, 0, s>>>(src, n, c_src, dst, split);
+}
+
+template <bool RES>
+static void launch_direct(const float* in, const float* res_in, const float* w, const float* bias, float* out,
+                          const int* count, int n_max, int H, int W, hipStream_t s) {
+  const int grid = (n_max * H * W + 31) / 32;
+  conv3x3_mfma_kernel<128, RES><<<grid, 256, conv_lds_bytes(32, W, RES), s>>>(
+      in, res_in, reinterpret_cast<const float4*>(w), bias, out, count, n_max, H, W);
+}
+
+void launch_forward(const NetDev& net, const void* x, const int* count, int n_max, int H, int W,
+                    int A, void* act_a, void* act_b, void* act_c, float* probs, float* values,
                     hipStream_t s, ConvTimer* timer, const Board* boards, int stem_first_chunk) {
   if (n_max <= 0) return;
   const int HW = H * W;
   constexpr int F = 128;
-  if (net.stem_u) {
-    // chess: 118 input planes zero-padded to F, the stem is one more Winograd conv
+  const bool f16 = net.algo == AZ_CONV_F16X2;
+  Conv16Args ca;
+  ca.count = count;
+  ca.n_max = n_max;
+  ca.H = H;
+  ca.W = W;
+  ca.wm = 1;
+  ca.err = net.err;
+  if (net.in_ch > 4) {
+    // chess: 118 input planes zero-padded to F, the stem is one more 3x3 conv;
     // stem_first_chunk: input chunks (32 planes) before it are known zero and
-    // skipped -- they would add exact zeros (chess self-play: planes 0-83)
-    if (net.wino_tiles == 16)
-      launch_w16(net, x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
-                         stem_first_chunk);
-    else
-      launch_wino_conv(x, nullptr, net.stem_u, nullptr, net.stem_b, act_a, count, n_max, H, W, s, nullptr,
-                       net.wino_ksplit);
+    // skipped -- they would add exact zeros (chess self-play: planes 0-63)
+    if (f16) {
+      Conv16Args a = ca;
+      a.in = x;
+      a.wpack = net.stem_k;
+      a.bias = net.stem_b;
+      a.oscale = net.stem_scale;
+      a.out = act_a;
+      a.first_chunk = stem_first_chunk;
+      launch_conv16(a, s);
+    } else {
+      launch_direct<false>(static_cast<const float*>(x), nullptr, net.stem_d, net.stem_b,
+                           static_cast<float*>(act_a), count, n_max, H, W, s);
+    }
   } else {
     const int total = n_max * HW * (F / 4);
-    if (boards)
-      stem_board_kernel<F><<<std::min((n_max * HW + 7) / 8, 1024), 256, 0, s>>>(
-          boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a);
-    else
-      stem_conv_kernel<F><<<(total + 255) / 256, 256, 0, s>>>(
-          reinterpret_cast<const float4*>(x), net.stem_w, net.stem_b, count, n_max, H, W, act_a);
+    if (boards) {
+      if (f16)
+        stem_board_kernel<F, true><<<std::min((n_max * HW + 7) / 8, 1024), 256, 0, s>>>(
+            boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a);
+      else
+        stem_board_kernel<F, false><<<std::min((n_max * HW + 7) / 8, 1024), 256, 0, s>>>(
+            boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a);
+    } else {
+      const float4* x4 = static_cast<const float4*>(x);
+      if (f16)
+        stem_conv_kernel<F, true><<<(total + 255) / 256, 256, 0, s>>>(x4, net.stem_w, net.stem_b, count, n_max,
+                                                                      H, W, act_a);
+      else
+        stem_conv_kernel<F, false><<<(total + 255) / 256, 256, 0, s>>>(x4, net.stem_w, net.stem_b, count, n_max,
+                                                                       H, W, act_a);
+    }
   }
-  float* cur = act_a;  // block input
-  float* mid = act_b;
-  float* nxt = act_c;
-  // AZ_CONV_VARIANT (A/B experiments, profiles/conv_variants.sh) overrides
-  // the engine's conv_algo: 0 Winograd, 6 direct, 1-5 direct variants
-  static const int env_variant = [] {
-    const char* v = getenv("AZ_CONV_VARIANT");
-    return v ? atoi(v) : -1;
-  }();
-  const int variant = env_variant >= 0 ? env_variant : (net.algo == 0 ? 0 : 6);
-  const int rows = n_max * HW;
-  bool fused_heads = false;
+  void* cur = act_a;  // block input
+  void* mid = act_b;
+  void* nxt = act_c;
   if (timer) timer->begin(s);
   for (int d = 0; d < net.depth; ++d) {
-    const float4* w1 = reinterpret_cast<const float4*>(net.c1_w[d]);
-    const float4* w2 = reinterpret_cast<const float4*>(net.c2_w[d]);
-#define AZ_CONV_PAIR(PREA, XSLAB, OCC, DIAG, TPW, RPW)                                          \
-  {                                                                                             \
-    constexpr int TR_ = 32 * (RPW) * (4 / (4 / (TPW)));                                         \
-    const int grid_ = (rows + TR_ - 1) / TR_;                                                   \
-    conv3x3_mfma_kernel<F, false, PREA, XSLAB, OCC, DIAG, TPW, RPW>                             \
-        <<<grid_, 256, conv_lds_bytes(TR_, W, false, XSLAB), s>>>(cur, nullptr, w1, net.c1_b[d], \
-                                                                 mid, count, n_max, H, W);      \
-    conv3x3_mfma_kernel<F, true, PREA, XSLAB, OCC, DIAG, TPW, RPW>                              \
-        <<<grid_, 256, conv_lds_bytes(TR_, W, true, XSLAB), s>>>(mid, cur, w2, net.c2_b[d], nxt, \
-                                                                count, n_max, H, W);            \
-  }
-    switch (variant) {
-      case 0:  // Winograd F(2x2,3x3) (az_wino.hip)
-      {
-        if (net.wino_tiles == 16)
-          launch_w16(net, cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s);
-        else
-          launch_wino_conv(cur, nullptr, net.u1_w[d], nullptr, net.c1_b[d], mid, count, n_max, H, W, s,
-                           nullptr, net.wino_ksplit);
-        // last block: the head 1x1 convs run in conv2's epilogue, features into nxt
-        HeadConv hc{net.pc_w, net.pc_b, net.vc_w, net.vc_b,
-                    d == net.depth - 1 && AZ_FUSE_HEADS ? reinterpret_cast<float4*>(nxt) : nullptr};
-        if (net.wino_tiles == 16)
-          launch_w16(net, mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc);
-        else
-          launch_wino_conv(mid, cur, net.u2_w[d], net.r2_w[d], net.c2_b[d], nxt, count, n_max, H, W, s, &hc,
-                           net.wino_ksplit);
-        fused_heads = hc.feat != nullptr;
-        break;
-      }
-      case 1: AZ_CONV_PAIR(false, true, 2, 0, 2, 1); break;   // 64 rows: waves 2x2, 1x2 tiles
-      case 2: AZ_CONV_PAIR(false, true, 2, 0, 1, 2); break;   // 64 rows: each wave 2x1 tiles
-      case 3: AZ_CONV_PAIR(false, false, 2, 0, 1, 4); break;  // 128 rows: each wave 4x1 tiles
-      case 4: AZ_CONV_PAIR(false, false, 2, 0, 2, 2); break;  // 128 rows: waves 2x2, 2x2 tiles
-      case 5: AZ_CONV_PAIR(false, true, 2, 1, 1, 1); break;   // DIAG: no B loads
-      default: AZ_CONV_PAIR(false, true, 2, 0, 1, 1); break;  // 6: direct, 32 rows, 1 tile per wave (r1m)
+    const bool last = d == net.depth - 1;
+    if (f16) {
+      Conv16Args a = ca;
+      a.in = cur;
+      a.wpack = net.k1[d];
+      a.bias = net.c1_b[d];
+      a.oscale = net.k1_scale[d];
+      a.out = mid;
+      launch_conv16(a, s);
+      // the last block's conv2 runs the heads' 1x1 convs in its epilogue:
+      // features [rows] float4 into nxt instead of the block output
+      Conv16Args b = ca;
+      b.in = mid;
+      b.res_in = cur;
+      b.wpack = net.k2[d];
+      b.bias = net.c2_b[d];
+      b.oscale = net.k2_scale[d];
+      b.out = nxt;
+      if (last) b.heads = Conv16Heads{net.pc_w, net.pc_b, net.vc_w, net.vc_b, static_cast<float4*>(nxt)};
+      launch_conv16(b, s);
+    } else {
+      launch_direct<false>(static_cast<const float*>(cur), nullptr, net.c1_w[d], net.c1_b[d],
+                           static_cast<float*>(mid), count, n_max, H, W, s);
+      launch_direct<true>(static_cast<const float*>(mid), static_cast<const float*>(cur), net.c2_w[d],
+                          net.c2_b[d], static_cast<float*>(nxt), count, n_max, H, W, s);
     }
-#undef AZ_CONV_PAIR
-    float* t = cur;
+    void* t = cur;
     cur = nxt;
     nxt = t;
   }
   if (timer) timer->end(s, 2 * net.depth);
+  const float* act = static_cast<const float*>(cur);  // f16: the fused head features; direct: block output
   HeadWeights hw{net.pc_w, net.pc_b, net.vc_w, net.vc_b, net.pd_w,
                  net.pd_b, net.v1_w, net.v1_b, net.v2_w, net.v2_b};
   const size_t wbytes = (size_t)(2 * HW * A + HW * net.hidden) * sizeof(float);
@@ -777,18 +737,19 @@ void launch_forward(const NetDev& net, const float* x, const int* count, int n_m
   const int hblocks = stage ? std::min((n_max + 3) / 4, 512) : (n_max + 3) / 4;
 #define AZ_HEADS(FEAT_, STAGE_)                                                                      \
   heads_kernel<F, FEAT_, STAGE_, kMaxActions><<<hblocks, 256, STAGE_ ? wbytes : 0, s>>>(           \
-      cur, hw, count, n_max, HW, A, net.hidden, probs, values)
+      act, hw, count, n_max, HW, A, net.hidden, probs, values)
   if (A > kMaxActions) {  // chess: 1880 actions
-    if (fused_heads && HW == 64 && A <= kTailThreads * kTailPer && net.pd_wt) {
-      const float4* feat = reinterpret_cast<const float4*>(cur);
+    if (f16 && HW == 64 && A <= kTailThreads * kTailPer && net.pd_wt) {
+      const float4* feat = reinterpret_cast<const float4*>(act);
       policy_dense_kernel<128><<<dim3((A + 63) / 64, (n_max + 31) / 32), 256, 0, s>>>(
           feat, net.pd_wt, net.pd_b, count, n_max, HW, A, probs);
       heads_tail_kernel<<<std::min(n_max, 2048), kTailThreads, 0, s>>>(feat, hw, count, n_max, HW, A,
                                                                        net.hidden, probs, values);
-    } else
-      heads_kernel<F, false, false, 2048><<<(n_max + 3) / 4, 256, 0, s>>>(cur, hw, count, n_max, HW, A,
+    } else {
+      heads_kernel<F, false, false, 2048><<<(n_max + 3) / 4, 256, 0, s>>>(act, hw, count, n_max, HW, A,
                                                                           net.hidden, probs, values);
-  } else if (fused_heads) {
+    }
+  } else if (f16) {
     if (stage) AZ_HEADS(true, true); else AZ_HEADS(true, false);
   } else {
     if (stage) AZ_HEADS(false, true); else AZ_HEADS(false, false);

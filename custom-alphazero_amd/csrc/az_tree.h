@@ -35,7 +35,8 @@ enum : int {
   kStatCount = 12        // (kStatCacheInserts counts since engine creation; CacheDev::ctl since a clear)
 };
 enum : unsigned long long {
-  kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16
+  kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16,
+  kErrActRange = 32  // a conv16 activation beyond the split16 range (|x| > 32752)
 };
 
 // All device state of a forest (struct of arrays over slots).

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 
 EVAL_NETWORK = 0
 EVAL_SYNTHETIC = 1
-CONV_WINOGRAD = 0
+CONV_F16X2 = 0  # include/az.h AZ_CONV_F16X2 (default)
 CONV_DIRECT = 1
 
 
@@ -203,7 +203,7 @@ class Engine:
     def __init__(self, height=6, width=7, n=4, gravity=True, mcts_iterations=100, slots=1,
                  evaluator=EVAL_NETWORK, index_move_greedy=8, exploration_constant=1.5,
                  filters=128, depth=4, value_hidden=256, bn_epsilon=1e-3, arena_edges=0,
-                 max_tree_visits=0, device=0, cache_log2=0, conv_algo=CONV_WINOGRAD,
+                 max_tree_visits=0, device=0, cache_log2=0, conv_algo=CONV_F16X2,
                  lanes=0):
         L = load_library()
         self.height, self.width, self.n, self.gravity = height, width, n, bool(gravity)
@@ -374,7 +374,7 @@ class ChessEngine:
 
     def __init__(self, mcts_iterations=800, slots=256, evaluator=EVAL_NETWORK, max_plies=512,
                  index_move_greedy=8, exploration_constant=1.5, filters=128, depth=4,
-                 value_hidden=256, bn_epsilon=1e-3, arena_edges=0, conv_algo=CONV_WINOGRAD,
+                 value_hidden=256, bn_epsilon=1e-3, arena_edges=0, conv_algo=CONV_F16X2,
                  device=0, lanes=0):
         L = load_library()
         self.slots, self.mcts_iterations = slots, mcts_iterations

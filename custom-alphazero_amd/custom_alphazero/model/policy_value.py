@@ -3,7 +3,7 @@
 
 PyTorch-ROCm only *holds* the weights (float32 tensors on the GPU, Keras
 layout, names from model/weights.py); the forward runs in libaz
-(az_forward: fp32-MFMA conv tower + heads, csrc/az_nn.hip).  Calling the
+(az_forward: the conv16 tower + heads, csrc/az_nn.hip, az_conv16.hip).  Calling the
 model returns (probabilities [B, A], value [B, 1]) as torch CPU tensors, so
 the reference's `.numpy()` idiom (mcts.py:134-137) works unchanged.
 """
@@ -117,7 +117,7 @@ class PolicyValueModel:
     def save_with_meta(self, path):
         os.makedirs(path, exist_ok=True)
         np.savez(os.path.join(path, ConfigPath.model_prefix + ".npz"),
-                 **{name: w for (name, _), w in zip(self.spec, self.get_weights())})
+                 **dict(zip(self.weight_names, self.get_weights())))
         meta = {"steps": int(self.steps), "learning_rate": float(self.learning_rate),
                 "hash": self.hash}
         with open(os.path.join(path, ConfigPath.model_meta), "w") as fp:
@@ -128,7 +128,7 @@ class PolicyValueModel:
         if not os.path.exists(os.path.join(path, ConfigPath.model_success)):
             raise AssertionError(f"No verification file of the model found at {path}!")
         with np.load(os.path.join(path, ConfigPath.model_prefix + ".npz"), allow_pickle=False) as z:
-            self.set_weights([z[name] for name, _ in self.spec])
+            self.set_weights([z[name] for name in self.weight_names])
         with open(os.path.join(path, ConfigPath.model_meta)) as fp:
             meta = json.load(fp)
         self.steps = int(meta.get("steps", 0))

@@ -22,21 +22,21 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 2
+#define AZ_ABI_VERSION 3
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
 #define AZ_E_HIP -2      /* HIP runtime error */
 #define AZ_E_STATE -3    /* call out of order (e.g. no weights) */
-#define AZ_E_DEVICE -4   /* a kernel flagged an error (arena/pow/path overflow) */
+#define AZ_E_DEVICE -4   /* a kernel flagged an error (arena/pow/path overflow, activation range) */
 
 #define AZ_EVAL_NETWORK 0    /* the policy/value network (model/tensorflow/model.py) */
 #define AZ_EVAL_SYNTHETIC 1  /* oracle/synth.py's exact evaluator (parity runs) */
 
 /* az_config.conv_algo */
-#define AZ_CONV_WINOGRAD 0   /* Winograd F(2x2,3x3); fp32 products formed from three bf16
-                                terms per operand on the bf16 MFMA (default) */
-#define AZ_CONV_DIRECT 1     /* direct implicit GEMM on fp32 MFMA */
+#define AZ_CONV_F16X2 0      /* direct implicit GEMM on the fp16 MFMA, fp32-accurate: both operands
+                                as two fp16 terms, three products per k-step (default) */
+#define AZ_CONV_DIRECT 1     /* direct implicit GEMM on fp32 MFMA (exact fp32 FMA chains) */
 
 typedef struct az_engine az_engine;
 
@@ -60,8 +60,9 @@ typedef struct az_config {
     int64_t max_tree_visits;       /* bound on visits through one node; 0 = mcts_iterations*H*W */
     int32_t cache_log2;            /* transposition cache entries = 2^cache_log2 (the reference's
                                       plays_inferences, mcts/mcts.py:122-143); 0 = off */
-    int32_t conv_algo;             /* residual-tower 3x3 convs: AZ_CONV_WINOGRAD (0, default) or
-                                      AZ_CONV_DIRECT (1); same layer, outputs within NET_TOL */
+    int32_t conv_algo;             /* residual-tower 3x3 convs: AZ_CONV_F16X2 (0, default; board width
+                                      <= 16, activations within +-32752) or AZ_CONV_DIRECT (1); same
+                                      layer, outputs within NET_TOL */
     int32_t lanes;                 /* self-play slot groups searched on separate HIP streams
                                       (0 = auto: 2 when slots >= 512); results do not depend on it */
     int32_t reserved[5];

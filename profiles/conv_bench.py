@@ -17,7 +17,7 @@ from custom_alphazero.model.weights import init_weights, weight_spec  # noqa: E4
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 H, W = 6, 7
-algo = int(sys.argv[3]) if len(sys.argv) > 3 else az.CONV_WINOGRAD
+algo = int(sys.argv[3]) if len(sys.argv) > 3 else az.CONV_F16X2
 eng = az.Engine(H, W, 4, True, 1, slots=B, evaluator=az.EVAL_NETWORK, conv_algo=algo)
 eng.set_weights(init_weights(weight_spec(H, W, W), seed=0).items())
 rng = np.random.RandomState(0)

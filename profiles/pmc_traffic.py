@@ -25,7 +25,7 @@ def per_kernel(d, name):
 
 res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, az_forward at B={B} boards",
        "correction": "fetch bytes = 2 x FETCH_SIZE KiB (gfx950, 16 B/lane streams); write = WRITE_SIZE KiB"}
-for algo, key in ((0, "winograd"), (1, "direct")):
+for algo, key in ((0, "f16x2"), (1, "direct")):
     if only is not None and algo != only:
         continue
     f = per_kernel(f"{out}/fetch_{algo}", "FETCH_SIZE")

@@ -59,12 +59,12 @@ def main():
         print("\n## HBM traffic per board (PMC, B = 4096, profiles/r1/pmc_conv_traffic.json)\n")
         print("| kernel | HBM KB/board |")
         print("|---|---:|")
-        for algo in ("winograd", "direct"):
+        for algo in ("f16x2", "winograd", "direct"):
             for k, v in t.get(algo, {}).get("hbm_bytes_per_board", {}).items():
                 print(f"| `{k}` | {v / 1e3:.1f} |")
     sq = glob.glob(f"{os.path.dirname(d)}/pmc_conv_4096_0/**/*counter_collection.csv", recursive=True)
     if sq:
-        print("\n## SQ counters, Winograd conv kernels (az_forward, B = 4096)\n")
+        print("\n## SQ counters, tower conv kernels (az_forward, B = 4096)\n")
         print("```")
         print(subprocess.run([sys.executable, os.path.join(HERE, "pmc_summary.py"),
                               f"{os.path.dirname(d)}/pmc_conv_4096_0", "wino"],

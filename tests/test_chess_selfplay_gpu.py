@@ -86,9 +86,17 @@ def _states(n, seed):
     return x.astype(np.float32)
 
 
-def test_chess_forward_matches_keras_restatement(chess_net):
+@pytest.mark.parametrize("algo", ["f16x2", "direct"])
+def test_chess_forward_matches_keras_restatement(chess_net, algo):
+    """Both tower/stem algorithms (AZ_CONV_F16X2, AZ_CONV_DIRECT) against the
+    float64 restatement, and batch invariant."""
     import keras_ref
+    from custom_alphazero import engine as az
     eng, w = chess_net
+    if algo == "direct":
+        eng = _engine(mcts_iterations=16, slots=64, evaluator=az.EVAL_NETWORK, max_plies=12,
+                      conv_algo=az.CONV_DIRECT)
+        eng.set_weights(w.items())
     x = _states(96, seed=21)  # more than one engine chunk (64 slots)
     probs, values = eng.forward(x)
     rp, rv = keras_ref.forward(w, x, depth=4)
@@ -97,6 +105,8 @@ def test_chess_forward_matches_keras_restatement(chess_net):
     # batch invariance (the replay parity below depends on it)
     p1, v1 = eng.forward(x[5:6])
     assert np.array_equal(p1[0], probs[5]) and v1[0] == values[5]
+    if algo == "direct":
+        eng.close()
 
 
 def test_chess_selfplay_network_replays_on_oracle(chess_net):

@@ -200,11 +200,11 @@ def test_encode_and_mask_match_reference(golden, name):
 
 
 # ------------------------------------------------------------------ network
-CONV_ALGOS = [az.CONV_WINOGRAD, az.CONV_DIRECT]
+CONV_ALGOS = [az.CONV_F16X2, az.CONV_DIRECT]
 
 
 def make_net_engine(H=6, W=7, n=4, grav=True, S=25, slots=256, seed=0, randomize_bn=True, depth=4,
-                    cache_log2=0, conv_algo=az.CONV_WINOGRAD, lanes=0):
+                    cache_log2=0, conv_algo=az.CONV_F16X2, lanes=0):
     A = W if grav else W * H
     spec = weight_spec(H, W, A, depth=depth)
     w = init_weights(spec, seed=seed, randomize_bn=randomize_bn)
