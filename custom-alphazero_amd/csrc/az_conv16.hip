@@ -20,8 +20,8 @@
 // then term 1.  Rows are pixels b*HW + y*W + x; a workgroup's TR rows cross
 // board boundaries freely.
 //
-// Workgroup = WM x 4 waves; wave (mh, nq) owns output rows mh*64 .. +64 (four
-// 16-row M blocks) and columns 32nq .. +32 (two 16-column N blocks).
+// Workgroup = 4 waves and TR = 16*MB output rows; wave nq owns the MB 16-row M
+// blocks x columns 32nq .. +32 (two 16-column N blocks).
 //  * A: the tile's input rows plus a halo of W+1 rows each side are copied
 //    ONCE into LDS by buffer_load ... lds (no VGPRs, no VALU; rows outside
 //    the batch come back as zeros from the buffer range check), 16-B slots
@@ -48,13 +48,15 @@ namespace az {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef AZ_C16_AKS
+#define AZ_C16_AKS 1  // A fragments of the next k-step read during this one (1) or of this k-step (0)
+#endif
+#ifndef AZ_C16_OCC
+#define AZ_C16_OCC 1  // minimum waves per SIMD the register allocator must allow (launch bounds)
+#endif
 #ifndef AZ_C16_PF
 #define AZ_C16_PF 2  // k-steps of B fragments in flight ahead of their MFMAs
 #endif
-#ifndef AZ_C16_APF
-#define AZ_C16_APF 0  // A fragments read one M block ahead (1) or just before their MFMAs (0)
-#endif
-constexpr int kC16Tile = 64;       // output rows per wave (4 M blocks)
 constexpr int kC16Pitch = 132;     // epilogue tile row pitch (floats)
 constexpr float kOverflow = 32752.f;  // |x| above this cannot be split (fp16 range)
 
@@ -73,14 +75,14 @@ __device__ __forceinline__ h8 unscale_b0(const uint4 v) {
   return b * (_Float16)0.000244140625f;
 }
 
-template <int WM, bool RES, bool HEADS, int C0>
-__global__ __launch_bounds__(256 * WM) void conv16_kernel(
+template <int MB, bool RES, bool HEADS, int C0>
+__global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     const uint4* __restrict__ in, const uint4* __restrict__ res_in, const uint4* __restrict__ wpack,
     const float* __restrict__ bias, float oscale, uint4* __restrict__ out, Conv16Heads hc,
     const int* __restrict__ count, int n_static, int H, int W, unsigned long long* __restrict__ err) {
   static_assert(!HEADS || RES, "the heads fuse into a block's second conv");
-  constexpr int TR = kC16Tile * WM;
-  constexpr int NT = 256 * WM;
+  constexpr int TR = 16 * MB;
+  constexpr int NT = 256;
   constexpr int CPT = 4 - C0;          // 32-channel chunks per tap
   constexpr int NK = 9 * CPT;          // tap k-steps
   constexpr int NKR = NK + (RES ? 4 : 0);
@@ -96,7 +98,7 @@ __global__ __launch_bounds__(256 * WM) void conv16_kernel(
   const int zrow = slab_rows;
 
   // ---- B stream: k-step s of the executed sequence -> packed k-step
-  const uint4* wl = wpack + (size_t)((wave & 3) * 2) * 2 * 64 + lane;
+  const uint4* wl = wpack + (size_t)(wave * 2) * 2 * 64 + lane;
   auto pk_of = [&](int s) { return s < NK ? (s / CPT) * 4 + C0 + s % CPT : 36 + (s - NK); };
   constexpr int PF = AZ_C16_PF, NB = PF + 1;
   uint4 bq[NB][4];
@@ -137,14 +139,14 @@ __global__ __launch_bounds__(256 * WM) void conv16_kernel(
   }
   __syncthreads();  // (its fence waits for the DMA)
 
-  // ---- per lane: the four M blocks' pixels
-  const int mh = wave >> 2, nq = wave & 3;
+  // ---- per lane: the MB M blocks' pixels
+  const int nq = wave;
   const int r16 = lane & 15, gq = lane >> 4;
-  int lr[4], py[4], px[4];
-  bool valid[4];
+  int lr[MB], py[MB], px[MB];
+  bool valid[MB];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
-    lr[mb] = mh * 64 + mb * 16 + r16;
+  for (int mb = 0; mb < MB; ++mb) {
+    lr[mb] = mb * 16 + r16;
     const int g = row0 + lr[mb];
     valid[mb] = g < rows;
     const int p = g % HW;
@@ -152,17 +154,17 @@ __global__ __launch_bounds__(256 * WM) void conv16_kernel(
     px[mb] = p - py[mb] * W;
   }
 
-  f32x4 acc[4][2];
+  f32x4 acc[MB][2];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int abase[4], akey[4];  // slab row (uint4 units) and swizzle key of each M block's tap row
+  int abase[MB], akey[MB];  // slab row (uint4 units) and swizzle key of each M block's tap row
   auto set_tap = [&](int t) {
     if (t >= 9) {  // the fused residual: the block input's own row, second region
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
+      for (int mb = 0; mb < MB; ++mb) {
         abase[mb] = valid[mb] ? slab_u4 + lr[mb] * 32 : zrow * 32;
         akey[mb] = lr[mb];
       }
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(256 * WM) void conv16_kernel(
     }
     const int dy = t / 3 - 1, dx = t % 3 - 1;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
       const bool ok = valid[mb] && py[mb] + dy >= 0 && py[mb] + dy < H && px[mb] + dx >= 0 && px[mb] + dx < W;
       const int sr = lr[mb] + halo + dy * W + dx;
       abase[mb] = (ok ? sr : zrow) * 32;
@@ -180,38 +182,47 @@ __global__ __launch_bounds__(256 * WM) void conv16_kernel(
   // executed k-step s -> (tap, 32-channel chunk)
   auto tap_of = [&](int s) { return s < NK ? s / CPT : 9; };
   auto chunk_of = [&](int s) { return s < NK ? C0 + s % CPT : s - NK; };
-  uint4 aq[2][2];
-  auto load_a = [&](int i) {  // flat index i = s * 4 + mb
-    const int s = i >> 2, mb = i & 3;
+  // A fragments of a whole k-step (4 M blocks x 2 terms), double-buffered:
+  // k-step s+1's LDS reads are issued before k-step s's MFMAs
+  uint4 aq[2][MB][2];
+  auto load_a = [&](int s, uint4 (&dst)[MB][2]) {
     if (s >= NKR) return;
-    if (mb == 0 && (s == 0 || tap_of(s) != tap_of(s - 1))) set_tap(tap_of(s));
-    const int sl = c16_phys(akey[mb], 4 * chunk_of(s) + gq);
-    aq[i & 1][0] = lds[abase[mb] + sl];
-    aq[i & 1][1] = lds[abase[mb] + 16 + sl];
+    if (s == 0 || tap_of(s) != tap_of(s - 1)) set_tap(tap_of(s));
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int sl = c16_phys(akey[mb], 4 * chunk_of(s) + gq);
+      dst[mb][0] = lds[abase[mb] + sl];
+      dst[mb][1] = lds[abase[mb] + 16 + sl];
+    }
   };
-  if (AZ_C16_APF) load_a(0);
+  if (AZ_C16_AKS) load_a(0, aq[0]);
 #pragma unroll
   for (int s = 0; s < NKR; ++s) {
     // k-steps stay in program order: without this the scheduler sinks the
     // B prefetch next to its use and waits vmcnt(0) every few k-steps
     __builtin_amdgcn_sched_barrier(0);
     load_b(s + PF, bq[(s + PF) % NB]);
+    if (AZ_C16_AKS) load_a(s + 1, aq[(s + 1) & 1]);
+    else load_a(s, aq[s & 1]);
     const uint4(&b)[4] = bq[s % NB];
     const h8 B00 = __builtin_bit_cast(h8, b[0]), B01 = __builtin_bit_cast(h8, b[1]);
     const h8 B10 = __builtin_bit_cast(h8, b[2]), B11 = __builtin_bit_cast(h8, b[3]);
     const h8 b00 = unscale_b0(b[0]), b10 = unscale_b0(b[2]);
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      const int i = s * 4 + mb;
-      load_a(i + AZ_C16_APF);  // 1: the next M block's fragments are in flight during these MFMAs
-      const h8 a0 = __builtin_bit_cast(h8, aq[i & 1][0]);
-      const h8 a1 = __builtin_bit_cast(h8, aq[i & 1][1]);
+    for (int mb = 0; mb < MB; ++mb) {
+      const h8 a0 = __builtin_bit_cast(h8, aq[s & 1][mb][0]);
+      const h8 a1 = __builtin_bit_cast(h8, aq[s & 1][mb][1]);
       acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b00, acc[mb][0], 0, 0, 0);
       acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B01, acc[mb][0], 0, 0, 0);
       acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B00, acc[mb][0], 0, 0, 0);
       acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b10, acc[mb][1], 0, 0, 0);
       acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B11, acc[mb][1], 0, 0, 0);
       acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B10, acc[mb][1], 0, 0, 0);
+    }
+    if (AZ_C16_AKS) {  // the next k-step's reads first, then this one's MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);   // VMEM reads (B, PF ahead)
+      __builtin_amdgcn_sched_group_barrier(0x0100, 2 * MB, 0);  // DS reads (A, next k-step)
+      __builtin_amdgcn_sched_group_barrier(0x0008, 6 * MB, 0);  // MFMA
     }
   }
 
@@ -224,12 +235,12 @@ __global__ __launch_bounds__(256 * WM) void conv16_kernel(
     const int col = 32 * nq + 16 * nb + r16;
     const float bc = bias[col];
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
+    for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const float y = fmaxf(fmaf(acc[mb][nb][v], oscale, bc), 0.f);
         vmax = fmaxf(vmax, y);
-        tile[(mh * 64 + mb * 16 + 4 * gq + v) * kC16Pitch + col] = y;
+        tile[(mb * 16 + 4 * gq + v) * kC16Pitch + col] = y;
       }
   }
   if (!HEADS && vmax > kOverflow && err) atomicOr(err, kErrActRange);
@@ -272,43 +283,44 @@ __global__ __launch_bounds__(256 * WM) void conv16_kernel(
   }
 }
 
-size_t conv16_lds_bytes(int WM, int W, bool res) {
-  const int TR = kC16Tile * WM;
+size_t conv16_lds_bytes(int MB, int W, bool res) {
+  const int TR = 16 * MB;
   const size_t slab = (size_t)(((TR + 2 * (W + 1) + 2) >> 1) << 1) * 512;
   const size_t tile = (size_t)TR * kC16Pitch * 4;
   return std::max(slab + (res ? (size_t)TR * 512 : 0), tile);
 }
 
-template <int WM, bool RES, bool HEADS, int C0>
+template <int MB, bool RES, bool HEADS, int C0>
 static void launch_one(const Conv16Args& a, hipStream_t s) {
-  const int TR = kC16Tile * WM;
+  const int TR = 16 * MB;
   const int grid = (a.n_max * a.H * a.W + TR - 1) / TR;
   if (grid <= 0) return;
-  const size_t bytes = conv16_lds_bytes(WM, a.W, RES);
+  const size_t bytes = conv16_lds_bytes(MB, a.W, RES);
   static bool attr = false;  // one instantiation per call site: set the LDS cap once
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv16_kernel<WM, RES, HEADS, C0>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv16_kernel<MB, RES, HEADS, C0>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  conv16_kernel<WM, RES, HEADS, C0><<<grid, 256 * WM, bytes, s>>>(
+  conv16_kernel<MB, RES, HEADS, C0><<<grid, 256, bytes, s>>>(
       reinterpret_cast<const uint4*>(a.in), reinterpret_cast<const uint4*>(a.res_in),
       reinterpret_cast<const uint4*>(a.wpack), a.bias, a.oscale, reinterpret_cast<uint4*>(a.out), a.heads,
       a.count, a.n_max, a.H, a.W, a.err);
 }
 
+template <int MB>
+static void launch_mb(const Conv16Args& a, hipStream_t s) {
+  if (a.heads.feat) launch_one<MB, true, true, 0>(a, s);
+  else if (a.res_in) launch_one<MB, true, false, 0>(a, s);
+  else if (a.first_chunk == 2) launch_one<MB, false, false, 2>(a, s);
+  else launch_one<MB, false, false, 0>(a, s);
+}
+
 void launch_conv16(const Conv16Args& a, hipStream_t s) {
-  const bool heads = a.heads.feat != nullptr;
-  if (a.wm == 2) {
-    if (heads) launch_one<2, true, true, 0>(a, s);
-    else if (a.res_in) launch_one<2, true, false, 0>(a, s);
-    else if (a.first_chunk == 2) launch_one<2, false, false, 2>(a, s);
-    else launch_one<2, false, false, 0>(a, s);
-  } else {
-    if (heads) launch_one<1, true, true, 0>(a, s);
-    else if (a.res_in) launch_one<1, true, false, 0>(a, s);
-    else if (a.first_chunk == 2) launch_one<1, false, false, 2>(a, s);
-    else launch_one<1, false, false, 0>(a, s);
+  switch (a.mb) {
+    case 2: launch_mb<2>(a, s); break;
+    case 3: launch_mb<3>(a, s); break;
+    default: launch_mb<4>(a, s); break;
   }
 }
 

@@ -114,12 +114,12 @@ struct Conv16Args {
   Conv16Heads heads{};
   const int* count = nullptr;    // live boards (device), or null -> n_max
   int n_max = 0, H = 0, W = 0;
-  int wm = 2;                    // 1: 64-row tiles (4 waves), 2: 128-row tiles (8 waves)
+  int mb = 4;                    // 16-row M blocks per workgroup tile (2, 3 or 4)
   int first_chunk = 0;           // 2: input channels 0..63 are known zero (chess self-play stem)
   unsigned long long* err = nullptr;  // device error word: kErrActRange if an output leaves the split16 range
 };
 void launch_conv16(const Conv16Args& a, hipStream_t s);
-size_t conv16_lds_bytes(int WM, int W, bool res);
+size_t conv16_lds_bytes(int MB, int W, bool res);
 // power-of-two prescale e of a conv's weights (max |w * 2^-e| in (4, 8])
 int conv16_prescale(const double* w, size_t n, const double* w2, size_t n2);
 // weights [3][3][cin_n][128] (+ 1x1 residual [128][128]) -> uint16 fp16 bits

@@ -655,7 +655,11 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
   ca.n_max = n_max;
   ca.H = H;
   ca.W = W;
-  ca.wm = 1;
+  // tile height by launch size (profiles/micro/conv16_ab.sh): 32-row tiles
+  // for chess self-play's 256 boards, 48 for Connect-4 lanes (~900 live of
+  // 2048 boards), 64 from ~3000 boards -- the work per CU evens out
+  const long rows_max = (long)n_max * HW;
+  ca.mb = rows_max <= 24576 ? 2 : (rows_max <= 131072 ? 3 : 4);
   ca.err = net.err;
   if (net.in_ch > 4) {
     // chess: 118 input planes zero-padded to F, the stem is one more 3x3 conv;

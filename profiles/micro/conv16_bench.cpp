@@ -2,7 +2,7 @@
 // data: split16 input rows, random 3x3 (+1x1 residual) weights, compared with
 // a float64 direct convolution of the UNSPLIT fp32 input on sampled boards.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 profiles/micro/conv16_bench.cpp -o conv16_bench
-//   ./conv16_bench boards H W wm mode(0 conv, 1 conv+res, 2 conv+res+heads) iters
+//   ./conv16_bench boards H W mb mode(0 conv, 1 conv+res, 2 conv+res+heads) iters
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -41,7 +41,7 @@ static float unsplit(const uint16_t* row, int c) {
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 870;
   const int H = argc > 2 ? atoi(argv[2]) : 6, W = argc > 3 ? atoi(argv[3]) : 7;
-  const int wm = argc > 4 ? atoi(argv[4]) : 2;
+  const int wm = argc > 4 ? atoi(argv[4]) : 4;  // M blocks per tile
   const int mode = argc > 5 ? atoi(argv[5]) : 1;
   const int iters = argc > 6 ? atoi(argv[6]) : 50;
   const int HW = H * W, F = 128, rows = B * HW;
@@ -70,7 +70,7 @@ int main(int argc, char** argv) {
   az::conv16_pack(w3.data(), F, res ? wr.data() : nullptr, e, pack);
 
   void *d_in, *d_res, *d_w, *d_out, *d_bias, *d_hw, *d_feat;
-  int* d_err;
+  unsigned long long* d_err;
   CK(hipMalloc(&d_in, xs.size() * 2));
   CK(hipMalloc(&d_res, xrs.size() * 2));
   CK(hipMalloc(&d_w, pack.size() * 2));
@@ -78,13 +78,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_bias, F * 4));
   CK(hipMalloc(&d_hw, hw.size() * 4));
   CK(hipMalloc(&d_feat, (size_t)rows * 16));
-  CK(hipMalloc(&d_err, 4));
+  CK(hipMalloc(&d_err, 8));
   CK(hipMemcpy(d_in, xs.data(), xs.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_res, xrs.data(), xrs.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_w, pack.data(), pack.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_bias, bias.data(), F * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_hw, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
-  CK(hipMemset(d_err, 0, 4));
+  CK(hipMemset(d_err, 0, 8));
 
   az::Conv16Args a;
   a.in = d_in;
@@ -100,7 +100,7 @@ int main(int argc, char** argv) {
   a.n_max = B;
   a.H = H;
   a.W = W;
-  a.wm = wm;
+  a.mb = wm;
   a.err = d_err;
   az::launch_conv16(a, 0);
   CK(hipDeviceSynchronize());
@@ -153,8 +153,8 @@ int main(int argc, char** argv) {
       }
     }
   }
-  int err_flag = 0;
-  CK(hipMemcpy(&err_flag, d_err, 4, hipMemcpyDeviceToHost));
+  unsigned long long err_flag = 0;
+  CK(hipMemcpy(&err_flag, d_err, 8, hipMemcpyDeviceToHost));
 
   // ---- timing
   hipEvent_t t0, t1;
@@ -173,7 +173,7 @@ int main(int argc, char** argv) {
   const double direct = (double)rows * F * F * 2 * (9 + (res ? 1 : 0));  // algorithmic
   printf("{\"boards\": %d, \"H\": %d, \"W\": %d, \"wm\": %d, \"mode\": %d, \"us\": %.2f, "
          "\"issued_tflops\": %.1f, \"frac_f16_peak\": %.4f, \"algorithmic_tflops\": %.1f, "
-         "\"max_abs_err\": %.3e, \"max_ref\": %.3f, \"rel\": %.3e, \"prescale\": %d, \"overflow_flag\": %d}\n",
+         "\"max_abs_err\": %.3e, \"max_ref\": %.3f, \"rel\": %.3e, \"prescale\": %d, \"overflow_flag\": %llu}\n",
          B, H, W, wm, mode, us, issued / us * 1e-6, issued / us * 1e-6 / 2500.0, direct / us * 1e-6, max_err,
          max_ref, max_err / std::max(max_ref, 1e-30), e, err_flag);
   return 0;

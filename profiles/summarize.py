@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a collect_r1.sh run into the markdown committed under profiles/.
 
-Usage: summarize.py <prof_dir>   (prof_dir = gpurun_out/prof_r1)
+Usage: summarize.py <prof_dir> [round]   (prof_dir = gpurun_out/prof_r2, round = r2)
 HBM bytes follow MI355X_MICROARCH.md's HBM/rocprofv3 section (FETCH_SIZE x2
 on gfx950 for 16 B/lane streams, WRITE_SIZE as is; KiB units)."""
 import csv
@@ -23,7 +23,8 @@ def main():
     st = glob.glob(f"{d}/trace/**/*kernel_stats.csv", recursive=True)[0]
     tr = glob.glob(f"{d}/trace/**/*kernel_trace.csv", recursive=True)[0]
     rows = list(csv.DictReader(open(st)))
-    print("## Kernel time (rocprofv3 --kernel-trace --stats, `bench.py --steps 5 --warmup 20`)\n")
+    rnd = sys.argv[2] if len(sys.argv) > 2 else "r1"
+    print("## Kernel time (rocprofv3 --kernel-trace --stats, `bench.py` short window)\n")
     print("| kernel | calls | total ms | avg us | % |")
     print("|---|---:|---:|---:|---:|")
     conv_calls = conv_ns = 0
@@ -32,7 +33,7 @@ def main():
             float(r["AverageNs"]), float(r["Percentage"])
         print(f"| `{n}` | {c} | {tot / 1e6:.1f} | {avg / 1e3:.1f} | {pct:.2f} |")
     for r in rows:
-        if "conv_kernel" in r["Name"] or "conv3x3_mfma" in r["Name"]:
+        if "conv_kernel" in r["Name"] or "conv3x3_mfma" in r["Name"] or "conv16_kernel" in r["Name"]:
             if "stem" in r["Name"]:
                 continue
             conv_calls += int(r["Calls"])
@@ -44,7 +45,7 @@ def main():
         rf = b["roofline"]
         print(f"same run, bench.py HIP events: avg_launch_ms {rf['avg_launch_ms']} "
               f"({rf['avg_launch_ms'] * 1e3:.1f} us), boards/launch {rf['boards_per_launch']}, "
-              f"achieved {rf['achieved']} TFLOP/s algorithmic, {rf['issued']['achieved']} issued ({rf['issued']['dtype']}); "
+              f"achieved {rf['achieved']} TFLOP/s issued ({rf['dtype']}), frac {rf['frac']}; "
               f"value {b['value']} games/s under the profiler")
     except Exception as ex:  # noqa: BLE001
         print(f"(bench_trace.json unreadable: {ex})")
@@ -53,21 +54,22 @@ def main():
     print(subprocess.run([sys.executable, os.path.join(HERE, "busy.py"), tr, "0.5"],
                          capture_output=True, text=True).stdout.rstrip())
     print("```")
-    tj = os.path.join(HERE, "r1", "pmc_conv_traffic.json")
+    tj = os.path.join(HERE, rnd, "pmc_conv_traffic.json")
     if os.path.exists(tj):
         t = json.load(open(tj))
-        print("\n## HBM traffic per board (PMC, B = 4096, profiles/r1/pmc_conv_traffic.json)\n")
+        print(f"\n## HBM traffic per board (PMC, B = 4096, profiles/{rnd}/pmc_conv_traffic.json)\n")
         print("| kernel | HBM KB/board |")
         print("|---|---:|")
         for algo in ("f16x2", "winograd", "direct"):
             for k, v in t.get(algo, {}).get("hbm_bytes_per_board", {}).items():
                 print(f"| `{k}` | {v / 1e3:.1f} |")
-    sq = glob.glob(f"{os.path.dirname(d)}/pmc_conv_4096_0/**/*counter_collection.csv", recursive=True)
+    sqd = next((p for p in (f"{d}/pmc_conv_4096_0", f"{os.path.dirname(d)}/pmc_conv_4096_0") if os.path.isdir(p)), "")
+    sq = glob.glob(f"{sqd}/**/*counter_collection.csv", recursive=True) if sqd else []
     if sq:
         print("\n## SQ counters, tower conv kernels (az_forward, B = 4096)\n")
         print("```")
         print(subprocess.run([sys.executable, os.path.join(HERE, "pmc_summary.py"),
-                              f"{os.path.dirname(d)}/pmc_conv_4096_0", "wino"],
+                              sqd, "conv"],
                              capture_output=True, text=True).stdout.rstrip())
         print("```")
 
