@@ -20,7 +20,11 @@
 
 #include "../../include/az_chess.h"
 
-#define AZC_HD __device__ __forceinline__
+// The rules compile for the host too (tests/native/chess_legal_check.cpp runs
+// them under AddressSanitizer/UBSan against the oracle); the wave-parallel
+// generators below are device-only (AZC_D).
+#define AZC_HD __host__ __device__ __forceinline__
+#define AZC_D __device__ __forceinline__
 
 namespace azc {
 
@@ -51,6 +55,23 @@ static inline void host_rays(uint64_t rays[8][64]) {
       rays[d][s] = r;
     }
 }
+// the host copy (host builds of the rules)
+static inline const uint64_t (*host_ray_table())[64] {
+  static uint64_t rays[8][64];
+  static bool init = false;
+  if (!init) {
+    host_rays(rays);
+    init = true;
+  }
+  return rays;
+}
+AZC_HD bb ray_at(int d, int s) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return c_rays[d][s];
+#else
+  return host_ray_table()[d][s];
+#endif
+}
 // for the current device (hipSetDevice first)
 static inline hipError_t upload_rays() {
   uint64_t rays[8][64];
@@ -59,18 +80,24 @@ static inline hipError_t upload_rays() {
 }
 
 AZC_HD bb sq_bb(int s) { return 1ull << s; }
+#ifdef __HIP_DEVICE_COMPILE__
 AZC_HD int msb(bb x) { return 63 - __clzll(x); }
 AZC_HD int lsb(bb x) { return __ffsll((long long)x) - 1; }
 AZC_HD int popc(bb x) { return __popcll(x); }
+#else  // host: the builtins, so UBSan reports a zero argument (no square)
+AZC_HD int msb(bb x) { return 63 - __builtin_clzll(x); }
+AZC_HD int lsb(bb x) { return __builtin_ctzll(x); }
+AZC_HD int popc(bb x) { return __builtin_popcountll(x); }
+#endif
 AZC_HD bb bswap(bb x) {
   uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   return ((bb)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
 }
 
 AZC_HD bb ray_attack(int d, int s, bb occ) {
-  bb a = c_rays[d][s];
+  bb a = ray_at(d, s);
   bb b = a & occ;
-  if (b) a ^= c_rays[d][d < 4 ? lsb(b) : msb(b)];
+  if (b) a ^= ray_at(d, d < 4 ? lsb(b) : msb(b));
   return a;
 }
 AZC_HD bb rook_att(int s, bb occ) {
@@ -111,12 +138,12 @@ AZC_HD int opp_dir(int d) { return d ^ 4; }
 // python-chess between(a, b): squares strictly between
 AZC_HD bb between(int a, int b) {
   int d = dir_of(a, b);
-  return d < 0 ? 0 : (c_rays[d][a] & c_rays[opp_dir(d)][b]);
+  return d < 0 ? 0 : (ray_at(d, a) & ray_at(opp_dir(d), b));
 }
 // python-chess ray(a, b): the whole line through a and b
 AZC_HD bb line(int a, int b) {
   int d = dir_of(a, b);
-  return d < 0 ? 0 : (c_rays[d][a] | c_rays[opp_dir(d)][a] | sq_bb(a));
+  return d < 0 ? 0 : (ray_at(d, a) | ray_at(opp_dir(d), a) | sq_bb(a));
 }
 
 struct Pos {
@@ -411,7 +438,7 @@ AZC_HD int legal_moves(const Pos& q, uint16_t* out, bool* check) {
 // counts, an exclusive prefix across the wave, then each lane writes its
 // moves at its offset.  Candidates go to LDS (`cand`), the _is_safe filter
 // runs one candidate per lane and compacts in order with a ballot.
-AZC_HD int wave_offset(int v, int lane, int* total) {
+AZC_D int wave_offset(int v, int lane, int* total) {
   int incl = v;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -421,10 +448,10 @@ AZC_HD int wave_offset(int v, int lane, int* total) {
   *total = __shfl(incl, 63, 64);
   return incl - v;
 }
-AZC_HD void wave_put(uint16_t* out, int k, int from, int to, int promo) {
+AZC_D void wave_put(uint16_t* out, int k, int from, int to, int promo) {
   if (k < AZ_CHESS_MAX_MOVES) out[k] = (uint16_t)(from | (to << 6) | (promo << 12));
 }
-AZC_HD int wave_put_pawn(uint16_t* out, int k, int from, int to) {
+AZC_D int wave_put_pawn(uint16_t* out, int k, int from, int to) {
   const int r = to >> 3;
   if (r == 0 || r == 7) {
     wave_put(out, k, from, to, QUEEN);
@@ -438,7 +465,7 @@ AZC_HD int wave_put_pawn(uint16_t* out, int k, int from, int to) {
 }
 // a lane-0-only generator step (castling, en passant: at most two moves)
 template <typename F>
-AZC_HD int wave_serial(uint16_t* out, int n, int lane, F&& gen) {
+AZC_D int wave_serial(uint16_t* out, int n, int lane, F&& gen) {
   int nn = n;
   if (lane == 0) {
     MoveOut o{out, n};
@@ -449,7 +476,7 @@ AZC_HD int wave_serial(uint16_t* out, int n, int lane, F&& gen) {
 }
 
 // gen_pseudo(from_mask, to_mask) appended at out[n..]; returns the new count
-AZC_HD int gen_pseudo_wave(const Pos& q, bb from_mask, bb to_mask, uint16_t* out, int n, int lane) {
+AZC_D int gen_pseudo_wave(const Pos& q, bb from_mask, bb to_mask, uint16_t* out, int n, int lane) {
   const int t = q.turn, sq = 63 - lane;
   const bb own = q.C(t), occ = q.occ();
   int total;
@@ -499,7 +526,7 @@ AZC_HD int gen_pseudo_wave(const Pos& q, bb from_mask, bb to_mask, uint16_t* out
 
 // legal_moves with the wave: candidates in `cand` (LDS, AZ_CHESS_MAX_MOVES),
 // the legal list in `out`; same return value and *check as legal_moves
-AZC_HD int legal_moves_wave(const Pos& q, uint16_t* cand, uint16_t* out, bool* check, int lane) {
+AZC_D int legal_moves_wave(const Pos& q, uint16_t* cand, uint16_t* out, bool* check, int lane) {
   const int king = king_sq(q, q.turn);
   *check = false;
   int n = 0;

@@ -2,6 +2,8 @@
 a20) against the chess oracle: legal moves (set and python-chess order),
 legal-move masks, outcomes, canonical play, full_state encoding, and perft on
 the device at full size; plus the reference Board API on top of them."""
+import os
+
 import numpy as np
 import pytest
 
@@ -145,3 +147,19 @@ def test_chess_abi_errors(K):
     assert L.az_chess_legal(0, None, -1, None, None, None, None) == -1  # AZ_E_INVALID
     assert L.az_chess_perft(0, None, 3, None) < 0
     assert L.az_chess_legal(99, None, 0, None, None, None, None) == 0  # n == 0: no work
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_round1_perft_scheme_is_deterministic(mode):
+    """tests/native/perft_repro.hip reconstructs the round-1 device perft
+    (per-lane scratch move list generated twice per position, child offsets
+    uploaded by a null-stream hipMemcpy (mode 0) or on the kernel's stream
+    (mode 1) before a non-blocking-stream expand kernel): Kiwipete perft(4)
+    exact on every run and both passes' lists identical at every position."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "_build", "perft_repro")
+    assert os.path.exists(exe), "tests/native not built (__graft_entry__.build() builds it)"
+    r = subprocess.run([exe, str(mode), "3"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 of 3 runs wrong, 0 count mismatches, 0 list mismatches" in r.stdout
