@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
     ap.add_argument("--cache-log2", type=int, default=25,
                     help="transposition cache (the reference's plays_inferences) entries = 2^N; 0 = off")
+    ap.add_argument("--compact", type=int, default=1,
+                    help="1: reclaim the subtrees a game has left after every move (az_config.compact)")
     ap.add_argument("--no-cache-window", action="store_true",
                     help="skip the second timed window with the cache bypassed")
     args = ap.parse_args()
@@ -438,7 +440,8 @@ def main():
 
     eng = az.Engine(args.height, args.width, args.n, True, args.sims, slots=args.slots,
                     evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index,
-                    cache_log2=args.cache_log2, lanes=args.lanes, conv_algo=args.conv_algo)
+                    cache_log2=args.cache_log2, lanes=args.lanes, conv_algo=args.conv_algo,
+                    compact=bool(args.compact))
     eng.set_weights(named)
     tree_steps = 3
     total_moves = MAX_PREROLL + 2 * args.steps + tree_steps + args.warmup
@@ -648,6 +651,17 @@ def main():
                 "semantics": "reference plays_inferences (mcts.py:122-143): board -> network output, shared "
                              "by all games on the GPU, emptied when weights change; bit-identical results",
             } if args.cache_log2 else None),
+            "tree_arena": {
+                "compact": bool(args.compact),
+                "edges_per_slot": (2 if args.compact else 1) * (
+                    8 * args.sims * A + HW * A if args.compact else args.sims * HW * A + A),
+                "bytes_total": 32 * args.slots * (2 if args.compact else 1) * (
+                    8 * args.sims * A + HW * A if args.compact else args.sims * HW * A + A),
+                "max_retained_edges": st1["max_retained"] if args.compact else None,
+                "rule": ("after every move the chosen child's subtree is copied into the other half of the "
+                         "slot's arena (Cheney scan); each half holds one move's search plus the reused "
+                         "subtree" if args.compact else "whole game tree kept (S*H*W*A edges per slot)"),
+            },
             "cache_off": off,
             "roofline_tree": roofline_tree,
             "roofline": roof,

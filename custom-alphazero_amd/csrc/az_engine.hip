@@ -289,7 +289,8 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
   L->g.slots = n;
   az::TreeDev t = e->t;
   const size_t f = (size_t)first;
-  t.edges += f * g.arena_cap;
+  t.edges += f * g.halves * g.arena_cap;
+  if (t.half) t.half += f;
   t.root_board += f;
   t.root_first += f;
   t.root_n += f;
@@ -485,7 +486,13 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   g.slots = c.slots;
   g.max_depth = g.HW + 1;
   const int64_t visits = c.max_tree_visits > 0 ? c.max_tree_visits : (int64_t)c.mcts_iterations * g.HW + 2;
-  const int64_t arena = c.arena_edges > 0 ? c.arena_edges : (int64_t)c.mcts_iterations * g.HW * A + A;
+  // compaction keeps one move's search plus the reused subtree per half: 8 S A
+  // covers a chosen child holding up to 7/8 of the root's visits move after
+  // move (the retained high-water mark is reported as az_stats.max_retained)
+  g.halves = c.compact ? 2 : 1;
+  const int64_t arena = c.arena_edges > 0 ? c.arena_edges
+                        : c.compact ? (int64_t)8 * c.mcts_iterations * A + (int64_t)g.HW * A
+                                    : (int64_t)c.mcts_iterations * g.HW * A + A;
   if (visits > (1 << 30) || arena > (1 << 30)) {
     delete e;
     return fail(AZ_E_INVALID, "tree bounds too large");
@@ -503,7 +510,9 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   if (c.lanes < 0) return cleanup(fail(AZ_E_INVALID, "lanes must be >= 0"));
   const size_t S = (size_t)g.slots;
   az::TreeDev& t = e->t;
-  if ((rc = e->alloc(&t.edges, S * g.arena_cap)) || (rc = e->alloc(&t.root_board, S)) ||
+  t.half = nullptr;
+  if (g.halves > 1 && (rc = e->alloc(&t.half, S))) return cleanup(rc);
+  if ((rc = e->alloc(&t.edges, S * g.halves * (size_t)g.arena_cap)) || (rc = e->alloc(&t.root_board, S)) ||
       (rc = e->alloc(&t.root_first, S)) || (rc = e->alloc(&t.root_n, S)) ||
       (rc = e->alloc(&t.root_value, S)) || (rc = e->alloc(&t.arena_top, S)) ||
       (rc = e->alloc(&t.ply, S)) || (rc = e->alloc(&t.game_id, S)) ||
@@ -730,6 +739,7 @@ int az_stats_get(az_engine* e, az_stats* st) {
     st->tree_launches += tm->launches;
   }
   st->path_edges = (int64_t)h[az::kStatPathEdges];
+  st->max_retained = (int64_t)h[az::kStatMaxRetained];
   st->cache_hits = (int64_t)h[az::kStatCacheHits];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
   if (e->cache.ctl) {
@@ -858,6 +868,7 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
         if ((rc = simulate(e, *L))) return rc;
     for (Lane* L : e->lanes) {
       az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
+      az::launch_compact(L->g, L->t, L->stream);
       if (multi) AZ_HIP(hipEventRecord(L->move_done[m % 3], L->stream));
     }
     AZ_HIP(hipGetLastError());
@@ -1040,12 +1051,13 @@ int az_tree_export(az_engine* e, int slot, double* prior, double* w, int32_t* n,
   if (!e || slot < 0 || slot >= e->g.slots) return fail(AZ_E_INVALID, "bad arguments");
   AZ_HIP(hipSetDevice(e->device));
   AZ_HIP(hipStreamSynchronize(e->stream));
-  int32_t top;
+  int32_t top, half = 0;
   AZ_HIP(hipMemcpy(&top, e->t.arena_top + slot, 4, hipMemcpyDeviceToHost));
+  if (e->g.halves > 1) AZ_HIP(hipMemcpy(&half, e->t.half + slot, 4, hipMemcpyDeviceToHost));
   std::vector<az::Edge> h(top);
   if (top)
-    AZ_HIP(hipMemcpy(h.data(), e->t.edges + (size_t)slot * e->g.arena_cap, top * sizeof(az::Edge),
-                     hipMemcpyDeviceToHost));
+    AZ_HIP(hipMemcpy(h.data(), e->t.edges + ((size_t)slot * e->g.halves + half) * e->g.arena_cap,
+                     top * sizeof(az::Edge), hipMemcpyDeviceToHost));
   for (int i = 0; i < top; ++i) {
     if (prior) prior[i] = h[i].prior;
     if (w) w[i] = h[i].W;

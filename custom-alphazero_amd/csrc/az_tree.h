@@ -32,6 +32,7 @@ enum : int {
   kStatNNEvals = 8,      // boards the evaluator actually computed
   kStatCacheInserts = 9,
   kStatPathEdges = 10,   // edges on the selected paths (sum of select depths)
+  kStatMaxRetained = 11, // compaction: most edges kept (atomicMax)
   kStatCount = 12        // (kStatCacheInserts counts since engine creation; CacheDev::ctl since a clear)
 };
 enum : unsigned long long {
@@ -41,7 +42,8 @@ enum : unsigned long long {
 
 // All device state of a forest (struct of arrays over slots).
 struct TreeDev {
-  Edge* edges;                 // [slots][arena_cap]
+  Edge* edges;                 // [slots][halves][arena_cap]
+  int32_t* half;               // [slots] half holding the live tree (halves == 2)
   Board* root_board;           // [slots]
   int32_t* root_first;         // [slots]
   int32_t* root_n;             // [slots]
@@ -138,7 +140,14 @@ size_t drain_record_bytes(const GameCfg& g);
 void launch_drain_pack(const GameCfg& g, const SampleDev& smp, int64_t from, int n, uint8_t* out,
                        hipStream_t s);
 
+// the live arena of slot s
+AZ_HD Edge* slot_edges(const GameCfg& g, const TreeDev& t, int s) {
+  return t.edges + ((size_t)s * g.halves + (g.halves > 1 ? t.half[s] : 0)) * g.arena_cap;
+}
+
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s);
+// self-play tree reuse (halves == 2): the new root's subtree into the other half
+void launch_compact(const GameCfg& g, const TreeDev& t, hipStream_t s);
 // cache on: misses are deduplicated inside select (step tag table); this
 // resolves the ones whose tag matched, by full-board compare
 void launch_dedup_resolve(const GameCfg& g, const TreeDev& t, hipStream_t s);

@@ -81,6 +81,7 @@ __device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gi
   t.root_n[s] = 0;
   t.root_value[s] = 0.f;
   t.arena_top[s] = 0;
+  if (g.halves > 1) t.half[s] = 0;
   t.ply[s] = 0;
   t.path_len[s] = 0;
   t.slot_expansions[s] = 0;
@@ -181,7 +182,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
 __global__ __launch_bounds__(64) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
-  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  Edge* E = slot_edges(g, t, s);
   int32_t* path = t.path + (size_t)s * g.max_depth;
   Board b = t.root_board[s];
   int first = t.root_first[s], cnt = t.root_n[s];
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = gid / L, j = gid % L;
   if (s >= g.slots || t.game_id[s] < 0) return;  // whole groups leave together
-  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  Edge* E = slot_edges(g, t, s);
   int32_t* path = t.path + (size_t)s * g.max_depth;
   Board b = t.root_board[s];
   int first = t.root_first[s], cnt = t.root_n[s];
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(64) void expand_kernel(GameCfg g, TreeDev t, CacheD
   int moves[MAXA];
   const int nm = moves_order(g, b, moves);
   const float sum = pairwise_sum_f32(masked, nl);
-  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  Edge* E = slot_edges(g, t, s);
   const int first = t.arena_top[s];
   if (first + nm > g.arena_cap) {
     flag_error(t, kErrArena);
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(64) void play_kernel(GameCfg g, TreeDev t, SampleDe
                                                    int greedy_mode, int deterministic, int refill) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
-  Edge* E = t.edges + (size_t)s * g.arena_cap;
+  Edge* E = slot_edges(g, t, s);
   const int first = t.root_first[s], cnt = t.root_n[s];
   if (cnt <= 0) {
     flag_error(t, kErrNoRoot);
@@ -527,6 +528,74 @@ __global__ __launch_bounds__(64) void play_kernel(GameCfg g, TreeDev t, SampleDe
     slot_reset(g, t, s, (int64_t)nid, (uint32_t)(smp.base_seed + (uint64_t)nid));
   else
     t.game_id[s] = -1;
+}
+
+// Tree reuse with reclamation (halves == 2), after play_kernel: the new
+// root's subtree -- the nodes MCTS.play keeps by moving current_root to the
+// chosen child (mcts.py:207) -- is copied into the slot's other arena half by
+// a Cheney scan, one wave per slot: the root's edge run first, then for each
+// scanned edge with an expanded child that child's run, placed by a
+// prefix sum over the wave's 64 edges (BFS order; edges before `scan` point
+// into the new half).  Everything else the game has left is dropped, so the
+// arena holds one move's search plus what it reuses.  Edge values are copied
+// bit for bit: the next search sees the same tree.
+__global__ __launch_bounds__(64) void compact_kernel(GameCfg g, TreeDev t) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  if (t.game_id[s] < 0) return;
+  const int h = t.half[s];
+  const Edge* E = t.edges + ((size_t)s * 2 + h) * g.arena_cap;
+  Edge* D = t.edges + ((size_t)s * 2 + (1 - h)) * g.arena_cap;
+  const int first = t.root_first[s], n = t.root_n[s];
+  if (n <= 0) {  // a fresh game (refilled slot) or a terminal root: nothing to keep
+    if (lane == 0) {
+      t.half[s] = 1 - h;
+      t.arena_top[s] = 0;
+      t.root_first[s] = 0;
+    }
+    return;
+  }
+  for (int j = lane; j < n; j += 64) D[j] = E[first + j];
+  __syncthreads();
+  int top = n, scan = 0;
+  bool overflow = false;
+  while (scan < top) {
+    const int top0 = top;
+    const int j = scan + lane;
+    Edge e;
+    int need = 0;
+    if (j < top0) {
+      e = D[j];
+      if (e.child >= 0) need = e.child_n;
+    }
+    int incl = need;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += o;
+    }
+    const int total = __shfl(incl, 63, 64);
+    if (top0 + total > g.arena_cap) {
+      overflow = true;
+      break;
+    }
+    if (need) {
+      const int nf = top0 + incl - need;
+      for (int k = 0; k < need; ++k) D[nf + k] = E[e.child + k];
+      e.child = nf;
+      D[j] = e;
+    }
+    top = top0 + total;
+    scan = min(scan + 64, top0);
+    __syncthreads();
+  }
+  if (lane == 0) {
+    if (overflow) flag_error(t, kErrArena);
+    t.half[s] = 1 - h;
+    t.arena_top[s] = overflow ? 0 : top;
+    t.root_first[s] = 0;
+    if (overflow) t.root_n[s] = 0;
+    atomicMax(t.stats + kStatMaxRetained, (unsigned long long)top);
+  }
 }
 
 // First n_first slots get games first_game .. first_game+n_first-1; the rest idle.
@@ -652,6 +721,10 @@ void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const
   else
     play_kernel<kMaxActions><<<game_blocks(g.slots), kGameBlock, 0, s>>>(
         g, t, smp, uniforms, greedy_mode, deterministic, refill);
+}
+
+void launch_compact(const GameCfg& g, const TreeDev& t, hipStream_t s) {
+  if (g.halves > 1 && g.slots > 0) compact_kernel<<<g.slots, 64, 0, s>>>(g, t);
 }
 
 void launch_slot_init(const GameCfg& g, const TreeDev& t, const SampleDev& smp, int64_t n_first,

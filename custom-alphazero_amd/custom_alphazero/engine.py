@@ -31,7 +31,7 @@ class Config(ctypes.Structure):
         ("value_hidden", ctypes.c_int32), ("bn_epsilon", ctypes.c_double),
         ("arena_edges", ctypes.c_int64), ("max_tree_visits", ctypes.c_int64),
         ("cache_log2", ctypes.c_int32), ("conv_algo", ctypes.c_int32),
-        ("lanes", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5),
+        ("lanes", ctypes.c_int32), ("compact", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4),
     ]
 
 
@@ -63,7 +63,7 @@ class Stats(ctypes.Structure):
         ("path_edges", ctypes.c_int64), ("cache_inserts", ctypes.c_int64),
         ("cache_generation", ctypes.c_int64), ("cache_gen_size", ctypes.c_int64),
         ("cache_capacity", ctypes.c_int64), ("games_drained", ctypes.c_int64),
-        ("reserved", ctypes.c_int64 * 3),
+        ("max_retained", ctypes.c_int64), ("reserved", ctypes.c_int64 * 2),
     ]
 
     def as_dict(self):
@@ -204,7 +204,10 @@ class Engine:
                  evaluator=EVAL_NETWORK, index_move_greedy=8, exploration_constant=1.5,
                  filters=128, depth=4, value_hidden=256, bn_epsilon=1e-3, arena_edges=0,
                  max_tree_visits=0, device=0, cache_log2=0, conv_algo=CONV_F16X2,
-                 lanes=0):
+                 lanes=0, compact=False):
+        """compact=True reclaims the subtrees a self-play game has left after
+        every move (az_config.compact; arena_edges is then per half); keep it
+        off for the tree API (az_tree_*), whose views need the whole tree."""
         L = load_library()
         self.height, self.width, self.n, self.gravity = height, width, n, bool(gravity)
         self.action_space = width if gravity else width * height
@@ -216,7 +219,7 @@ class Engine:
                      filters=filters, depth=depth, value_hidden=value_hidden,
                      bn_epsilon=bn_epsilon, arena_edges=arena_edges,
                      max_tree_visits=max_tree_visits, cache_log2=cache_log2, conv_algo=conv_algo,
-                     lanes=lanes)
+                     lanes=lanes, compact=int(bool(compact)))
         handle = ctypes.c_void_p()
         _check(L.az_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
         self._h = handle

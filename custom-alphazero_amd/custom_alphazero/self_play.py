@@ -99,7 +99,7 @@ def _batched_engine(model, n_slots):
                         exploration_constant=ConfigMCTS.exploration_constant,
                         filters=ConfigModel.filters, depth=ConfigModel.depth,
                         value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon,
-                        cache_log2=ConfigSelfPlay.cache_log2, lanes=ConfigSelfPlay.lanes)
+                        cache_log2=ConfigSelfPlay.cache_log2, lanes=ConfigSelfPlay.lanes, compact=True)
         eng.weights_key = None
         _ENGINES.clear()
         _ENGINES[key] = eng

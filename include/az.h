@@ -65,7 +65,12 @@ typedef struct az_config {
                                       layer, outputs within NET_TOL */
     int32_t lanes;                 /* self-play slot groups searched on separate HIP streams
                                       (0 = auto: 2 when slots >= 512); results do not depend on it */
-    int32_t reserved[5];
+    int32_t compact;               /* 1: after every self-play move the chosen child's subtree is
+                                      copied into the other half of the slot's arena (the subtrees
+                                      the game has left are reclaimed, mcts.py:207); arena_edges is
+                                      then per half (0 = 8*mcts_iterations*A + H*W*A).  The tree API
+                                      (az_tree_*) does not compact: use 0 there */
+    int32_t reserved[4];
 } az_config;
 
 /* One named weight tensor in Keras layout ("Weights"). */
@@ -99,7 +104,9 @@ typedef struct az_stats {
     int64_t cache_gen_size;   /* inserts per generation (0 = no eviction: the table only fills) */
     int64_t cache_capacity;   /* cache entries (2^cache_log2; 0 = no cache) */
     int64_t games_drained;    /* finished games az_selfplay_drain has returned this batch */
-    int64_t reserved[3];
+    int64_t max_retained;     /* compact: most edges a compaction kept (the arena high-water mark
+                                 before the next search) since engine creation */
+    int64_t reserved[2];
 } az_stats;
 
 int az_abi_version(void);

@@ -17,10 +17,10 @@ pytestmark = pytest.mark.gpu
 NET_TOL = 1e-5  # north_star: value/policy outputs within 1e-5 (fp32)
 
 
-def synth_engine(z, slots, cache_log2=0, lanes=0):
+def synth_engine(z, slots, cache_log2=0, lanes=0, compact=False):
     H, W, n, grav, S = (int(z[k]) for k in ("height", "width", "n", "gravity", "sims"))
     return az.Engine(H, W, n, bool(grav), S, slots=slots, evaluator=az.EVAL_SYNTHETIC,
-                     cache_log2=cache_log2, lanes=lanes)
+                     cache_log2=cache_log2, lanes=lanes, compact=compact)
 
 
 def selfplay_games(eng, first, n_games, base_seed=0):
@@ -51,17 +51,19 @@ def check_selfplay_game(z, g, got):
     assert got["expansions"] == z["expansions"][g]
 
 
-@pytest.mark.parametrize("cache_log2,lanes", [(0, 1), (16, 1), (16, 2)])
+@pytest.mark.parametrize("cache_log2,lanes,compact", [(0, 1, False), (16, 1, False), (16, 2, False),
+                                                      (0, 1, True), (16, 2, True)])
 @pytest.mark.parametrize("name", MCTS_FIXTURES)
-def test_selfplay_synthetic_matches_reference(golden, name, cache_log2, lanes):
+def test_selfplay_synthetic_matches_reference(golden, name, cache_log2, lanes, compact):
     """Batched device self-play == the reference's play_game, game by game,
     with and without the shared transposition cache (plays_inferences), on one
-    stream or two lanes (slot groups on separate streams sharing the cache)."""
+    stream or two lanes (slot groups on separate streams sharing the cache),
+    and with the left subtrees reclaimed after every move (compact)."""
     z = golden("mcts_" + name)
     seeds = z["seed"].astype(np.int64)
     assert np.all(np.diff(seeds) == 1)
     for slots in sorted({len(seeds), max(1, len(seeds) // 2)}):  # also exercises slot refill
-        eng = synth_engine(z, slots, cache_log2, lanes)
+        eng = synth_engine(z, slots, cache_log2, lanes, compact)
         games = selfplay_games(eng, int(seeds[0]), len(seeds))
         for g, got in enumerate(games):
             check_selfplay_game(z, g, got)
@@ -100,13 +102,15 @@ def test_tree_api_edges_match_reference(golden, name):
     assert A == z["policy"].shape[1]
 
 
-@pytest.mark.parametrize("cache_log2,lanes", [(0, 1), (10, 1), (20, 1), (20, 3), (0, 2)])
-def test_selfplay_synthetic_many_games_vs_oracle(cache_log2, lanes):
+@pytest.mark.parametrize("cache_log2,lanes,compact", [(0, 1, False), (10, 1, False), (20, 1, False),
+                                                      (20, 3, False), (0, 2, False), (20, 2, True)])
+def test_selfplay_synthetic_many_games_vs_oracle(cache_log2, lanes, compact):
     """256 games at S=50 on 96 slots (heavy refill) == the C oracle, bitwise;
     cache_log2=10 fills the table (probe limit / no-insert path); 2-3 lanes
-    race on the shared cache and the refill counter."""
+    race on the shared cache and the refill counter; compact reclaims the
+    left subtrees after every move."""
     eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC,
-                    cache_log2=cache_log2, lanes=lanes)
+                    cache_log2=cache_log2, lanes=lanes, compact=compact)
     games = selfplay_games(eng, 1000, 256, base_seed=7)
     for g, got in enumerate(games):
         ref = oracle.play_game(6, 7, 4, True, 50, 7 + 1000 + g)
@@ -204,12 +208,12 @@ CONV_ALGOS = [az.CONV_F16X2, az.CONV_DIRECT]
 
 
 def make_net_engine(H=6, W=7, n=4, grav=True, S=25, slots=256, seed=0, randomize_bn=True, depth=4,
-                    cache_log2=0, conv_algo=az.CONV_F16X2, lanes=0):
+                    cache_log2=0, conv_algo=az.CONV_F16X2, lanes=0, compact=False):
     A = W if grav else W * H
     spec = weight_spec(H, W, A, depth=depth)
     w = init_weights(spec, seed=seed, randomize_bn=randomize_bn)
     eng = az.Engine(H, W, n, grav, S, slots=slots, evaluator=az.EVAL_NETWORK, depth=depth,
-                    cache_log2=cache_log2, conv_algo=conv_algo, lanes=lanes)
+                    cache_log2=cache_log2, conv_algo=conv_algo, lanes=lanes, compact=compact)
     eng.set_weights(w.items())
     return eng, w
 
@@ -324,3 +328,28 @@ def test_abi_error_behaviour():
     moves, status, _ = eng.tree_play([0.5])
     assert 0 <= moves[0] < 7 and status[0] == 0
     eng.close()
+
+
+def test_compaction_bounds_the_arena_and_reports_overflow():
+    """With compact, a slot's arena holds one move's search plus the reused
+    subtree: 8*S*A + H*W*A edges per half against S*H*W*A without (5.9k vs
+    29.4k at S=100); the high-water mark is reported and stays inside; an
+    arena too small for a search is a device error, not a wrong tree."""
+    eng = az.Engine(6, 7, 4, True, 100, slots=64, evaluator=az.EVAL_SYNTHETIC, compact=True)
+    eng.selfplay_run(0, 128, 3)
+    st = eng.stats()
+    assert st["errors"] == 0 and st["games_done"] == 128
+    assert 0 < st["max_retained"] <= 8 * 100 * 7 + 42 * 7
+    r = eng.selfplay_results()
+    eng.close()
+    ref = az.Engine(6, 7, 4, True, 100, slots=64, evaluator=az.EVAL_SYNTHETIC)
+    ref.selfplay_run(0, 128, 3)
+    rr = ref.selfplay_results()
+    ref.close()
+    for k in ("lengths", "moves", "expansions"):
+        np.testing.assert_array_equal(r[k], rr[k])
+    np.testing.assert_array_equal(r["policies"].view(np.uint64), rr["policies"].view(np.uint64))
+    small = az.Engine(6, 7, 4, True, 100, slots=8, evaluator=az.EVAL_SYNTHETIC, compact=True, arena_edges=300)
+    with pytest.raises(az.AzError, match="arena-overflow"):
+        small.selfplay_run(0, 8, 3)
+    small.close()

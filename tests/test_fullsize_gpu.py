@@ -9,8 +9,8 @@ last of 8 ranks: games 28672..32767, seeds base + game index).  configs[4]: ches
 (2048 across 8), random-init network, games capped at 3 plies so the test
 finishes in seconds.  The small-size parity tests (test_engine_gpu.py,
 test_chess_selfplay_gpu.py) pin the arithmetic; these pin that nothing
-changes at the sizes the bench runs (arena sizing, queue chunking, cache
-pressure, slot counts past one workgroup grid).
+changes at the sizes the bench runs (arena sizing and subtree reclamation,
+queue chunking, cache pressure, slot counts past one workgroup grid).
 """
 import numpy as np
 import pytest
@@ -32,7 +32,9 @@ GREEDY_PLY = 8  # ConfigSelfPlay.index_move_greedy (reference config.py)
 def c4_games():
     out = {}
     for cache_log2 in (0, 25):
-        eng, _ = make_net_engine(**C4, seed=11, cache_log2=cache_log2)
+        # the cached run also reclaims left subtrees (compact, as bench.py runs): its games
+        # equal the plain run's bit for bit (test_c4_fullsize_cache_is_transparent)
+        eng, _ = make_net_engine(**C4, seed=11, cache_log2=cache_log2, compact=cache_log2 > 0)
         out[cache_log2] = (eng, selfplay_games(eng, 0, C4["slots"], base_seed=C4_SEED))
     yield out
     for eng, _ in out.values():
@@ -115,7 +117,7 @@ def test_connect_n_fullsize_configs(cfg):
     rules and policies for every game, sampled games replayed on the oracle
     (a shard's game i uses seed base + first + i, as bench.py's ranks do)."""
     H, W, n, S = cfg["H"], cfg["W"], cfg["n"], cfg["S"]
-    eng, _ = make_net_engine(H, W, n, True, S=S, slots=cfg["slots"], seed=13, cache_log2=25)
+    eng, _ = make_net_engine(H, W, n, True, S=S, slots=cfg["slots"], seed=13, cache_log2=25, compact=True)
     try:
         games = selfplay_games(eng, cfg["first"], cfg["slots"], base_seed=C4_SEED)
         check_rules_and_policies(games, H, W, n)
