@@ -1,0 +1,102 @@
+"""bench.py's N>1 glue at world size 2 over gloo on the CPU: the weight
+broadcast (_device_weights), the max/sum reductions of the timing and the
+counters (_reduce), and the window games' gather to rank 0 (WindowGames +
+distributed.gather_games) -- the same functions bench.main runs per rank,
+fed with drained-game records of the engine's layout (selfplay_drain).
+The GPU side of the same path is tests/test_distributed_gpu.py."""
+import argparse
+import importlib.util
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+H, W = 6, 7
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(REPO, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _drained(rank, step, n):
+    """n finished games as selfplay_drain returns them (leading game axis,
+    padded to H*W plies); contents tagged by (rank, step, game)."""
+    P = H * W
+    rng = np.random.RandomState(1000 * rank + step)
+    lengths = rng.randint(7, P + 1, n).astype(np.int32)
+    out = dict(game_ids=np.arange(n, dtype=np.int64) + 100 * rank + 10 * step,
+               lengths=lengths, results=rng.randint(-1, 2, n).astype(np.int32),
+               expansions=rng.randint(1, 5000, n).astype(np.int32),
+               boards=np.zeros((n, P, H, W), np.int8), policies=np.zeros((n, P, W)),
+               moves=np.zeros((n, P), np.int32))
+    for g in range(n):
+        T = lengths[g]
+        out["boards"][g, :T] = rng.randint(-1, 2, (T, H, W))
+        out["policies"][g, :T] = rng.dirichlet(np.ones(W), T)
+        out["moves"][g, :T] = rng.randint(0, W, T)
+    return out
+
+
+def _worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    bench = _bench()
+    from custom_alphazero import distributed as D
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = argparse.Namespace(dist_backend="gloo")
+    dev = torch.device("cpu")
+
+    spec = weight_spec(H, W, W, depth=1)
+    host_w = init_weights(spec, seed=0) if rank == 0 else init_weights(spec, seed=123)
+    named, flat = bench._device_weights(spec, host_w, rank, world, args, dev)
+    ref = init_weights(spec, seed=0)
+    for (name, t), (n2, shape) in zip(named, spec):
+        assert name == n2
+        np.testing.assert_array_equal(t.numpy(), ref[name].reshape(-1))
+
+    (el,) = bench._reduce([1.5 + rank], dist.ReduceOp.MAX, world, args, dev)
+    assert el == 1.5 + world - 1
+    tot = bench._reduce([rank + 1, 10], dist.ReduceOp.SUM, world, args, dev)
+    assert tot == [world * (world + 1) / 2, 10 * world]
+
+    window = bench.WindowGames()
+    for step, n in enumerate((2, 0, 3 + rank)):  # a step that drained nothing is skipped
+        window.add(_drained(rank, step, n))
+    g = D.gather_games(window.results(), device=None)
+    if rank == 0:
+        np.savez(os.path.join(outdir, "gathered.npz"), **g)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_glue_world2(tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
+    got = dict(np.load(tmp_path / "gathered.npz"))
+    bench = _bench()
+    from custom_alphazero import distributed as D
+    expect = []
+    for r in range(world):
+        w = bench.WindowGames()
+        for step, n in enumerate((2, 0, 3 + r)):
+            w.add(_drained(r, step, n))
+        expect.append(D._pack(w.results()))
+    for k in ("lengths", "results", "expansions", "boards", "policies", "moves"):
+        np.testing.assert_array_equal(got[k], np.concatenate([e[k] for e in expect]), err_msg=k)
+    assert len(got["lengths"]) == 2 + 3 + 2 + 4
+    # and the gathered games expand to the reference's sample layout
+    states, pol, rew = D.to_samples(got)
+    assert states.shape == (int(got["lengths"].sum()), H, W, 4) and len(rew) == len(pol) == len(states)

@@ -1,0 +1,127 @@
+"""The N>1 path with the real engine, rehearsed on one GPU:
+ranks share cuda:0 over gloo (RCCL does not put two ranks on one device; the
+8-GPU run is the driver's).
+
+* custom_alphazero.distributed: rank 0's weights reach the other ranks by one
+  broadcast, each rank's engine plays its contiguous shard of game ids, the
+  compact games are gathered to rank 0 -- identical, game by game, to one
+  engine playing every game (the seed depends only on the global game id).
+* bench.py under torch.distributed.run with 2 ranks: the line reports both
+  ranks' games, and the replay-buffer gather brings every rank's window games
+  to rank 0.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+H, W, N, S = 6, 7, 4, 16
+N_GAMES = 24
+BASE_SEED = 77
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _paths():
+    for p in (os.path.join(REPO, "custom-alphazero_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _engine(evaluator, named=None):
+    from custom_alphazero import engine as az
+    eng = az.Engine(H, W, N, True, S, slots=8, evaluator=evaluator, compact=True)
+    if named is not None:
+        eng.set_weights(named)
+    return eng
+
+
+def _worker(rank, world, port, outdir, network):
+    _paths()
+    import torch
+    import torch.distributed as dist
+    from custom_alphazero import distributed as D
+    from custom_alphazero import engine as az
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    named = None
+    if network:
+        spec = weight_spec(H, W, W)
+        host = init_weights(spec, seed=9, randomize_bn=True)
+        local = [(n, torch.from_numpy(host[n]) if rank == 0 else torch.zeros(tuple(s))) for n, s in spec]
+        named = D.broadcast_weights(local)  # gloo: CPU tensors; the engine copies them to the device
+    eng = _engine(az.EVAL_NETWORK if network else az.EVAL_SYNTHETIC, named)
+    g = D.selfplay_sharded(D.engine_runner(eng), N_GAMES, BASE_SEED, device="cpu")
+    eng.close()
+    if rank == 0:
+        np.savez(os.path.join(outdir, f"world{world}.npz"), **g)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single(network):
+    _paths()
+    from custom_alphazero import distributed as D
+    from custom_alphazero import engine as az
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    named = None
+    if network:
+        spec = weight_spec(H, W, W)
+        host = init_weights(spec, seed=9, randomize_bn=True)
+        named = [(n, host[n]) for n, _ in spec]
+    eng = _engine(az.EVAL_NETWORK if network else az.EVAL_SYNTHETIC, named)
+    eng.selfplay_run(0, N_GAMES, BASE_SEED)
+    r = D._pack(eng.selfplay_results())
+    eng.close()
+    return r
+
+
+@pytest.mark.parametrize("network", [False, True], ids=["synthetic", "network"])
+def test_sharded_engine_selfplay_equals_one_engine(tmp_path, network):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), network), nprocs=world,
+                       start_method="spawn")
+    got = dict(np.load(tmp_path / f"world{world}.npz"))
+    ref = _single(network)
+    for k in ("lengths", "results", "expansions", "boards", "moves"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    np.testing.assert_array_equal(got["policies"].view(np.uint64), ref["policies"].view(np.uint64))
+    if not network:  # and the synthetic games are the reference's (oracle)
+        import oracle
+        off = 0
+        for g in range(N_GAMES):
+            r = oracle.play_game(H, W, N, True, S, BASE_SEED + g)
+            T = r["T"]
+            assert got["lengths"][g] == T
+            np.testing.assert_array_equal(got["moves"][off:off + T], r["moves"])
+            off += T
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_gathers_every_rank():
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--slots", "512", "--steps", "3", "--warmup", "2",
+           "--cache-log2", "16", "--no-cpu-baseline", "--no-cache-window"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=REPO,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    gather = line["replay_buffer_gather"]
+    assert gather is not None and gather["games"] == line["games_timed"] > 0
+    assert gather["samples"] >= 7 * gather["games"]
