@@ -246,7 +246,18 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
   if (!HEADS && vmax > kOverflow && err) atomicOr(err, kErrActRange);
   __syncthreads();
 
-  // 16 threads per row, 8 channels each
+  // 16 threads per row, 8 channels each (a thread keeps its channels: NT % 16 == 0,
+  // so the head weights of them are read once, not per row)
+  float hwp[8][3];
+  if constexpr (HEADS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = 8 * (tid & 15) + e;
+      hwp[e][0] = hc.wpc[2 * c];
+      hwp[e][1] = hc.wpc[2 * c + 1];
+      hwp[e][2] = hc.wvc[c];
+    }
+  }
   for (int idx = tid; idx < TR * 16; idx += NT) {
     const int r = idx >> 4, q = idx & 15;
     const int g = row0 + r;
@@ -260,10 +271,9 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
       float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int c = 8 * q + e;
-        s0 = fmaf(x[e], hc.wpc[2 * c], s0);
-        s1 = fmaf(x[e], hc.wpc[2 * c + 1], s1);
-        s2 = fmaf(x[e], hc.wvc[c], s2);
+        s0 = fmaf(x[e], hwp[e][0], s0);
+        s1 = fmaf(x[e], hwp[e][1], s1);
+        s2 = fmaf(x[e], hwp[e][2], s2);
       }
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) {
