@@ -33,7 +33,11 @@
 //  * conv2 fuses the block's 1x1 projection residual: four more k-steps on
 //    the block input's rows (prefetched into registers during the taps,
 //    written over the slab after them); with HEADS the policy/value 1x1
-//    convs run in the epilogue (feat = [rows] float4) instead of a store.
+//    convs run in the epilogue (feat = [rows] float4) instead of a store;
+//    that variant passes the weights as the MFMA's A operand, so a lane's
+//    accumulators are 4 channels of one pixel and the 1x1 sums need no LDS
+//    tile (plain convs keep the tile: their 512-B row stores measured faster
+//    than 8-B stores from the accumulators, profiles/r2/epilogue_ab.txt).
 // Every output element is summed in a fixed order (k-step, then term), so a
 // board's outputs do not depend on what else is in the batch.
 #include <algorithm>
@@ -212,12 +216,21 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     for (int mb = 0; mb < MB; ++mb) {
       const h8 a0 = __builtin_bit_cast(h8, aq[s & 1][mb][0]);
       const h8 a1 = __builtin_bit_cast(h8, aq[s & 1][mb][1]);
-      acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b00, acc[mb][0], 0, 0, 0);
-      acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B01, acc[mb][0], 0, 0, 0);
-      acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B00, acc[mb][0], 0, 0, 0);
-      acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b10, acc[mb][1], 0, 0, 0);
-      acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B11, acc[mb][1], 0, 0, 0);
-      acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B10, acc[mb][1], 0, 0, 0);
+      if constexpr (HEADS) {  // weights as the A operand: D = out^T, a lane holds 4 channels of one pixel
+        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b00, a1, acc[mb][0], 0, 0, 0);
+        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B01, a0, acc[mb][0], 0, 0, 0);
+        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B00, a0, acc[mb][0], 0, 0, 0);
+        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b10, a1, acc[mb][1], 0, 0, 0);
+        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B11, a0, acc[mb][1], 0, 0, 0);
+        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B10, a0, acc[mb][1], 0, 0, 0);
+      } else {
+        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b00, acc[mb][0], 0, 0, 0);
+        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B01, acc[mb][0], 0, 0, 0);
+        acc[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B00, acc[mb][0], 0, 0, 0);
+        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b10, acc[mb][1], 0, 0, 0);
+        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B11, acc[mb][1], 0, 0, 0);
+        acc[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, B10, acc[mb][1], 0, 0, 0);
+      }
     }
     if (AZ_C16_AKS) {  // the next k-step's reads first, then this one's MFMAs
       __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);   // VMEM reads (B, PF ahead)
@@ -226,7 +239,73 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     }
   }
 
-  // ---- epilogue: BN bias (+ residual's) + ReLU into an fp32 tile in LDS
+  if constexpr (HEADS) {
+    // ---- epilogue of the last conv: the heads' 1x1 convs straight from the
+    // accumulators (weights were the MFMA's A operand, so lane (gq, r16) of
+    // N block nb holds channels 32nq + 16nb + 4gq .. +3 of pixel row mb*16 + r16)
+    // policy conv F->2, value conv F->1 (+ folded BN, ReLU; model.py:68-149):
+    // per lane its 8 channels (nb, then v), a fixed xor tree over the four
+    // lane groups, then the four waves' column quarters in order through LDS
+    float hw[2][4][3];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int c = 32 * nq + 16 * nb + 4 * gq + v;
+        hw[nb][v][0] = hc.wpc[2 * c];
+        hw[nb][v][1] = hc.wpc[2 * c + 1];
+        hw[nb][v][2] = hc.wvc[c];
+      }
+    float4 b4[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) b4[nb] = *reinterpret_cast<const float4*>(bias + 32 * nq + 16 * nb + 4 * gq);
+    float part[MB][3];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float y = fmaxf(fmaf(acc[mb][nb][v], oscale, (&b4[nb].x)[v]), 0.f);
+          s0 = fmaf(y, hw[nb][v][0], s0);
+          s1 = fmaf(y, hw[nb][v][1], s1);
+          s2 = fmaf(y, hw[nb][v][2], s2);
+        }
+      s0 += __shfl_xor(s0, 16);
+      s1 += __shfl_xor(s1, 16);
+      s2 += __shfl_xor(s2, 16);
+      s0 += __shfl_xor(s0, 32);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      part[mb][0] = s0;
+      part[mb][1] = s1;
+      part[mb][2] = s2;
+    }
+    __syncthreads();  // slab no longer read
+    float* red = reinterpret_cast<float*>(lds);  // [TR][4 waves][3]
+    if (gq == 0)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) red[((mb * 16 + r16) * 4 + nq) * 3 + k] = part[mb][k];
+    __syncthreads();
+    for (int r = tid; r < TR; r += NT) {
+      const int g = row0 + r;
+      if (g >= rows) continue;
+      float t[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        t[k] = ((red[(r * 4 + 0) * 3 + k] + red[(r * 4 + 1) * 3 + k]) + red[(r * 4 + 2) * 3 + k]) +
+               red[(r * 4 + 3) * 3 + k];
+      hc.feat[g] = make_float4(fmaxf(t[0] + hc.bpc[0], 0.f), fmaxf(t[1] + hc.bpc[1], 0.f),
+                               fmaxf(t[2] + hc.bvc[0], 0.f), 0.f);
+    }
+    return;
+  }
+  // ---- epilogue: BN bias (+ residual's) + ReLU into an fp32 tile in LDS,
+  // then split16 rows (a wave's accumulators hold 16-row column strips; the
+  // tile turns them into 512-B row stores)
   __syncthreads();  // slab no longer read
   float* tile = reinterpret_cast<float*>(lds);
   float vmax = 0.f;
@@ -243,21 +322,10 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
         tile[(mb * 16 + 4 * gq + v) * kC16Pitch + col] = y;
       }
   }
-  if (!HEADS && vmax > kOverflow && err) atomicOr(err, kErrActRange);
+  if (vmax > kOverflow && err) atomicOr(err, kErrActRange);
   __syncthreads();
 
-  // 16 threads per row, 8 channels each (a thread keeps its channels: NT % 16 == 0,
-  // so the head weights of them are read once, not per row)
-  float hwp[8][3];
-  if constexpr (HEADS) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = 8 * (tid & 15) + e;
-      hwp[e][0] = hc.wpc[2 * c];
-      hwp[e][1] = hc.wpc[2 * c + 1];
-      hwp[e][2] = hc.wvc[c];
-    }
-  }
+  // 16 threads per row, 8 channels each
   for (int idx = tid; idx < TR * 16; idx += NT) {
     const int r = idx >> 4, q = idx & 15;
     const int g = row0 + r;
@@ -265,31 +333,10 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     const float4 u = *reinterpret_cast<const float4*>(tile + r * kC16Pitch + 8 * q);
     const float4 w = *reinterpret_cast<const float4*>(tile + r * kC16Pitch + 8 * q + 4);
     const float x[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
-    if constexpr (HEADS) {
-      // policy conv F->2, value conv F->1 (+ folded BN, ReLU; model.py:68-149):
-      // 8 channels per thread in order, then a fixed xor tree over the 16
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s0 = fmaf(x[e], hwp[e][0], s0);
-        s1 = fmaf(x[e], hwp[e][1], s1);
-        s2 = fmaf(x[e], hwp[e][2], s2);
-      }
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) {
-        s0 += __shfl_xor(s0, o, 16);
-        s1 += __shfl_xor(s1, o, 16);
-        s2 += __shfl_xor(s2, o, 16);
-      }
-      if (q == 0)
-        hc.feat[g] = make_float4(fmaxf(s0 + hc.bpc[0], 0.f), fmaxf(s1 + hc.bpc[1], 0.f),
-                                 fmaxf(s2 + hc.bvc[0], 0.f), 0.f);
-    } else {
-      uint4 t0, t1;
-      split16x8(x, t0, t1);
-      out[(size_t)g * 32 + q] = t0;
-      out[(size_t)g * 32 + 16 + q] = t1;
-    }
+    uint4 t0, t1;
+    split16x8(x, t0, t1);
+    out[(size_t)g * 32 + q] = t0;
+    out[(size_t)g * 32 + 16 + q] = t1;
   }
 }
 

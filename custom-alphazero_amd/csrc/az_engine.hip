@@ -51,6 +51,7 @@ int fail_abi(int code, const std::string& msg) { return fail(code, msg); }
 // the evaluator is deterministic per board).
 struct Lane {
   int first = 0, n = 0;
+  int32_t* counts = nullptr;  // [2][4] eval/miss/nn/dup counts by simulation parity
   hipStream_t stream = nullptr;
   az::GameCfg g{};
   az::TreeDev t{};
@@ -135,6 +136,15 @@ az::Board board_from_cells(const int8_t* cells, int HW) {
   return b;
 }
 
+// point a tree view's four counters at parity p of the [2][4] block at base
+void set_counts(az::TreeDev& t, int32_t* base, int p) {
+  t.eval_count = base + 4 * p;
+  t.miss_count = t.eval_count + 1;
+  t.nn_count = t.eval_count + 2;
+  t.dup_count = t.eval_count + 3;
+  t.next_counts = base + 4 * (p ^ 1);
+}
+
 void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
   for (int c = 0; c < HW; ++c)
     cells[c] = az::bit(b.own, c) ? 1 : (az::bit(b.opp, c) ? -1 : 0);
@@ -144,9 +154,10 @@ void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
 // mcts.py:171-180), enqueued on the lane's stream
 int simulate(az_engine* e, Lane& L) {
   hipStream_t s = L.stream;
-  // eval_count, miss_count, nn_count, dup_count are one contiguous block
-  AZ_HIP(hipMemsetAsync(L.t.eval_count, 0, 4 * sizeof(int32_t), s));
   L.t.epoch += 1;  // fresh per-simulation dedup table (tags of older epochs read as empty)
+  // eval_count, miss_count, nn_count, dup_count: the epoch parity's block of
+  // four (zeroed by the previous simulation's select kernel, or at creation)
+  set_counts(L.t, L.counts, L.t.epoch & 1);
   if (L.tree_timer.enabled) L.tree_timer.begin(s);
   az::launch_select(L.g, L.t, e->cache, s);
   if (L.tree_timer.enabled) L.tree_timer.end(s, 1);
@@ -315,16 +326,16 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
     int rc;
     size_t cap = 1024;
     while (cap < 4 * (size_t)n) cap <<= 1;
-    if ((rc = e->alloc(&t.eval_count, 4)) || (rc = e->alloc(&t.step_tag, cap)) ||
+    if ((rc = e->alloc(&t.eval_count, 8)) || (rc = e->alloc(&t.step_tag, cap)) ||
         (rc = e->alloc(&t.step_row, cap)))
       return rc;
     AZ_HIP(hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)));
-    t.miss_count = t.eval_count + 1;
-    t.nn_count = t.eval_count + 2;
-    t.dup_count = t.eval_count + 3;
+    AZ_HIP(hipMemset(t.eval_count, 0, 8 * sizeof(int32_t)));
+    set_counts(t, t.eval_count, 0);
     t.step_mask = (uint32_t)(cap - 1);
     t.epoch = 0;
   }
+  L->counts = t.eval_count;
   L->t = t;
   L->x = e->x + f * g.HW * 4;
   for (int i = 0; i < 3; ++i) L->act[i] = e->act[i] ? e->act[i] + f * g.HW * 128 : nullptr;
@@ -521,7 +532,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_board, S)) ||
       (rc = e->alloc(&t.eval_src, S)) || (rc = e->alloc(&t.miss_q, S)) ||
       (rc = e->alloc(&t.nn_board, S)) ||
-      (rc = e->alloc(&t.eval_count, 4)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
+      (rc = e->alloc(&t.eval_count, 8)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
       (rc = e->alloc(&t.last_move, S)) || (rc = e->alloc(&t.last_status, S)) ||
       (rc = e->alloc(&t.last_policy, S * A)))
     return cleanup(rc);
@@ -535,9 +546,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   }
   t.powtab = powtab;
   t.mt_stride = g.slots;
-  t.miss_count = t.eval_count + 1;
-  t.nn_count = t.eval_count + 2;
-  t.dup_count = t.eval_count + 3;
+  set_counts(t, t.eval_count, 0);
   {
     size_t cap = 1024;
     while (cap < 4 * S) cap <<= 1;  // load factor <= 25%
@@ -568,6 +577,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       return cleanup(fail(AZ_E_HIP, "cache memset failed"));
   }
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(t.eval_count, 0, 8 * sizeof(int32_t)) != hipSuccess ||
       hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
     return cleanup(fail(AZ_E_HIP, "memset failed"));
   // evaluator buffers (batch = slots)

@@ -66,6 +66,10 @@ struct TreeDev {
   int32_t* nn_count;           // [1]
   int32_t* dup_q;              // [slots] misses whose board tag matched another miss
   int32_t* dup_count;          // [1]
+  // eval/miss/nn/dup counts are one block of 4; two blocks alternate by
+  // simulation (epoch parity): the select kernel zeroes the other block, the
+  // next simulation's, so no memset launch sits between simulations
+  int32_t* next_counts;        // [4] the block the next simulation uses
   uint64_t* step_tag;          // [step_cap] per-simulation dedup table: (epoch << 32) | fp32
   int32_t* step_row;           // [step_cap] evaluator row of the tag's owner
   uint32_t step_mask;          // step_cap - 1

@@ -180,6 +180,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
 
 // Serial descent, one lane per game (used when the action space exceeds 64).
 __global__ __launch_bounds__(64) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
+  if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
   Edge* E = slot_edges(g, t, s);
@@ -230,6 +231,7 @@ __global__ __launch_bounds__(64) void select_kernel(GameCfg g, TreeDev t, CacheD
 // expressions as the serial loop, so the chosen edge is identical.
 template <int L>
 __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
+  if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = gid / L, j = gid % L;
   if (s >= g.slots || t.game_id[s] < 0) return;  // whole groups leave together
