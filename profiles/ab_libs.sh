@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/ab_libs
 for spec in "$@"; do
-  v=${spec%%:*}; flags=""; [ "$spec" != "$v" ] && flags="${spec#*:}"
+  v=${spec%%:*}; flags=""; [ "$spec" != "$v" ] && flags="${spec#*:}"; flags=${flags//,/ }
   if [ "$v" = base ]; then lib=custom-alphazero_amd/custom_alphazero/_lib/libaz.so; else lib=profiles/ab_libs/$v/libaz.so; fi
   AZ_LIB_PATH=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline $flags > gpurun_out/ab_libs/$spec.json 2> gpurun_out/ab_libs/$spec.err || { tail gpurun_out/ab_libs/$spec.err; exit 1; }
   python3 - "gpurun_out/ab_libs/$spec.json" "$spec" <<'PY'
