@@ -520,7 +520,7 @@ def main():
     bytes_per_sim = 16 * A * depth + 24 * depth + f_exp * (16 * A + 672 + 672 + 64)
     tree_gbs = bytes_per_sim * sims_t / (sb["tree_ms"] * 1e-3) / 1e9 if sb["tree_ms"] else 0.0
     roofline_tree = {
-        "kernels": "select_group_kernel + expand_kernel (PUCT descent, backup, prior normalisation)",
+        "kernels": "select_group_kernel + expand_kernel (PUCT descent, backup, prior normalisation; the expand launch also carries the cache inserts)",
         "bound": "hbm", "achieved": round(tree_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(tree_gbs / HBM_PEAK_GBS, 5), "traffic": None,
         "bytes_per_simulation": round(bytes_per_sim, 1), "mean_depth": round(depth, 3),

@@ -178,7 +178,6 @@ int simulate(az_engine* e, Lane& L) {
   if (L.tree_timer.enabled) L.tree_timer.begin(s);
   az::launch_expand(L.g, L.t, e->cache, L.probs, L.values, s);
   if (L.tree_timer.enabled) L.tree_timer.end(s, 1);
-  if (e->cache.enabled) az::launch_cache_insert(L.g, L.t, e->cache, L.probs, L.values, s);
   AZ_HIP(hipGetLastError());
   return 0;
 }

@@ -159,8 +159,6 @@ void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* cou
                        float* values, hipStream_t s);
 void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
                    const float* values, hipStream_t s);
-void launch_cache_insert(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
-                         const float* values, hipStream_t s);
 // uniforms: device [slots] draws for play (MCTS API), or null -> per-slot MT19937;
 // greedy_mode -1 = by ply (self-play), 0/1 = caller's flag
 void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const double* uniforms,

@@ -332,10 +332,8 @@ __global__ __launch_bounds__(256) void dedup_resolve_kernel(GameCfg g, TreeDev t
 // plays_inferences[repr(board)] = probabilities, value (mcts.py:142): one
 // writer per distinct board (dedup), racing only for empty slots or slots
 // whose entry is kCacheReuseAge generations old (az_tree.h).
-__global__ __launch_bounds__(256) void cache_insert_kernel(GameCfg g, TreeDev t, CacheDev c,
-                                                           const float* __restrict__ probs,
-                                                           const float* __restrict__ values) {
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void cache_insert_row(const GameCfg& g, const TreeDev& t, const CacheDev& c,
+                                 const float* __restrict__ probs, const float* __restrict__ values, int u) {
   if (u >= *t.nn_count) return;
   const Board b = t.nn_board[u];
   const uint64_t h = board_hash(b);
@@ -375,10 +373,19 @@ __global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, const Board*
 // ------------------------------------------------------------------- expand
 // MCTS.evaluate_and_expand (mcts.py:145-161) with normalize_probabilities
 // (mcts/utils.py:4-16), then backup(-value) (mcts.py:175, 163-168).
-template <int MAXA>
+// With INSERT the same launch also publishes this simulation's evaluated
+// boards to the cache (blocks from exp_blocks on, one nn row per thread):
+// the leaves expanded here read only entries live at select time, which an
+// insert never reuses (kCacheLiveGens < kCacheReuseAge, az_tree.h), so the
+// two halves are independent and share one launch instead of two.
+template <int MAXA, bool INSERT>
 __global__ __launch_bounds__(64) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
                                                      const float* __restrict__ probs,
-                                                     const float* __restrict__ values) {
+                                                     const float* __restrict__ values, int exp_blocks) {
+  if (INSERT && (int)blockIdx.x >= exp_blocks) {  // block-uniform
+    cache_insert_row(g, t, c, probs, values, ((int)blockIdx.x - exp_blocks) * blockDim.x + threadIdx.x);
+    return;
+  }
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= *t.eval_count) return;
   const int s = t.eval_slot[i];
@@ -704,15 +711,16 @@ void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* cou
 
 void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
                    const float* values, hipStream_t s) {
-  if (g.A <= 16)
-    expand_kernel<16><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c, probs, values);
-  else
-    expand_kernel<kMaxActions><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c, probs, values);
-}
-
-void launch_cache_insert(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,
-                         const float* values, hipStream_t s) {
-  cache_insert_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, c, probs, values);
+  const int eb = game_blocks(g.slots);
+  const bool ins = c.enabled;
+  const int grid = eb + (ins ? game_blocks(g.slots) : 0);
+  if (g.A <= 16) {
+    if (ins) expand_kernel<16, true><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
+    else expand_kernel<16, false><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
+  } else {
+    if (ins) expand_kernel<kMaxActions, true><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
+    else expand_kernel<kMaxActions, false><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
+  }
 }
 
 void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const double* uniforms,
