@@ -24,6 +24,42 @@ namespace az {
 __device__ __forceinline__ void stat_add(const TreeDev& t, int which, unsigned long long v) {
   atomicAdd(t.stats + which, v);
 }
+
+// Wave-aggregated counters.  Every game of a launch adds to the same few
+// words (queue counts, stats); one atomic per wave instead of one per game
+// keeps those words' L2 channel from serialising a launch's worth of
+// same-address atomics.  Called by the lanes active at the call site (a
+// divergent branch is fine: __ballot sees exactly those lanes).
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+// one unit per active lane: returns this lane's slot (base + rank among the active lanes)
+__device__ __forceinline__ int wave_claim(int32_t* counter) {
+  const unsigned long long m = __ballot(1);
+  const int leader = __ffsll((long long)m) - 1;
+  const int rank = __popcll(m & ((1ull << lane_id()) - 1));
+  int base = 0;
+  if (lane_id() == leader) base = atomicAdd(counter, __popcll(m));
+  return __shfl(base, leader) + rank;
+}
+__device__ __forceinline__ unsigned long long wave_claim64(unsigned long long* counter) {
+  const unsigned long long m = __ballot(1);
+  const int leader = __ffsll((long long)m) - 1;
+  const int rank = __popcll(m & ((1ull << lane_id()) - 1));
+  unsigned long long base = 0;
+  if (lane_id() == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
+  return __shfl(base, leader) + (unsigned long long)rank;
+}
+__device__ __forceinline__ void wave_count(int32_t* counter) {
+  const unsigned long long m = __ballot(1);
+  if (lane_id() == __ffsll((long long)m) - 1) atomicAdd(counter, __popcll(m));
+}
+// stats: the active lanes' v summed bit-slice by bit-slice (v < 2^8)
+__device__ __forceinline__ void wave_stat(const TreeDev& t, int which, unsigned v = 1) {
+  const unsigned long long m = __ballot(1);
+  unsigned long long sum = 0;
+#pragma unroll
+  for (int bit = 0; bit < 8; ++bit) sum += (unsigned long long)__popcll(__ballot((v >> bit) & 1u)) << bit;
+  if (lane_id() == __ffsll((long long)m) - 1 && sum) atomicAdd(t.stats + which, sum);
+}
 __device__ __forceinline__ void flag_error(const TreeDev& t, unsigned long long f) {
   atomicOr(t.stats + kStatErrors, f);
 }
@@ -103,21 +139,21 @@ __device__ __forceinline__ bool same_board(const Board& a, const Board& b) {
 // the eval queue + plays_inferences probe + per-simulation dedup.
 __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c, int s, Edge* E,
                           const int32_t* path, int depth, int status, const Board& b) {
-  stat_add(t, kStatSims, 1);
-  if (depth) stat_add(t, kStatPathEdges, (unsigned long long)depth);
+  wave_stat(t, kStatSims);
+  wave_stat(t, kStatPathEdges, (unsigned)depth);
   if (depth > 0 && status != kOngoing) {
     // get_result(keep_same_player=True): 1 for the player who just moved, 0 draw
     backup(E, path, depth, status == kWin ? 1.0 : 0.0);
-    stat_add(t, kStatTerminal, 1);
+    wave_stat(t, kStatTerminal);
     return;
   }
-  const int q = atomicAdd(t.eval_count, 1);
+  const int q = wave_claim(t.eval_count);
   t.eval_slot[q] = s;
   t.eval_board[q] = b;
   t.path_len[s] = depth;
   if (!c.enabled) {
     t.eval_src[q] = -(q + 1);
-    stat_add(t, kStatNNEvals, 1);
+    wave_stat(t, kStatNNEvals);
     return;
   }
   // repr(board) in plays_inferences (mcts.py:123).  Entries may be published
@@ -138,7 +174,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
       if ((st & 3u) == kCacheReady && (st >> 16) == fp && cache_age(st, gen) < kCacheLiveGens &&
           same_board(c.keys[idx], b)) {
         t.eval_src[q] = (int32_t)idx;
-        stat_add(t, kStatCacheHits, 1);
+        wave_stat(t, kStatCacheHits);
         return;
       }
       idx = (idx + 1) & c.mask;
@@ -148,7 +184,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   // (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
   // empty, so the table needs no clearing.  A tag match is only a candidate:
   // dedup_resolve compares the full boards after this kernel.
-  atomicAdd(t.miss_count, 1);
+  wave_count(t.miss_count);
   const uint64_t tag = ((uint64_t)t.epoch << 32) | (uint32_t)(h >> 32);
   uint32_t slot = (uint32_t)h & t.step_mask;
   for (uint32_t p = 0; p <= t.step_mask; ++p) {
@@ -156,7 +192,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
     if ((uint32_t)(cur >> 32) != t.epoch) {  // empty in this epoch: try to own it
       const uint64_t prev = atomicCAS((unsigned long long*)(t.step_tag + slot), cur, tag);
       if (prev == cur) {
-        const int row = atomicAdd(t.nn_count, 1);
+        const int row = wave_claim(t.nn_count);
         t.nn_board[row] = b;
         t.step_row[slot] = row;
         t.eval_src[q] = -(row + 1);
@@ -164,14 +200,14 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
       }
       if (prev == tag) {  // lost the race to the same tag
         t.eval_src[q] = (int32_t)(0x80000000u | slot);
-        t.dup_q[atomicAdd(t.dup_count, 1)] = q;
+        t.dup_q[wave_claim(t.dup_count)] = q;
         return;
       }
       continue;  // someone else took this slot with another tag: re-read it
     }
     if (cur == tag) {
       t.eval_src[q] = (int32_t)(0x80000000u | slot);
-      t.dup_q[atomicAdd(t.dup_count, 1)] = q;
+      t.dup_q[wave_claim(t.dup_count)] = q;
       return;
     }
     slot = (slot + 1) & t.step_mask;
@@ -350,9 +386,9 @@ __device__ void cache_insert_row(const GameCfg& g, const TreeDev& t, const Cache
       dst[g.A] = values[u];
       __threadfence();
       atomicExch(c.state + idx, cache_word(fp, gen, kCacheReady));
-      stat_add(t, kStatCacheInserts, 1);
+      wave_stat(t, kStatCacheInserts);
       // every gen_size-th insert since the clear opens a new generation
-      const unsigned long long n = atomicAdd(c.ctl + 1, 1ull) + 1;
+      const unsigned long long n = wave_claim64(c.ctl + 1) + 1;
       if (c.gen_size && n % c.gen_size == 0) atomicAdd(c.ctl, 1ull);
       return;
     }
@@ -442,7 +478,7 @@ __global__ __launch_bounds__(64) void expand_kernel(GameCfg g, TreeDev t, CacheD
   }
   backup(E, path, depth, -(double)v);
   t.slot_expansions[s] += 1;
-  stat_add(t, kStatExpansions, 1);
+  wave_stat(t, kStatExpansions);
 }
 
 // --------------------------------------------------------------------- play
