@@ -922,11 +922,12 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
   e->net.hidden = c.value_hidden;
   e->net.err = t.stats + az::kStatErrors;
   if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));
-  // auto = 1: at 256 games a chess step is bound by its launch chain; extra
-  // streams measured slower (375k expansions/s with 1 lane, 311k with 2,
-  // 159k with 4: more launches per simulation from one host thread, streams
-  // sharing the 4 hardware queues)
-  int nl = c.lanes > 0 ? c.lanes : 1;
+  // auto = 2 from 128 games: a lane's simulation is a latency-bound chain of
+  // ~14 launches, and a second stream's chain fills the CUs its small kernels
+  // leave idle (round 2, conv16: 1 lane 1.17M expansions/s, 2 lanes 1.37-1.42M,
+  // 3-4 lanes 0.82M -- tiny per-lane batches, and the streams then share
+  // the 4 hardware queues; profiles/r2/chess_lanes.txt)
+  int nl = c.lanes > 0 ? c.lanes : (g.slots >= 128 ? 2 : 1);
   nl = std::min(nl, std::min(g.slots, 16));
   for (int l = 0; l < nl; ++l) {
     CLane* L = new CLane();

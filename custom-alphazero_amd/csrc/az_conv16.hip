@@ -58,9 +58,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef AZ_C16_OCC
 #define AZ_C16_OCC 1  // minimum waves per SIMD the register allocator must allow (launch bounds)
 #endif
-#ifndef AZ_C16_PF
-#define AZ_C16_PF 2  // k-steps of B fragments in flight ahead of their MFMAs
-#endif
 constexpr int kC16Pitch = 132;     // epilogue tile row pitch (floats)
 constexpr float kOverflow = 32752.f;  // |x| above this cannot be split (fp16 range)
 
@@ -104,7 +101,10 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
   // ---- B stream: k-step s of the executed sequence -> packed k-step
   const uint4* wl = wpack + (size_t)(wave * 2) * 2 * 64 + lane;
   auto pk_of = [&](int s) { return s < NK ? (s / CPT) * 4 + C0 + s % CPT : 36 + (s - NK); };
-  constexpr int PF = AZ_C16_PF, NB = PF + 1;
+  // k-steps of B fragments in flight ahead of their MFMAs: 3 for 64-row
+  // tiles (168 vs 177 us at 4096 boards), 2 below (deeper was no faster at
+  // 32/48 rows: profiles/r2/conv16_pf.txt)
+  constexpr int PF = MB >= 4 ? 3 : 2, NB = PF + 1;
   uint4 bq[NB][4];
   auto load_b = [&](int s, uint4 (&dst)[4]) {
     if (s >= NKR) return;

@@ -111,8 +111,8 @@ typedef struct az_chess_config {
     int64_t arena_edges;          /* edges per arena half per slot (0 = 96 * mcts_iterations) */
     int32_t conv_algo;            /* AZ_CONV_F16X2 (default) / AZ_CONV_DIRECT: the tower and the
                                      stem over the 118 planes zero-padded to 128 */
-    int32_t lanes;                /* slot groups searched on separate HIP streams (0 = auto = 1);
-                                     results do not depend on it */
+    int32_t lanes;                /* slot groups searched on separate HIP streams (0 = auto: 2 from
+                                     128 slots, else 1); results do not depend on it */
     int32_t reserved[6];
 } az_chess_config;
 
