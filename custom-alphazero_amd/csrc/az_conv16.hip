@@ -76,6 +76,17 @@ __device__ __forceinline__ h8 unscale_b0(const uint4 v) {
   return b * (_Float16)0.000244140625f;
 }
 
+#ifdef AZ_C16_STAMPS  // diagnostic build only (profiles/micro/conv16_bench.cpp): phase clocks per tile
+__device__ unsigned long long g_c16_stamps[8192][6];
+#define C16_STAMP(k)                                                    \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {                          \
+    g_c16_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();          \
+    if ((k) == 0 || (k) == 3) g_c16_stamps[blockIdx.x][4 + ((k) == 3)] = __builtin_amdgcn_s_memrealtime(); \
+  }
+#else
+#define C16_STAMP(k)
+#endif
+
 template <int MB, bool RES, bool HEADS, int C0>
 __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     const uint4* __restrict__ in, const uint4* __restrict__ res_in, const uint4* __restrict__ wpack,
@@ -94,6 +105,7 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
   const int rows = n_boards * HW;
   const int row0 = blockIdx.x * TR;
   if (row0 >= rows) return;  // block-uniform
+  C16_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int slab_rows = TR + 2 * halo;  // + the zero row at index slab_rows
   const int zrow = slab_rows;
@@ -142,6 +154,7 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     }
   }
   __syncthreads();  // (its fence waits for the DMA)
+  C16_STAMP(1);
 
   // ---- per lane: the MB M blocks' pixels
   const int nq = wave;
@@ -303,6 +316,7 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     }
     return;
   }
+  C16_STAMP(2);
   // ---- epilogue: BN bias (+ residual's) + ReLU into an fp32 tile in LDS,
   // then split16 rows (a wave's accumulators hold 16-row column strips; the
   // tile turns them into 512-B row stores)
@@ -338,6 +352,7 @@ __global__ __launch_bounds__(256, AZ_C16_OCC) void conv16_kernel(
     out[(size_t)g * 32 + q] = t0;
     out[(size_t)g * 32 + 16 + q] = t1;
   }
+  C16_STAMP(3);
 }
 
 size_t conv16_lds_bytes(int MB, int W, bool res) {

@@ -168,6 +168,25 @@ int main(int argc, char** argv) {
   float ms = 0;
   CK(hipEventElapsedTime(&ms, t0, t1));
   const double us = 1e3 * ms / iters;
+#ifdef AZ_C16_STAMPS
+  {  // phase clocks of the last launch per tile: prologue (slab DMA), K loop, epilogue; shader clock
+    static unsigned long long st[8192][6];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(az::g_c16_stamps), sizeof(st)));
+    double ph[3] = {0, 0, 0}, clk = 0, t0 = 1e300, t1 = 0;
+    int n = 0;
+    for (int w = 0; w < 8192; ++w) {
+      if (!st[w][0] || st[w][3] < st[w][0] || st[w][5] <= st[w][4]) continue;
+      ++n;
+      for (int k = 0; k < 3; ++k) ph[k] += (double)(st[w][k + 1] - st[w][k]);
+      clk += (double)(st[w][3] - st[w][0]) / (double)(st[w][5] - st[w][4]) * 0.1;  // GHz (realtime 100 MHz)
+      t0 = std::min(t0, (double)st[w][4]);
+      t1 = std::max(t1, (double)st[w][5]);
+    }
+    if (n)
+      fprintf(stderr, "stamps: %d tiles, mean cycles prologue %.0f loop %.0f epilogue %.0f, clock %.2f GHz, "
+              "first start to last end %.1f us\n", n, ph[0] / n, ph[1] / n, ph[2] / n, clk / n, (t1 - t0) / 100.0);
+  }
+#endif
   const int nks = res ? 40 : 36;
   const double issued = (double)rows * F * 32.0 * nks * 2 * 3;         // fp16 MFMA FLOP issued
   const double direct = (double)rows * F * F * 2 * (9 + (res ? 1 : 0));  // algorithmic
