@@ -7,7 +7,9 @@ simulations per move, 4096 concurrent games per GPU, random-init
 A "step" is one move for every game slot: `sims` lockstep simulations
 (select -> batched network forward -> expand/backup), a move commit, and
 the D2H copy of the games that finished (az_selfplay_drain: a game counts
-when its samples are on the host).  Finished games are
+when its samples are on the host) -- in the timed window the
+drain of move m-1 overlaps move m, and the window ends with a synchronize
+and a last drain.  Finished games are
 replaced by new ones (game g seeded MT19937(g)).
 
 Steady state, whatever --warmup says: all slots start at ply 0 together
@@ -472,9 +474,17 @@ def main():
     t0 = time.perf_counter()
     drained = 0
     for _ in range(args.steps):
-        _, k = step_and_drain(eng, window)
-        drained += k
+        # enqueue move m, then copy to the host the games finished by move m-1
+        # (az_selfplay_drain waits for move m-1's count snapshot, never for
+        # the running move: the GPU stays busy across move boundaries)
+        eng.selfplay_step(1, sync=False)
+        d = eng.selfplay_drain()
+        window.add(d)
+        drained += len(d["lengths"])
     torch.cuda.synchronize()
+    d = eng.selfplay_drain()  # the window's last moves' games, still inside the timed region
+    window.add(d)
+    drained += len(d["lengths"])
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -631,7 +641,8 @@ def main():
                              f"turned over {CACHE_TURNOVER_GENS} eviction generations (stationary hit rate)"),
             "games_timed": int(drained_all),
             "games_timed_basis": "games whose samples reached the host in the window (az_selfplay_drain "
-                                 "after every step, D2H inside the timed region)",
+                                 "after every step -- the previous move's games while the next move runs "
+                                 "-- and once more after the final synchronize; D2H inside the timed region)",
             "games_finished_on_device": int(games_all),
             "expansions_per_s": round(exp_all / elapsed, 1),
             "simulations_per_s": round(sims_all / elapsed, 1),

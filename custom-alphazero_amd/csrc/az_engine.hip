@@ -92,6 +92,14 @@ struct az_engine {
   int64_t drained = 0;             // finished games az_selfplay_drain has returned
   uint8_t* drain_dev = nullptr;    // packed records (device) and their pinned host copy
   uint8_t* drain_host = nullptr;
+  // games-finished count at the end of every move (smp.done_count copied on
+  // snap_stream once every lane has played the move): the drain packs up to a
+  // completed snapshot on pack_stream, so it never waits for the move that is
+  // running (az_selfplay_step without stats returns without a sync)
+  hipStream_t snap_stream = nullptr, pack_stream = nullptr;
+  hipEvent_t snap_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  unsigned long long* snap_host = nullptr;  // [4] pinned, move m in slot m % 4
+  int64_t batch_first_move = 0;             // moves_issued at az_selfplay_begin
   size_t drain_cap = 0;            // records the two buffers hold
 
   template <typename T>
@@ -185,6 +193,8 @@ int simulate(az_engine* e, Lane& L) {
 int sync_all(az_engine* e) {
   AZ_HIP(hipStreamSynchronize(e->stream));
   for (hipStream_t s : e->lane_streams) AZ_HIP(hipStreamSynchronize(s));
+  if (e->snap_stream) AZ_HIP(hipStreamSynchronize(e->snap_stream));
+  if (e->pack_stream) AZ_HIP(hipStreamSynchronize(e->pack_stream));
   return 0;
 }
 
@@ -616,6 +626,17 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
           return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
     }
   }
+  if (nl == 1)
+    for (hipEvent_t& ev : e->whole.move_done)
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+        return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
+  if (hipStreamCreateWithFlags(&e->snap_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->pack_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(&e->snap_host, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+    return cleanup(fail(AZ_E_HIP, "drain stream setup failed"));
+  for (hipEvent_t& ev : e->snap_ev)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
   e->net.hidden = c.value_hidden;
   *out = e;
   return 0;
@@ -629,11 +650,22 @@ int az_engine_destroy(az_engine* eng) {
     (void)hipStreamSynchronize(s);
     (void)hipStreamDestroy(s);
   }
+  for (hipStream_t s : {eng->snap_stream, eng->pack_stream})
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  for (hipEvent_t ev : eng->snap_ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (eng->snap_host) (void)hipHostFree(eng->snap_host);
   for (Lane* L : eng->lanes) {
     for (hipEvent_t ev : L->move_done)
       if (ev) (void)hipEventDestroy(ev);
     if (L != &eng->whole) delete L;
   }
+  if (eng->lanes.size() > 1)
+    for (hipEvent_t ev : eng->whole.move_done)
+      if (ev) (void)hipEventDestroy(ev);
   if (eng->drain_dev) (void)hipFree(eng->drain_dev);
   if (eng->drain_host) (void)hipHostFree(eng->drain_host);
   for (void* p : eng->sample_bufs) (void)hipFree(p);
@@ -845,6 +877,7 @@ int az_selfplay_begin(az_engine* e, int64_t first_game, int64_t n_games, uint32_
       (rc = get((void**)&smp.done_count, sizeof(unsigned long long))))
     return rc;
   e->drained = 0;
+  e->batch_first_move = e->moves_issued;
   unsigned long long st[az::kStatCount] = {0};
   const int64_t first_wave = std::min<int64_t>(n_games, e->g.slots);
   st[az::kStatNextGame] = (unsigned long long)(first_game + first_wave);
@@ -876,16 +909,22 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
       for (Lane* L : e->lanes)
         if ((rc = simulate(e, *L))) return rc;
     for (Lane* L : e->lanes) {
+      // move m's games may finish only after move m-1's count snapshot exists
+      if (m > e->batch_first_move) AZ_HIP(hipStreamWaitEvent(L->stream, e->snap_ev[(m - 1) % 4], 0));
       az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
       az::launch_compact(L->g, L->t, L->stream);
-      if (multi) AZ_HIP(hipEventRecord(L->move_done[m % 3], L->stream));
+      AZ_HIP(hipEventRecord(L->move_done[m % 3], L->stream));
     }
+    for (Lane* L : e->lanes) AZ_HIP(hipStreamWaitEvent(e->snap_stream, L->move_done[m % 3], 0));
+    AZ_HIP(hipMemcpyAsync(e->snap_host + m % 4, e->smp.done_count, sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, e->snap_stream));
+    AZ_HIP(hipEventRecord(e->snap_ev[m % 4], e->snap_stream));
     AZ_HIP(hipGetLastError());
   }
+  if (!st) return 0;  // asynchronous: the moves run on while the caller drains earlier ones
   if ((rc = sync_all(e))) return rc;
   if ((rc = check_device_errors(e))) return rc;
-  if (st) return az_stats_get(e, st);
-  return 0;
+  return az_stats_get(e, st);
 }
 
 int az_selfplay_run(az_engine* e, int64_t first_game, int64_t n_games, uint32_t base_seed,
@@ -933,10 +972,18 @@ int az_selfplay_drain(az_engine* e, int64_t max_games, int64_t* n_out, int64_t* 
   *n_out = 0;
   if (!e->smp.done_count) return 0;  // no self-play batch begun
   AZ_HIP(hipSetDevice(e->device));
-  int rc;
-  if ((rc = sync_all(e))) return rc;
-  unsigned long long done = 0;
-  AZ_HIP(hipMemcpy(&done, e->smp.done_count, sizeof(done), hipMemcpyDeviceToHost));
+  // the newest move whose count snapshot is complete; if the last issued
+  // move is still running, wait for the one before it (never for the running one)
+  const int64_t last = e->moves_issued - 1;
+  int64_t k = -1;
+  if (last >= e->batch_first_move && hipEventQuery(e->snap_ev[last % 4]) == hipSuccess) {
+    k = last;
+  } else if (last - 1 >= e->batch_first_move) {
+    k = last - 1;
+    AZ_HIP(hipEventSynchronize(e->snap_ev[k % 4]));
+  }
+  if (k < 0) return 0;
+  const unsigned long long done = e->snap_host[k % 4];
   const int64_t n = std::min<int64_t>((int64_t)done - e->drained, max_games);
   if (n <= 0) return 0;
   const size_t rec = az::drain_record_bytes(e->g);
@@ -951,10 +998,12 @@ int az_selfplay_drain(az_engine* e, int64_t max_games, int64_t* n_out, int64_t* 
     AZ_HIP(hipHostMalloc(&e->drain_host, cap * rec, hipHostMallocDefault));
     e->drain_cap = cap;
   }
-  az::launch_drain_pack(e->g, e->smp, e->drained, (int)n, e->drain_dev, e->stream);
+  // pack_stream, ordered after snapshot k only: games up to move k are complete
+  AZ_HIP(hipStreamWaitEvent(e->pack_stream, e->snap_ev[k % 4], 0));
+  az::launch_drain_pack(e->g, e->smp, e->drained, (int)n, e->drain_dev, e->pack_stream);
   AZ_HIP(hipGetLastError());
-  AZ_HIP(hipMemcpyAsync(e->drain_host, e->drain_dev, (size_t)n * rec, hipMemcpyDeviceToHost, e->stream));
-  AZ_HIP(hipStreamSynchronize(e->stream));
+  AZ_HIP(hipMemcpyAsync(e->drain_host, e->drain_dev, (size_t)n * rec, hipMemcpyDeviceToHost, e->pack_stream));
+  AZ_HIP(hipStreamSynchronize(e->pack_stream));
   const size_t HW = (size_t)e->g.HW, A = (size_t)e->g.A;
   for (int64_t i = 0; i < n; ++i) {
     const uint8_t* r = e->drain_host + (size_t)i * rec;

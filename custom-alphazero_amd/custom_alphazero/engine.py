@@ -264,7 +264,15 @@ class Engine:
                                          int(base_seed) & 0xFFFFFFFF))
         self._n_games = int(n_games)
 
-    def selfplay_step(self, n_moves=1):
+    def selfplay_step(self, n_moves=1, sync=True):
+        """Enqueue n_moves moves for every slot.  sync=False returns at once
+        (no stats): the moves run while the caller drains earlier ones --
+        selfplay_drain then returns the games of the newest move whose
+        snapshot is complete and waits at most for the move before the
+        running one (az_selfplay_step with st = NULL)."""
+        if not sync:
+            _check(self._L.az_selfplay_step(self._h, int(n_moves), None))
+            return None
         st = Stats()
         _check(self._L.az_selfplay_step(self._h, int(n_moves), ctypes.byref(st)))
         return st.as_dict()

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 3
+#define AZ_ABI_VERSION 4
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
@@ -134,7 +134,9 @@ int az_forward(az_engine* eng, const float* x, int n, float* probs, float* value
  * first_game .. first_game+n_games-1, game g seeded with MT19937(base_seed+g)
  * (the reference seeds np.random per game, self_play.py:45), slots refilled
  * as games end.  begin+step lets a caller time a window of moves; run does
- * begin + steps until every game is done. */
+ * begin + steps until every game is done.  step with st = NULL only enqueues
+ * the moves and returns (no synchronize, device errors surface at the next
+ * synchronizing call); with st it waits for them and fills the stats. */
 int az_selfplay_begin(az_engine* eng, int64_t first_game, int64_t n_games, uint32_t base_seed);
 int az_selfplay_step(az_engine* eng, int n_moves, az_stats* st);
 int az_selfplay_run(az_engine* eng, int64_t first_game, int64_t n_games, uint32_t base_seed,
@@ -151,7 +153,11 @@ int az_selfplay_results(az_engine* eng, int32_t* lengths, int32_t* results, int3
  * self_play.py:112-118, one step at a time).  *n_out = games copied; per game
  * i: game_ids[i], lengths/results/expansions[i] as az_selfplay_results,
  * boards [i][H*W][H][W] int8, policies [i][H*W][A] f64, moves [i][H*W]
- * (rows past the game's length are zero).  Any output but n_out may be NULL. */
+ * (rows past the game's length are zero).  Any output but n_out may be NULL.
+ * "Finished" = by the end of the newest move whose games-finished snapshot is
+ * complete; if the last enqueued move is still running the drain waits for
+ * the move before it, never for the running one (after a synchronizing step
+ * or a device synchronize, every finished game). */
 int az_selfplay_drain(az_engine* eng, int64_t max_games, int64_t* n_out, int64_t* game_ids,
                       int32_t* lengths, int32_t* results, int32_t* expansions, int8_t* boards,
                       double* policies, int32_t* moves);

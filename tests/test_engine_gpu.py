@@ -181,6 +181,41 @@ def test_drain_returns_every_game_once(lanes):
     assert len(eng.selfplay_drain()["lengths"]) == 0
 
 
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_async_steps_drain_every_game_once(lanes):
+    """selfplay_step(sync=False) returns without waiting; each drain returns the
+    games of the newest move whose count snapshot is complete (never waiting
+    for the running move), and after a synchronize the rest: every game once,
+    records identical to az_selfplay_results, and the same games as a
+    synchronous run of the batch."""
+    import torch
+    def run(sync):
+        eng = az.Engine(6, 7, 4, True, 20, slots=40, evaluator=az.EVAL_SYNTHETIC, cache_log2=12, lanes=lanes,
+                        compact=True)
+        eng.selfplay_begin(100, 150, 5)
+        parts = []
+        for _ in range(200):  # more moves than any game needs; idle slots just skip
+            eng.selfplay_step(1, sync=sync)
+            parts.append(eng.selfplay_drain())
+        torch.cuda.synchronize()
+        parts.append(eng.selfplay_drain())
+        parts.append(eng.selfplay_drain())  # nothing left
+        assert len(parts[-1]["lengths"]) == 0
+        return eng, {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    eng_a, got = run(False)
+    assert sorted(got["game_ids"].tolist()) == list(range(100, 250))
+    ref = eng_a.selfplay_results()
+    order = np.argsort(got["game_ids"])
+    gi = got["game_ids"][order] - 100
+    for k in ("lengths", "results", "expansions", "moves", "boards"):
+        np.testing.assert_array_equal(got[k][order], ref[k][gi], err_msg=k)
+    np.testing.assert_array_equal(got["policies"][order].view(np.uint64), ref["policies"][gi].view(np.uint64))
+    _, got_s = run(True)
+    order_s = np.argsort(got_s["game_ids"])
+    for k in ("lengths", "results", "expansions", "moves", "boards"):
+        np.testing.assert_array_equal(got[k][order], got_s[k][order_s], err_msg=k)
+
+
 def test_pow_table_is_python_pow(golden):
     z = golden("numerics")
     eng = az.Engine(6, 7, 4, True, 100, slots=1, evaluator=az.EVAL_SYNTHETIC,
