@@ -61,7 +61,7 @@ struct Lane {
   float* values = nullptr;
   az::ConvTimer timer;
   az::ConvTimer tree_timer;  // select and expand launches (bench.py roofline_tree)
-  hipEvent_t move_done[3] = {nullptr, nullptr, nullptr};  // end of move m on this lane, m mod 3
+  hipEvent_t move_done[4] = {nullptr, nullptr, nullptr, nullptr};  // end of move m on this lane, m mod 4
 };
 
 struct az_engine {
@@ -92,13 +92,19 @@ struct az_engine {
   int64_t drained = 0;             // finished games az_selfplay_drain has returned
   uint8_t* drain_dev = nullptr;    // packed records (device) and their pinned host copy
   uint8_t* drain_host = nullptr;
-  // games-finished count at the end of every move (smp.done_count copied on
-  // snap_stream once every lane has played the move): the drain packs up to a
-  // completed snapshot on pack_stream, so it never waits for the move that is
-  // running (az_selfplay_step without stats returns without a sync)
-  hipStream_t snap_stream = nullptr, pack_stream = nullptr;
-  hipEvent_t snap_ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  unsigned long long* snap_host = nullptr;  // [4] pinned, move m in slot m % 4
+  // games-finished count at the end of every move: the last lane to finish
+  // move m stores smp.done_count into snap_host[m % 4] (move_end_kernel), and
+  // the drain packs up to a completed snapshot on pack_stream, so it never
+  // waits for the move that is running (az_selfplay_step without stats returns
+  // without a sync).  No stream of its own: HIP maps streams onto 4 hardware
+  // queues per process (GPU_MAX_HW_QUEUES), and a snapshot or pack stream
+  // sharing a lane's queue runs behind that lane's queued moves -- with two
+  // lanes the pack uses `stream`, idle while moves run.
+  hipStream_t pack_stream = nullptr;
+  bool own_pack_stream = false;
+  int32_t* move_arrive = nullptr;           // [4] lanes done with move m, slot m % 4
+  unsigned long long* snap_host = nullptr;  // [4] pinned coherent, move m in slot m % 4
+  unsigned long long* snap_dev = nullptr;   // snap_host's device address
   int64_t batch_first_move = 0;             // moves_issued at az_selfplay_begin
   size_t drain_cap = 0;            // records the two buffers hold
 
@@ -193,8 +199,7 @@ int simulate(az_engine* e, Lane& L) {
 int sync_all(az_engine* e) {
   AZ_HIP(hipStreamSynchronize(e->stream));
   for (hipStream_t s : e->lane_streams) AZ_HIP(hipStreamSynchronize(s));
-  if (e->snap_stream) AZ_HIP(hipStreamSynchronize(e->snap_stream));
-  if (e->pack_stream) AZ_HIP(hipStreamSynchronize(e->pack_stream));
+  if (e->own_pack_stream) AZ_HIP(hipStreamSynchronize(e->pack_stream));
   return 0;
 }
 
@@ -630,13 +635,21 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
     for (hipEvent_t& ev : e->whole.move_done)
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
         return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
-  if (hipStreamCreateWithFlags(&e->snap_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->pack_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc(&e->snap_host, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
-    return cleanup(fail(AZ_E_HIP, "drain stream setup failed"));
-  for (hipEvent_t& ev : e->snap_ev)
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
-      return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
+  // drain: one lane runs on `stream`, so the pack needs a stream of its own;
+  // with more lanes `stream` is idle while moves run
+  e->own_pack_stream = nl == 1;
+  if (e->own_pack_stream) {
+    if (hipStreamCreateWithFlags(&e->pack_stream, hipStreamNonBlocking) != hipSuccess)
+      return cleanup(fail(AZ_E_HIP, "hipStreamCreate failed"));
+  } else {
+    e->pack_stream = e->stream;
+  }
+  if ((rc = e->alloc(&e->move_arrive, 4))) return cleanup(rc);
+  if (hipMemset(e->move_arrive, 0, 4 * sizeof(int32_t)) != hipSuccess ||
+      hipHostMalloc(&e->snap_host, 4 * sizeof(unsigned long long), hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&e->snap_dev, e->snap_host, 0) != hipSuccess)
+    return cleanup(fail(AZ_E_HIP, "drain snapshot setup failed"));
+  for (int i = 0; i < 4; ++i) e->snap_host[i] = 0;
   e->net.hidden = c.value_hidden;
   *out = e;
   return 0;
@@ -650,13 +663,10 @@ int az_engine_destroy(az_engine* eng) {
     (void)hipStreamSynchronize(s);
     (void)hipStreamDestroy(s);
   }
-  for (hipStream_t s : {eng->snap_stream, eng->pack_stream})
-    if (s) {
-      (void)hipStreamSynchronize(s);
-      (void)hipStreamDestroy(s);
-    }
-  for (hipEvent_t ev : eng->snap_ev)
-    if (ev) (void)hipEventDestroy(ev);
+  if (eng->own_pack_stream && eng->pack_stream) {
+    (void)hipStreamSynchronize(eng->pack_stream);
+    (void)hipStreamDestroy(eng->pack_stream);
+  }
   if (eng->snap_host) (void)hipHostFree(eng->snap_host);
   for (Lane* L : eng->lanes) {
     for (hipEvent_t ev : L->move_done)
@@ -852,7 +862,7 @@ int az_selfplay_begin(az_engine* e, int64_t first_game, int64_t n_games, uint32_
   int rc;
   if ((rc = ready_to_search(e))) return rc;
   AZ_HIP(hipSetDevice(e->device));
-  AZ_HIP(hipStreamSynchronize(e->stream));
+  if ((rc = sync_all(e))) return rc;  // moves of an earlier batch may still be running (async steps)
   for (void* p : e->sample_bufs) (void)hipFree(p);
   e->sample_bufs.clear();
   az::SampleDev& smp = e->smp;
@@ -898,27 +908,24 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
   const bool multi = e->lanes.size() > 1;
   for (int mv = 0; mv < n_moves; ++mv) {
     const int64_t m = e->moves_issued++;
-    // a lane starts move m once every other lane has finished move m - 2:
-    // lanes drift at most two moves apart (the cache eviction bound, az_tree.h)
-    if (multi && m >= 2)
-      for (Lane* L : e->lanes)
-        for (Lane* O : e->lanes)
-          if (O != L) AZ_HIP(hipStreamWaitEvent(L->stream, O->move_done[(m - 2) % 3], 0));
     // lanes interleaved per simulation so every stream always has work queued
     for (int s = 0; s < e->g.sims; ++s)
       for (Lane* L : e->lanes)
         if ((rc = simulate(e, *L))) return rc;
     for (Lane* L : e->lanes) {
-      // move m's games may finish only after move m-1's count snapshot exists
-      if (m > e->batch_first_move) AZ_HIP(hipStreamWaitEvent(L->stream, e->snap_ev[(m - 1) % 4], 0));
+      // a lane plays move m once every other lane has finished move m - 1, so
+      // move m - 1's snapshot (taken by the last of them) holds no game of
+      // move m; it also keeps the lanes within two moves of each other (the
+      // cache eviction bound, az_tree.h)
+      if (multi && m > e->batch_first_move)
+        for (Lane* O : e->lanes)
+          if (O != L) AZ_HIP(hipStreamWaitEvent(L->stream, O->move_done[(m - 1) % 4], 0));
       az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
       az::launch_compact(L->g, L->t, L->stream);
-      AZ_HIP(hipEventRecord(L->move_done[m % 3], L->stream));
+      az::launch_move_end(e->move_arrive + m % 4, (int)e->lanes.size(), e->smp.done_count,
+                          e->snap_dev + m % 4, L->stream);
+      AZ_HIP(hipEventRecord(L->move_done[m % 4], L->stream));
     }
-    for (Lane* L : e->lanes) AZ_HIP(hipStreamWaitEvent(e->snap_stream, L->move_done[m % 3], 0));
-    AZ_HIP(hipMemcpyAsync(e->snap_host + m % 4, e->smp.done_count, sizeof(unsigned long long),
-                          hipMemcpyDeviceToHost, e->snap_stream));
-    AZ_HIP(hipEventRecord(e->snap_ev[m % 4], e->snap_stream));
     AZ_HIP(hipGetLastError());
   }
   if (!st) return 0;  // asynchronous: the moves run on while the caller drains earlier ones
@@ -974,16 +981,20 @@ int az_selfplay_drain(az_engine* e, int64_t max_games, int64_t* n_out, int64_t* 
   AZ_HIP(hipSetDevice(e->device));
   // the newest move whose count snapshot is complete; if the last issued
   // move is still running, wait for the one before it (never for the running one)
+  // (a move's snapshot is complete once every lane has finished the move)
   const int64_t last = e->moves_issued - 1;
   int64_t k = -1;
-  if (last >= e->batch_first_move && hipEventQuery(e->snap_ev[last % 4]) == hipSuccess) {
+  bool last_done = last >= e->batch_first_move;
+  if (last_done)
+    for (Lane* L : e->lanes) last_done = last_done && hipEventQuery(L->move_done[last % 4]) == hipSuccess;
+  if (last_done) {
     k = last;
   } else if (last - 1 >= e->batch_first_move) {
     k = last - 1;
-    AZ_HIP(hipEventSynchronize(e->snap_ev[k % 4]));
+    for (Lane* L : e->lanes) AZ_HIP(hipEventSynchronize(L->move_done[k % 4]));
   }
   if (k < 0) return 0;
-  const unsigned long long done = e->snap_host[k % 4];
+  const unsigned long long done = __atomic_load_n(e->snap_host + k % 4, __ATOMIC_ACQUIRE);
   const int64_t n = std::min<int64_t>((int64_t)done - e->drained, max_games);
   if (n <= 0) return 0;
   const size_t rec = az::drain_record_bytes(e->g);
@@ -998,8 +1009,8 @@ int az_selfplay_drain(az_engine* e, int64_t max_games, int64_t* n_out, int64_t* 
     AZ_HIP(hipHostMalloc(&e->drain_host, cap * rec, hipHostMallocDefault));
     e->drain_cap = cap;
   }
-  // pack_stream, ordered after snapshot k only: games up to move k are complete
-  AZ_HIP(hipStreamWaitEvent(e->pack_stream, e->snap_ev[k % 4], 0));
+  // pack_stream (nothing else queued on it; the host has seen move k finish
+  // on every lane): games up to move k are complete
   az::launch_drain_pack(e->g, e->smp, e->drained, (int)n, e->drain_dev, e->pack_stream);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipMemcpyAsync(e->drain_host, e->drain_dev, (size_t)n * rec, hipMemcpyDeviceToHost, e->pack_stream));

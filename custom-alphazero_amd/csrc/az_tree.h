@@ -152,6 +152,10 @@ AZ_HD Edge* slot_edges(const GameCfg& g, const TreeDev& t, int s) {
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s);
 // self-play tree reuse (halves == 2): the new root's subtree into the other half
 void launch_compact(const GameCfg& g, const TreeDev& t, hipStream_t s);
+// end of a lane's move: the last of n_lanes lanes to arrive stores the
+// games-finished count into *snap (pinned host memory) and resets *arrive
+void launch_move_end(int32_t* arrive, int n_lanes, const unsigned long long* done_count,
+                     unsigned long long* snap, hipStream_t s);
 // cache on: misses are deduplicated inside select (step tag table); this
 // resolves the ones whose tag matched, by full-board compare
 void launch_dedup_resolve(const GameCfg& g, const TreeDev& t, hipStream_t s);

@@ -773,6 +773,24 @@ void launch_compact(const GameCfg& g, const TreeDev& t, hipStream_t s) {
   if (g.halves > 1 && g.slots > 0) compact_kernel<<<g.slots, 64, 0, s>>>(g, t);
 }
 
+// Every lane's play kernel for move m + 1 waits for the other lanes' move m
+// (az_engine.hip), so when the last lane arrives here no game of move m + 1
+// has been appended: done_count is exactly the games finished by move m.
+__global__ void move_end_kernel(int32_t* arrive, int n_lanes, const unsigned long long* done_count,
+                                unsigned long long* snap) {
+  if (threadIdx.x != 0) return;
+  const int prev = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev != n_lanes - 1) return;
+  __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long d = __hip_atomic_load(done_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(snap, d, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_move_end(int32_t* arrive, int n_lanes, const unsigned long long* done_count,
+                     unsigned long long* snap, hipStream_t s) {
+  move_end_kernel<<<1, 64, 0, s>>>(arrive, n_lanes, done_count, snap);
+}
+
 void launch_slot_init(const GameCfg& g, const TreeDev& t, const SampleDev& smp, int64_t n_first,
                       hipStream_t s) {
   slot_init_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t, smp, n_first);

@@ -36,4 +36,5 @@ for q, iv in sorted(by.items(), key=lambda x: -len(x[1])):
     for i in range(len(iv) - 1):
         after[iv[i + 1][2]].append(max(0, iv[i + 1][0] - iv[i][1]))
     for n, g in sorted(after.items(), key=lambda x: -sum(x[1]))[:8]:
-        print(f"      gap before {n:34s} mean {sum(g) / len(g) / 1e3:6.1f} us  x{len(g)}")
+        print(f"      gap before {n:34s} mean {sum(g) / len(g) / 1e3:6.1f} us  "
+              f"median {statistics.median(g) / 1e3:6.1f} us  x{len(g)}")
