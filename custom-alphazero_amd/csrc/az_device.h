@@ -36,8 +36,14 @@ struct Board {
   uint64_t opp[2];
 };
 
-AZ_HD bool bit(const uint64_t m[2], int c) { return (m[c >> 6] >> (c & 63)) & 1ull; }
-AZ_HD void set_bit(uint64_t m[2], int c) { m[c >> 6] |= 1ull << (c & 63); }
+// word chosen by a select, not by indexing: a dynamically indexed two-word
+// array is moved to LDS by the compiler (a ds_read per tested cell)
+AZ_HD bool bit(const uint64_t m[2], int c) { return ((c < 64 ? m[0] : m[1]) >> (c & 63)) & 1ull; }
+AZ_HD void set_bit(uint64_t m[2], int c) {
+  const uint64_t v = 1ull << (c & 63);
+  m[0] |= c < 64 ? v : 0ull;
+  m[1] |= c < 64 ? 0ull : v;
+}
 AZ_HD bool empty_cell(const Board& b, int c) { return !bit(b.own, c) && !bit(b.opp, c); }
 
 // Action index -> landing cell (or -1 if illegal).  Action order is

@@ -128,6 +128,21 @@ __device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gi
 }
 
 // ------------------------------------------------------------------- select
+#ifdef AZ_SEL_STAMPS
+// diagnostic build (profiles/sel_stamps.py): per-slot 100 MHz wall-clock
+// stamps of the select phases, read back with az_diag_sel_stamps
+__device__ unsigned long long g_sel_stamps[16384][12];
+// (row: the slot's game_id address, unique across lanes for 16384 slots)
+#define AZ_SEL_ROW(s) ((((uintptr_t)(t.game_id + (s))) >> 3) & 16383)
+#define AZ_SEL_STAMP(s, k) (g_sel_stamps[AZ_SEL_ROW(s)][k] = wall_clock64())
+#define AZ_SEL_VALUE(s, k, v) (g_sel_stamps[AZ_SEL_ROW(s)][k] = (unsigned long long)(v))
+extern "C" int az_diag_sel_stamps(unsigned long long* out, int n_slots) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_stamps), (size_t)std::min(n_slots, 16384) * 96) == hipSuccess ? 0 : -1;
+}
+#else
+#define AZ_SEL_STAMP(s, k) ((void)0)
+#define AZ_SEL_VALUE(s, k, v) ((void)0)
+#endif
 // MCTS.select (mcts.py:111-120) + the terminal branch of MCTS.search
 // (mcts.py:176-180).  Non-terminal leaves are appended to the eval queue.
 __device__ __forceinline__ bool same_board(const Board& a, const Board& b) {
@@ -141,6 +156,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
                           const int32_t* path, int depth, int status, const Board& b) {
   wave_stat(t, kStatSims);
   wave_stat(t, kStatPathEdges, (unsigned)depth);
+  AZ_SEL_STAMP(s, 3);
   if (depth > 0 && status != kOngoing) {
     // get_result(keep_same_player=True): 1 for the player who just moved, 0 draw
     backup(E, path, depth, status == kWin ? 1.0 : 0.0);
@@ -151,6 +167,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   t.eval_slot[q] = s;
   t.eval_board[q] = b;
   t.path_len[s] = depth;
+  AZ_SEL_STAMP(s, 4);
   if (!c.enabled) {
     t.eval_src[q] = -(q + 1);
     wave_stat(t, kStatNNEvals);
@@ -174,12 +191,16 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
       if ((st & 3u) == kCacheReady && (st >> 16) == fp && cache_age(st, gen) < kCacheLiveGens &&
           same_board(c.keys[idx], b)) {
         t.eval_src[q] = (int32_t)idx;
+        AZ_SEL_STAMP(s, 5);
+        AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
         wave_stat(t, kStatCacheHits);
         return;
       }
       idx = (idx + 1) & c.mask;
     }
   }
+  AZ_SEL_STAMP(s, 5);
+  AZ_SEL_VALUE(s, 7, depth | (2 << 16) | ((uint64_t)s << 32));
   // miss: one evaluator row per distinct board in this simulation.  Tag =
   // (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
   // empty, so the table needs no clearing.  A tag match is only a candidate:
@@ -270,7 +291,25 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = gid / L, j = gid % L;
+#ifdef AZ_SEL_STAMPS
+  if (s < g.slots && j == 0) {
+    AZ_SEL_STAMP(s, 0);
+    for (int k = 1; k < 12; ++k) AZ_SEL_VALUE(s, k, 0);
+  }
+  // per-level phase sums (descent): edge data arrived, choice broadcast, play done
+  unsigned long long ph_load = 0, ph_reduce = 0, ph_play = 0, ph_t = 0;
+#define AZ_SEL_PHASE(acc)                   \
+  do {                                      \
+    __builtin_amdgcn_s_waitcnt(0);          \
+    const unsigned long long now_ = wall_clock64(); \
+    acc += now_ - ph_t;                     \
+    ph_t = now_;                            \
+  } while (0)
+#else
+#define AZ_SEL_PHASE(acc) ((void)0)
+#endif
   if (s >= g.slots || t.game_id[s] < 0) return;  // whole groups leave together
+  if (j == 0) AZ_SEL_STAMP(s, 1);
   Edge* E = slot_edges(g, t, s);
   int32_t* path = t.path + (size_t)s * g.max_depth;
   Board b = t.root_board[s];
@@ -282,6 +321,9 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
   // level instead of two
   int sum_next = -1;
   while (cnt > 0) {
+#ifdef AZ_SEL_STAMPS
+    ph_t = wall_clock64();
+#endif
     const bool mine = j < cnt;
     double sq;
     int sum;
@@ -305,6 +347,7 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
       }
       sq = t.powtab[sum];
     }
+    AZ_SEL_PHASE(ph_load);
     double best_v = -INFINITY;
     int best = L;
     if (mine) {
@@ -330,9 +373,11 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
     const int child = __shfl(mine ? e.child : 0, best, L);
     const int child_n = __shfl(mine ? (int)e.child_n : 0, best, L);
     sum_next = __shfl(mine ? e.N : 0, best, L) - 1;
+    AZ_SEL_PHASE(ph_reduce);
     if (j == 0) path[depth] = first + best;
     ++depth;
     status = play(g, b, action);
+    AZ_SEL_PHASE(ph_play);
     if (status < 0) {
       if (j == 0) flag_error(t, kErrIllegal);
       return;
@@ -340,7 +385,14 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
     first = child;
     cnt = child_n;
   }
-  if (j == 0) leaf_tail(g, t, c, s, E, path, depth, status, b);
+  if (j == 0) {
+    AZ_SEL_STAMP(s, 2);
+    AZ_SEL_VALUE(s, 8, ph_load);
+    AZ_SEL_VALUE(s, 9, ph_reduce);
+    AZ_SEL_VALUE(s, 10, ph_play);
+    leaf_tail(g, t, c, s, E, path, depth, status, b);
+    AZ_SEL_STAMP(s, 6);
+  }
 }
 
 // ----------------------------------------------------------- dedup resolve

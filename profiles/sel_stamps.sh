@@ -1,0 +1,9 @@
+#!/bin/bash
+# select_group phase stamps (diagnostic build profiles/ab_libs/selst), network and synthetic evaluators
+set -o pipefail
+mkdir -p gpurun_out/sel_stamps
+export AZ_LIB_PATH=$PWD/profiles/ab_libs/selst/libaz.so
+
+
+timeout -k 10 300 python3 profiles/sel_stamps.py --synth > gpurun_out/sel_stamps/synth.txt 2>&1 || { tail gpurun_out/sel_stamps/synth.txt; exit 1; }
+cat gpurun_out/sel_stamps/synth.txt
