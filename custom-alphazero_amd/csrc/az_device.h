@@ -126,6 +126,90 @@ AZ_HD int play(const GameCfg& g, Board& b, int a) {
   return status;
 }
 
+// Board.play as bitboard arithmetic (the select descent's hot path): the same
+// status and board as play() for every board the search reaches.  The win
+// test runs over the whole board: a position the search plays from is never
+// terminal, so the mover had no n-in-a-row before the stone, and any run
+// after it passes through the new stone -- exactly play()'s test.  With
+// gravity a column's empty cells are its top rows, so the landing row is the
+// column's empty count minus one (action_cell's scan from the top).
+struct M128 {
+  uint64_t lo, hi;
+};
+AZ_HD M128 m_or(M128 a, M128 b) { return {a.lo | b.lo, a.hi | b.hi}; }
+AZ_HD M128 m_and(M128 a, M128 b) { return {a.lo & b.lo, a.hi & b.hi}; }
+AZ_HD M128 m_shl(M128 x, int k) {  // bit p + k of the result = bit p of x, 0 <= k < 128
+  if (k == 0) return x;
+  if (k >= 64) return {0ull, x.lo << (k - 64)};
+  return {x.lo << k, (x.hi << k) | (x.lo >> (64 - k))};
+}
+AZ_HD M128 m_shr(M128 x, int k) {  // bit p of the result = bit p + k of x
+  if (k == 0) return x;
+  if (k >= 64) return {x.hi >> (k - 64), 0ull};
+  return {(x.lo >> k) | (x.hi << (64 - k)), x.hi >> k};
+}
+AZ_HD int m_popc(M128 x) { return __builtin_popcountll(x.lo) + __builtin_popcountll(x.hi); }
+
+// per-configuration masks: column 0, cells that start a run of n to the right
+// (x <= W - n), cells that start one to the left (x >= n - 1), the top row
+struct BoardMasks {
+  M128 col0, left, right, top;
+};
+AZ_HD BoardMasks board_masks(const GameCfg& g) {
+  BoardMasks mk{{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+  for (int y = 0; y < g.H; ++y) mk.col0 = m_or(mk.col0, m_shl({1ull, 0ull}, y * g.W));
+  for (int x = 0; x < g.W; ++x) {
+    const M128 cx = m_shl(mk.col0, x);
+    if (x <= g.W - g.n) mk.left = m_or(mk.left, cx);
+    if (x >= g.n - 1) mk.right = m_or(mk.right, cx);
+    mk.top = m_or(mk.top, m_shl({1ull, 0ull}, x));
+  }
+  return mk;
+}
+
+AZ_HD bool m_run(M128 own, M128 start, int step, int n) {  // n stones from a start cell, stride step
+  M128 m = m_and(own, start);
+  for (int i = 1; i < n; ++i) {
+    if (i * step >= kMaxCells) return false;  // the run would leave the 128 cells
+    m = m_and(m, m_shr(own, i * step));
+  }
+  return (m.lo | m.hi) != 0;
+}
+
+AZ_HD int play_bb(const GameCfg& g, const BoardMasks& mk, Board& b, int a) {
+  M128 occ{b.own[0] | b.opp[0], b.own[1] | b.opp[1]};
+  int c;
+  if (g.gravity) {
+    const M128 col = m_shl(mk.col0, a);
+    const int k = m_popc(m_and({~occ.lo, ~occ.hi}, col));
+    if (k == 0) return -1;
+    c = (k - 1) * g.W + a;
+  } else {
+    const int x = a / g.H, y = a % g.H;
+    c = y * g.W + x;
+    if (bit(b.own, c) || bit(b.opp, c)) return -1;
+  }
+  set_bit(b.own, c);
+  const M128 own{b.own[0], b.own[1]};
+  occ = m_or(occ, m_shl({1ull, 0ull}, c));
+  const M128 all{~0ull, ~0ull};
+  const bool win = m_run(own, mk.left, 1, g.n) || m_run(own, all, g.W, g.n) ||
+                   m_run(own, mk.left, g.W + 1, g.n) || m_run(own, mk.right, g.W - 1, g.n);
+  int status = kOngoing;
+  if (win) {
+    status = kWin;
+  } else if (g.gravity ? ((~occ.lo & mk.top.lo) | (~occ.hi & mk.top.hi)) == 0 : m_popc(occ) == g.HW) {
+    status = kDraw;
+  }
+  Board m;
+  m.own[0] = b.opp[0];
+  m.own[1] = b.opp[1];
+  m.opp[0] = b.own[0];
+  m.opp[1] = b.own[1];
+  b = m;
+  return status;
+}
+
 // ---------------------------------------------------------------- numerics
 // numpy float32 add.reduce = identity 0 + pairwise_sum (8 accumulators from
 // n >= 8, 128-element blocks).  normalize_probabilities (mcts/utils.py:4-16)

@@ -240,6 +240,7 @@ __global__ __launch_bounds__(64) void select_kernel(GameCfg g, TreeDev t, CacheD
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
+  const BoardMasks mk = board_masks(g);
   Edge* E = slot_edges(g, t, s);
   int32_t* path = t.path + (size_t)s * g.max_depth;
   Board b = t.root_board[s];
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(64) void select_kernel(GameCfg g, TreeDev t, CacheD
     }
     const Edge& e = E[first + best];
     path[depth++] = first + best;
-    status = play(g, b, e.action);
+    status = play_bb(g, mk, b, e.action);
     if (status < 0) {
       flag_error(t, kErrIllegal);
       return;
@@ -310,6 +311,7 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
 #endif
   if (s >= g.slots || t.game_id[s] < 0) return;  // whole groups leave together
   if (j == 0) AZ_SEL_STAMP(s, 1);
+  const BoardMasks mk = board_masks(g);
   Edge* E = slot_edges(g, t, s);
   int32_t* path = t.path + (size_t)s * g.max_depth;
   Board b = t.root_board[s];
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
     AZ_SEL_PHASE(ph_reduce);
     if (j == 0) path[depth] = first + best;
     ++depth;
-    status = play(g, b, action);
+    status = play_bb(g, mk, b, action);
     AZ_SEL_PHASE(ph_play);
     if (status < 0) {
       if (j == 0) flag_error(t, kErrIllegal);
