@@ -64,12 +64,31 @@ __device__ __forceinline__ void flag_error(const TreeDev& t, unsigned long long 
   atomicOr(t.stats + kStatErrors, f);
 }
 
-__device__ __forceinline__ void backup(Edge* E, const int32_t* path, int depth, double v) {
-  for (int d = depth - 1; d >= 0; --d) {
-    Edge& e = E[path[d]];
-    e.N += 1;
-    e.W += v;
-    v = -v;
+// MCTS.backup (mcts.py:163-168): N += 1, W += value along the path, the sign
+// flipping per level.  A path's edges are distinct, so eight levels at a time
+// issue their path and edge loads together instead of one dependent pair of
+// round trips per level (the same additions, so the same bits).
+__device__ __forceinline__ void backup(Edge* E, const int32_t* __restrict__ path, int depth, double v) {
+  constexpr int K = 8;
+  for (int d1 = depth; d1 > 0; d1 -= K) {
+    int id[K], n[K];
+    double w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < d1) id[k] = path[d1 - 1 - k];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < d1) {
+        n[k] = E[id[k]].N;
+        w[k] = E[id[k]].W;
+      }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < d1) {
+        E[id[k]].N = n[k] + 1;
+        E[id[k]].W = w[k] + v;
+        v = -v;
+      }
   }
 }
 
@@ -322,6 +341,10 @@ __global__ __launch_bounds__(64) void select_group_kernel(GameCfg g, TreeDev t, 
   // children's edges arrive instead of after them: one dependent load per
   // level instead of two
   int sum_next = -1;
+#ifdef AZ_SEL_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  if (j == 0) AZ_SEL_STAMP(s, 11);  // root loads done, loop entry
+#endif
   while (cnt > 0) {
 #ifdef AZ_SEL_STAMPS
     ph_t = wall_clock64();
