@@ -38,3 +38,9 @@ for q, iv in sorted(by.items(), key=lambda x: -len(x[1])):
     for n, g in sorted(after.items(), key=lambda x: -sum(x[1]))[:8]:
         print(f"      gap before {n:34s} mean {sum(g) / len(g) / 1e3:6.1f} us  "
               f"median {statistics.median(g) / 1e3:6.1f} us  x{len(g)}")
+    dur = defaultdict(list)
+    for s, e, n in iv:
+        dur[n].append(e - s)
+    print("      kernel durations: " + "; ".join(
+        f"{n.strip()} {sum(d) / len(d) / 1e3:.1f} us x{len(d)}"
+        for n, d in sorted(dur.items(), key=lambda x: -sum(x[1]))[:9]))

@@ -3,7 +3,8 @@
 bench.py's C4 configuration (4096 slots, 100 sims/move, 2 lanes) after a
 warm-up; --synth swaps the network for the synthetic evaluator (no conv
 beside the tree kernels).  Stamps (100 MHz s_memrealtime) per slot of the
-last select launch of a move: 0 entry, 1 game_id read, 2 end of descent,
+last select launch of a move: 0 entry, 1 game_id read, 11 root loads done (masks, edge base,
+root board), 2 end of descent,
 3 after the two per-wave stats atomics, 4 after the eval-queue claim + stores,
 5 after the cache probe, 6 end (dedup-table claim for misses); per-level sums: 8 loads, 9 UCB +
 reductions, 10 play.
@@ -35,7 +36,7 @@ for _ in range(40):
     eng.selfplay_drain()
 
 buf = np.zeros((16384, 12), np.uint64)
-phases = ["dispatch", "game_id", "descent", "stats", "queue", "probe", "tail"]
+phases = ["dispatch", "game_id", "prologue", "descent", "stats", "queue", "probe", "tail"]
 acc = {p: [] for p in phases}
 span, depth_all, per_level = [], [], []
 lv_load, lv_reduce, lv_play = [], [], []
@@ -54,7 +55,8 @@ for mv in range(6):
         span.append((part[:, 6].max() - t0) / 100.0)
         acc["dispatch"].append((part[:, 0] - t0) / 100.0)
         acc["game_id"].append((part[:, 1] - part[:, 0]) / 100.0)
-        acc["descent"].append((part[:, 2] - part[:, 1]) / 100.0)
+        acc["prologue"].append((part[:, 11] - part[:, 1]) / 100.0)
+        acc["descent"].append((part[:, 2] - part[:, 11]) / 100.0)
         acc["stats"].append((part[:, 3] - part[:, 2]) / 100.0)
         q = part[:, 4] != 0
         acc["queue"].append((part[q, 4] - part[q, 3]) / 100.0)
@@ -63,7 +65,7 @@ for mv in range(6):
         acc["tail"].append((part[p5, 6] - part[p5, 5]) / 100.0)
         d = part[:, 7] & 0xFFFF
         depth_all.append(d)
-        per_level.append((part[d > 0, 2] - part[d > 0, 1]) / 100.0 / d[d > 0])
+        per_level.append((part[d > 0, 2] - part[d > 0, 11]) / 100.0 / d[d > 0])
         lv_load.append(part[d > 0, 8] / 100.0 / d[d > 0])
         lv_reduce.append(part[d > 0, 9] / 100.0 / d[d > 0])
         lv_play.append(part[d > 0, 10] / 100.0 / d[d > 0])
