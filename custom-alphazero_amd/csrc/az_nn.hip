@@ -655,11 +655,16 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
   ca.n_max = n_max;
   ca.H = H;
   ca.W = W;
-  // tile height by launch size (profiles/micro/conv16_ab.sh): 32-row tiles
-  // for chess self-play's 256 boards, 48 for Connect-4 lanes (~900 live of
-  // 2048 boards), 64 from ~3000 boards -- the work per CU evens out
+  // tile height by launch capacity: 32-row tiles for chess self-play's 256
+  // boards, 48 for a lone launch of ~900 boards (profiles/micro/conv16_ab.sh),
+  // 64 from ~1600 boards -- Connect-4 self-play lanes (2048 slots, ~870 live):
+  // with the two lanes' convs sharing the CUs the larger tile's operand reuse
+  // wins, 3207 vs 3137 games/s in-bench (profiles/r2/hw_queues.txt)
   const long rows_max = (long)n_max * HW;
-  ca.mb = rows_max <= 24576 ? 2 : (rows_max <= 131072 ? 3 : 4);
+  ca.mb = rows_max <= 24576 ? 2 : (rows_max <= 65536 ? 3 : 4);
+#ifdef AZ_FORCE_MB  // A/B builds (profiles/ab_libs.sh)
+  ca.mb = AZ_FORCE_MB;
+#endif
   ca.err = net.err;
   if (net.in_ch > 4) {
     // chess: 118 input planes zero-padded to F, the stem is one more 3x3 conv;
