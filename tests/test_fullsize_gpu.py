@@ -144,16 +144,16 @@ def chess_games():
     eng.close()
 
 
-def test_chess_fullsize_rules_and_policies(chess_games):
-    """All 256 games: positions chain through Board.play on the oracle rules,
-    each move is legal, each root policy covers exactly the legal moves (in
-    the 1880-action space) and is normalised; 800 sims expand every root."""
-    _, r = chess_games
+def check_chess_games(r, n_games, plies):
+    """Positions chain through Board.play on the oracle rules, each move is
+    legal, each root policy covers exactly the legal moves (in the 1880-action
+    space) and is normalised; games end at the ply cap or earlier with a
+    terminal position."""
     all_mv = C.all_moves()
     start = C.from_fen()
-    for g in range(CHESS["slots"]):
+    for g in range(n_games):
         T = int(r["lengths"][g])
-        assert T == CHESS["plies"] and r["terminations"][g] == 5, g  # the ply cap
+        assert T == plies and r["terminations"][g] == 5 or T < plies and r["terminations"][g] != 5, g
         pos = start
         for t in range(T):
             assert r["positions"][g, t].tobytes() == pos.tobytes(), (g, t)
@@ -167,7 +167,46 @@ def test_chess_fullsize_rules_and_policies(chess_games):
             assert (probs >= 0).all() and abs(probs.sum() - 1.0) < 1e-12, (g, t)
             assert probs[list(all_mv[acts]).index(mv)] > 0, (g, t)
             pos = C.play_canonical(pos, mv)
-        assert r["expansions"][g] >= CHESS["plies"], g
+        assert r["expansions"][g] >= T, g
+
+
+def test_chess_fullsize_rules_and_policies(chess_games):
+    """All 256 games at 800 sims/move (BASELINE configs[4]'s per-GPU shard),
+    3-ply cap: every game reaches the cap."""
+    _, r = chess_games
+    check_chess_games(r, CHESS["slots"], CHESS["plies"])
+    assert (r["lengths"][:CHESS["slots"]] == CHESS["plies"]).all()
+
+
+CHESS_LONG = dict(sims=800, slots=32, plies=64)
+
+
+@pytest.mark.timeout(300)
+def test_chess_long_games_at_800_sims():
+    """configs[4]'s 800 sims/move over 64 plies (the subtree kept across
+    moves grows with the search, compaction every move): rules and policies
+    for all 32 games, games 0 and 31 replayed bit for bit on the oracle."""
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    w = init_weights(weight_spec(8, 8, 1880, in_channels=118), seed=6)
+    eng = az.ChessEngine(mcts_iterations=CHESS_LONG["sims"], slots=CHESS_LONG["slots"],
+                         evaluator=az.EVAL_NETWORK, max_plies=CHESS_LONG["plies"])
+    try:
+        eng.set_weights(w.items())
+        st = eng.selfplay_run(0, CHESS_LONG["slots"], CHESS_SEED)
+        assert st["errors"] == 0 and st["games_done"] == CHESS_LONG["slots"]
+        r = eng.selfplay_results()
+        check_chess_games(r, CHESS_LONG["slots"], CHESS_LONG["plies"])
+
+        def cb(pos, initial):
+            x = C.full_state(*C.reference_history(pos, bool(initial)), pos)[None].astype(np.float32)
+            p, v = eng.forward(x)
+            return p[0], float(v[0])
+
+        for g in (0, CHESS_LONG["slots"] - 1):
+            ref = C.play_game(CHESS_LONG["sims"], CHESS_SEED + g, CHESS_LONG["plies"], callback=cb)
+            _compare(r, g, ref, "long")
+    finally:
+        eng.close()
 
 
 @pytest.mark.parametrize("g", [0, 255])
