@@ -90,8 +90,10 @@ struct TreeDev {
 // Eviction by generations (the reference's dict grows without bound until
 // the next model; a fixed table would fill up and every miss would then
 // probe to max_probe).  Each `gen_size` inserts start a new generation;
-// lookups use entries of the current and previous generation only, and an
-// insert may overwrite an entry at least kCacheReuseAge generations old.  A
+// lookups use entries of the current and previous generation only (a hit on
+// the previous generation moves the entry into the current one, so boards
+// the games keep reaching stay live), and an insert may overwrite an entry
+// at least kCacheReuseAge generations old.  A
 // reader checks liveness in select and reads the payload in expand, one
 // simulation later; an overwrite in between needs kCacheReuseAge - 1 = 2
 // generation turns inside that window, i.e. 2 * gen_size inserts.  The engine

@@ -210,6 +210,10 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
       if ((st & 3u) == kCacheReady && (st >> 16) == fp && cache_age(st, gen) < kCacheLiveGens &&
           same_board(c.keys[idx], b)) {
         t.eval_src[q] = (int32_t)idx;
+        // a hit on the previous generation moves the entry into the current
+        // one, so boards the games keep reaching stay live (the reference's
+        // dict never forgets them); at most one CAS per entry per generation
+        if (cache_age(st, gen) != 0) atomicCAS(c.state + idx, st, cache_word(fp, gen, kCacheReady));
         AZ_SEL_STAMP(s, 5);
         AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
         wave_stat(t, kStatCacheHits);
