@@ -54,7 +54,7 @@ F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16/fp16 MFMA (no 
 BOX_CPU_SHARE = 16              # CPUs one GPU's box grants a job (gpurun); workers stay inside it
 MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
 MAX_PREROLL = 800
-CACHE_TURNOVER_GENS = 3         # cache generations before the window (hit rate stationary)
+CACHE_TURNOVER_GENS = 8         # cache generations before the window (>= reuse age + 1: hit rate stationary)
 
 
 def parse():
@@ -608,7 +608,9 @@ def main():
     cap = st1["cache_capacity"]
     gen_size = st1["cache_gen_size"]
     gen = st1["cache_generation"]
-    live = (st1["cache_inserts"] - gen * gen_size + (gen_size if gen >= 1 else 0)) if gen_size else \
+    live_gens = st1["cache_live_gens"]
+    # inserts of the live generations (refreshed older entries come on top)
+    live = (st1["cache_inserts"] - max(gen - live_gens + 1, 0) * gen_size) if gen_size else \
         st1["cache_inserts"]
     game_name = "Connect-4 6x7" if (args.height, args.width, args.n) == (6, 7, 4) else \
         f"Connect-{args.n} {args.height}x{args.width}"
@@ -651,12 +653,13 @@ def main():
             "transposition_cache": ({
                 "capacity": cap,
                 "hit_rate": round(hits_all / max(exp_all, 1), 4),
-                "eviction": ({"inserts_per_generation": gen_size, "live_generations": 2,
-                              "rule": "lookups use the current and previous generation; inserts reuse "
-                                      "entries 3+ generations old (az_tree.h)"} if gen_size else None),
+                "eviction": ({"inserts_per_generation": gen_size, "live_generations": live_gens,
+                              "rule": f"lookups use the last {live_gens} generations and a hit moves the "
+                                      f"entry into the current one; inserts reuse entries "
+                                      f"{live_gens + 1}+ generations old (az_tree.h)"} if gen_size else None),
                 "generation_at_window_end": gen,
-                "live_entries": int(live),
-                "fill": round(live / cap, 4) if cap else None,
+                "inserted_in_live_generations": int(live),
+                "fill_lower_bound": round(live / cap, 4) if cap else None,
                 "age_moves_at_window_start": pre,
                 "inserts_in_window": d["cache_inserts"],
                 "semantics": "reference plays_inferences (mcts.py:122-143): board -> network output, shared "

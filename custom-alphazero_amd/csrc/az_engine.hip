@@ -572,7 +572,8 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
     t.step_mask = (uint32_t)(cap - 1);
     t.epoch = 0;
   }
-  if (c.cache_log2 < 0 || c.cache_log2 > 30) return cleanup(fail(AZ_E_INVALID, "cache_log2 must be 0..30"));
+  if (c.cache_log2 < 0 || c.cache_log2 > 30 || (c.cache_log2 > 0 && c.cache_log2 < 4))
+    return cleanup(fail(AZ_E_INVALID, "cache_log2 must be 0 (no cache) or 4..30"));
   if (c.cache_log2 > 0) {
     const size_t cap = (size_t)1 << c.cache_log2;
     az::CacheDev& cd = e->cache;
@@ -581,10 +582,10 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       return cleanup(rc);
     cd.mask = (uint32_t)(cap - 1);
     cd.enabled = 1;
-    // eviction by generations of cap/8 inserts, when a generation outlasts
+    // eviction by generations of cap/kCacheGenDiv inserts, when a generation outlasts
     // three moves of every slot's inserts (the lane-drift bound, az_tree.h);
     // otherwise the table only fills (entries are never overwritten)
-    const unsigned long long gen = cap / 8;
+    const unsigned long long gen = cap / az::kCacheGenDiv;
     cd.gen_size = gen > 3ull * (unsigned long long)g.slots * (unsigned long long)g.sims ? gen : 0;
     if (hipMemset(cd.state, 0, cap * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(cd.ctl, 0, 2 * sizeof(unsigned long long)) != hipSuccess)
@@ -799,6 +800,7 @@ int az_stats_get(az_engine* e, az_stats* st) {
     st->cache_generation = (int64_t)ctl[0];
     st->cache_inserts = (int64_t)ctl[1];
     st->cache_gen_size = (int64_t)e->cache.gen_size;
+    st->cache_live_gens = (int64_t)az::kCacheLiveGens;
     st->cache_capacity = (int64_t)e->cache.mask + 1;
   }
   st->games_drained = e->drained;

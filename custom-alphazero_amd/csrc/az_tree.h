@@ -84,19 +84,23 @@ struct TreeDev {
 
 // Transposition cache = the reference's plays_inferences (mcts/mcts.py:122-143,
 // utils.py:38-39): board -> (probs[A], value), shared by every game on the
-// device, cleared when the weights change.  Open addressing, linear probing.
+// device, cleared when the weights change.  Set-associative: a board hashes
+// to one bucket of kCacheBucket slots (its state words are one 64-B segment,
+// read in one round trip); inserts take the bucket's first reusable slot and
+// are dropped when every slot is live.  (Round 2 probed linearly across the
+// table: once stale entries had filled it, a miss walked max_probe = 32
+// acquire loads one after another, and games/s fell the longer a run went.)
 // The evaluator is deterministic per board, so hits never change a search.
 //
 // Eviction by generations (the reference's dict grows without bound until
-// the next model; a fixed table would fill up and every miss would then
-// probe to max_probe).  Each `gen_size` inserts start a new generation;
+// the next model; a fixed table would fill up and stop taking inserts).  Each `gen_size` inserts start a new generation;
 // lookups use entries of the current and previous generation only (a hit on
 // the previous generation moves the entry into the current one, so boards
 // the games keep reaching stay live), and an insert may overwrite an entry
 // at least kCacheReuseAge generations old.  A
 // reader checks liveness in select and reads the payload in expand, one
-// simulation later; an overwrite in between needs kCacheReuseAge - 1 = 2
-// generation turns inside that window, i.e. 2 * gen_size inserts.  The engine
+// simulation later; an overwrite in between needs kCacheReuseAge -
+// (kCacheLiveGens - 1) = 2 generation turns inside that window, i.e. 2 * gen_size inserts.  The engine
 // bounds the drift between lanes to two moves (move events, az_engine.hip)
 // and enables eviction only when 2 * gen_size > lanes' inserts in three moves
 // (slots * sims * 3), so a payload is never overwritten while a reader holds
@@ -106,8 +110,15 @@ struct TreeDev {
 // need no key read), [15:2] generation mod 2^14, [1:0] status.
 enum : uint32_t { kCacheEmpty = 0, kCacheClaimed = 1, kCacheReady = 2 };
 constexpr uint32_t kCacheGenMask = 0x3fff;
-constexpr uint32_t kCacheLiveGens = 2;  // age 0 (current) and 1 are looked up
-constexpr uint32_t kCacheReuseAge = 3;  // age >= 3 may be overwritten
+#ifndef AZ_CACHE_GEN_DIV  // A/B builds (profiles/ab_libs.sh)
+#define AZ_CACHE_GEN_DIV 16
+#endif
+#ifndef AZ_CACHE_LIVE
+#define AZ_CACHE_LIVE 6
+#endif
+constexpr uint32_t kCacheGenDiv = AZ_CACHE_GEN_DIV;       // a generation = capacity / kCacheGenDiv inserts
+constexpr uint32_t kCacheLiveGens = AZ_CACHE_LIVE;        // ages 0 .. kCacheLiveGens - 1 are looked up
+constexpr uint32_t kCacheReuseAge = kCacheLiveGens + 1;  // older entries may be overwritten
 AZ_HD uint32_t cache_fp(uint64_t h) { return (uint32_t)(h >> 48); }
 AZ_HD uint32_t cache_age(uint32_t st, uint32_t gen) { return (gen - (st >> 2)) & kCacheGenMask; }
 AZ_HD uint32_t cache_word(uint32_t fp, uint32_t gen, uint32_t status) {
@@ -119,10 +130,13 @@ struct CacheDev {
   float* pay = nullptr;        // [cap][A+1]: probs then value
   uint32_t mask = 0;           // cap - 1
   int enabled = 0;
-  int max_probe = 32;
   unsigned long long* ctl = nullptr;  // device [0] generation, [1] inserts since the last clear
   unsigned long long gen_size = 0;    // inserts per generation; 0 = no eviction
 };
+constexpr int kCacheBucket = 16;  // slots per bucket (cache_log2 >= 4)
+AZ_HD uint32_t cache_bucket(const CacheDev& c, uint64_t h) {
+  return (uint32_t)h & c.mask & ~(uint32_t)(kCacheBucket - 1);
+}
 
 // Self-play sample sink, indexed by game id - first_game.
 struct SampleDev {

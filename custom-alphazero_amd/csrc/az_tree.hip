@@ -200,26 +200,46 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   // treated as the end of the probe chain.
   const uint64_t h = board_hash(b);
   {
+    // the board's bucket: kCacheBucket state words (one 64-B segment) read
+    // at once with relaxed loads, scanned in registers; a candidate's key is
+    // read after an acquire fence (pairs with the insert's release)
     const uint32_t gen =
         (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t fp = cache_fp(h);
-    uint32_t idx = (uint32_t)h & c.mask;
-    for (int p = 0; p < c.max_probe; ++p) {
-      const uint32_t st = __hip_atomic_load(c.state + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      if (st == kCacheEmpty) break;
-      if ((st & 3u) == kCacheReady && (st >> 16) == fp && cache_age(st, gen) < kCacheLiveGens &&
-          same_board(c.keys[idx], b)) {
-        t.eval_src[q] = (int32_t)idx;
-        // a hit on the previous generation moves the entry into the current
-        // one, so boards the games keep reaching stay live (the reference's
-        // dict never forgets them); at most one CAS per entry per generation
-        if (cache_age(st, gen) != 0) atomicCAS(c.state + idx, st, cache_word(fp, gen, kCacheReady));
-        AZ_SEL_STAMP(s, 5);
-        AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
-        wave_stat(t, kStatCacheHits);
-        return;
+    const uint32_t base = cache_bucket(c, h);
+    uint32_t w[kCacheBucket];
+#pragma unroll
+    for (int k = 0; k < kCacheBucket; ++k)
+      w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int hit = -1;
+    uint32_t hst = 0;
+    bool stop = false;
+#pragma unroll
+    for (int k = 0; k < kCacheBucket; ++k) {
+      const uint32_t st = w[k];
+      if (stop) continue;
+      if (st == kCacheEmpty) {  // inserts fill a bucket in slot order: nothing past this
+        stop = true;
+      } else if ((st & 3u) == kCacheReady && (st >> 16) == fp && cache_age(st, gen) < kCacheLiveGens) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (same_board(c.keys[base + k], b)) {
+          hit = k;
+          hst = st;
+          stop = true;
+        }
       }
-      idx = (idx + 1) & c.mask;
+    }
+    if (hit >= 0) {
+      const uint32_t idx = base + hit;
+      t.eval_src[q] = (int32_t)idx;
+      // a hit on an older live generation moves the entry into the current
+      // one, so boards the games keep reaching stay live (the reference's
+      // dict never forgets them); at most one CAS per entry per generation
+      if (cache_age(hst, gen) != 0) atomicCAS(c.state + idx, hst, cache_word(fp, gen, kCacheReady));
+      AZ_SEL_STAMP(s, 5);
+      AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
+      wave_stat(t, kStatCacheHits);
+      return;
     }
   }
   AZ_SEL_STAMP(s, 5);
@@ -456,25 +476,31 @@ __device__ void cache_insert_row(const GameCfg& g, const TreeDev& t, const Cache
   const uint64_t h = board_hash(b);
   const uint32_t gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t fp = cache_fp(h);
-  uint32_t idx = (uint32_t)h & c.mask;
-  for (int p = 0; p < c.max_probe; ++p) {
-    const uint32_t st = __hip_atomic_load(c.state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t base = cache_bucket(c, h);
+  uint32_t w[kCacheBucket];
+#pragma unroll
+  for (int k = 0; k < kCacheBucket; ++k)
+    w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int slot = -1;
+#pragma unroll
+  for (int k = 0; k < kCacheBucket; ++k) {  // the first reusable slot this insert wins
+    const uint32_t st = w[k];
+    if (slot >= 0) continue;
     const bool reusable = st == kCacheEmpty || (c.gen_size && cache_age(st, gen) >= kCacheReuseAge);
-    if (reusable && atomicCAS(c.state + idx, st, cache_word(fp, gen, kCacheClaimed)) == st) {
-      c.keys[idx] = b;
-      float* dst = c.pay + (size_t)idx * (g.A + 1);
-      for (int a = 0; a < g.A; ++a) dst[a] = probs[(size_t)u * g.A + a];
-      dst[g.A] = values[u];
-      __threadfence();
-      atomicExch(c.state + idx, cache_word(fp, gen, kCacheReady));
-      wave_stat(t, kStatCacheInserts);
-      // every gen_size-th insert since the clear opens a new generation
-      const unsigned long long n = wave_claim64(c.ctl + 1) + 1;
-      if (c.gen_size && n % c.gen_size == 0) atomicAdd(c.ctl, 1ull);
-      return;
-    }
-    idx = (idx + 1) & c.mask;
+    if (reusable && atomicCAS(c.state + base + k, st, cache_word(fp, gen, kCacheClaimed)) == st) slot = k;
   }
+  if (slot < 0) return;  // every slot of the bucket is live: the board is evaluated again when met
+  const uint32_t idx = base + slot;
+  c.keys[idx] = b;
+  float* dst = c.pay + (size_t)idx * (g.A + 1);
+  for (int a = 0; a < g.A; ++a) dst[a] = probs[(size_t)u * g.A + a];
+  dst[g.A] = values[u];
+  __threadfence();
+  atomicExch(c.state + idx, cache_word(fp, gen, kCacheReady));
+  wave_stat(t, kStatCacheInserts);
+  // every gen_size-th insert since the clear opens a new generation
+  const unsigned long long n = wave_claim64(c.ctl + 1) + 1;
+  if (c.gen_size && n % c.gen_size == 0) atomicAdd(c.ctl, 1ull);
 }
 
 // ------------------------------------------------------ synthetic evaluator

@@ -63,7 +63,8 @@ class Stats(ctypes.Structure):
         ("path_edges", ctypes.c_int64), ("cache_inserts", ctypes.c_int64),
         ("cache_generation", ctypes.c_int64), ("cache_gen_size", ctypes.c_int64),
         ("cache_capacity", ctypes.c_int64), ("games_drained", ctypes.c_int64),
-        ("max_retained", ctypes.c_int64), ("reserved", ctypes.c_int64 * 2),
+        ("max_retained", ctypes.c_int64), ("cache_live_gens", ctypes.c_int64),
+        ("reserved", ctypes.c_int64 * 1),
     ]
 
     def as_dict(self):

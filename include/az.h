@@ -59,7 +59,8 @@ typedef struct az_config {
     int64_t arena_edges;           /* tree edges per slot; 0 = mcts_iterations*H*W*A */
     int64_t max_tree_visits;       /* bound on visits through one node; 0 = mcts_iterations*H*W */
     int32_t cache_log2;            /* transposition cache entries = 2^cache_log2 (the reference's
-                                      plays_inferences, mcts/mcts.py:122-143); 0 = off */
+                                      plays_inferences, mcts/mcts.py:122-143); 0 = off, else 4..30
+                                      (16-slot buckets) */
     int32_t conv_algo;             /* residual-tower 3x3 convs: AZ_CONV_F16X2 (0, default; board width
                                       <= 16, activations within +-32752) or AZ_CONV_DIRECT (1); same
                                       layer, outputs within NET_TOL */
@@ -106,7 +107,9 @@ typedef struct az_stats {
     int64_t games_drained;    /* finished games az_selfplay_drain has returned this batch */
     int64_t max_retained;     /* compact: most edges a compaction kept (the arena high-water mark
                                  before the next search) since engine creation */
-    int64_t reserved[2];
+    int64_t cache_live_gens;  /* generations a lookup accepts (ages 0 .. n-1; a hit moves the entry
+                                 into the current one); entries n+ generations old may be overwritten */
+    int64_t reserved[1];
 } az_stats;
 
 int az_abi_version(void);

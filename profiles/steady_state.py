@@ -38,7 +38,8 @@ def main():
         d = {k: st[k] - prev[k] for k in ("games_done", "expansions", "cache_hits", "evaluations")}
         print(json.dumps({"move": mv, "ms": round(1e3 * dt, 2), "games": d["games_done"],
                           "hit_rate": round(d["cache_hits"] / max(d["expansions"], 1), 4),
-                          "evals": d["evaluations"], "expansions": d["expansions"]}), flush=True)
+                          "evals": d["evaluations"], "expansions": d["expansions"],
+                          "gen": st["cache_generation"]}), flush=True)
         prev = st
 
 

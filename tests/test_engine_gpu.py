@@ -106,7 +106,7 @@ def test_tree_api_edges_match_reference(golden, name):
                                                       (20, 3, False), (0, 2, False), (20, 2, True)])
 def test_selfplay_synthetic_many_games_vs_oracle(cache_log2, lanes, compact):
     """256 games at S=50 on 96 slots (heavy refill) == the C oracle, bitwise;
-    cache_log2=10 fills the table (probe limit / no-insert path); 2-3 lanes
+    cache_log2=10 fills the table (full buckets: the no-insert path); 2-3 lanes
     race on the shared cache and the refill counter; compact reclaims the
     left subtrees after every move."""
     eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC,
@@ -131,13 +131,14 @@ def test_selfplay_synthetic_many_games_vs_oracle(cache_log2, lanes, compact):
 @pytest.mark.parametrize("lanes", [1, 2, 3])
 def test_cache_eviction_generations_are_transparent(lanes):
     """A cache small enough to turn over many eviction generations (az_tree.h:
-    entries 3+ generations old are overwritten while other lanes read the
-    table) leaves every game bitwise equal to the oracle."""
-    eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC, cache_log2=17, lanes=lanes)
-    games = selfplay_games(eng, 3000, 256, base_seed=9)
+    entries older than the live generations are overwritten while other lanes
+    read the table, hits move entries into the current generation) leaves
+    every game bitwise equal to the oracle."""
+    eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC, cache_log2=18, lanes=lanes)
+    games = selfplay_games(eng, 3000, 384, base_seed=9)
     st = eng.stats()
-    assert st["cache_gen_size"] == 2 ** 17 // 8
-    assert st["cache_generation"] >= 4, st["cache_generation"]
+    assert st["cache_gen_size"] == 2 ** 18 // 16  # kCacheGenDiv
+    assert st["cache_generation"] >= st["cache_live_gens"] + 2, st["cache_generation"]
     assert st["cache_hits"] > 0 and st["errors"] == 0
     for g, got in enumerate(games):
         ref = oracle.play_game(6, 7, 4, True, 50, 9 + 3000 + g)
