@@ -54,7 +54,7 @@ F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16/fp16 MFMA (no 
 BOX_CPU_SHARE = 16              # CPUs one GPU's box grants a job (gpurun); workers stay inside it
 MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
 MAX_PREROLL = 800
-CACHE_TURNOVER_GENS = 8         # cache generations before the window (>= reuse age + 1: hit rate stationary)
+CACHE_TURNOVER_GENS = 2         # cache generations past the live ones before the window (hit rate stationary)
 
 
 def parse():
@@ -456,7 +456,7 @@ def main():
         st, _ = step_and_drain(eng)
         pre += 1
         gen_ok = (not args.cache_log2 or not st["cache_gen_size"]
-                  or st["cache_generation"] >= CACHE_TURNOVER_GENS)
+                  or st["cache_generation"] >= st["cache_live_gens"] + CACHE_TURNOVER_GENS)
         done = pre >= max(args.warmup, MIN_PREROLL) and gen_ok
         if world > 1:  # every rank runs the same number of untimed moves
             (done,) = _reduce([0.0 if done else 1.0], SUM, world, args, dev)
@@ -640,7 +640,7 @@ def main():
             },
             "untimed_moves": pre,
             "untimed_rule": (f"max(--warmup, {MIN_PREROLL}) moves and until the transposition cache has "
-                             f"turned over {CACHE_TURNOVER_GENS} eviction generations (stationary hit rate)"),
+                             f"turned over its live generations + {CACHE_TURNOVER_GENS} (stationary hit rate)"),
             "games_timed": int(drained_all),
             "games_timed_basis": "games whose samples reached the host in the window (az_selfplay_drain "
                                  "after every step -- the previous move's games while the next move runs "
