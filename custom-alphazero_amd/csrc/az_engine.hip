@@ -131,7 +131,8 @@ int check_device_errors(az_engine* e) {
     if (err & az::kErrIllegal) m += " illegal-move";
     if (err & az::kErrNoRoot) m += " play-before-search";
     if (err & az::kErrActRange)
-      m += " activation-range(|x| > 32752 for the fp16x2 convs: use conv_algo=AZ_CONV_DIRECT)";
+      m += " activation-range(a non-finite activation, or |x| > 32752 in the per-layer fp16x2 convs: "
+           "use conv_algo=AZ_CONV_F16X2 or AZ_CONV_DIRECT)";
     // play on a slot without a searched root changes nothing: that flag is
     // cleared once reported (the others mean a broken tree and stay)
     if (err == az::kErrNoRoot) AZ_HIP(hipMemset(e->t.stats + az::kStatErrors, 0, sizeof(err)));
@@ -459,6 +460,39 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       if ((rc = upload(owned, &net.pd_wt, t))) return rc;
     }
   }
+  if (in_ch == 4 && net.use_tower) {
+    if (net.depth > kTowerMaxDepth || net.hidden > 256) return fail(AZ_E_INVALID, "tower: depth/hidden too large");
+    TowerNet tn{};
+    for (int d = 0; d < net.depth; ++d) {
+      tn.k1[d] = reinterpret_cast<const uint4*>(net.k1[d]);
+      tn.k2[d] = reinterpret_cast<const uint4*>(net.k2[d]);
+      tn.b1[d] = net.c1_b[d];
+      tn.b2[d] = net.c2_b[d];
+      tn.s1[d] = net.k1_scale[d];
+      tn.s2[d] = net.k2_scale[d];
+    }
+    tn.stem_w = net.stem_w;
+    tn.stem_b = net.stem_b;
+    tn.wpc = net.pc_w;
+    tn.bpc = net.pc_b;
+    tn.wvc = net.vc_w;
+    tn.bvc = net.vc_b;
+    tn.wpd = net.pd_w;
+    tn.bpd = net.pd_b;
+    tn.wv1 = net.v1_w;
+    tn.bv1 = net.v1_b;
+    tn.wv2 = net.v2_w;
+    tn.bv2 = net.v2_b;
+    tn.depth = net.depth;
+    tn.hidden = net.hidden;
+    if (!net.tower) {
+      void* q = nullptr;
+      AZ_HIP(hipMalloc(&q, sizeof(TowerNet)));
+      owned.push_back(q);
+      net.tower = reinterpret_cast<TowerNet*>(q);
+    }
+    AZ_HIP(hipMemcpy(net.tower, &tn, sizeof(TowerNet), hipMemcpyHostToDevice));
+  }
   net.ready = true;
   return 0;
 }
@@ -479,10 +513,14 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   const int A = c.gravity ? c.board_width : c.board_width * c.board_height;
   if (A > az::kMaxActions) return fail(AZ_E_INVALID, "action space too large");
   if (c.slots < 1 || c.mcts_iterations < 1) return fail(AZ_E_INVALID, "slots and mcts_iterations must be >= 1");
-  if (c.conv_algo != AZ_CONV_F16X2 && c.conv_algo != AZ_CONV_DIRECT)
-    return fail(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2 or AZ_CONV_DIRECT");
-  if (c.evaluator == AZ_EVAL_NETWORK && c.conv_algo == AZ_CONV_F16X2 && c.board_width > 16)
-    return fail(AZ_E_INVALID, "AZ_CONV_F16X2 supports boards up to 16 columns (use AZ_CONV_DIRECT)");
+  if (c.conv_algo != AZ_CONV_F16X2 && c.conv_algo != AZ_CONV_DIRECT && c.conv_algo != AZ_CONV_F16X2_LAYERS)
+    return fail(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2, AZ_CONV_DIRECT or AZ_CONV_F16X2_LAYERS");
+  if (c.evaluator == AZ_EVAL_NETWORK && c.conv_algo == AZ_CONV_F16X2_LAYERS && c.board_width > 16)
+    return fail(AZ_E_INVALID, "AZ_CONV_F16X2_LAYERS supports boards up to 16 columns");
+  if (c.evaluator == AZ_EVAL_NETWORK && c.conv_algo == AZ_CONV_F16X2 &&
+      (c.depth > az::kTowerMaxDepth || c.value_hidden > 256))
+    return fail(AZ_E_INVALID, "AZ_CONV_F16X2 supports depth <= 16 and value_hidden <= 256 "
+                              "(use AZ_CONV_F16X2_LAYERS or AZ_CONV_DIRECT)");
   if (c.evaluator == AZ_EVAL_NETWORK && (int64_t)c.slots * c.board_height * c.board_width * 512 >= (1ll << 31))
     return fail(AZ_E_INVALID, "slots * H * W * 512 must stay below 2^31 (32-bit activation byte offsets)");
   if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC)
@@ -607,7 +645,8 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       if ((rc = e->alloc(&e->act[i], act))) return cleanup(rc);
   }
   e->net.depth = c.depth;
-  e->net.algo = c.conv_algo;
+  e->net.algo = c.conv_algo == AZ_CONV_F16X2_LAYERS ? AZ_CONV_F16X2 : c.conv_algo;
+  e->net.use_tower = c.conv_algo == AZ_CONV_F16X2;
   e->net.err = e->t.stats + az::kStatErrors;
   // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
   int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);

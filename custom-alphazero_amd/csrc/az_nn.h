@@ -7,6 +7,34 @@
 
 namespace az {
 
+// tower16_kernel (az_tower16.hip): the whole Connect-N forward in one launch.
+// Its view of the network, resident in device memory (kernel reads it with
+// scalar loads).
+constexpr int kTowerMaxDepth = 16;   // residual blocks
+constexpr int kTowerMaxBoards = 8;   // boards per workgroup tile
+struct TowerNet {
+  const uint4* k1[kTowerMaxDepth];   // conv16 packs: conv1 (36 k-steps)
+  const uint4* k2[kTowerMaxDepth];   // conv2 + 1x1 projection residual (40)
+  const float* b1[kTowerMaxDepth];   // folded biases
+  const float* b2[kTowerMaxDepth];   // conv2 + the residual's
+  float s1[kTowerMaxDepth];          // 2^(e - 12) of each pack's prescale e
+  float s2[kTowerMaxDepth];
+  const float* stem_w;               // [36][F] (k = tap*4 + c)
+  const float* stem_b;               // [F]
+  const float *wpc, *bpc, *wvc, *bvc;  // head 1x1 convs [F][2], [2], [F], [1]
+  const float *wpd, *bpd;            // policy dense [2HW][A], [A]
+  const float *wv1, *bv1, *wv2, *bv2;  // value dense [HW][hidden], [hidden], [hidden], [1]
+  int depth, hidden;
+};
+// 0 when the board does not fit a tile (HW > 128); else 96 or 128
+int tower16_tile_rows(int HW);
+int tower16_boards_per_tile(int HW);
+size_t tower16_lds_bytes(int HW);
+// boards (self-play: the eval queue's boards) or x ([n][HW][4] one-hot planes,
+// az_forward) -> probs [n][A], values [n]; count (device, may be null -> n_max)
+void launch_tower16(const TowerNet* net, const Board* boards, const float4* x, const int* count, int n_max,
+                    int H, int W, int A, float* probs, float* values, unsigned long long* err, hipStream_t s);
+
 // Folded (BatchNorm-in) weights resident in HBM, packed for the kernels (not
 // Keras layouts).  AZ_CONV_F16X2 (default): conv16_kernel packs (fp16 term
 // pairs, az_conv16.hip) and split16 activations; AZ_CONV_DIRECT: fp32 MFMA
@@ -14,6 +42,8 @@ namespace az {
 struct NetDev {
   int filters = 128, depth = 0, hidden = 256;
   int algo = 0;             // AZ_CONV_F16X2 / AZ_CONV_DIRECT (one algorithm for every forward)
+  bool use_tower = false;   // Connect-N, AZ_CONV_F16X2: the whole forward in tower16_kernel (else per layer)
+  TowerNet* tower = nullptr;  // device copy of the tower's view (load_network)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   float* stem_w = nullptr;  // in_ch == 4: [36][F] (k = tap*4 + c), VALU stem kernels
   float* stem_b = nullptr;  // [F]

@@ -15,6 +15,7 @@ EVAL_NETWORK = 0
 EVAL_SYNTHETIC = 1
 CONV_F16X2 = 0  # include/az.h AZ_CONV_F16X2 (default)
 CONV_DIRECT = 1
+CONV_F16X2_LAYERS = 2  # AZ_CONV_F16X2_LAYERS: the same arithmetic one layer per launch (A/B runs)
 
 
 class AzError(RuntimeError):

@@ -35,8 +35,11 @@ extern "C" {
 
 /* az_config.conv_algo */
 #define AZ_CONV_F16X2 0      /* direct implicit GEMM on the fp16 MFMA, fp32-accurate: both operands
-                                as two fp16 terms, three products per k-step (default) */
+                                as two fp16 terms, three products per k-step (default); Connect-N
+                                runs the whole forward in one kernel, activations held in LDS */
 #define AZ_CONV_DIRECT 1     /* direct implicit GEMM on fp32 MFMA (exact fp32 FMA chains) */
+#define AZ_CONV_F16X2_LAYERS 2  /* AZ_CONV_F16X2's arithmetic one layer per launch (activations in
+                                   HBM between layers; the round-2 path, kept for A/B runs) */
 
 typedef struct az_engine az_engine;
 
@@ -61,8 +64,9 @@ typedef struct az_config {
     int32_t cache_log2;            /* transposition cache entries = 2^cache_log2 (the reference's
                                       plays_inferences, mcts/mcts.py:122-143); 0 = off, else 4..30
                                       (16-slot buckets) */
-    int32_t conv_algo;             /* residual-tower 3x3 convs: AZ_CONV_F16X2 (0, default; board width
-                                      <= 16, activations within +-32752) or AZ_CONV_DIRECT (1); same
+    int32_t conv_algo;             /* residual-tower 3x3 convs: AZ_CONV_F16X2 (0, default; depth <= 16,
+                                      value_hidden <= 256), AZ_CONV_DIRECT (1) or AZ_CONV_F16X2_LAYERS
+                                      (2; board width <= 16, activations within +-32752); same
                                       layer, outputs within NET_TOL */
     int32_t lanes;                 /* self-play slot groups searched on separate HIP streams
                                       (0 = auto: 2 when slots >= 512); results do not depend on it */

@@ -1,0 +1,41 @@
+"""Isolated forward timing of the current libaz (AZ_LIB_PATH for A/B builds):
+HIP-event time of the timed region per forward at the given batch sizes."""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "custom-alphazero_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle  # noqa: E402
+from custom_alphazero import engine as az  # noqa: E402
+from custom_alphazero.model.weights import init_weights, weight_spec  # noqa: E402
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else ""
+    algo = int(os.environ.get("AZ_ALGO", "0"))
+    rng = np.random.RandomState(5)
+    spec = weight_spec(6, 7, 7, depth=4)
+    w = init_weights(spec, seed=0, randomize_bn=True)
+    out = []
+    for nb in (673, 1346, 4096):
+        xx = oracle.full_state(rng.randint(-1, 2, (nb, 6, 7)).astype(np.int8))
+        eng = az.Engine(6, 7, 4, True, 25, slots=max(nb, 2048), evaluator=az.EVAL_NETWORK, depth=4,
+                        conv_algo=algo)
+        eng.set_weights(w.items())
+        eng.forward(xx)
+        eng.timer(True)
+        for _ in range(20):
+            eng.forward(xx)
+        st = eng.stats()
+        eng.timer(False)
+        per = st["conv_ms"] / 20
+        out.append(f"B={nb} {per * 1e3:.1f}us {nb * 313.8e6 / (per * 1e-3) / 1e12:.0f}TF")
+        eng.close()
+    print(tag, "algo", algo, " | ".join(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -240,7 +240,7 @@ def test_encode_and_mask_match_reference(golden, name):
 
 
 # ------------------------------------------------------------------ network
-CONV_ALGOS = [az.CONV_F16X2, az.CONV_DIRECT]
+CONV_ALGOS = [az.CONV_F16X2, az.CONV_DIRECT, az.CONV_F16X2_LAYERS]
 
 
 def make_net_engine(H=6, W=7, n=4, grav=True, S=25, slots=256, seed=0, randomize_bn=True, depth=4,
@@ -262,8 +262,9 @@ def random_boards(rng, k, H, W):
 @pytest.mark.parametrize("conv_algo", CONV_ALGOS)
 @pytest.mark.parametrize("shape", [(6, 7, True), (9, 9, True), (5, 5, False), (7, 6, True)])
 def test_forward_matches_keras_restatement(shape, conv_algo):
-    """Both conv algorithms (Winograd F(2x2,3x3), direct) within NET_TOL of the
-    float64 Keras restatement; odd H and W exercise the partial 2x2 tiles."""
+    """Every conv algorithm (the one-launch fp16x2 tower, fp32 direct, the
+    per-layer fp16x2 kernels) within NET_TOL of the float64 Keras restatement;
+    9x9 runs the tower's 96-row tiles, 5x5 five boards per tile."""
     H, W, grav = shape
     eng, w = make_net_engine(H, W, 4, grav, slots=300, conv_algo=conv_algo)
     rng = np.random.RandomState(5)
