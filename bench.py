@@ -104,17 +104,39 @@ def _cpu_model():
     return platform.processor()
 
 
+def cpu_quota():
+    """CPUs this job may use: the cgroup CPU quota (cgroup v2 cpu.max, or v1
+    cfs_quota/period) and the affinity mask, with where each came from."""
+    quota, src = None, "no cgroup CPU quota"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota, src = -(-int(q) // int(per)), f"cgroup v2 cpu.max {q} {per}"
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota, src = -(-q // per), f"cgroup v1 cfs_quota_us {q} / cfs_period_us {per}"
+        except (OSError, ValueError):
+            pass
+    aff = len(os.sched_getaffinity(0))
+    return quota, aff, src
+
+
 def cpu_workers(args):
     """The reference's fan-out is os.cpu_count() - 1 worker processes
-    (self_play.py:98); on a GPU box os.cpu_count() is the whole machine while
-    a job's share is BOX_CPU_SHARE CPUs, so the pool stays inside that share."""
+    (self_play.py:98).  On a GPU box os.cpu_count() counts the whole machine
+    while the job's cgroup grants a share of it, so the pool is
+    min(os.cpu_count() - 1, quota - 1, affinity - 1): the reference's rule
+    applied to the CPUs this job may actually use."""
     total = os.cpu_count() or 1
-    aff = len(os.sched_getaffinity(0))
+    quota, aff, src = cpu_quota()
     ref = max(1, total - 1)
-    w = args.cpu_workers or max(1, min(ref, aff - 1, BOX_CPU_SHARE - 1))
-    why = (f"reference n_jobs = os.cpu_count() - 1 = {ref}; this host: os.cpu_count() {total}, "
-           f"affinity {aff}; capped at the box's {BOX_CPU_SHARE}-CPU share - 1" if w < ref else
-           f"reference n_jobs = os.cpu_count() - 1 = {ref}")
+    avail = min(aff, quota) if quota else aff
+    w = args.cpu_workers or max(1, min(ref, avail - 1))
+    why = (f"reference n_jobs = os.cpu_count() - 1 = {ref}; this job: os.cpu_count() {total}, affinity {aff}, "
+           f"{src}" + (f" -> {avail} usable CPUs - 1" if w < ref else ""))
     return w, why
 
 
@@ -145,6 +167,29 @@ def cpu_baseline(args, weights):
                    f"x 1 torch-CPU thread, batch-1 forward, one plays_inferences Manager dict shared by "
                    f"all workers ({entries} entries at the end); {games} games in {wall:.1f}s "
                    f"({_cpu_model()})"),
+    }
+
+
+def cpu_baseline_native(args, weights):
+    """SURVEY.md 8(d)'s stronger CPU line: oracle/az_cpu.c -- the oracle's C
+    MCTS (bit-exact on the reference's fixtures) + a batch-1 fp32 C forward,
+    one thread per game, the reference's fan-out of worker count, one shared
+    insert-only plays_inferences table; same bounded sample length."""
+    import cpu_native
+    workers, why = cpu_workers(args)
+    A = args.width
+    flat = cpu_native.fold_for_cpu(weights, args.height, args.width, A, args.depth)
+    r = cpu_native.selfplay(flat, args.height, args.width, args.n, True, args.sims, args.depth, workers,
+                            args.cpu_baseline_seconds)
+    wall = r["seconds"]
+    return {
+        "value": round(r["games"] / wall, 4), "unit": "games/s", "cores": workers, "kind": "port",
+        "expansions_per_s": round(r["expansions"] / wall, 1), "cores_reason": why,
+        "cache_hit_rate": round(r["cache_hits"] / max(r["expansions"], 1), 4),
+        "sample": (f"oracle/az_cpu.c: C MCTS (oracle/az_oracle.c) + batch-1 fp32 C forward (BN folded, 4 pixels x "
+                   f"32 channels per register block), {workers} threads x 1 game, one shared insert-only cache "
+                   f"(2^22 entries); C4 {args.sims} sims/move, {r['games']} games / {r['expansions']} expansions in "
+                   f"{wall:.1f}s ({_cpu_model()})"),
     }
 
 
@@ -202,34 +247,41 @@ def _reduce(values, op, world, args, dev):
 
 
 def conv_kernel_name(conv_algo, chess=False):
-    if conv_algo != 0:
-        return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual)"
+    if conv_algo == 1:
+        return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual), one launch per conv"
+    if conv_algo == 0 and not chess:
+        return ("tower16_kernel (the whole forward in one launch per lane-simulation: VALU stem, the residual "
+                "tower's 8 3x3 convs as implicit GEMMs on the 16x16x32 fp16 MFMA -- fp32-accurate, both operands "
+                "as two fp16 terms, 3 products per k-step -- with activations held in LDS, 1x1 projection "
+                "residuals, head 1x1 convs, dense heads, softmax, tanh)")
     return ("conv16_kernel (direct 3x3 implicit GEMM on the 16x16x32 fp16 MFMA; fp32-accurate: both operands as "
-            "two fp16 terms, 3 products per k-step; fused BN/ReLU, 1x1 projection residual and head 1x1 convs"
-            + (", residual tower, 8 launches per forward)" if chess else ")"))
+            "two fp16 terms, 3 products per k-step; fused BN/ReLU, 1x1 projection residual and head 1x1 convs; "
+            "one launch per conv)")
 
 
-def conv_roofline(args, conv_algo, boards_per_launch, avg_ms, busy_ms, boards_total, launches,
-                  direct_flop_per_board, issued_per_board, pmc_file, chess=False):
-    """roofline for the residual tower's 3x3 convs (the dominant kernel).
-    achieved = FLOP the kernel issues per launch (boards per launch x issued
-    FLOP per board / 8 launches per forward) / the launch's mean duration
-    (HIP events on its lane's stream); frac against the peak of the pipe it
-    issues on.  The direct-convolution FLOP at the fp32 peak is given beside
-    it as the algorithmic equivalent (SURVEY.md 8d's count)."""
-    n_conv = 2 * args.depth
-    flop, peak, dtype = issued_per_board, (F16_MFMA_PEAK_TFLOPS if conv_algo == 0 else FP32_MFMA_PEAK_TFLOPS), \
-        ("fp16 (2 terms per fp32 operand, 3 products)" if conv_algo == 0 else "fp32")
-    achieved = boards_per_launch * flop / n_conv / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
-    alg = boards_per_launch * direct_flop_per_board / n_conv / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
-    union = boards_total * flop / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
+def conv_roofline(args, conv_algo, per_forward, boards_per_launch, avg_ms, busy_ms, boards_total, launches,
+                  direct_flop_per_board, issued_per_board, pmc_file, pmc_key, chess=False):
+    """roofline of the dominant kernel (the residual tower's convs: the whole
+    forward in one tower16_kernel launch, or one conv per launch).
+    achieved = ALGORITHMIC FLOP per launch -- the direct convolution's
+    2*MACs (19 F*F MACs per pixel per block) x live boards per
+    launch / launches per forward -- / the launch's mean duration (HIP events
+    on its lane's stream over the timed window); peak = the dense MFMA peak of
+    the pipe the kernel issues on (fp16: the two-term split issues 3 fp16
+    products per MAC, reported beside it as `issued`)."""
+    f16 = conv_algo != 1
+    peak = F16_MFMA_PEAK_TFLOPS if f16 else FP32_MFMA_PEAK_TFLOPS
+    dtype = "fp16 MFMA (2 terms per fp32 operand, 3 products per MAC)" if f16 else "fp32 MFMA"
+    per_launch = boards_per_launch / per_forward
+    achieved = per_launch * direct_flop_per_board / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
+    issued = per_launch * issued_per_board / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
+    union = boards_total * direct_flop_per_board / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
     traffic = None
     if os.path.exists(pmc_file):  # PMC bytes/board (rocprofv3 FETCH_SIZE/WRITE_SIZE) x live batch
         with open(pmc_file) as fp:
             tj = json.load(fp)
-        key = "f16x2" if conv_algo == 0 else "direct"
-        if key in tj:
-            traffic = int(tj[key]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+        if pmc_key in tj:
+            traffic = int(tj[pmc_key]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
     return {
         "kernel": conv_kernel_name(conv_algo, chess),
         "bound": "mfma",
@@ -238,21 +290,19 @@ def conv_roofline(args, conv_algo, boards_per_launch, avg_ms, busy_ms, boards_to
         "unit": "TFLOP/s",
         "frac": round(achieved / peak, 4),
         "traffic": traffic,
-        "traffic_unit": f"HBM bytes per launch (PMC bytes/board, {os.path.relpath(pmc_file, REPO)}, "
+        "traffic_unit": f"HBM bytes per launch (PMC bytes/board, {os.path.relpath(pmc_file, REPO)} [{pmc_key}], "
                         f"x live boards/launch)",
         "dtype": dtype,
-        "achieved_basis": "issued MFMA FLOP per launch (boards_per_launch x issued_flop_per_board / "
-                          f"{n_conv} launches) / avg_launch_ms (HIP events on each lane's stream, timed region)",
-        "issued_flop_per_board": int(flop),
-        "algorithmic_equivalent": {
-            "achieved": round(alg, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-            "frac": round(alg / FP32_MFMA_PEAK_TFLOPS, 4),
-            "flop_per_board": int(direct_flop_per_board),
-            "basis": "direct-convolution FLOP (SURVEY.md 8d) per launch / avg_launch_ms, priced at the fp32 "
-                     "MFMA peak: the rate an exact fp32 MFMA kernel would need for the same layer time (the "
-                     "fp16 two-term products run at 16x the fp32 rate, so this can exceed 1)"},
+        "achieved_basis": (f"direct-convolution FLOP per launch ({int(direct_flop_per_board)} per board x "
+                           f"boards_per_launch / {per_forward} launch(es) per forward) / avg_launch_ms (HIP events "
+                           f"on each lane's stream, timed region)"),
+        "flop_per_board": int(direct_flop_per_board),
+        "issued": {"achieved": round(issued, 2), "frac": round(issued / peak, 4),
+                   "flop_per_board": int(issued_per_board),
+                   "basis": "MFMA FLOP the kernel issues (3 fp16 products per MAC) per launch / avg_launch_ms"},
         "busy_union": {"achieved": round(union, 2), "frac": round(union / peak, 4),
-                       "basis": "all timed boards' issued FLOP / union of the conv intervals of all lanes"},
+                       "basis": "all timed boards' direct FLOP / union of the kernel intervals of all lanes"},
+        "launches_per_forward": per_forward,
         "boards_per_launch": round(boards_per_launch, 1),
         "avg_launch_ms": round(avg_ms, 4),
         "conv_busy_ms": round(busy_ms, 2),
@@ -330,7 +380,7 @@ def chess_main(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    st1 = eng.stats()
+    st1 = check_device(eng, "the timed window")
     eng.timer(False)
     d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
                                       "terminal_visits", "evaluations")}
@@ -342,11 +392,13 @@ def chess_main(args):
     direct_flop = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
     issued = 3 * direct_flop if args.conv_algo == 0 else direct_flop  # fp16x2: 3 products per MAC
     launches = st1["conv_launches"]
-    boards_per_launch = local_evals / max(launches / (2 * args.depth), 1)
+    per_forward = 2 * args.depth
+    boards_per_launch = local_evals / max(launches / per_forward, 1)
     avg_ms = st1["conv_ms"] / max(launches, 1)
-    roof = conv_roofline(args, args.conv_algo, boards_per_launch, avg_ms, st1["conv_busy_ms"], local_evals,
-                         launches, direct_flop, issued,
-                         os.path.join(REPO, "profiles", "r1", "pmc_chess_traffic.json"), chess=True)
+    roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, avg_ms, st1["conv_busy_ms"],
+                         local_evals, launches, direct_flop, issued,
+                         os.path.join(REPO, "profiles", "r3", "pmc_chess_traffic.json"),
+                         "f16x2" if args.conv_algo != 1 else "direct", chess=True)
     if rank == 0:
         line = {
             "metric": f"MCTS node-expansions/s (Chess, {args.sims} sims/move)",
@@ -410,8 +462,50 @@ def step_and_drain(eng, sink=None):
     return st, len(d["lengths"])
 
 
+def launch_ranks(args):
+    """--gpus N is authoritative.  Under a launcher (WORLD_SIZE set) it must
+    equal the world size; without one and N > 1, this process starts the N
+    ranks itself -- a torch.distributed.run child, before anything here has
+    touched the GPU -- and exits with its status (the reference's fan-out is
+    likewise one call, self_play.py:98-110).  Returns None when this process
+    is a rank and should run the benchmark."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}; refusing to report a mislabelled run",
+                  file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_device(eng, where):
+    """The engine's device error word after a window of asynchronous steps
+    (az_selfplay_step without stats returns before the kernels finish): a
+    flagged window is not reported."""
+    st = eng.stats()
+    if st["errors"]:
+        print(f"bench.py: device error flags {st['errors']:#x} after {where}; no result reported", file=sys.stderr)
+        sys.exit(3)
+    return st
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     if args.game == "chess":
         return chess_main(args)
     rank = int(os.environ.get("RANK", "0"))
@@ -423,9 +517,10 @@ def main():
     spec = weight_spec(args.height, args.width, A, depth=args.depth)
     host_w = init_weights(spec, seed=0)
 
-    base = base0 = None
+    base = base0 = native = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline(args, host_w)
+        native = cpu_baseline_native(args, host_w)
         if (args.height, args.width, args.n) == (6, 7, 4) and args.cpu_configs0_seconds > 0:
             base0 = cpu_configs0(args, host_w)
 
@@ -437,6 +532,10 @@ def main():
     SUM = dist.ReduceOp.SUM if world > 1 else None
     MAX = dist.ReduceOp.MAX if world > 1 else None
     dev_index, dev = _init_dist(args, world, local_rank)
+    devices = [dev_index]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, dev_index)
     # weights: rank 0's init, one flat RCCL broadcast (~5 MB) to every rank
     named, _flat = _device_weights(spec, host_w, rank, world, args, dev)
 
@@ -464,6 +563,7 @@ def main():
         if done or pre >= MAX_PREROLL:
             break
 
+    check_device(eng, "the untimed moves")
     # ---- timed window: K steps, each drained to the host
     window = WindowGames()
     if world > 1:
@@ -488,7 +588,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    st1 = eng.stats()
+    st1 = check_device(eng, "the timed window")
     eng.timer(False)
     d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
                                       "terminal_visits", "cache_hits", "evaluations", "cache_inserts")}
@@ -572,20 +672,20 @@ def main():
     if st1["active_slots"] < args.slots:
         print(f"warning: rank {rank} ran out of game budget", file=sys.stderr)
 
-    # dominant kernel: the residual tower's 3x3 convs (8 launches per forward at
-    # depth 4).  Direct FLOP = SURVEY.md 8d's count (19 F*F MACs per pixel per
-    # block: 9F + 9F + the 1x1 F); conv16_kernel issues each MAC as three fp16
-    # MFMA products.
+    # dominant kernel: the forward's residual-tower convs -- one tower16_kernel
+    # launch per forward (AZ_CONV_F16X2), else one launch per conv.  Direct
+    # FLOP = SURVEY.md 8d's count (19 F*F MACs per pixel per block: 9F + 9F +
+    # the 1x1 F); the fp16x2 kernels issue each MAC as three fp16 products.
     HW, F = args.height * args.width, 128
     direct_flop = HW * 2 * F * F * 19 * args.depth
-    issued = 3 * direct_flop if args.conv_algo == 0 else direct_flop  # fp16x2: 3 products per MAC
+    issued = 3 * direct_flop if args.conv_algo != 1 else direct_flop
+    per_forward = 1 if args.conv_algo == 0 else 2 * args.depth
     conv_avg_ms = conv_ms / max(conv_launches, 1)
-    boards_per_launch = local_evals / max(conv_launches / (2 * args.depth), 1)
-    pmc = os.path.join(REPO, "profiles", "r2", "pmc_conv_traffic.json")
-    if not os.path.exists(pmc):
-        pmc = os.path.join(REPO, "profiles", "r1", "pmc_conv_traffic.json")
-    roof = conv_roofline(args, args.conv_algo, boards_per_launch, conv_avg_ms, busy_ms, local_evals,
-                         conv_launches, direct_flop, issued, pmc)
+    boards_per_launch = local_evals / max(conv_launches / per_forward, 1)
+    pmc = os.path.join(REPO, "profiles", "r3", "pmc_conv_traffic.json")
+    pmc_key = {0: "tower16", 1: "direct", 2: "f16x2"}[args.conv_algo]
+    roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, conv_avg_ms, busy_ms, local_evals,
+                         conv_launches, direct_flop, issued, pmc, pmc_key)
 
     # the same kernels alone on one stream at the live per-lane batch (what a
     # launch costs without the other lane's kernels sharing the CUs)
@@ -601,7 +701,7 @@ def main():
         si = eng.stats()
         eng.timer(False)
         iso_ms = si["conv_ms"] / max(si["conv_launches"], 1)
-        iso = nb * issued / (2 * args.depth) / (iso_ms * 1e-3) / 1e12
+        iso = nb * direct_flop / per_forward / (iso_ms * 1e-3) / 1e12
         roof["isolated"] = {"boards": nb, "avg_launch_ms": round(iso_ms, 4), "achieved": round(iso, 2),
                             "frac": round(iso / roof["peak"], 4)}
 
@@ -623,6 +723,8 @@ def main():
             "value": round(drained_all / elapsed, 3),
             "unit": "games/s",
             "n_gpus": world,
+            "rank_devices": devices,
+            "dist_backend": args.dist_backend if world > 1 else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
@@ -681,10 +783,13 @@ def main():
             "roofline": roof,
             "replay_buffer_gather": gather,
             "cpu_baseline": base,
+            "cpu_baseline_native": native,
             "cpu_baseline_configs0": base0,
         }
         if base:
             line["gpu_over_cpu"] = round(line["value"] / base["value"], 1) if base["value"] else None
+        if native:
+            line["gpu_over_cpu_native"] = round(line["value"] / native["value"], 1) if native["value"] else None
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

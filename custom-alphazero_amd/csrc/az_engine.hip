@@ -378,6 +378,23 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
   std::vector<double> w, b, wr, br;
   int rc;
   if ((rc = fold_unit(m, "stem", 3, in_ch, F, eps, w, b))) return rc;
+  // host copies for the one-launch tower (tower16_kernel): its stem pack and the small-weight blob
+  const bool tower = in_ch == 4 && net.use_tower;
+  std::vector<float> tb_b1, tb_b2, tb_stemb(b.begin(), b.end()), tb_pcw, tb_vcw, tb_hb(4, 0.f), tb_pdw, tb_pdb,
+      tb_v1w, tb_v1b, tb_v2w;
+  uint16_t* stem16 = nullptr;
+  float stem_s = 1.f;
+  if (tower) {
+    const int e = conv16_prescale(w.data(), w.size(), nullptr, 0);
+    std::vector<uint16_t> pack;
+    tower16_stem_pack(w.data(), e, pack);
+    stem_s = std::ldexp(1.f, e - 12);
+    void* q = nullptr;
+    AZ_HIP(hipMalloc(&q, pack.size() * sizeof(uint16_t)));
+    owned.push_back(q);
+    stem16 = reinterpret_cast<uint16_t*>(q);
+    AZ_HIP(hipMemcpy(q, pack.data(), pack.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  }
   {
     std::vector<float> bs(F);
     for (int i = 0; i < F; ++i) bs[i] = (float)b[i];
@@ -411,6 +428,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     for (int n2 = 0; n2 < F; ++n2)
       for (int k = 0; k < 9 * F; ++k) wt[(size_t)n2 * 9 * F + k] = (float)w[(size_t)k * F + n2];
     for (int i = 0; i < F; ++i) bt[i] = (float)b[i];
+    tb_b1.insert(tb_b1.end(), bt.begin(), bt.end());
     if ((rc = upload(owned, &net.c1_w[d], pack_fragments(wt, F, 9 * F))) ||
         (rc = upload_conv16(owned, &net.k1[d], &net.k1_scale[d], w, F, nullptr)) ||
         (rc = upload(owned, &net.c1_b[d], bt)))
@@ -423,6 +441,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       for (int c = 0; c < F; ++c) wt2[(size_t)n2 * 10 * F + 9 * F + c] = (float)wr[(size_t)c * F + n2];
     }
     for (int i = 0; i < F; ++i) bt2[i] = (float)(b[i] + br[i]);
+    tb_b2.insert(tb_b2.end(), bt2.begin(), bt2.end());
     if ((rc = upload(owned, &net.c2_w[d], pack_fragments(wt2, F, 10 * F))) ||
         (rc = upload_conv16(owned, &net.k2[d], &net.k2_scale[d], w, F, &wr)) ||
         (rc = upload(owned, &net.c2_b[d], bt2)))
@@ -432,11 +451,16 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
   if ((rc = fold_unit(m, "policy.conv", 1, F, 2, eps, w, b))) return rc;
   {
     std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    tb_pcw = a;
+    tb_hb[0] = c[0];
+    tb_hb[1] = c[1];
     if ((rc = upload(owned, &net.pc_w, a)) || (rc = upload(owned, &net.pc_b, c))) return rc;
   }
   if ((rc = fold_unit(m, "value.conv", 1, F, 1, eps, w, b))) return rc;
   {
     std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
+    tb_vcw = a;
+    tb_hb[2] = c[0];
     if ((rc = upload(owned, &net.vc_w, a)) || (rc = upload(owned, &net.vc_b, c))) return rc;
   }
   struct DenseSpec {
@@ -452,6 +476,16 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     if ((rc = fetch(m, std::string(ds.name) + ".bias", ds.out, b))) return rc;
     std::vector<float> a(w.begin(), w.end()), c(b.begin(), b.end());
     if ((rc = upload(owned, ds.w, a)) || (rc = upload(owned, ds.b, c))) return rc;
+    if (ds.w == &net.pd_w) {
+      tb_pdw = a;
+      tb_pdb = c;
+    } else if (ds.w == &net.v1_w) {
+      tb_v1w = a;
+      tb_v1b = c;
+    } else {
+      tb_v2w = a;
+      tb_hb[3] = c[0];
+    }
     if (ds.w == &net.pd_w && A > kMaxActions) {
       const int K = ds.in, tiles = (A + 63) / 64;
       std::vector<float> t((size_t)tiles * K * 64, 0.f);
@@ -460,29 +494,42 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       if ((rc = upload(owned, &net.pd_wt, t))) return rc;
     }
   }
-  if (in_ch == 4 && net.use_tower) {
+  if (tower) {
     if (net.depth > kTowerMaxDepth || net.hidden > 256) return fail(AZ_E_INVALID, "tower: depth/hidden too large");
     TowerNet tn{};
     for (int d = 0; d < net.depth; ++d) {
       tn.k1[d] = reinterpret_cast<const uint4*>(net.k1[d]);
       tn.k2[d] = reinterpret_cast<const uint4*>(net.k2[d]);
-      tn.b1[d] = net.c1_b[d];
-      tn.b2[d] = net.c2_b[d];
       tn.s1[d] = net.k1_scale[d];
       tn.s2[d] = net.k2_scale[d];
     }
-    tn.stem_w = net.stem_w;
-    tn.stem_b = net.stem_b;
-    tn.wpc = net.pc_w;
-    tn.bpc = net.pc_b;
-    tn.wvc = net.vc_w;
-    tn.bvc = net.vc_b;
-    tn.wpd = net.pd_w;
-    tn.bpd = net.pd_b;
-    tn.wv1 = net.v1_w;
-    tn.bv1 = net.v1_b;
-    tn.wv2 = net.v2_w;
-    tn.bv2 = net.v2_b;
+    tn.stem16 = reinterpret_cast<const uint4*>(stem16);
+    tn.stem_s = stem_s;
+    // the small-weight blob (TowerNet), every part padded to a multiple of 4 floats
+    std::vector<float> blob;
+    auto put = [&](const std::vector<float>& v) {
+      const int off = (int)blob.size();
+      blob.insert(blob.end(), v.begin(), v.end());
+      while (blob.size() % 4) blob.push_back(0.f);
+      return off;
+    };
+    tn.off_b1 = put(tb_b1);
+    tn.off_b2 = put(tb_b2);
+    tn.off_stemb = put(tb_stemb);
+    tn.off_wpc = put(tb_pcw);
+    tn.off_wvc = put(tb_vcw);
+    tn.off_hb = put(tb_hb);
+    tn.off_bpd = put(tb_pdb);
+    tn.off_wpd = put(tb_pdw);
+    tn.off_bv1 = put(tb_v1b);
+    tn.off_wv2 = put(tb_v2w);
+    tn.off_wv1 = put(tb_v1w);
+    tn.blob_floats = (int)blob.size();
+    // wv1 (HW x hidden) joins the staged prefix when the workgroup's LDS holds it
+    tn.wv1_lds = tower16_lds_bytes(HW, tn.blob_floats) <= kTowerLdsMax;
+    tn.staged_floats = tn.wv1_lds ? tn.blob_floats : tn.off_wv1;
+    if (tower16_lds_bytes(HW, tn.staged_floats) > kTowerLdsMax)
+      return fail(AZ_E_INVALID, "tower: the board's head weights do not fit LDS (use AZ_CONV_F16X2_LAYERS)");
     tn.depth = net.depth;
     tn.hidden = net.hidden;
     if (!net.tower) {
@@ -491,7 +538,13 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       owned.push_back(q);
       net.tower = reinterpret_cast<TowerNet*>(q);
     }
+    void* qb = nullptr;
+    AZ_HIP(hipMalloc(&qb, blob.size() * sizeof(float)));
+    owned.push_back(qb);
+    AZ_HIP(hipMemcpy(qb, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice));
+    tn.blob = reinterpret_cast<const float*>(qb);
     AZ_HIP(hipMemcpy(net.tower, &tn, sizeof(TowerNet), hipMemcpyHostToDevice));
+    net.tower_staged = tn.staged_floats;
   }
   net.ready = true;
   return 0;

@@ -41,6 +41,7 @@
 // the tile or on the rest of the batch -- the oracle replay tests rely on it.
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 
 #include "az_nn.h"
 #include "az_tree.h"
@@ -53,12 +54,79 @@ typedef float t_f4 __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr float kRange = 32752.f;  // largest |x| a split16 term pair holds
-constexpr int kThreads = 512;
+// LDS activation rows: 34 16-byte slots (term 0 of the 128 channels in slots
+// 0..15, term 1 in 16..31, two pad slots).  A row's slot s sits in bank quad
+// (2 row + s) mod 16: a ds_read_b128 lane group (8 consecutive rows at slot g
+// and the same 8 at g + 1) covers the even quads with one half and the odd
+// ones with the other, for any tap shift, with no swizzle, and a chunk's slot
+// is an immediate offset (PMC: a 33-slot pitch conflicted 2-way).  8 zero rows
+// follow the tile: an off-board tap of row r reads zero row (r & 7), the quad
+// its own row has.
+constexpr int kPitch = 544;
+constexpr int kZeroRows = 8;
 
-__device__ __forceinline__ int phys_slot(int x, int j) { return (j & 16) | ((j + 2 * x) & 15); }
+#ifdef AZ_T16_STAMPS  // diagnostic build only: phase clocks of wave 0 per workgroup (az_t16_stamps)
+constexpr int kStampBlocks = 4096, kStamps = 48;
+__device__ unsigned long long g_t16_stamps[kStampBlocks][kStamps];
+#define T16_STAMP(k)                                                             \
+  if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) {                           \
+    g_t16_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();                  \
+  }
+#define T16_RSTAMP(k)                                                            \
+  if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) {                           \
+    g_t16_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();              \
+  }
+#define T16_STAMP4(k)  /* wave 4 (wave 0's SIMD partner) */                    \
+  if (threadIdx.x == 256 && blockIdx.x < kStampBlocks) {                         \
+    g_t16_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();                  \
+  }
+#else
+#define T16_STAMP4(k)
+#define T16_STAMP(k)
+#define T16_RSTAMP(k)
+#endif
 
-__device__ __forceinline__ t_h8 unscale_b0(const uint4 v) {
-  return __builtin_bit_cast(t_h8, v) * (_Float16)0.000244140625f;
+// Pointers read from the TowerNet struct are generic to the compiler, and a
+// generic load is a FLAT load: counted in both vmcnt and lgkmcnt and waited
+// for with vmcnt(0) -- which waited out the whole B prefetch every k-step.
+// Every global read goes through this cast (global_load_*).
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gbl(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+// the same for class types (float4, uint4, Board): a global load of their bits
+template <typename T>
+__device__ __forceinline__ T gld(const T* p) {
+  static_assert(sizeof(T) % 4 == 0, "32-bit words");
+  typedef unsigned int V __attribute__((ext_vector_type(sizeof(T) / 4)));
+  return __builtin_bit_cast(T, *(const __attribute__((address_space(1))) V*)p);
+}
+
+
+// The tower's activation terms: x ~= t0 + t1 with t0 = fp16_rn(x) and t1 =
+// fp16_rn(x - t0) (the subtraction exact), NOT scaled by 2^12 like az_nn.h's
+// split16: then t1 * B0 (B0 = 2^12 b0, the pack's main weight term) is the
+// correction product at the main term's scale and the K loop needs no b0.
+// t1 reaches the fp16 subnormals below |x| ~ 2^-3; its absolute error there
+// is <= 2^-25, far inside the 1e-5 network tolerance (measured ~2e-8).
+__device__ __forceinline__ void split_u4(const float4 v, uint2& t0, uint2& t1) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t p[2], q[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    p[i] = pk_f16(x[2 * i], x[2 * i + 1]);
+    const az_h2 h = __builtin_bit_cast(az_h2, p[i]);
+    q[i] = pk_f16(x[2 * i] - (float)h[0], x[2 * i + 1] - (float)h[1]);
+  }
+  t0 = make_uint2(p[0], p[1]);
+  t1 = make_uint2(q[0], q[1]);
+}
+__device__ __forceinline__ void split_u8(const float (&x)[8], uint4& t0, uint4& t1) {
+  uint2 a0, a1, b0, b1;
+  split_u4(make_float4(x[0], x[1], x[2], x[3]), a0, a1);
+  split_u4(make_float4(x[4], x[5], x[6], x[7]), b0, b1);
+  t0 = make_uint4(a0.x, a0.y, b0.x, b0.y);
+  t1 = make_uint4(a1.x, a1.y, b1.x, b1.y);
 }
 
 __device__ __forceinline__ float wsum(float v) {
@@ -85,16 +153,16 @@ struct TowerSmem {
   int sc[2][kTowerMaxBoards];  // per-board scale exponent of the two activation buffers' contents
   unsigned bmax[kTowerMaxBoards];  // board maxima (float bits, values >= 0) on the rare rescale path
   float vred[kTowerMaxBoards][4];  // value-head partial sums per board and wave
+  Board boards[kTowerMaxBoards];   // the tile's boards (self-play input)
 };
 
 // store 4 channels (channel quad cq) of activation row r as split16 terms
 __device__ __forceinline__ void put4(uint4* act, int r, int cq, const float4 y) {
   uint2 t0, t1;
-  split16x4(y, t0, t1);
-  char* row = reinterpret_cast<char*>(act) + (size_t)r * 512;
-  const int j = cq >> 1, half = (cq & 1) * 8;
-  *reinterpret_cast<uint2*>(row + phys_slot(r, j) * 16 + half) = t0;
-  *reinterpret_cast<uint2*>(row + phys_slot(r, 16 + j) * 16 + half) = t1;
+  split_u4(y, t0, t1);
+  char* q = reinterpret_cast<char*>(act) + r * kPitch + cq * 8;
+  *reinterpret_cast<uint2*>(q) = t0;
+  *reinterpret_cast<uint2*>(q + 256) = t1;
 }
 
 __device__ __forceinline__ float max4(const float4 v) { return fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)); }
@@ -102,32 +170,32 @@ __device__ __forceinline__ float4 scale4(const float4 v, float s) {
   return make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
 }
 
-// Store one layer's output (NI float4 items per thread: row, channel quad,
-// board, value >= 0; row < 0 = no item).  Optimistic at scale 0; if any
+// Store one layer's output (2*MBW float4 items per thread, values >= 0).  Optimistic at scale 0; if any
 // value left the split16 range, the boards concerned are stored again at
 // their scale.  Returns whether any board of this buffer is scaled (then
 // sc_out holds the exponents).  Contains the barrier that publishes the
 // stores.  `par` alternates per layer (flag[par] is this layer's).
-template <int NI>
-__device__ __forceinline__ bool store_layer(uint4* act, const int (&row_)[NI], const int (&cq_)[NI], const int (&brd_)[NI],
-                            const float4 (&y)[NI], TowerSmem& sm, int par, int* sc_out, int nbrd,
-                            unsigned long long* err) {
-  // rows, quads and boards laundered (as in k_loop): the addresses derived
-  // from them are recomputed here, not hoisted out of the depth loop and spilled
-  int row[NI], cq[NI], brd[NI];
+template <int MBW>
+__device__ __forceinline__ bool store_layer(uint4* act, const int (&r_)[MBW], const bool (&valid_)[MBW],
+                                            const int (&brd_)[MBW], int cq0, const float4 (&y)[2 * MBW],
+                                            TowerSmem& sm, int par, int* sc_out, int nbrd,
+                                            unsigned long long* err) {
+  // item mb*2 + nb: row r[mb] (if valid), channel quad cq0 + 4 nb, board brd[mb];
+  // rows and boards laundered (as in k_loop): the addresses derived from them
+  // are recomputed here, not hoisted out of the depth loop and spilled
+  int row[MBW], brd[MBW];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    row[i] = row_[i];
-    cq[i] = cq_[i];
-    brd[i] = brd_[i];
-    asm volatile("" : "+v"(row[i]), "+v"(cq[i]), "+v"(brd[i]));
+  for (int mb = 0; mb < MBW; ++mb) {
+    row[mb] = valid_[mb] ? r_[mb] : -1;
+    brd[mb] = brd_[mb];
+    asm volatile("" : "+v"(row[mb]), "+v"(brd[mb]));
   }
   float vmax = 0.f;
 #pragma unroll
-  for (int i = 0; i < NI; ++i)
-    if (row[i] >= 0) {
+  for (int i = 0; i < 2 * MBW; ++i)
+    if (row[i / 2] >= 0) {
       vmax = fmaxf(vmax, max4(y[i]));
-      put4(act, row[i], cq[i], y[i]);
+      put4(act, row[i / 2], cq0 + 4 * (i & 1), y[i]);
     }
   if (!(vmax <= kRange)) sm.flag[par] = 1;  // also NaN
   if (threadIdx.x == 0) sm.flag[par ^ 1] = 0;  // next layer's flag (nobody reads it before then)
@@ -137,16 +205,16 @@ __device__ __forceinline__ bool store_layer(uint4* act, const int (&row_)[NI], c
   if ((int)threadIdx.x < nbrd) sm.bmax[threadIdx.x] = 0u;
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < NI; ++i)
-    if (row[i] >= 0) atomicMax(&sm.bmax[brd[i]], __float_as_uint(max4(y[i])));
+  for (int i = 0; i < 2 * MBW; ++i)
+    if (row[i / 2] >= 0) atomicMax(&sm.bmax[brd[i / 2]], __float_as_uint(max4(y[i])));
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    if (row[i] < 0) continue;
-    const float m = __uint_as_float(sm.bmax[brd[i]]);
+  for (int i = 0; i < 2 * MBW; ++i) {
+    if (row[i / 2] < 0) continue;
+    const float m = __uint_as_float(sm.bmax[brd[i / 2]]);
     if (!(m <= 3.0e38f)) continue;  // inf/NaN: flagged below, nothing to rescale
     const int s = range_exp(m);
-    if (s) put4(act, row[i], cq[i], scale4(y[i], ldexpf(1.f, -s)));
+    if (s) put4(act, row[i / 2], cq0 + 4 * (i & 1), scale4(y[i], ldexpf(1.f, -s)));
   }
   if ((int)threadIdx.x < nbrd) {
     const float m = __uint_as_float(sm.bmax[threadIdx.x]);
@@ -161,22 +229,41 @@ __device__ __forceinline__ bool store_layer(uint4* act, const int (&row_)[NI], c
   return true;
 }
 
-// one k-step's 6*MBW MFMAs: weights as the A operand, so D = out^T
+// one k-step's 6*MBW MFMAs: weights as the A operand, so D = out^T; per
+// (M block, N block): t1*B0 + t0*b1 + t0*B0 (= 2^12 x w' up to the dropped
+// t1*b1), smallest first
 template <int MBW>
-__device__ __forceinline__ void mfma_kstep(t_f4 (&C)[MBW][2], const uint4 (&a)[MBW][2], const t_h8 B00,
-                                           const t_h8 B01, const t_h8 B10, const t_h8 B11, const t_h8 b00,
-                                           const t_h8 b10) {
+__device__ __forceinline__ void mfma_kstep(t_f4 (&C)[MBW][2], const uint4 (&a)[MBW][2], const uint4 (&b)[4]) {
+  const t_h8 B0[2] = {__builtin_bit_cast(t_h8, b[0]), __builtin_bit_cast(t_h8, b[2])};
+  const t_h8 B1[2] = {__builtin_bit_cast(t_h8, b[1]), __builtin_bit_cast(t_h8, b[3])};
+#ifdef AZ_T16_CHAIN  // A/B: each accumulator's three products back to back
 #pragma unroll
-  for (int mb = 0; mb < MBW; ++mb) {
-    const t_h8 a0 = __builtin_bit_cast(t_h8, a[mb][0]);
-    const t_h8 a1 = __builtin_bit_cast(t_h8, a[mb][1]);
-    C[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b00, a1, C[mb][0], 0, 0, 0);
-    C[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B01, a0, C[mb][0], 0, 0, 0);
-    C[mb][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B00, a0, C[mb][0], 0, 0, 0);
-    C[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b10, a1, C[mb][1], 0, 0, 0);
-    C[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B11, a0, C[mb][1], 0, 0, 0);
-    C[mb][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B10, a0, C[mb][1], 0, 0, 0);
-  }
+  for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][1]), C[mb][nb], 0, 0, 0);
+      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
+      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
+    }
+#else
+  // term-major: 2*MBW independent accumulators between an accumulator's
+  // dependent products (the same per-element order, so the same bits)
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][1]), C[mb][nb], 0, 0, 0);
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
+#endif
 }
 
 #ifndef AZ_T16_PF
@@ -195,8 +282,8 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
                                        t_f4 (&accr)[MBW][2], const int (&r_)[MBW], const int (&py_)[MBW],
                                        const int (&px_)[MBW], const bool (&valid_)[MBW], int H, int W,
                                        int zrow, int nq, int lane) {
-  static_assert(R == 0 || R == 4, "ring slots = k-step mod 4");
-  constexpr int PF = AZ_T16_PF, NB = 4;
+  static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
+  constexpr int PF = AZ_T16_PF, NB = PF == 1 ? 2 : 4;
   static_assert(PF >= 1 && PF <= 3, "prefetch depth");
   const int gq = lane >> 4;
   // the tap geometry laundered through an empty asm per call: the k-loops sit
@@ -214,22 +301,25 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     valid[mb] = v != 0;
   }
   const uint4* wm = wmain + (size_t)(nq * 2) * 2 * 64 + lane;
-  const uint4* wr = R ? wres + (size_t)(nq * 2) * 2 * 64 + lane + (size_t)36 * 1024 : nullptr;
+  const uint4* wr = R ? wres + (size_t)(nq * 2) * 2 * 64 + lane + (size_t)36 * 1024 : wmain;
   uint4 bq[NB][4];
   auto load_b = [&](const uint4* p, uint4(&dst)[4]) {
+#ifdef AZ_T16_DIAG_NOB  // diagnostic (wrong outputs): no weight stream in the loop
+    if (&dst != &bq[0] && &dst != &bq[1]) return;
+#endif
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = p[q * 64];
+    for (int q = 0; q < 4; ++q) dst[q] = gld(p + q * 64);
   };
   // k-step s of the phase -> its B fragments (s < R: residual)
   auto bsrc = [&](int s) { return s < R ? wr + (size_t)s * 1024 : wm + (size_t)(s - R) * 1024; };
 
-  int abase[MBW], akey[MBW];
+  // per M block: the byte address of the tap row's term-0 slot gq; chunk c
+  // and term 1 are immediate offsets (+64 c, +256)
+  int aaddr[MBW];
+  const char* actb = reinterpret_cast<const char*>(act);
   auto set_own = [&]() {
 #pragma unroll
-    for (int mb = 0; mb < MBW; ++mb) {
-      abase[mb] = (valid[mb] ? r[mb] : zrow) * 32;
-      akey[mb] = r[mb];
-    }
+    for (int mb = 0; mb < MBW; ++mb) aaddr[mb] = (valid[mb] ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
   };
   auto set_tap = [&](int t) {  // runtime tap
     const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
@@ -237,45 +327,56 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     for (int mb = 0; mb < MBW; ++mb) {
       const bool ok = valid[mb] && py[mb] + dy >= 0 && py[mb] + dy < H && px[mb] + dx >= 0 && px[mb] + dx < W;
       const int sr = r[mb] + dy * W + dx;
-      abase[mb] = (ok ? sr : zrow) * 32;
-      akey[mb] = sr;  // also for the zero row: the lane keeps its bank quad
+      aaddr[mb] = (ok ? sr : zrow + (sr & 7)) * kPitch + gq * 16;
     }
   };
-  uint4 aq[2][MBW][2];
-  auto load_a = [&](int chunk, uint4(&dst)[MBW][2]) {
+  // activation fragments, one buffer: an M block's fragments for the next
+  // k-step are read right after its last MFMA of this one, and the other
+  // MBW - 1 blocks' MFMAs hide the LDS latency
+  uint4 aq[MBW][2];
+  auto load_a1 = [&](int chunk, int mb) {
+    const char* q = actb + aaddr[mb] + 64 * chunk;
+    aq[mb][0] = *reinterpret_cast<const uint4*>(q);
+    aq[mb][1] = *reinterpret_cast<const uint4*>(q + 256);
+  };
+  // one k-step: per M block its 6 MFMAs (t1*B0 + t0*b1 + t0*B0 per N block,
+  // smallest first), then its reads for the next k-step (next_chunk < 0: none;
+  // the caller moved aaddr to the next tap first when the tap changes)
+  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], int next_chunk) {
+    const t_h8 B0[2] = {__builtin_bit_cast(t_h8, b[0]), __builtin_bit_cast(t_h8, b[2])};
+    const t_h8 B1[2] = {__builtin_bit_cast(t_h8, b[1]), __builtin_bit_cast(t_h8, b[3])};
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      const int sl = phys_slot(akey[mb], 4 * chunk + gq);
-      dst[mb][0] = act[abase[mb] + sl];
-      dst[mb][1] = act[abase[mb] + 16 + sl];
+      const t_h8 a0 = __builtin_bit_cast(t_h8, aq[mb][0]), a1 = __builtin_bit_cast(t_h8, aq[mb][1]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a1, C[mb][nb], 0, 0, 0);
+        C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], a0, C[mb][nb], 0, 0, 0);
+        C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a0, C[mb][nb], 0, 0, 0);
+      }
+      if (next_chunk >= 0) load_a1(next_chunk, mb);
     }
-  };
-  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], const uint4(&a)[MBW][2]) {
-    const t_h8 B00 = __builtin_bit_cast(t_h8, b[0]), B01 = __builtin_bit_cast(t_h8, b[1]);
-    const t_h8 B10 = __builtin_bit_cast(t_h8, b[2]), B11 = __builtin_bit_cast(t_h8, b[3]);
-    mfma_kstep<MBW>(C, a, B00, B01, B10, B11, unscale_b0(b[0]), unscale_b0(b[2]));
   };
 
 #pragma unroll
   for (int k = 0; k < PF; ++k) load_b(bsrc(k), bq[k]);
   if (R) set_own();
   else set_tap(0);
-  load_a(0, aq[0]);
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb) load_a1(0, mb);
   // ---- residual k-steps (static)
 #pragma unroll
   for (int s = 0; s < R; ++s) {
     __builtin_amdgcn_sched_barrier(0);
     load_b(bsrc(s + PF), bq[(s + PF) % NB]);
-    if (s + 1 < R) {
-      load_a(s + 1, aq[(s + 1) & 1]);
-    } else {
+    if (s + 1 == R) {
+      // the next k-step is tap 0's first chunk: the addresses move before the
+      // per-block reads (this k-step's MFMAs read registers only)
       set_tap(0);
-      load_a(0, aq[(s + 1) & 1]);
+      kstep(accr, bq[s % NB], 0);
+    } else {
+      kstep(accr, bq[s % NB], s + 1);
     }
-    kstep(accr, bq[s % NB], aq[s & 1]);
-    __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);        // VMEM reads (B, PF ahead)
-    __builtin_amdgcn_sched_group_barrier(0x0100, 2 * MBW, 0);  // DS reads (A, next k-step)
-    __builtin_amdgcn_sched_group_barrier(0x0008, 6 * MBW, 0);  // MFMA
   }
   // ---- 9 taps x 4 chunks
 #pragma unroll 1
@@ -287,21 +388,37 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
       const int ahead = 4 * t + c + PF;
       if (c + PF < 4 || t < 8) load_b(wm + (size_t)ahead * 1024, bq[(c + PF) % NB]);
       if (c < 3) {
-        load_a(c + 1, aq[(c + 1) & 1]);
+        kstep(acc, bq[c % NB], c + 1);
       } else if (t < 8) {
         set_tap(t + 1);
-        load_a(0, aq[0]);
+        kstep(acc, bq[c % NB], 0);
+      } else {
+        kstep(acc, bq[c % NB], -1);
       }
-      kstep(acc, bq[c % NB], aq[c & 1]);
-      __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x0100, 2 * MBW, 0);
-      __builtin_amdgcn_sched_group_barrier(0x0008, 6 * MBW, 0);
     }
   }
 }
 
-template <int MBW>
-__global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __restrict__ net,
+// LDS-DMA of n_u4 16-byte words from global src into LDS dst (both
+// 16-byte aligned), the workgroup's waves in turn: no VGPRs, completes in the
+// background (the first vmcnt wait of a K loop covers it)
+template <int NT>
+__device__ __forceinline__ void dma_to_lds(uint4* dst, const float* src, int n_u4, int wave, int lane) {
+  if (n_u4 <= 0) return;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, n_u4 * 16, 0x00020000);
+  for (int base = wave * 64; base < n_u4; base += NT) {  // wave-uniform
+    const int i = base + lane;
+    const unsigned voff = i < n_u4 ? (unsigned)(i * 16) : 0x80000000u;  // past the end: range-checked to 0
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(dst + base), 16,
+                                             voff, 0, 0, 0);
+  }
+}
+
+// MBT 16-row M blocks per tile (8: 128 rows, 6: 96); NWM wave groups over M:
+// 2 = 8 waves, two per SIMD, each MBT/2 blocks; 1 = 4 waves, one per SIMD,
+// each all MBT blocks of its 32 output channels
+template <int MBT, int NWM>
+__global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet* __restrict__ net,
                                                                const Board* __restrict__ boards,
                                                                const float4* __restrict__ x,
                                                                const int* __restrict__ count, int n_static,
@@ -309,10 +426,13 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
                                                                float* __restrict__ probs,
                                                                float* __restrict__ values,
                                                                unsigned long long* __restrict__ err) {
-  constexpr int TR = 32 * MBW;  // tile rows (two M halves of MBW 16-row blocks)
-  extern __shared__ __attribute__((aligned(16))) uint4 act[];  // [TR + 1][32]: rows, then the zero row
-  TowerSmem& sm = *reinterpret_cast<TowerSmem*>(act + (TR + 1) * 32);
+  constexpr int MBW = MBT / NWM;  // M blocks per wave
+  constexpr int TR = 16 * MBT;    // tile rows
+  constexpr int NT = NWM * 256;
+  extern __shared__ __attribute__((aligned(16))) uint4 act[];  // [TR + kZeroRows] rows of kPitch bytes
+  TowerSmem& sm = *reinterpret_cast<TowerSmem*>(reinterpret_cast<char*>(act) + (TR + kZeroRows) * kPitch);
   float* red = reinterpret_cast<float*>(&sm + 1);  // [TR][4][3] heads partial sums
+  float* blob = red + TR * 12;                     // the staged small weights (TowerNet::blob)
 
   const int HW = H * W;
   const int n = count ? *count : n_static;
@@ -323,80 +443,18 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int zrow = TR;
   const TowerNet& T = *net;
-
-  if (tid < 32) act[zrow * 32 + tid] = make_uint4(0u, 0u, 0u, 0u);
+  T16_RSTAMP(22);
+  T16_STAMP(0);
+#ifdef AZ_T16_PRIO  // A/B: the second-dispatched half of the waves at priority 1 (MI355X_MICROARCH.md 2-waves item 4)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+  // small weights into LDS, in the background of the stem
+  dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob, T.staged_floats / 4, wave, lane);
+  for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 2) sm.flag[tid] = 0;
-  __syncthreads();  // the flags before any layer may set one
+  if (boards && tid < nbrd) sm.boards[tid] = gld(boards + b0 + tid);
+  __syncthreads();  // the flags before any layer may set one; the boards
 
-  // ---------------------------------------------------------------- stem
-  // conv3x3 4 -> F + folded BN + ReLU, fp32 on the VALU: the fmaf chain of
-  // stem_conv_kernel (az_nn.hip), from the one-hot planes x or, bitwise the
-  // same, from the boards (only the two nonzero terms per in-board tap)
-  constexpr int NIS = TR * 32 / kThreads;
-  int srow[NIS], scq[NIS], sbrd[NIS];
-  float4 sy[NIS];
-#pragma unroll
-  for (int i = 0; i < NIS; ++i) {
-    const int idx = tid + i * kThreads;
-    const int rr = idx >> 5, cg = idx & 31;
-    srow[i] = rr < live ? rr : -1;
-    scq[i] = cg;
-    sbrd[i] = 0;
-    sy[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rr >= live) continue;
-    const int b = rr / HW, p = rr - b * HW;
-    sbrd[i] = b;
-    const int y0 = p / W, x0 = p - y0 * W;
-    float4 acc = reinterpret_cast<const float4*>(T.stem_b)[cg];
-    const float4* ws = reinterpret_cast<const float4*>(T.stem_w);
-    if (boards) {
-      const Board bd = boards[b0 + b];
-      const uint64_t own0 = bd.own[0], own1 = bd.own[1], opp0 = bd.opp[0], opp1 = bd.opp[1];
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ny = y0 + tap / 3 - 1, nx = x0 + tap % 3 - 1;
-        if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
-        const int q = ny * W + nx;
-        const uint64_t ow = q < 64 ? own0 : own1, op = q < 64 ? opp0 : opp1;
-        const int sh = q & 63;
-        const int st = ((ow >> sh) & 1ull) ? 1 : (((op >> sh) & 1ull) ? 2 : 0);
-        const float4 w1 = ws[(tap * 4 + st) * 32 + cg];
-        const float4 w3 = ws[(tap * 4 + 3) * 32 + cg];
-        acc.x = fmaf(1.0f, w1.x, acc.x);
-        acc.y = fmaf(1.0f, w1.y, acc.y);
-        acc.z = fmaf(1.0f, w1.z, acc.z);
-        acc.w = fmaf(1.0f, w1.w, acc.w);
-        acc.x = fmaf(1.0f, w3.x, acc.x);
-        acc.y = fmaf(1.0f, w3.y, acc.y);
-        acc.z = fmaf(1.0f, w3.z, acc.z);
-        acc.w = fmaf(1.0f, w3.w, acc.w);
-      }
-    } else {
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ny = y0 + tap / 3 - 1, nx = x0 + tap % 3 - 1;
-        if (ny < 0 || ny >= H || nx < 0 || nx >= W) continue;
-        const float4 v = x[(size_t)(b0 + b) * HW + ny * W + nx];
-        const float vin[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float4 wv = ws[(tap * 4 + c) * 32 + cg];
-          acc.x = fmaf(vin[c], wv.x, acc.x);
-          acc.y = fmaf(vin[c], wv.y, acc.y);
-          acc.z = fmaf(vin[c], wv.z, acc.z);
-          acc.w = fmaf(vin[c], wv.w, acc.w);
-        }
-      }
-    }
-    sy[i] = make_float4(fmaxf(acc.x, 0.f), fmaxf(acc.y, 0.f), fmaxf(acc.z, 0.f), fmaxf(acc.w, 0.f));
-  }
-  int par = 0;
-  // scale state: buffer contents X (block input) and H (conv1 output)
-  bool anyX = store_layer<NIS>(act, srow, scq, sbrd, sy, sm, par, sm.sc[0], nbrd, err);
-  bool anyH = false;
-  par ^= 1;
-
-  // ---------------------------------------------------------------- tower
   const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
   int r[MBW], py[MBW], px[MBW], brd[MBW];
   bool valid[MBW];
@@ -410,18 +468,87 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
     py[mb] = p / W;
     px[mb] = p - py[mb] * W;
   }
-  int orow[2 * MBW], ocq[2 * MBW], obrd[2 * MBW];
-#pragma unroll
-  for (int mb = 0; mb < MBW; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      orow[mb * 2 + nb] = valid[mb] ? r[mb] : -1;
-      ocq[mb * 2 + nb] = 8 * nq + 4 * nb + gq;
-      obrd[mb * 2 + nb] = brd[mb];
-    }
-  const int depth = T.depth;
+  const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
   t_f4 acc[MBW][2], accr[MBW][2];
   float4 yv[2 * MBW];
+
+  // ---------------------------------------------------------------- stem
+  // conv3x3 4 -> F + folded BN + ReLU on the MFMA: k = tap*4 + plane (36 of
+  // two 32-wide k-steps), the im2col operand built in registers from the
+  // boards' bits (one-hot planes [empty, own, opp, 1], board.py:83-98: exact
+  // in fp16, second term 0) or from x split into two fp16 terms -- for a
+  // one-hot x the operands, and so the outputs, are bitwise the boards'.
+  {
+    const uint4* ws = T.stem16 + (size_t)(nq * 2) * 2 * 64 + lane;
+    uint4 bs[2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bs[ks][q] = gld(ws + (size_t)ks * 1024 + q * 64);
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 a[MBW][2];
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb) {
+        float v[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int t = 8 * ks + 2 * gq + h;  // tap of k = 32 ks + 8 gq + 4 h + plane
+          const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
+          const bool ok = t < 9 && valid[mb] && py[mb] + dy >= 0 && py[mb] + dy < H && px[mb] + dx >= 0 &&
+                          px[mb] + dx < W;
+          float4 pl = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok) {
+            const int q = (py[mb] + dy) * W + px[mb] + dx;
+            if (boards) {
+              const Board& bd = sm.boards[brd[mb]];
+              const uint64_t ow = q < 64 ? bd.own[0] : bd.own[1], op = q < 64 ? bd.opp[0] : bd.opp[1];
+              const bool o = (ow >> (q & 63)) & 1ull, e = (op >> (q & 63)) & 1ull;
+              pl = make_float4(o || e ? 0.f : 1.f, o ? 1.f : 0.f, e ? 1.f : 0.f, 1.f);
+            } else {
+              pl = gld(x + (size_t)(b0 + brd[mb]) * HW + q);
+            }
+          }
+          v[4 * h + 0] = pl.x;
+          v[4 * h + 1] = pl.y;
+          v[4 * h + 2] = pl.z;
+          v[4 * h + 3] = pl.w;
+        }
+        split_u8(v, a[mb][0], a[mb][1]);
+      }
+      mfma_kstep<MBW>(acc, a, bs[ks]);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
+  __syncthreads();                // ... and every wave's: the blob is readable
+  T16_STAMP(1);
+  {
+    const float osc = T.stem_s;
+    const float* bb = blob + T.off_stemb;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const float4 bc = *reinterpret_cast<const float4*>(bb + 32 * nq + 16 * nb + 4 * gq);
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb) {
+        const t_f4 a = acc[mb][nb];
+        yv[mb * 2 + nb] = make_float4(fmaxf(fmaf(a[0], osc, bc.x), 0.f), fmaxf(fmaf(a[1], osc, bc.y), 0.f),
+                                      fmaxf(fmaf(a[2], osc, bc.z), 0.f), fmaxf(fmaf(a[3], osc, bc.w), 0.f));
+      }
+    }
+  }
+  int par = 0;
+  // scale state: buffer contents X (block input) and H (conv1 output)
+  bool anyX = store_layer<MBW>(act, r, valid, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+  bool anyH = false;
+  par ^= 1;
+  T16_STAMP(21);
+
+  // ---------------------------------------------------------------- tower
+  const int depth = T.depth;
   for (int d = 0; d < depth; ++d) {
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
@@ -432,12 +559,16 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
       }
     // conv1 (+ the projection residual into accr), input X
     k_loop<MBW, 4>(act, T.k1[d], T.k2[d], acc, accr, r, py, px, valid, H, W, zrow, nq, lane);
+    if (d < 4) T16_STAMP(2 + 4 * d);
+    if (d < 4) T16_STAMP4(24 + 4 * d);
     __syncthreads();  // every wave is done reading X: H overwrites it
+    if (d < 4) T16_STAMP(40 + d);
     {
       const float osc = T.s1[d];
+      const float* bb = blob + T.off_b1 + d * 128;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const float4 bc = *reinterpret_cast<const float4*>(T.b1[d] + 32 * nq + 16 * nb + 4 * gq);
+        const float4 bc = *reinterpret_cast<const float4*>(bb + 32 * nq + 16 * nb + 4 * gq);
 #pragma unroll
         for (int mb = 0; mb < MBW; ++mb) {
           const float o = anyX ? ldexpf(osc, sm.sc[0][brd[mb]]) : osc;
@@ -447,8 +578,9 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
         }
       }
     }
-    anyH = store_layer<2 * MBW>(act, orow, ocq, obrd, yv, sm, par, sm.sc[1], nbrd, err);
+    anyH = store_layer<MBW>(act, r, valid, brd, cq0, yv, sm, par, sm.sc[1], nbrd, err);
     par ^= 1;
+    if (d < 4) T16_STAMP(3 + 4 * d);
     // the residual was accumulated at X's scale, conv2 runs at H's
     if (anyX || anyH) {
 #pragma unroll
@@ -463,12 +595,15 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
     }
     // conv2 on H, on top of the residual
     k_loop<MBW, 0>(act, T.k2[d], nullptr, accr, accr, r, py, px, valid, H, W, zrow, nq, lane);
+    if (d < 4) T16_STAMP(4 + 4 * d);
+    if (d < 4) T16_STAMP4(26 + 4 * d);
     const float osc = T.s2[d];
+    const float* bb = blob + T.off_b2 + d * 128;
     if (d + 1 < depth) {
       __syncthreads();  // every wave is done reading H: the block output overwrites it
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const float4 bc = *reinterpret_cast<const float4*>(T.b2[d] + 32 * nq + 16 * nb + 4 * gq);
+        const float4 bc = *reinterpret_cast<const float4*>(bb + 32 * nq + 16 * nb + 4 * gq);
 #pragma unroll
         for (int mb = 0; mb < MBW; ++mb) {
           const float o = anyH ? ldexpf(osc, sm.sc[1][brd[mb]]) : osc;
@@ -477,8 +612,9 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
                                         fmaxf(fmaf(a[2], o, bc.z), 0.f), fmaxf(fmaf(a[3], o, bc.w), 0.f));
         }
       }
-      anyX = store_layer<2 * MBW>(act, orow, ocq, obrd, yv, sm, par, sm.sc[0], nbrd, err);
+      anyX = store_layer<MBW>(act, r, valid, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
       par ^= 1;
+      if (d < 4) T16_STAMP(5 + 4 * d);
       continue;
     }
     // ------------------------------------------------------------ heads
@@ -486,61 +622,54 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
     // F -> 2, value F -> 1, folded BN, ReLU; model.py:68-149): per lane its 8
     // channels, a fixed xor tree over the four lane groups, the four N
     // quarters in order through LDS
-    float s3[MBW][3];
-    {
-      float hw[2][4][3];
+    const float* wpc = blob + T.off_wpc;
+    const float* wvc = blob + T.off_wvc;
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
+    for (int mb = 0; mb < MBW; ++mb) {
+      const float o = anyH ? ldexpf(osc, sm.sc[1][brd[mb]]) : osc;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int c0 = 32 * nq + 16 * nb + 4 * gq;
+        const float4 bc = *reinterpret_cast<const float4*>(bb + c0);
+        const float4 p01 = *reinterpret_cast<const float4*>(wpc + 2 * c0);      // channels c0, c0+1
+        const float4 p23 = *reinterpret_cast<const float4*>(wpc + 2 * c0 + 4);  // c0+2, c0+3
+        const float4 vv = *reinterpret_cast<const float4*>(wvc + c0);
+        const float wp[4][2] = {{p01.x, p01.y}, {p01.z, p01.w}, {p23.x, p23.y}, {p23.z, p23.w}};
+        const float wv[4] = {vv.x, vv.y, vv.z, vv.w};
+        const float bcv[4] = {bc.x, bc.y, bc.z, bc.w};
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int c = 32 * nq + 16 * nb + 4 * gq + v;
-          hw[nb][v][0] = T.wpc[2 * c];
-          hw[nb][v][1] = T.wpc[2 * c + 1];
-          hw[nb][v][2] = T.wvc[c];
+          const float yy = fmaxf(fmaf(accr[mb][nb][v], o, bcv[v]), 0.f);
+          a0 = fmaf(yy, wp[v][0], a0);
+          a1 = fmaf(yy, wp[v][1], a1);
+          a2 = fmaf(yy, wv[v], a2);
         }
-      float4 bc[2];
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) bc[nb] = *reinterpret_cast<const float4*>(T.b2[d] + 32 * nq + 16 * nb + 4 * gq);
-#pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) {
-        const float o = anyH ? ldexpf(osc, sm.sc[1][brd[mb]]) : osc;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const float yy = fmaxf(fmaf(accr[mb][nb][v], o, (&bc[nb].x)[v]), 0.f);
-            a0 = fmaf(yy, hw[nb][v][0], a0);
-            a1 = fmaf(yy, hw[nb][v][1], a1);
-            a2 = fmaf(yy, hw[nb][v][2], a2);
-          }
-        a0 += __shfl_xor(a0, 16);
-        a1 += __shfl_xor(a1, 16);
-        a2 += __shfl_xor(a2, 16);
-        a0 += __shfl_xor(a0, 32);
-        a1 += __shfl_xor(a1, 32);
-        a2 += __shfl_xor(a2, 32);
-        s3[mb][0] = a0;
-        s3[mb][1] = a1;
-        s3[mb][2] = a2;
+      }
+      a0 += __shfl_xor(a0, 16);
+      a1 += __shfl_xor(a1, 16);
+      a2 += __shfl_xor(a2, 16);
+      a0 += __shfl_xor(a0, 32);
+      a1 += __shfl_xor(a1, 32);
+      a2 += __shfl_xor(a2, 32);
+      if (gq == 0 && valid[mb]) {
+        red[(r[mb] * 4 + nq) * 3 + 0] = a0;
+        red[(r[mb] * 4 + nq) * 3 + 1] = a1;
+        red[(r[mb] * 4 + nq) * 3 + 2] = a2;
       }
     }
-    if (gq == 0)
-#pragma unroll
-      for (int mb = 0; mb < MBW; ++mb)
-        if (valid[mb])
-#pragma unroll
-          for (int k = 0; k < 3; ++k) red[(r[mb] * 4 + nq) * 3 + k] = s3[mb][k];
   }
   __syncthreads();  // red complete; the activation rows are no longer read
+  T16_STAMP(18);
 
   // flattened head features per board (Keras Flatten of NHWC: [p][c]) in the
   // activation area: pf [bpw][2HW], vf [bpw][HW], logits [bpw][A]
   float* pf = reinterpret_cast<float*>(act);
   float* vf = pf + bpw * 2 * HW;
   float* lg = vf + bpw * HW;
-  const float bpc0 = T.bpc[0], bpc1 = T.bpc[1], bvc0 = T.bvc[0];
-  for (int rr = tid; rr < live; rr += kThreads) {
+  const float* hb = blob + T.off_hb;
+  const float bpc0 = hb[0], bpc1 = hb[1], bvc0 = hb[2], bv2 = hb[3];
+  for (int rr = tid; rr < live; rr += NT) {
     const int b = rr / HW, p = rr - b * HW;
     float t[3];
 #pragma unroll
@@ -552,44 +681,56 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
     vf[b * HW + p] = fmaxf(t[2] + bvc0, 0.f);
   }
   __syncthreads();
-  // policy Dense(A) logits, one thread per (board, action)
-  for (int idx = tid; idx < nbrd * A; idx += kThreads) {
-    const int b = idx / A, a = idx - b * A;
-    float s = T.bpd[a];
-    const float* pb = pf + b * 2 * HW;
-    for (int i = 0; i < 2 * HW; ++i) s = fmaf(pb[i], T.wpd[i * A + a], s);
-    lg[b * A + a] = s;
-  }
-  // value Dense(hidden) ReLU -> Dense(1): thread j of each 256-thread half,
-  // boards half, half + 2, ...; its weight column read once for all of them
+  T16_STAMP(44);
+  // policy Dense(A) logits, one thread per (board, action); weights in LDS
   {
+    const float* wpd = blob + T.off_wpd;
+    const float* bpd = blob + T.off_bpd;
+    for (int idx = tid; idx < nbrd * A; idx += NT) {
+      const int b = idx / A, a = idx - b * A;
+      float s = bpd[a];
+      const float* pb = pf + b * 2 * HW;
+      for (int i = 0; i < 2 * HW; ++i) s = fmaf(pb[i], wpd[i * A + a], s);
+      lg[b * A + a] = s;
+    }
+  }
+  T16_STAMP(45);
+  // value Dense(hidden) ReLU -> Dense(1): thread j of each 256-thread group g,
+  // boards g, g + NWM, ...; its weight column read once for all of them
+  {
+    constexpr int NBG = kTowerMaxBoards / NWM;  // boards per group
     const int j = tid & 255, half = tid >> 8;
     const int hidden = T.hidden;
-    float sv[kTowerMaxBoards / 2];
+    const float* bv1 = blob + T.off_bv1;
+    const float* wv2 = blob + T.off_wv2;
+    float sv[NBG];
 #pragma unroll
-    for (int k = 0; k < kTowerMaxBoards / 2; ++k) sv[k] = j < hidden ? T.bv1[j] : 0.f;
-    if (j < hidden)
+    for (int k = 0; k < NBG; ++k) sv[k] = j < hidden ? bv1[j] : 0.f;
+    if (j < hidden) {
+      const float* wv1 = T.wv1_lds ? blob + T.off_wv1 : T.blob + T.off_wv1;
       for (int p = 0; p < HW; ++p) {
-        const float w = T.wv1[p * hidden + j];
+        const float w = T.wv1_lds ? wv1[p * hidden + j] : gbl(wv1)[p * hidden + j];
 #pragma unroll
-        for (int k = 0; k < kTowerMaxBoards / 2; ++k) {
-          const int b = half + 2 * k;
+        for (int k = 0; k < NBG; ++k) {
+          const int b = half + NWM * k;
           if (b < nbrd) sv[k] = fmaf(vf[b * HW + p], w, sv[k]);
         }
       }
-    const float w2 = j < hidden ? T.wv2[j] : 0.f;
+    }
+    const float w2 = j < hidden ? wv2[j] : 0.f;
 #pragma unroll
-    for (int k = 0; k < kTowerMaxBoards / 2; ++k) {
-      const int b = half + 2 * k;
+    for (int k = 0; k < NBG; ++k) {
+      const int b = half + NWM * k;
       if (b >= nbrd) break;  // wave-uniform
       const float part = wsum(fmaxf(sv[k], 0.f) * w2);
       if (lane == 0) sm.vred[b][wave & 3] = part;
     }
   }
+  T16_STAMP(46);
   __syncthreads();
+  T16_STAMP(47);
   // softmax (one wave per board) and tanh
-  if (wave < nbrd) {
-    const int b = wave;
+  for (int b = wave; b < nbrd; b += NT / 64) {  // wave-uniform
     float m = -INFINITY;
     for (int a = lane; a < A; a += 64) m = fmaxf(m, lg[b * A + a]);
     m = wmax(m);
@@ -598,11 +739,21 @@ __global__ __launch_bounds__(kThreads, 2) void tower16_kernel(const TowerNet* __
     z = wsum(z);
     for (int a = lane; a < A; a += 64) probs[(size_t)(b0 + b) * A + a] = expf(lg[b * A + a] - m) / z;
     if (lane == 0)
-      values[b0 + b] = tanhf((((sm.vred[b][0] + sm.vred[b][1]) + sm.vred[b][2]) + sm.vred[b][3]) + T.bv2[0]);
+      values[b0 + b] = tanhf((((sm.vred[b][0] + sm.vred[b][1]) + sm.vred[b][2]) + sm.vred[b][3]) + bv2);
   }
+  T16_STAMP(19);
+  T16_RSTAMP(23);
 }
 
 }  // namespace
+
+#ifdef AZ_T16_STAMPS
+}  // namespace az
+extern "C" int az_t16_stamps(unsigned long long* out) {  // [4096][24] of the last launch(es)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(az::g_t16_stamps), sizeof(az::g_t16_stamps)) == hipSuccess ? 0 : -1;
+}
+namespace az {
+#endif
 
 int tower16_tile_rows(int HW) {
   // 128-row tiles unless 96 rows hold the same boards (more rows per tile, same work per board)
@@ -617,35 +768,59 @@ int tower16_boards_per_tile(int HW) {
   return tr ? std::min(tr / HW, kTowerMaxBoards) : 0;
 }
 
-size_t tower16_lds_bytes(int HW) {
+size_t tower16_lds_bytes(int HW, int staged_floats) {
   const int tr = tower16_tile_rows(HW);
-  return (size_t)(tr + 1) * 512 + sizeof(TowerSmem) + (size_t)tr * 4 * 3 * sizeof(float);
+  return (size_t)(tr + kZeroRows) * kPitch + sizeof(TowerSmem) + (size_t)tr * 4 * 3 * sizeof(float) +
+         (size_t)staged_floats * sizeof(float);
 }
 
-template <int MBW>
-static void launch_mbw(const TowerNet* net, const Board* boards, const float4* x, const int* count, int n_max,
-                       int H, int W, int A, float* probs, float* values, unsigned long long* err,
+void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
+  // conv16_pack's fragment layout ([k-step][n-block][term][lane] x 8 fp16) over k = tap*4 + plane
+  const int F = 128;
+  out.assign((size_t)2 * 8 * 2 * 64 * 8, 0);
+  const double sc = std::ldexp(1.0, -e);
+  for (int k = 0; k < 36; ++k)
+    for (int co = 0; co < F; ++co) {
+      const float ws = (float)(w[(size_t)k * F + co] * sc);  // Keras [3][3][4][F]: k = tap*4 + plane
+      const _Float16 b0 = (_Float16)ws;
+      const _Float16 b1 = (_Float16)((ws - (float)b0) * 4096.f);
+      const _Float16 B0 = (_Float16)((float)b0 * 4096.f);  // exact
+      const int ks = k / 32, kk = k % 32, nb = co / 16;
+      const int ln = (kk / 8) * 16 + (co % 16), j = kk % 8;
+      const size_t base = ((((size_t)ks * 8 + nb) * 2) * 64 + ln) * 8 + j;
+      memcpy(&out[base], &B0, 2);
+      memcpy(&out[base + 64 * 8], &b1, 2);
+    }
+}
+
+template <int MBT, int NWM>
+static void launch_mbw(const TowerNet* net, int staged, const Board* boards, const float4* x, const int* count,
+                       int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
                        hipStream_t s) {
   const int bpw = tower16_boards_per_tile(H * W);
   const int grid = (n_max + bpw - 1) / bpw;
-  const size_t bytes = tower16_lds_bytes(H * W);
+  const size_t bytes = tower16_lds_bytes(H * W, staged);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBW>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBT, NWM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTowerLdsMax);
     attr = true;
   }
-  tower16_kernel<MBW><<<grid, kThreads, bytes, s>>>(net, boards, x, count, n_max, H, W, A, bpw, probs, values,
+  tower16_kernel<MBT, NWM><<<grid, NWM * 256, bytes, s>>>(net, boards, x, count, n_max, H, W, A, bpw, probs, values,
                                                      err);
 }
 
-void launch_tower16(const TowerNet* net, const Board* boards, const float4* x, const int* count, int n_max,
-                    int H, int W, int A, float* probs, float* values, unsigned long long* err, hipStream_t s) {
+void launch_tower16(const TowerNet* net, int staged, const Board* boards, const float4* x, const int* count,
+                    int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
+                    hipStream_t s) {
   if (n_max <= 0) return;
+#ifndef AZ_T16_NWM
+#define AZ_T16_NWM 2  // wave groups over M: 2 = two waves per SIMD (default), 1 = one (64% vs 80% of the MFMA rate in the K loop)
+#endif
   if (tower16_tile_rows(H * W) == 96)
-    launch_mbw<3>(net, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<6, AZ_T16_NWM>(net, staged, boards, x, count, n_max, H, W, A, probs, values, err, s);
   else
-    launch_mbw<4>(net, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<8, AZ_T16_NWM>(net, staged, boards, x, count, n_max, H, W, A, probs, values, err, s);
 }
 
 }  // namespace az

@@ -277,6 +277,50 @@ def test_forward_matches_keras_restatement(shape, conv_algo):
     np.testing.assert_allclose(p.sum(axis=1), 1.0, atol=1e-6)
 
 
+def _range_weights(S=2.0 ** 18):
+    """Weights whose stem output and block-0 conv1 output are S times the
+    network's (BN gamma/beta scaled: ReLU is positively homogeneous) while the
+    next convs' kernels are divided by S: the same function, with activations
+    far beyond the fp16 split range (|x| > 32752)."""
+    spec = weight_spec(6, 7, 7, depth=2)
+    w = init_weights(spec, seed=4, randomize_bn=True)
+    for u in ("stem", "block0.conv1"):
+        w[u + ".gamma"] = (w[u + ".gamma"] * S).astype(np.float32)
+        w[u + ".beta"] = (w[u + ".beta"] * S).astype(np.float32)
+    for u in ("block0.conv1", "block0.res", "block0.conv2"):
+        w[u + ".kernel"] = (w[u + ".kernel"] / S).astype(np.float32)
+    # block0.conv1 saw an S-times input with a 1/S kernel, then its BN x S: its
+    # output is S times; conv2's 1/S kernel brings block 0's sum back
+    return w
+
+
+def test_activation_range_is_rescaled_not_failed():
+    """SURVEY 8 a18 + VERDICT r2 item 3: activations past the fp16 split range.
+    The one-launch tower stores such a board's layer at a power-of-two scale
+    and completes within NET_TOL of the float64 restatement, in self-play too;
+    the per-layer path reports it as a device error instead of a wrong result."""
+    w = _range_weights()
+    rng = np.random.RandomState(9)
+    x = oracle.full_state(random_boards(rng, 40, 6, 7))
+    rp, rv = keras_ref.forward(w, x, depth=2)
+    # the stem's activations really are out of the fp16 range
+    stem = keras_ref.inner(np.asarray(x, np.float64), w, "stem", 1e-3)
+    assert stem.max() > 32752 * 4
+    eng = az.Engine(6, 7, 4, True, 16, slots=64, evaluator=az.EVAL_NETWORK, depth=2, conv_algo=az.CONV_F16X2)
+    eng.set_weights(w.items())
+    p, v = eng.forward(x)
+    assert np.abs(p - rp).max() < NET_TOL and np.abs(v - rv).max() < NET_TOL
+    eng.selfplay_run(0, 4, 3)
+    assert eng.stats()["errors"] == 0
+    eng.close()
+    lay = az.Engine(6, 7, 4, True, 16, slots=64, evaluator=az.EVAL_NETWORK, depth=2,
+                    conv_algo=az.CONV_F16X2_LAYERS)
+    lay.set_weights(w.items())
+    with pytest.raises(az.AzError, match="activation-range"):
+        lay.selfplay_run(0, 4, 3)
+    lay.close()
+
+
 @pytest.mark.parametrize("conv_algo", CONV_ALGOS)
 def test_forward_is_batch_invariant(conv_algo):
     eng, _ = make_net_engine(slots=512, conv_algo=conv_algo)
