@@ -769,14 +769,13 @@ def main():
             } if args.cache_log2 else None),
             "tree_arena": {
                 "compact": bool(args.compact),
-                "edges_per_slot": (2 if args.compact else 1) * (
-                    8 * args.sims * A + HW * A if args.compact else args.sims * HW * A + A),
-                "bytes_total": 32 * args.slots * (2 if args.compact else 1) * (
-                    8 * args.sims * A + HW * A if args.compact else args.sims * HW * A + A),
+                "edges_per_slot": (2 if args.compact else 1) * st1["arena_edges"],
+                "bytes_total": 32 * args.slots * (2 if args.compact else 1) * st1["arena_edges"],
                 "max_retained_edges": st1["max_retained"] if args.compact else None,
                 "rule": ("after every move the chosen child's subtree is copied into the other half of the "
-                         "slot's arena (Cheney scan); each half holds one move's search plus the reused "
-                         "subtree" if args.compact else "whole game tree kept (S*H*W*A edges per slot)"),
+                         "slot's arena (Cheney scan); each half holds one move's search plus the reused subtree, "
+                         "sized S*H*W*A + A (no game can overflow it) when that fits 40% of the free HBM"
+                         if args.compact else "whole game tree kept (S*H*W*A edges per slot)"),
             },
             "cache_off": off,
             "roofline_tree": roofline_tree,

@@ -204,6 +204,24 @@ int sync_all(az_engine* e) {
   return 0;
 }
 
+// Entry of an ABI call that reads or writes engine buffers: the device, then
+// every queued move finished (az_selfplay_step without stats returns while
+// the lanes' kernels run on non-blocking streams; their samples, trees and
+// evaluator slices must not be read or overwritten under them).
+int enter(az_engine* e) {
+  AZ_HIP(hipSetDevice(e->device));
+  return sync_all(e);
+}
+
+// the tree API never compacts (its views are the whole tree, like the
+// reference's object graph): an engine created with compact = 1 sizes each
+// arena half for one move, which a reused tree outgrows
+int tree_api_ok(az_engine* e) {
+  if (e->g.halves > 1)
+    return fail(AZ_E_INVALID, "the tree API (az_tree_*) needs an engine created with compact = 0");
+  return 0;
+}
+
 int cache_clear(az_engine* e) {
   if (!e->cache.state) return 0;
   int rc;
@@ -606,9 +624,23 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   // covers a chosen child holding up to 7/8 of the root's visits move after
   // move (the retained high-water mark is reported as az_stats.max_retained)
   g.halves = c.compact ? 2 : 1;
-  const int64_t arena = c.arena_edges > 0 ? c.arena_edges
-                        : c.compact ? (int64_t)8 * c.mcts_iterations * A + (int64_t)g.HW * A
-                                    : (int64_t)c.mcts_iterations * g.HW * A + A;
+  // a slot's tree holds at most mcts_iterations * H*W expansions of <= A edges
+  // (one game), so a half of that size cannot overflow.  Compacted, each half
+  // holds one move's search plus the subtree kept -- measured a few thousand
+  // edges at configs[1] with random weights, but a trained network that keeps
+  // most visits on the chosen child grows the kept subtree toward the game's
+  // whole search -- so the default is the safe size whenever two such halves
+  // per slot fit in 40% of the free HBM, else the most that does (at least
+  // 8 S A + H W A; an overflow is reported as kErrArena, never overrun).
+  const int64_t safe = (int64_t)c.mcts_iterations * g.HW * A + A;
+  int64_t arena = c.arena_edges > 0 ? c.arena_edges : safe;
+  if (c.arena_edges <= 0 && c.compact) {
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+      const int64_t fit = (int64_t)(0.4 * (double)free_b / ((double)c.slots * 2.0 * sizeof(az::Edge)));
+      arena = std::min(safe, std::max(fit, (int64_t)8 * c.mcts_iterations * A + (int64_t)g.HW * A));
+    }
+  }
   if (visits > (1 << 30) || arena > (1 << 30)) {
     delete e;
     return fail(AZ_E_INVALID, "tree bounds too large");
@@ -781,7 +813,7 @@ int az_engine_destroy(az_engine* eng) {
 
 int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
   if (!e || (!tensors && n)) return fail(AZ_E_INVALID, "null argument");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
   int rc;
   if ((rc = az::load_network(e->net, tensors, n, 4, e->g.HW, e->g.A, e->cfg.bn_epsilon, e->owned)))
     return rc;
@@ -790,7 +822,7 @@ int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {
 
 int az_encode(az_engine* e, const int8_t* boards, int n, float* state, uint8_t* mask) {
   if (!e || n < 0 || (n && !boards)) return fail(AZ_E_INVALID, "bad arguments");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
   const int HW = e->g.HW, A = e->g.A;
   const int chunk = e->g.slots;
   std::vector<az::Board> hb(std::min(n, chunk));
@@ -816,7 +848,7 @@ int az_encode(az_engine* e, const int8_t* boards, int n, float* state, uint8_t* 
 int az_forward(az_engine* e, const float* x, int n, float* probs, float* values) {
   if (!e || n < 0 || (n && (!x || !probs || !values))) return fail(AZ_E_INVALID, "bad arguments");
   if (!e->net.ready) return fail(AZ_E_STATE, "az_engine_set_weights was not called");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
   const int HW = e->g.HW, A = e->g.A, chunk = e->g.slots;
   for (int off = 0; off < n; off += chunk) {
     const int m = std::min(chunk, n - off);
@@ -896,6 +928,7 @@ int az_stats_get(az_engine* e, az_stats* st) {
     st->cache_capacity = (int64_t)e->cache.mask + 1;
   }
   st->games_drained = e->drained;
+  st->arena_edges = e->g.arena_cap;
   return 0;
 }
 
@@ -1044,7 +1077,7 @@ int az_selfplay_run(az_engine* e, int64_t first_game, int64_t n_games, uint32_t 
 int az_selfplay_results(az_engine* e, int32_t* lengths, int32_t* results, int32_t* expansions,
                         int8_t* boards, double* policies, int32_t* moves) {
   if (!e) return fail(AZ_E_INVALID, "null engine");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
   AZ_HIP(hipStreamSynchronize(e->stream));
   const size_t G = (size_t)e->sp_n, P = (size_t)e->g.HW, A = (size_t)e->g.A, HW = (size_t)e->g.HW;
   if (G == 0) return 0;
@@ -1131,7 +1164,8 @@ int az_selfplay_drain(az_engine* e, int64_t max_games, int64_t* n_out, int64_t* 
 // ------------------------------------------------------------------ tree API
 int az_tree_reset(az_engine* e, int n, const int32_t* slots, const int8_t* boards) {
   if (!e || n < 0 || n > e->g.slots || (n && (!slots || !boards))) return fail(AZ_E_INVALID, "bad arguments");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
+  if (int rc_ = tree_api_ok(e)) return rc_;
   std::vector<az::Board> hb(n);
   for (int i = 0; i < n; ++i) {
     if (slots[i] < 0 || slots[i] >= e->g.slots) return fail(AZ_E_INVALID, "slot out of range");
@@ -1148,7 +1182,7 @@ int az_tree_reset(az_engine* e, int n, const int32_t* slots, const int8_t* board
 
 int az_tree_release(az_engine* e, int n, const int32_t* slots) {
   if (!e || n < 0 || n > e->g.slots || (n && !slots)) return fail(AZ_E_INVALID, "bad arguments");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
   for (int i = 0; i < n; ++i)
     if (slots[i] < 0 || slots[i] >= e->g.slots) return fail(AZ_E_INVALID, "slot out of range");
   AZ_HIP(hipMemcpyAsync(e->dev_i32, slots, n * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
@@ -1162,7 +1196,8 @@ int az_tree_search(az_engine* e, int n_sims) {
   if (!e || n_sims < 0) return fail(AZ_E_INVALID, "bad arguments");
   int rc;
   if ((rc = ready_to_search(e))) return rc;
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
+  if (int rc_ = tree_api_ok(e)) return rc_;
   for (int s = 0; s < n_sims; ++s)
     if ((rc = simulate(e, e->whole))) return rc;
   AZ_HIP(hipStreamSynchronize(e->stream));
@@ -1172,7 +1207,8 @@ int az_tree_search(az_engine* e, int n_sims) {
 int az_tree_play(az_engine* e, const double* uniforms, int greedy, int deterministic,
                  int32_t* moves, int32_t* status, double* policy) {
   if (!e || (!deterministic && !uniforms)) return fail(AZ_E_INVALID, "bad arguments");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
+  if (int rc_ = tree_api_ok(e)) return rc_;
   const size_t S = (size_t)e->g.slots;
   if (!deterministic)
     AZ_HIP(hipMemcpyAsync(e->uniforms, uniforms, S * sizeof(double), hipMemcpyHostToDevice, e->stream));
@@ -1191,7 +1227,7 @@ int az_tree_play(az_engine* e, const double* uniforms, int greedy, int determini
 
 int az_tree_info(az_engine* e, int slot, int64_t* info, float* root_value) {
   if (!e || !info || slot < 0 || slot >= e->g.slots) return fail(AZ_E_INVALID, "bad arguments");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
   AZ_HIP(hipStreamSynchronize(e->stream));
   int32_t top, first, cnt, ply;
   int64_t gid;
@@ -1212,7 +1248,7 @@ int az_tree_info(az_engine* e, int slot, int64_t* info, float* root_value) {
 int az_tree_export(az_engine* e, int slot, double* prior, double* w, int32_t* n, int32_t* child,
                    int32_t* child_n, int32_t* action, float* child_value) {
   if (!e || slot < 0 || slot >= e->g.slots) return fail(AZ_E_INVALID, "bad arguments");
-  AZ_HIP(hipSetDevice(e->device));
+  if (int rc_ = enter(e)) return rc_;
   AZ_HIP(hipStreamSynchronize(e->stream));
   int32_t top, half = 0;
   AZ_HIP(hipMemcpy(&top, e->t.arena_top + slot, 4, hipMemcpyDeviceToHost));

@@ -64,6 +64,9 @@ constexpr float kRange = 32752.f;  // largest |x| a split16 term pair holds
 // its own row has.
 constexpr int kPitch = 544;
 constexpr int kZeroRows = 8;
+// a tile row's board-local pixel, packed (y << 8) | x; rows past the tile's
+// boards get y = x = 127, outside every board, so each tap reads a zero row
+constexpr int kNoPixel = (127 << 8) | 127;
 
 #ifdef AZ_T16_STAMPS  // diagnostic build only: phase clocks of wave 0 per workgroup (az_t16_stamps)
 constexpr int kStampBlocks = 4096, kStamps = 48;
@@ -176,7 +179,7 @@ __device__ __forceinline__ float4 scale4(const float4 v, float s) {
 // sc_out holds the exponents).  Contains the barrier that publishes the
 // stores.  `par` alternates per layer (flag[par] is this layer's).
 template <int MBW>
-__device__ __forceinline__ bool store_layer(uint4* act, const int (&r_)[MBW], const bool (&valid_)[MBW],
+__device__ __forceinline__ bool store_layer(uint4* act, const int (&r_)[MBW], const int (&yx_)[MBW],
                                             const int (&brd_)[MBW], int cq0, const float4 (&y)[2 * MBW],
                                             TowerSmem& sm, int par, int* sc_out, int nbrd,
                                             unsigned long long* err) {
@@ -186,7 +189,7 @@ __device__ __forceinline__ bool store_layer(uint4* act, const int (&r_)[MBW], co
   int row[MBW], brd[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
-    row[mb] = valid_[mb] ? r_[mb] : -1;
+    row[mb] = yx_[mb] != kNoPixel ? r_[mb] : -1;
     brd[mb] = brd_[mb];
     asm volatile("" : "+v"(row[mb]), "+v"(brd[mb]));
   }
@@ -267,7 +270,7 @@ __device__ __forceinline__ void mfma_kstep(t_f4 (&C)[MBW][2], const uint4 (&a)[M
 }
 
 #ifndef AZ_T16_PF
-#define AZ_T16_PF 2  // k-steps of B fragments in flight ahead of their MFMAs
+#define AZ_T16_PF 1  // k-steps of B fragments in flight ahead of their MFMAs (1 and 2 measured equal; 1 needs no spill)
 #endif
 
 // One conv phase's K loop: R residual k-steps (the block input's own rows x
@@ -279,26 +282,34 @@ __device__ __forceinline__ void mfma_kstep(t_f4 (&C)[MBW][2], const uint4 (&a)[M
 template <int MBW, int R>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
-                                       t_f4 (&accr)[MBW][2], const int (&r_)[MBW], const int (&py_)[MBW],
-                                       const int (&px_)[MBW], const bool (&valid_)[MBW], int H, int W,
-                                       int zrow, int nq, int lane) {
+                                       t_f4 (&accr)[MBW][2], const int (&r_)[MBW], const int (&yx_)[MBW], int H, int W,
+                                       int zrow, int nq, int lane, int mh) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
+#ifndef AZ_T16_NOALTPRIO
+  // the two waves of a SIMD (M halves mh = 0, 1) take turns at priority 1,
+  // one k-step each, so neither falls a whole phase behind the other (without:
+  // the older wave finished its K loop ~7k cycles first and its partner ran
+  // the tail alone; with: ~2k, -1 to -2% kernel time)
+  auto turn = [&](int k) {
+    if ((k ^ mh) & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  };
+#else
+  auto turn = [&](int) {};
+  (void)mh;
+#endif
   constexpr int PF = AZ_T16_PF, NB = PF == 1 ? 2 : 4;
   static_assert(PF >= 1 && PF <= 3, "prefetch depth");
   const int gq = lane >> 4;
   // the tap geometry laundered through an empty asm per call: the k-loops sit
   // in the runtime depth loop, and without this the compiler hoists every
   // k-step's LDS address out of it (loop invariant) and spills them
-  int r[MBW], py[MBW], px[MBW];
-  bool valid[MBW];
+  int r[MBW], yx[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
     r[mb] = r_[mb];
-    py[mb] = py_[mb];
-    px[mb] = px_[mb];
-    int v = valid_[mb];
-    asm volatile("" : "+v"(r[mb]), "+v"(py[mb]), "+v"(px[mb]), "+v"(v));
-    valid[mb] = v != 0;
+    yx[mb] = yx_[mb];
+    asm volatile("" : "+v"(r[mb]), "+v"(yx[mb]));
   }
   const uint4* wm = wmain + (size_t)(nq * 2) * 2 * 64 + lane;
   const uint4* wr = R ? wres + (size_t)(nq * 2) * 2 * 64 + lane + (size_t)36 * 1024 : wmain;
@@ -319,13 +330,15 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   const char* actb = reinterpret_cast<const char*>(act);
   auto set_own = [&]() {
 #pragma unroll
-    for (int mb = 0; mb < MBW; ++mb) aaddr[mb] = (valid[mb] ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
+    for (int mb = 0; mb < MBW; ++mb)
+      aaddr[mb] = (yx[mb] != kNoPixel ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
   };
   auto set_tap = [&](int t) {  // runtime tap
     const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      const bool ok = valid[mb] && py[mb] + dy >= 0 && py[mb] + dy < H && px[mb] + dx >= 0 && px[mb] + dx < W;
+      const int py = yx[mb] >> 8, px = yx[mb] & 255;
+      const bool ok = py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
       const int sr = r[mb] + dy * W + dx;
       aaddr[mb] = (ok ? sr : zrow + (sr & 7)) * kPitch + gq * 16;
     }
@@ -356,6 +369,18 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
       }
       if (next_chunk >= 0) load_a1(next_chunk, mb);
     }
+#ifndef AZ_T16_FREESCHED
+    // the order above, kept: the weight loads of the k-step PF ahead first,
+    // then per M block its six MFMAs and its two reads for the next k-step
+    // (left alone, the scheduler bunched the reads and waited for all of
+    // them, and for the weight loads just issued, in mid k-step)
+    __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);  // VMEM reads
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) {
+      __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);  // MFMA
+      if (next_chunk >= 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS reads
+    }
+#endif
   };
 
 #pragma unroll
@@ -368,6 +393,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #pragma unroll
   for (int s = 0; s < R; ++s) {
     __builtin_amdgcn_sched_barrier(0);
+    turn(s);
     load_b(bsrc(s + PF), bq[(s + PF) % NB]);
     if (s + 1 == R) {
       // the next k-step is tap 0's first chunk: the addresses move before the
@@ -384,6 +410,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       __builtin_amdgcn_sched_barrier(0);
+      turn(c);
       // main k-step PF ahead (the prologue or the residual steps fetched 0 .. PF - 1)
       const int ahead = 4 * t + c + PF;
       if (c + PF < 4 || t < 8) load_b(wm + (size_t)ahead * 1024, bq[(c + PF) % NB]);
@@ -397,6 +424,9 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
       }
     }
   }
+#ifndef AZ_T16_NOALTPRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 // LDS-DMA of n_u4 16-byte words from global src into LDS dst (both
@@ -456,17 +486,15 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   __syncthreads();  // the flags before any layer may set one; the boards
 
   const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
-  int r[MBW], py[MBW], px[MBW], brd[MBW];
-  bool valid[MBW];
+  int r[MBW], yx[MBW], brd[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
     r[mb] = (mh * MBW + mb) * 16 + r16;
-    valid[mb] = r[mb] < live;
-    const int b = valid[mb] ? r[mb] / HW : 0;
+    const bool valid = r[mb] < live;
+    const int b = valid ? r[mb] / HW : 0;
     brd[mb] = b;
     const int p = r[mb] - b * HW;
-    py[mb] = p / W;
-    px[mb] = p - py[mb] * W;
+    yx[mb] = valid ? ((p / W) << 8) | (p - (p / W) * W) : kNoPixel;
   }
   const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
   t_f4 acc[MBW][2], accr[MBW][2];
@@ -480,17 +508,15 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // one-hot x the operands, and so the outputs, are bitwise the boards'.
   {
     const uint4* ws = T.stem16 + (size_t)(nq * 2) * 2 * 64 + lane;
-    uint4 bs[2][4];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bs[ks][q] = gld(ws + (size_t)ks * 1024 + q * 64);
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      uint4 bs[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bs[q] = gld(ws + (size_t)ks * 1024 + q * 64);
       uint4 a[MBW][2];
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb) {
@@ -499,11 +525,11 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         for (int h = 0; h < 2; ++h) {
           const int t = 8 * ks + 2 * gq + h;  // tap of k = 32 ks + 8 gq + 4 h + plane
           const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
-          const bool ok = t < 9 && valid[mb] && py[mb] + dy >= 0 && py[mb] + dy < H && px[mb] + dx >= 0 &&
-                          px[mb] + dx < W;
+          const int py = yx[mb] >> 8, px = yx[mb] & 255;
+          const bool ok = t < 9 && py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
           float4 pl = make_float4(0.f, 0.f, 0.f, 0.f);
           if (ok) {
-            const int q = (py[mb] + dy) * W + px[mb] + dx;
+            const int q = (py + dy) * W + px + dx;
             if (boards) {
               const Board& bd = sm.boards[brd[mb]];
               const uint64_t ow = q < 64 ? bd.own[0] : bd.own[1], op = q < 64 ? bd.opp[0] : bd.opp[1];
@@ -520,7 +546,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         }
         split_u8(v, a[mb][0], a[mb][1]);
       }
-      mfma_kstep<MBW>(acc, a, bs[ks]);
+      mfma_kstep<MBW>(acc, a, bs);
     }
   }
   __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
@@ -542,7 +568,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   }
   int par = 0;
   // scale state: buffer contents X (block input) and H (conv1 output)
-  bool anyX = store_layer<MBW>(act, r, valid, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+  bool anyX = store_layer<MBW>(act, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
   bool anyH = false;
   par ^= 1;
   T16_STAMP(21);
@@ -558,7 +584,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         accr[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
       }
     // conv1 (+ the projection residual into accr), input X
-    k_loop<MBW, 4>(act, T.k1[d], T.k2[d], acc, accr, r, py, px, valid, H, W, zrow, nq, lane);
+    k_loop<MBW, 4>(act, T.k1[d], T.k2[d], acc, accr, r, yx, H, W, zrow, nq, lane, mh);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
     __syncthreads();  // every wave is done reading X: H overwrites it
@@ -578,7 +604,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         }
       }
     }
-    anyH = store_layer<MBW>(act, r, valid, brd, cq0, yv, sm, par, sm.sc[1], nbrd, err);
+    anyH = store_layer<MBW>(act, r, yx, brd, cq0, yv, sm, par, sm.sc[1], nbrd, err);
     par ^= 1;
     if (d < 4) T16_STAMP(3 + 4 * d);
     // the residual was accumulated at X's scale, conv2 runs at H's
@@ -594,7 +620,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     }
     // conv2 on H, on top of the residual
-    k_loop<MBW, 0>(act, T.k2[d], nullptr, accr, accr, r, py, px, valid, H, W, zrow, nq, lane);
+    k_loop<MBW, 0>(act, T.k2[d], nullptr, accr, accr, r, yx, H, W, zrow, nq, lane, mh);
     if (d < 4) T16_STAMP(4 + 4 * d);
     if (d < 4) T16_STAMP4(26 + 4 * d);
     const float osc = T.s2[d];
@@ -612,7 +638,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
                                         fmaxf(fmaf(a[2], o, bc.z), 0.f), fmaxf(fmaf(a[3], o, bc.w), 0.f));
         }
       }
-      anyX = store_layer<MBW>(act, r, valid, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+      anyX = store_layer<MBW>(act, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
       par ^= 1;
       if (d < 4) T16_STAMP(5 + 4 * d);
       continue;
@@ -624,13 +650,23 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     // quarters in order through LDS
     const float* wpc = blob + T.off_wpc;
     const float* wvc = blob + T.off_wvc;
+    int hr[MBW], hyx[MBW], hb[MBW];  // laundered (see k_loop): addresses recomputed here, not hoisted and spilled
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      const float o = anyH ? ldexpf(osc, sm.sc[1][brd[mb]]) : osc;
+      hr[mb] = r[mb];
+      hyx[mb] = yx[mb];
+      hb[mb] = brd[mb];
+      asm volatile("" : "+v"(hr[mb]), "+v"(hyx[mb]), "+v"(hb[mb]));
+    }
+    int hq = 32 * nq + 4 * gq;  // the lane's first channel (N block 0)
+    asm volatile("" : "+v"(hq));
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) {
+      const float o = anyH ? ldexpf(osc, sm.sc[1][hb[mb]]) : osc;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const int c0 = 32 * nq + 16 * nb + 4 * gq;
+        const int c0 = hq + 16 * nb;
         const float4 bc = *reinterpret_cast<const float4*>(bb + c0);
         const float4 p01 = *reinterpret_cast<const float4*>(wpc + 2 * c0);      // channels c0, c0+1
         const float4 p23 = *reinterpret_cast<const float4*>(wpc + 2 * c0 + 4);  // c0+2, c0+3
@@ -652,13 +688,15 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       a0 += __shfl_xor(a0, 32);
       a1 += __shfl_xor(a1, 32);
       a2 += __shfl_xor(a2, 32);
-      if (gq == 0 && valid[mb]) {
-        red[(r[mb] * 4 + nq) * 3 + 0] = a0;
-        red[(r[mb] * 4 + nq) * 3 + 1] = a1;
-        red[(r[mb] * 4 + nq) * 3 + 2] = a2;
+      if (gq == 0 && hyx[mb] != kNoPixel) {
+        red[(hr[mb] * 4 + nq) * 3 + 0] = a0;
+        red[(hr[mb] * 4 + nq) * 3 + 1] = a1;
+        red[(hr[mb] * 4 + nq) * 3 + 2] = a2;
       }
     }
   }
+  T16_STAMP(42);
+  T16_STAMP4(43);
   __syncthreads();  // red complete; the activation rows are no longer read
   T16_STAMP(18);
 
@@ -682,15 +720,27 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   }
   __syncthreads();
   T16_STAMP(44);
-  // policy Dense(A) logits, one thread per (board, action); weights in LDS
+  // policy Dense(A) logits, one thread per (board, action); weights in LDS,
+  // reads issued 4 at a time ahead of their FMAs (the chain order is i)
   {
     const float* wpd = blob + T.off_wpd;
     const float* bpd = blob + T.off_bpd;
+    const int K = 2 * HW;
     for (int idx = tid; idx < nbrd * A; idx += NT) {
       const int b = idx / A, a = idx - b * A;
       float s = bpd[a];
-      const float* pb = pf + b * 2 * HW;
-      for (int i = 0; i < 2 * HW; ++i) s = fmaf(pb[i], wpd[i * A + a], s);
+      const float* pb = pf + b * K;
+      int i = 0;
+      for (; i + 4 <= K; i += 4) {
+        const float p0 = pb[i], p1 = pb[i + 1], p2 = pb[i + 2], p3 = pb[i + 3];
+        const float w0 = wpd[i * A + a], w1 = wpd[(i + 1) * A + a], w2 = wpd[(i + 2) * A + a],
+                    w3 = wpd[(i + 3) * A + a];
+        s = fmaf(p0, w0, s);
+        s = fmaf(p1, w1, s);
+        s = fmaf(p2, w2, s);
+        s = fmaf(p3, w3, s);
+      }
+      for (; i < K; ++i) s = fmaf(pb[i], wpd[i * A + a], s);
       lg[b * A + a] = s;
     }
   }
@@ -706,15 +756,39 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     float sv[NBG];
 #pragma unroll
     for (int k = 0; k < NBG; ++k) sv[k] = j < hidden ? bv1[j] : 0.f;
-    if (j < hidden) {
-      const float* wv1 = T.wv1_lds ? blob + T.off_wv1 : T.blob + T.off_wv1;
-      for (int p = 0; p < HW; ++p) {
-        const float w = T.wv1_lds ? wv1[p * hidden + j] : gbl(wv1)[p * hidden + j];
+    auto dot = [&](auto wcol) {  // wcol(p) = wv1[p][j]; 4 pixels' reads ahead of their FMAs
+      int p = 0;
+      for (; p + 4 <= HW; p += 4) {
+        const float w0 = wcol(p), w1 = wcol(p + 1), w2 = wcol(p + 2), w3 = wcol(p + 3);
+#pragma unroll
+        for (int k = 0; k < NBG; ++k) {
+          const int b = half + NWM * k;
+          if (b < nbrd) {
+            const float* v = vf + b * HW + p;
+            const float v0 = v[0], v1 = v[1], v2 = v[2], v3 = v[3];
+            sv[k] = fmaf(v0, w0, sv[k]);
+            sv[k] = fmaf(v1, w1, sv[k]);
+            sv[k] = fmaf(v2, w2, sv[k]);
+            sv[k] = fmaf(v3, w3, sv[k]);
+          }
+        }
+      }
+      for (; p < HW; ++p) {
+        const float w = wcol(p);
 #pragma unroll
         for (int k = 0; k < NBG; ++k) {
           const int b = half + NWM * k;
           if (b < nbrd) sv[k] = fmaf(vf[b * HW + p], w, sv[k]);
         }
+      }
+    };
+    if (j < hidden) {
+      if (T.wv1_lds) {
+        const float* wv1 = blob + T.off_wv1;
+        dot([&](int p) { return wv1[p * hidden + j]; });
+      } else {
+        const auto* wv1 = gbl(T.blob + T.off_wv1);
+        dot([&](int p) { return wv1[p * hidden + j]; });
       }
     }
     const float w2 = j < hidden ? wv2[j] : 0.f;

@@ -65,7 +65,7 @@ class Stats(ctypes.Structure):
         ("cache_generation", ctypes.c_int64), ("cache_gen_size", ctypes.c_int64),
         ("cache_capacity", ctypes.c_int64), ("games_drained", ctypes.c_int64),
         ("max_retained", ctypes.c_int64), ("cache_live_gens", ctypes.c_int64),
-        ("reserved", ctypes.c_int64 * 1),
+        ("arena_edges", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -299,21 +299,33 @@ class Engine:
         return dict(lengths=lengths, results=results, expansions=expansions, boards=boards,
                     policies=policies, moves=moves)
 
-    def selfplay_drain(self, max_games=None):
+    def selfplay_drain(self, max_games=None, chunk=4096):
         """Games finished since the previous drain, copied to the host (the
         samples of a running batch, az_selfplay_drain): dict of arrays with
-        a leading game axis plus `game_ids` (finish order)."""
-        G = int(max_games if max_games is not None else max(self._n_games, 1))
+        a leading game axis plus `game_ids` (finish order).  Drained in
+        chunks of `chunk` games, so a call allocates for what it returns, not
+        for the whole batch."""
+        left = int(max_games if max_games is not None else max(self._n_games, 1))
         P, A = self.height * self.width, self.action_space
-        n = ctypes.c_int64(0)
-        out = dict(game_ids=np.zeros(G, np.int64), lengths=np.zeros(G, np.int32),
-                   results=np.zeros(G, np.int32), expansions=np.zeros(G, np.int32),
-                   boards=np.zeros((G, P, self.height, self.width), np.int8),
-                   policies=np.zeros((G, P, A), np.float64), moves=np.zeros((G, P), np.int32))
-        _check(self._L.az_selfplay_drain(self._h, G, ctypes.byref(n), *(_ptr(out[k]) for k in (
-            "game_ids", "lengths", "results", "expansions", "boards", "policies", "moves"))))
-        k = int(n.value)
-        return {key: v[:k] for key, v in out.items()}
+        parts = []
+        while left > 0:
+            G = min(chunk, left)
+            n = ctypes.c_int64(0)
+            out = dict(game_ids=np.zeros(G, np.int64), lengths=np.zeros(G, np.int32),
+                       results=np.zeros(G, np.int32), expansions=np.zeros(G, np.int32),
+                       boards=np.zeros((G, P, self.height, self.width), np.int8),
+                       policies=np.zeros((G, P, A), np.float64), moves=np.zeros((G, P), np.int32))
+            _check(self._L.az_selfplay_drain(self._h, G, ctypes.byref(n), *(_ptr(out[k]) for k in (
+                "game_ids", "lengths", "results", "expansions", "boards", "policies", "moves"))))
+            k = int(n.value)
+            parts.append({key: v[:k] for key, v in out.items()} if k < G else out)
+            left -= k
+            if k < G:
+                break
+        if len(parts) == 1:
+            p = parts[0]
+            return {key: (v.copy() if v.base is not None else v) for key, v in p.items()}
+        return {key: np.concatenate([p[key] for p in parts]) for key in parts[0]}
 
     # ------------------------------------------------------------- tree API
     def tree_reset(self, slots, boards):

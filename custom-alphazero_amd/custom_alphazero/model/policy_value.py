@@ -118,8 +118,12 @@ class PolicyValueModel:
         os.makedirs(path, exist_ok=True)
         np.savez(os.path.join(path, ConfigPath.model_prefix + ".npz"),
                  **dict(zip(self.weight_names, self.get_weights())))
+        # `hash` is the reference's (sum of md5(str(w)), model.py:172-177): it
+        # depends on numpy's str() of an array, so a checkpoint moved between
+        # numpy versions may not reproduce it; `content_hash` (md5 of the raw
+        # bytes) is recorded beside it and accepted on load
         meta = {"steps": int(self.steps), "learning_rate": float(self.learning_rate),
-                "hash": self.hash}
+                "hash": self.hash, "content_hash": self.content_hash}
         with open(os.path.join(path, ConfigPath.model_meta), "w") as fp:
             json.dump(meta, fp, sort_keys=True, indent=4)
         open(os.path.join(path, ConfigPath.model_success), "wb").close()
@@ -133,7 +137,11 @@ class PolicyValueModel:
             meta = json.load(fp)
         self.steps = int(meta.get("steps", 0))
         self.learning_rate = float(meta.get("learning_rate", self.learning_rate))
-        if self.hash != meta.get("hash"):
+        # the reference's hash (a meta.json the reference wrote), or the raw-bytes
+        # hash this package records (also what its earlier builds stored as
+        # `hash`): either identifies the weights
+        content = self.content_hash
+        if self.hash != meta.get("hash") and content not in (meta.get("content_hash"), meta.get("hash")):
             raise AssertionError(f"Unexpected weights hash recovered during model loading at {path}!")
 
     def get_learning_rate(self) -> float:

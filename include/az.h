@@ -9,9 +9,11 @@
  *
  * Conventions: every function returns 0 on success or a negative AZ_E* code;
  * az_last_error() then holds a thread-local message.  Host buffers are owned
- * by the caller; the engine owns all device memory.  One engine = one device
- * = one HIP stream; calls are synchronous (results are in the caller's
- * buffers on return).  No exception or abort crosses the ABI.
+ * by the caller; the engine owns all device memory.  One engine = one device;
+ * calls are synchronous (results are in the caller's buffers on return),
+ * except az_selfplay_step without stats and az_selfplay_drain, which run
+ * beside the queued moves -- every other call that touches engine buffers
+ * first waits for them.  No exception or abort crosses the ABI.
  */
 #ifndef AZ_H_
 #define AZ_H_
@@ -22,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 4
+#define AZ_ABI_VERSION 5
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
@@ -73,8 +75,11 @@ typedef struct az_config {
     int32_t compact;               /* 1: after every self-play move the chosen child's subtree is
                                       copied into the other half of the slot's arena (the subtrees
                                       the game has left are reclaimed, mcts.py:207); arena_edges is
-                                      then per half (0 = 8*mcts_iterations*A + H*W*A).  The tree API
-                                      (az_tree_*) does not compact: use 0 there */
+                                      then per half (0 = mcts_iterations*H*W*A + A, a half no game
+                                      can overflow, or, when two such halves per slot exceed 40% of
+                                      the free HBM, the most that fits there and at least
+                                      8*mcts_iterations*A + H*W*A; overflow is AZ_E_DEVICE).  The tree
+                                      API (az_tree_*) does not compact: it refuses such an engine */
     int32_t reserved[4];
 } az_config;
 
@@ -113,7 +118,7 @@ typedef struct az_stats {
                                  before the next search) since engine creation */
     int64_t cache_live_gens;  /* generations a lookup accepts (ages 0 .. n-1; a hit moves the entry
                                  into the current one); entries n+ generations old may be overwritten */
-    int64_t reserved[1];
+    int64_t arena_edges;      /* tree edges per slot (per half with compaction) this engine allocated */
 } az_stats;
 
 int az_abi_version(void);

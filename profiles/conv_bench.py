@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Forward-pass microbenchmark: az_forward on B random Connect-4 boards, the
 conv kernels timed with the engine's HIP events (same method as bench.py).
-Usage: python3 profiles/conv_bench.py [B] [reps] [algo: 0 Winograd, 1 direct]
+Usage: python3 profiles/conv_bench.py [B] [reps] [algo: 0 one-launch tower, 1 fp32 direct, 2 fp16x2 per layer]
 TFLOP/s are direct-convolution (algorithmic) FLOP per second."""
 import os
 import sys
@@ -32,6 +32,6 @@ for _ in range(reps):
 wall = time.perf_counter() - t0
 st = eng.stats()
 flop = B * H * W * 2 * 128 * 128 * 19 * 4
-avg = st["conv_ms"] / st["conv_launches"]
+avg = st["conv_ms"] / st["conv_launches"]  # (the tower: one launch per forward, else one per conv)
 print(f"algo={algo} B={B} reps={reps}: conv {st['conv_ms'] / reps:.3f} ms/forward ({avg * 1e3:.1f} us/launch), "
       f"{flop * reps / (st['conv_ms'] * 1e-3) / 1e12:.1f} TFLOP/s; wall {wall / reps * 1e3:.2f} ms/forward incl. H2D/D2H")

@@ -33,19 +33,17 @@ def main():
             float(r["AverageNs"]), float(r["Percentage"])
         print(f"| `{n}` | {c} | {tot / 1e6:.1f} | {avg / 1e3:.1f} | {pct:.2f} |")
     for r in rows:
-        if "conv_kernel" in r["Name"] or "conv3x3_mfma" in r["Name"] or "conv16_kernel" in r["Name"]:
-            if "stem" in r["Name"]:
-                continue
+        if "tower16_kernel" in r["Name"]:
             conv_calls += int(r["Calls"])
             conv_ns += float(r["TotalDurationNs"])
-    print(f"\nresidual-tower conv kernels: {conv_calls} launches, rocprof average "
-          f"{conv_ns / max(conv_calls, 1) / 1e3:.1f} us per launch")
+    print(f"\ntower16_kernel (the whole forward): {conv_calls} launches, rocprof average "
+          f"{conv_ns / max(conv_calls, 1) / 1e3:.1f} us per launch (whole trace, preroll included)")
     try:
         b = json.loads(open(f"{d}/bench_trace.json").read().strip().splitlines()[-1])
         rf = b["roofline"]
         print(f"same run, bench.py HIP events: avg_launch_ms {rf['avg_launch_ms']} "
               f"({rf['avg_launch_ms'] * 1e3:.1f} us), boards/launch {rf['boards_per_launch']}, "
-              f"achieved {rf['achieved']} TFLOP/s issued ({rf['dtype']}), frac {rf['frac']}; "
+              f"achieved {rf['achieved']} TFLOP/s algorithmic ({rf['dtype']}), frac {rf['frac']}; "
               f"value {b['value']} games/s under the profiler")
     except Exception as ex:  # noqa: BLE001
         print(f"(bench_trace.json unreadable: {ex})")
@@ -57,10 +55,10 @@ def main():
     tj = os.path.join(HERE, rnd, "pmc_conv_traffic.json")
     if os.path.exists(tj):
         t = json.load(open(tj))
-        print(f"\n## HBM traffic per board (PMC, B = 4096, profiles/{rnd}/pmc_conv_traffic.json)\n")
+        print(f"\n## HBM traffic per board (PMC, profiles/{rnd}/pmc_conv_traffic.json: {t.get('source', '')})\n")
         print("| kernel | HBM KB/board |")
         print("|---|---:|")
-        for algo in ("f16x2", "winograd", "direct"):
+        for algo in ("tower16", "f16x2", "direct"):
             for k, v in t.get(algo, {}).get("hbm_bytes_per_board", {}).items():
                 print(f"| `{k}` | {v / 1e3:.1f} |")
     sqd = next((p for p in (f"{d}/pmc_conv_4096_0", f"{os.path.dirname(d)}/pmc_conv_4096_0") if os.path.isdir(p)), "")

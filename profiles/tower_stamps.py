@@ -45,7 +45,8 @@ def main():
         print(f"  {n:10s} {med[i]:9.0f}  (+{med[i] - prev:7.0f})")
         prev = med[i]
     print(f"  heads: pf/vf {med[44]:.0f}, policy {med[45]:.0f}, value {med[46]:.0f}, barrier {med[47]:.0f}, "
-          f"end {med[19]:.0f}; last conv2 wave0 {med[16]:.0f} wave4 {med[38]:.0f}")
+          f"end {med[19]:.0f}; last conv2 wave0 {med[16]:.0f} wave4 {med[38]:.0f}; 1x1 done wave0 {med[42]:.0f} "
+          f"wave4 {med[43]:.0f}")
     for d in range(4):
         print(f"  b{d}: wave4 c1loop end {med[24 + 4 * d]:.0f} (wave0 {med[2 + 4 * d]:.0f}), after barrier "
               f"{med[40 + d]:.0f}, c1epi end {med[3 + 4 * d]:.0f}; wave4 c2loop end {med[26 + 4 * d]:.0f} "

@@ -33,16 +33,73 @@ def test_library_exports_every_declared_symbol():
     for name in header_functions():
         assert hasattr(lib, name), name
     L = az.load_library()
-    assert L.az_abi_version() == 4
+    assert L.az_abi_version() == 5
 
 
-def test_struct_sizes_match_header():
-    # az_config: 8 int32 + double + 4 int32 ... computed by hand from az.h
-    assert ctypes.sizeof(az.Config) == 4 * 6 + 8 + 4 * 5 + 4 + 8 + 8 + 8 + 32
-    assert ctypes.sizeof(az.Tensor) == 8 + 8 + 8 + 4 + 4
-    assert ctypes.sizeof(az.Stats) == 8 * 8 + 8 + 8 * 7 + 8 * 7
-    # az_chess_config: 2 int32, double, 6 int32, double, int64, int32 + 7 reserved
-    assert ctypes.sizeof(az.ChessConfig) == 8 + 8 + 24 + 8 + 8 + 4 + 28
+def _header_structs():
+    """{struct name: [field names]} of every `typedef struct x { ... } x;` in include/*.h"""
+    out = {}
+    for h in sorted(os.listdir(os.path.join(REPO, "include"))):
+        if not h.endswith(".h"):
+            continue
+        src = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", h)).read(), flags=re.S)
+        for name, body in re.findall(r"typedef struct (\w+) \{(.*?)\} \1;", src, re.S):
+            fields = []
+            for decl in body.split(";"):
+                decl = decl.strip()
+                if not decl:
+                    continue
+                # "int32_t filters, depth, value_hidden" or "uint64_t pieces[6]"
+                _, rest = decl.split(None, 1) if not decl.startswith("const ") else decl[6:].split(None, 1)
+                for v in rest.split(","):
+                    fields.append(re.sub(r"\[.*\]", "", v).strip().lstrip("*"))
+            out[name] = fields
+    return out
+
+
+def _compiler_layout(structs):
+    """sizeof and offsetof of every field, printed by a C program built from the headers with gcc."""
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "az.h"', '#include "az_chess.h"',
+             "int main(void) {"]
+    for name, fields in structs.items():
+        lines.append(f'  printf("{name} sizeof %zu\\n", sizeof({name}));')
+        for f in fields:
+            lines.append(f'  printf("{name} {f} %zu\\n", offsetof({name}, {f}));')
+    lines += ["  return 0;", "}"]
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "probe.c")
+        open(c, "w").write("\n".join(lines))
+        exe = os.path.join(d, "probe")
+        subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
+        text = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
+    lay = {}
+    for ln in text.splitlines():
+        s_, f, v = ln.split()
+        lay.setdefault(s_, {})[f] = int(v)
+    return lay
+
+
+def test_struct_layouts_match_the_compiler():
+    """Every header struct's size and every field's offset, as gcc lays out
+    include/*.h, equal the ctypes / numpy bindings' (a reordered field of the
+    same total size fails here)."""
+    structs = _header_structs()
+    assert set(structs) == {"az_config", "az_tensor", "az_stats", "az_chess_pos", "az_chess_config"}
+    lay = _compiler_layout(structs)
+    from custom_alphazero.chess import kernels as K
+    bindings = {"az_config": az.Config, "az_tensor": az.Tensor, "az_stats": az.Stats,
+                "az_chess_config": az.ChessConfig}
+    for name, cls in bindings.items():
+        assert lay[name]["sizeof"] == ctypes.sizeof(cls), name
+        assert [f for f, _ in cls._fields_] == structs[name], name
+        for f, _ in cls._fields_:
+            assert getattr(cls, f).offset == lay[name][f], (name, f)
+    assert lay["az_chess_pos"]["sizeof"] == K.POS_DTYPE.itemsize
+    assert list(K.POS_DTYPE.names) == structs["az_chess_pos"]
+    for f in K.POS_DTYPE.names:
+        assert K.POS_DTYPE.fields[f][1] == lay["az_chess_pos"][f], f
 
 
 def test_engine_fails_loudly_without_gpu():

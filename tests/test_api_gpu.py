@@ -220,3 +220,12 @@ def test_load_with_meta_accepts_reference_hash(tmp_path, game_cfg, golden):
     (tmp_path / ConfigPath.model_meta).write_text(json.dumps({"steps": 3, "hash": int(case["hash"]) + 1}))
     with pytest.raises(AssertionError):
         m.load_with_meta(str(tmp_path))
+    # a checkpoint an earlier build of this package wrote (raw-bytes md5 as
+    # `hash`), and this build's own meta.json (both hashes) also load
+    (tmp_path / ConfigPath.model_meta).write_text(json.dumps({"steps": 4, "hash": m.content_hash}))
+    m.load_with_meta(str(tmp_path))
+    assert m.steps == 4
+    m.save_with_meta(str(tmp_path))
+    meta = json.loads((tmp_path / ConfigPath.model_meta).read_text())
+    assert meta["hash"] == int(case["hash"]) and meta["content_hash"] == m.content_hash
+    m.load_with_meta(str(tmp_path))
