@@ -382,8 +382,9 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
 namespace az {
 // Folds (BatchNorm into conv) and uploads the network weights, Keras names
 // of custom_alphazero/model/weights.py.  in_ch = 4: the Connect-N stem
-// kernels (stem_w [36][F]); in_ch > 4 (chess, 118 planes): the stem is a
-// Winograd conv over the input zero-padded to F channels (stem_u).
+// kernels (stem_w [36][F]; the one-launch tower's stem16 pack and its
+// small-weight blob); in_ch > 4 (chess, 118 planes): the stem is one more
+// conv16 3x3 conv over the input zero-padded to F channels (stem_k).
 int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW, int A, double eps,
                  std::vector<void*>& owned) {
   std::map<std::string, const az_tensor*> m;

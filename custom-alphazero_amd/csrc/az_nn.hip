@@ -25,6 +25,7 @@
 #include <algorithm>
 
 #include "az_nn.h"
+#include "az_tree.h"
 
 namespace az {
 
@@ -61,7 +62,8 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
                                                         const float* __restrict__ ws,
                                                         const float* __restrict__ bias,
                                                         const int* __restrict__ count, int n_static,
-                                                        int H, int W, void* __restrict__ out) {
+                                                        int H, int W, void* __restrict__ out,
+                                                        unsigned long long* __restrict__ err) {
   // weights (18 KB) are read through L1 by every thread: no per-block LDS
   // staging (which cost ~18 KB of L2 traffic per 256 outputs)
   constexpr int G4 = F / 4;
@@ -92,6 +94,7 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const float4* __restrict
   acc.y = fmaxf(acc.y, 0.0f);
   acc.z = fmaxf(acc.z, 0.0f);
   acc.w = fmaxf(acc.w, 0.0f);
+  if (SPLIT && err && !(fmaxf(fmaxf(acc.x, acc.y), fmaxf(acc.z, acc.w)) <= 32752.f)) atomicOr(err, kErrActRange);
   store_act4<SPLIT>(out, (size_t)r, cg, acc);
 }
 
@@ -144,7 +147,8 @@ __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict
                                                          const float* __restrict__ ws,
                                                          const float* __restrict__ bias,
                                                          const int* __restrict__ count, int n_static,
-                                                         int H, int W, void* __restrict__ out) {
+                                                         int H, int W, void* __restrict__ out,
+                                                         unsigned long long* __restrict__ err) {
   constexpr int G4 = F / 4;
   static_assert(256 % G4 == 0, "a pass covers whole pixels");
   constexpr int PPB = 256 / G4;  // pixels per pass
@@ -188,6 +192,8 @@ __global__ __launch_bounds__(256) void stem_board_kernel(const Board* __restrict
     acc.y = fmaxf(acc.y, 0.0f);
     acc.z = fmaxf(acc.z, 0.0f);
     acc.w = fmaxf(acc.w, 0.0f);
+    // the split16 row format holds |x| <= 32752 (the per-layer convs flag theirs too)
+    if (SPLIT && err && !(fmaxf(fmaxf(acc.x, acc.y), fmaxf(acc.z, acc.w)) <= 32752.f)) atomicOr(err, kErrActRange);
     store_act4<SPLIT>(out, (size_t)r, cg, acc);
   }
 }
@@ -371,7 +377,7 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // FEAT: the 1x1 head convs already ran in the last conv's epilogue (feat =
-// [boards][HW] float4 from wino_conv_kernel<.., HEADS>); same fmaf chains.
+// [boards][HW] float4 from conv16_kernel<.., HEADS>); same fmaf chains.
 // Blocks loop over boards (4 per pass, one per wave); with STAGE the dense
 // layers' weights (policy [2HW][A], value1 [HW][hidden]) are copied into LDS
 // once per block instead of being re-read through L1 for every board.  The
@@ -695,18 +701,18 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
     if (boards) {
       if (f16)
         stem_board_kernel<F, true><<<std::min((n_max * HW + 7) / 8, 1024), 256, 0, s>>>(
-            boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a);
+            boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a, net.err);
       else
         stem_board_kernel<F, false><<<std::min((n_max * HW + 7) / 8, 1024), 256, 0, s>>>(
-            boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a);
+            boards, net.stem_w, net.stem_b, count, n_max, H, W, act_a, nullptr);
     } else {
       const float4* x4 = static_cast<const float4*>(x);
       if (f16)
         stem_conv_kernel<F, true><<<(total + 255) / 256, 256, 0, s>>>(x4, net.stem_w, net.stem_b, count, n_max,
-                                                                      H, W, act_a);
+                                                                      H, W, act_a, net.err);
       else
         stem_conv_kernel<F, false><<<(total + 255) / 256, 256, 0, s>>>(x4, net.stem_w, net.stem_b, count, n_max,
-                                                                       H, W, act_a);
+                                                                       H, W, act_a, nullptr);
     }
   }
   void* cur = act_a;  // block input

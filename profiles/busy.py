@@ -8,7 +8,8 @@ from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 win = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
-iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][-40:])
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+             r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-40:])
             for r in rows)
 t_end = max(e for _, e, _ in iv)
 t0 = t_end - int(win * 1e9)

@@ -14,7 +14,7 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         k = row["Kernel_Name"]
         if pat not in k:
             continue
-        short = k.split("(")[0][-60:]
+        short = k.replace("(anonymous namespace)::", "").split("(")[0][-60:]
         acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, cs in acc.items():
     print(k)

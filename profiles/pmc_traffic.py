@@ -19,7 +19,7 @@ def per_kernel(d, name, pat):
             k = r["Kernel_Name"]
             if r["Counter_Name"] != name or pat not in k or "stem" in k:
                 continue
-            k = k.split("(")[0].replace("void ", "")
+            k = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             acc.setdefault(k, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def short(name):
-    return name.replace("void ", "").split("(")[0][:64]
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:64]
 
 
 def main():

@@ -100,3 +100,46 @@ def test_bench_glue_world2(tmp_path):
     # and the gathered games expand to the reference's sample layout
     states, pol, rew = D.to_samples(got)
     assert states.shape == (int(got["lengths"].sum()), H, W, 4) and len(rew) == len(pol) == len(states)
+
+
+def test_bench_refuses_a_mislabelled_world():
+    """--gpus N is authoritative: under a launcher whose WORLD_SIZE differs,
+    bench.py exits non-zero before touching the GPU or printing a line."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=120, cwd=REPO, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_launch_command_for_n_ranks(monkeypatch):
+    """Without a launcher and N > 1, bench.py starts N ranks itself: one
+    torch.distributed.run child on 127.0.0.1 with the same arguments."""
+    import subprocess
+    bench = _bench()
+    seen = {}
+
+    class Done:
+        returncode = 0
+
+    def fake_run(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return Done()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(bench.sys, "argv", ["bench.py", "--gpus", "4", "--steps", "7"])
+    args = argparse.Namespace(gpus=4)
+    assert bench.launch_ranks(args) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "7"] and cmd[-5].endswith("bench.py")
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # one rank, or already under a launcher with the same world: run in-process
+    assert bench.launch_ranks(argparse.Namespace(gpus=1)) is None
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.launch_ranks(args) is None

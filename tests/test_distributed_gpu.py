@@ -111,17 +111,25 @@ def test_sharded_engine_selfplay_equals_one_engine(tmp_path, network):
 
 
 @pytest.mark.timeout(300)
-def test_bench_two_ranks_gathers_every_rank():
+@pytest.mark.parametrize("outer_launcher", [True, False])
+def test_bench_two_ranks_gathers_every_rank(outer_launcher):
+    """bench.py --gpus 2 under torch.distributed.run, and on its own (it
+    starts the two ranks itself before touching the GPU): the line reports
+    both ranks (their devices and the backend) and the replay-buffer gather
+    brings every rank's window games to rank 0."""
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--dist-backend", "gloo", "--slots", "512", "--steps", "3", "--warmup", "2",
-           "--cache-log2", "16", "--no-cpu-baseline", "--no-cache-window"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=REPO,
-                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    args = [os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--slots", "512",
+            "--steps", "3", "--warmup", "2", "--cache-log2", "16", "--no-cpu-baseline", "--no-cache-window"]
+    cmd = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", str(port)] if outer_launcher else [sys.executable]) + args
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=REPO, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["dist_backend"] == "gloo" and len(line["rank_devices"]) == 2
     gather = line["replay_buffer_gather"]
     assert gather is not None and gather["games"] == line["games_timed"] > 0
     assert gather["samples"] >= 7 * gather["games"]

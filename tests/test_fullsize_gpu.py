@@ -127,7 +127,7 @@ def test_connect_n_fullsize_configs(cfg):
         eng.close()
 
 
-CHESS = dict(sims=800, slots=256, plies=3)
+CHESS = dict(sims=800, slots=256, plies=32)
 CHESS_SEED = 900
 
 
@@ -170,12 +170,17 @@ def check_chess_games(r, n_games, plies):
         assert r["expansions"][g] >= T, g
 
 
+@pytest.mark.timeout(400)
 def test_chess_fullsize_rules_and_policies(chess_games):
-    """All 256 games at 800 sims/move (BASELINE configs[4]'s per-GPU shard),
-    3-ply cap: every game reaches the cap."""
+    """All 256 games at 800 sims/move (BASELINE configs[4]'s per-GPU shard)
+    over 32 plies (the kept subtree compacted every move): positions, legal
+    moves and root policies checked ply by ply on the oracle rules."""
     _, r = chess_games
     check_chess_games(r, CHESS["slots"], CHESS["plies"])
-    assert (r["lengths"][:CHESS["slots"]] == CHESS["plies"]).all()
+    assert (r["lengths"][:CHESS["slots"]] <= CHESS["plies"]).all()
+    # random-init play mates early in a few games (the terminal positions are
+    # checked above); most run to the cap
+    assert (r["lengths"][:CHESS["slots"]] == CHESS["plies"]).mean() > 0.75
 
 
 CHESS_LONG = dict(sims=800, slots=32, plies=64)
@@ -209,6 +214,7 @@ def test_chess_long_games_at_800_sims():
         eng.close()
 
 
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("g", [0, 255])
 def test_chess_fullsize_game_replays_on_oracle(chess_games, g):
     """Games of the 256 replay bit for bit through the chess oracle's MCTS
