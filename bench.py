@@ -250,9 +250,9 @@ def conv_kernel_name(conv_algo, chess=False):
     if conv_algo == 1:
         return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual), one launch per conv"
     if conv_algo == 0 and not chess:
-        return ("tower16_kernel (the whole forward in one launch per lane-simulation: VALU stem, the residual "
-                "tower's 8 3x3 convs as implicit GEMMs on the 16x16x32 fp16 MFMA -- fp32-accurate, both operands "
-                "as two fp16 terms, 3 products per k-step -- with activations held in LDS, 1x1 projection "
+        return ("tower16_kernel (the whole forward in one launch per lane-simulation: the stem and the "
+                "residual tower's 8 3x3 convs as implicit GEMMs on the 16x16x32 fp16 MFMA -- fp32-accurate, both operands "
+                "as two fp16 terms, 3 products per k-step -- with activations double-buffered in LDS, 1x1 projection "
                 "residuals, head 1x1 convs, dense heads, softmax, tanh)")
     return ("conv16_kernel (direct 3x3 implicit GEMM on the 16x16x32 fp16 MFMA; fp32-accurate: both operands as "
             "two fp16 terms, 3 products per k-step; fused BN/ReLU, 1x1 projection residual and head 1x1 convs; "

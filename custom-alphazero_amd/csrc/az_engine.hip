@@ -539,16 +539,31 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     tn.off_wvc = put(tb_vcw);
     tn.off_hb = put(tb_hb);
     tn.off_bpd = put(tb_pdb);
-    tn.off_wpd = put(tb_pdw);
     tn.off_bv1 = put(tb_v1b);
     tn.off_wv2 = put(tb_v2w);
+    tn.off_wpd = put(tb_pdw);
     tn.off_wv1 = put(tb_v1w);
     tn.blob_floats = (int)blob.size();
-    // wv1 (HW x hidden) joins the staged prefix when the workgroup's LDS holds it
-    tn.wv1_lds = tower16_lds_bytes(HW, tn.blob_floats) <= kTowerLdsMax;
-    tn.staged_floats = tn.wv1_lds ? tn.blob_floats : tn.off_wv1;
-    if (tower16_lds_bytes(HW, tn.staged_floats) > kTowerLdsMax)
-      return fail(AZ_E_INVALID, "tower: the board's head weights do not fit LDS (use AZ_CONV_F16X2_LAYERS)");
+    // the largest staging that fits, double-buffered tiles first: the whole
+    // blob, then without wv1, then without wpd too (those then read from L2);
+    // AZ_TOWER_INPLACE=1 forces the single in-place tile (A/B)
+    const char* inplace = getenv("AZ_TOWER_INPLACE");
+    const bool allow_db = !(inplace && inplace[0] == '1');
+    const int prefix[3] = {tn.blob_floats, tn.off_wv1, tn.off_wpd};
+    bool found = false;
+    for (int db = allow_db ? 1 : 0; db >= 0 && !found; --db) {
+      if (!tower16_heads_fit(HW, A, net.hidden, db)) continue;
+      for (int i = 0; i < 3 && !found; ++i)
+        if (tower16_lds_bytes(HW, prefix[i], db) <= kTowerLdsMax) {
+          tn.dbuf = db;
+          tn.staged_floats = prefix[i];
+          tn.wv1_lds = i == 0;
+          tn.wpd_lds = i <= 1;
+          found = true;
+        }
+    }
+    if (!found) return fail(AZ_E_INVALID, "tower: the board's activations and head weights do not fit LDS (use AZ_CONV_F16X2_LAYERS)");
+    tn.wv1_xtile = tn.dbuf && !tn.wv1_lds && tower16_wv1_xtile_fits(HW, net.hidden);
     tn.depth = net.depth;
     tn.hidden = net.hidden;
     if (!net.tower) {
@@ -564,6 +579,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     tn.blob = reinterpret_cast<const float*>(qb);
     AZ_HIP(hipMemcpy(net.tower, &tn, sizeof(TowerNet), hipMemcpyHostToDevice));
     net.tower_staged = tn.staged_floats;
+    net.tower_dbuf = tn.dbuf != 0;
   }
   net.ready = true;
   return 0;

@@ -19,29 +19,37 @@ struct TowerNet {
   float s2[kTowerMaxDepth];
   const uint4* stem16;               // the stem as 2 k-steps over k = tap*4 + plane (tower16_stem_pack)
   float stem_s;                      // its 2^(e - 12)
-  // small weights, one contiguous float blob copied into LDS at kernel start
-  // (offsets in floats, each a multiple of 4): folded biases b1[depth][F],
-  // b2[depth][F] (+ the residual's), stem bias [F]; head 1x1 convs wpc [F][2],
-  // wvc [F], hb = {bpc0, bpc1, bvc0, bv2}; policy dense bpd [A], wpd [2HW][A];
-  // value dense bv1 [hidden], wv2 [hidden], wv1 [HW][hidden] (last: in LDS only
-  // when it fits, wv1_lds)
+  // small weights, one contiguous float blob; a prefix of it is copied into
+  // LDS at kernel start (offsets in floats, each a multiple of 4): folded
+  // biases b1[depth][F], b2[depth][F] (+ the residual's), stem bias [F]; head
+  // 1x1 convs wpc [F][2], wvc [F], hb = {bpc0, bpc1, bvc0, bv2}; policy bias
+  // bpd [A]; value dense bv1 [hidden], wv2 [hidden]; then the two large
+  // matrices, staged only when the LDS holds them (else read from L2):
+  // policy dense wpd [2HW][A] (wpd_lds), value dense wv1 [HW][hidden] (wv1_lds)
   const float* blob;
   int blob_floats, staged_floats;    // whole blob; the prefix staged in LDS
-  int off_b1, off_b2, off_stemb, off_wpc, off_wvc, off_hb, off_bpd, off_wpd, off_bv1, off_wv2, off_wv1;
-  int wv1_lds;
+  int off_b1, off_b2, off_stemb, off_wpc, off_wvc, off_hb, off_bpd, off_bv1, off_wv2, off_wpd, off_wv1;
+  int wpd_lds, wv1_lds;
+  int wv1_xtile;                     // not staged, but DMA'd behind the heads' partials in X's tile (dbuf)
+  int dbuf;                          // two activation tiles (else one, updated in place)
   int depth, hidden;
 };
 // 0 when the board does not fit a tile (HW > 128); else 96 or 128
 int tower16_tile_rows(int HW);
 int tower16_boards_per_tile(int HW);
-// LDS of one workgroup: activation rows + bookkeeping + heads partials + staged blob floats
-size_t tower16_lds_bytes(int HW, int staged_floats);
+// LDS of one workgroup: activation rows (one or two tiles + zero rows) +
+// bookkeeping + staged blob floats
+size_t tower16_lds_bytes(int HW, int staged_floats, bool dbuf);
+// whether the heads' scratch (features, logits, partials) fits the tiles
+bool tower16_heads_fit(int HW, int A, int hidden, bool dbuf);
+// whether wv1 [HW][hidden] fits X's tile behind the heads' partials (dbuf)
+bool tower16_wv1_xtile_fits(int HW, int hidden);
 constexpr size_t kTowerLdsMax = 160 * 1024;
 // host: folded stem [3][3][4][F] (Keras order) -> the stem16 pack with prescale e
 void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out);
 // boards (self-play: the eval queue's boards) or x ([n][HW][4] one-hot planes,
 // az_forward) -> probs [n][A], values [n]; count (device, may be null -> n_max)
-void launch_tower16(const TowerNet* net, int staged_floats, const Board* boards, const float4* x, const int* count,
+void launch_tower16(const TowerNet* net, int staged_floats, bool dbuf, const Board* boards, const float4* x, const int* count,
                     int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
                     hipStream_t s);
 
@@ -55,6 +63,7 @@ struct NetDev {
   bool use_tower = false;   // Connect-N, AZ_CONV_F16X2: the whole forward in tower16_kernel (else per layer)
   TowerNet* tower = nullptr;  // device copy of the tower's view (load_network)
   int tower_staged = 0;       // its blob floats staged in LDS
+  bool tower_dbuf = false;    // its activations double-buffered (TowerNet::dbuf)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   float* stem_w = nullptr;  // in_ch == 4: [36][F] (k = tap*4 + c), VALU stem kernels
   float* stem_b = nullptr;  // [F]

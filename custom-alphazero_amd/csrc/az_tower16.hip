@@ -69,7 +69,7 @@ constexpr int kZeroRows = 8;
 constexpr int kNoPixel = (127 << 8) | 127;
 
 #ifdef AZ_T16_STAMPS  // diagnostic build only: phase clocks of wave 0 per workgroup (az_t16_stamps)
-constexpr int kStampBlocks = 4096, kStamps = 48;
+constexpr int kStampBlocks = 4096, kStamps = 64;
 __device__ unsigned long long g_t16_stamps[kStampBlocks][kStamps];
 #define T16_STAMP(k)                                                             \
   if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) {                           \
@@ -132,15 +132,30 @@ __device__ __forceinline__ void split_u8(const float (&x)[8], uint4& t0, uint4& 
   t1 = make_uint4(a1.x, a1.y, b1.x, b1.y);
 }
 
+// wave64 reductions without LDS round trips: DPP inside each 16-lane row
+// (xor 1, xor 2 by quad_perm, then rotations by 4 and 8), the four row
+// totals combined by readlane; a fixed order, the result wave-uniform
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <typename F>
+__device__ __forceinline__ float wreduce(float v, F op) {
+  v = op(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_f<0x124>(v));  // row_ror:4
+  v = op(v, dpp_f<0x128>(v));  // row_ror:8
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return op(op(r0, r1), op(r2, r3));
+}
 __device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wreduce(v, [](float a, float b) { return a + b; });
 }
 __device__ __forceinline__ float wmax(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wreduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
 // smallest s >= 0 with m * 2^-s <= kRange (m >= 0, finite)
@@ -155,8 +170,6 @@ struct TowerSmem {
   int flag[2];              // overflow seen in the layer being stored (alternating by layer)
   int sc[2][kTowerMaxBoards];  // per-board scale exponent of the two activation buffers' contents
   unsigned bmax[kTowerMaxBoards];  // board maxima (float bits, values >= 0) on the rare rescale path
-  float vred[kTowerMaxBoards][4];  // value-head partial sums per board and wave
-  Board boards[kTowerMaxBoards];   // the tile's boards (self-play input)
 };
 
 // store 4 channels (channel quad cq) of activation row r as split16 terms
@@ -316,7 +329,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   uint4 bq[NB][4];
   auto load_b = [&](const uint4* p, uint4(&dst)[4]) {
 #ifdef AZ_T16_DIAG_NOB  // diagnostic (wrong outputs): no weight stream in the loop
-    if (&dst != &bq[0] && &dst != &bq[1]) return;
+    if (p != wr && p != wm) return;
 #endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[q] = gld(p + q * 64);
@@ -348,6 +361,9 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   // MBW - 1 blocks' MFMAs hide the LDS latency
   uint4 aq[MBW][2];
   auto load_a1 = [&](int chunk, int mb) {
+#ifdef AZ_T16_DIAG_NOA  // diagnostic (wrong outputs): the activation fragments are read once per K loop
+    if (chunk > 0) return;
+#endif
     const char* q = actb + aaddr[mb] + 64 * chunk;
     aq[mb][0] = *reinterpret_cast<const uint4*>(q);
     aq[mb][1] = *reinterpret_cast<const uint4*>(q + 256);
@@ -361,12 +377,21 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
       const t_h8 a0 = __builtin_bit_cast(t_h8, aq[mb][0]), a1 = __builtin_bit_cast(t_h8, aq[mb][1]);
+#ifdef AZ_T16_ILV
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a1, C[mb][nb], 0, 0, 0);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], a0, C[mb][nb], 0, 0, 0);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a0, C[mb][nb], 0, 0, 0);
+#else
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a1, C[mb][nb], 0, 0, 0);
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], a0, C[mb][nb], 0, 0, 0);
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a0, C[mb][nb], 0, 0, 0);
       }
+#endif
       if (next_chunk >= 0) load_a1(next_chunk, mb);
     }
 #ifndef AZ_T16_FREESCHED
@@ -460,9 +485,19 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   constexpr int TR = 16 * MBT;    // tile rows
   constexpr int NT = NWM * 256;
   extern __shared__ __attribute__((aligned(16))) uint4 act[];  // [TR + kZeroRows] rows of kPitch bytes
-  TowerSmem& sm = *reinterpret_cast<TowerSmem*>(reinterpret_cast<char*>(act) + (TR + kZeroRows) * kPitch);
-  float* red = reinterpret_cast<float*>(&sm + 1);  // [TR][4][3] heads partial sums
-  float* blob = red + TR * 12;                     // the staged small weights (TowerNet::blob)
+  const TowerNet& T = *net;
+  // activation buffers X (block input) and H (conv1 output): two tiles around
+  // the shared zero rows when the LDS holds them (T.dbuf: an epilogue writes
+  // the other tile, so a wave that finishes its K loop stores its outputs
+  // while its SIMD partner still computes, and one barrier per layer
+  // publishes them), else one tile updated in place behind a second barrier
+  const bool dbuf = T.dbuf;
+  uint4* const bufX = act;
+  uint4* const bufH = dbuf ? act + (TR + kZeroRows) * (kPitch / 16) : act;
+  const int zX = TR, zH = dbuf ? -kZeroRows : TR;  // each tile's zero rows, relative to it
+  TowerSmem& sm = *reinterpret_cast<TowerSmem*>(reinterpret_cast<char*>(act) +
+                                                ((dbuf ? 2 : 1) * TR + kZeroRows) * kPitch);
+  float* blob = reinterpret_cast<float*>(&sm + 1);  // the staged small weights (TowerNet::blob prefix)
 
   const int HW = H * W;
   const int n = count ? *count : n_static;
@@ -472,7 +507,6 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   const int live = nbrd * HW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int zrow = TR;
-  const TowerNet& T = *net;
   T16_RSTAMP(22);
   T16_STAMP(0);
 #ifdef AZ_T16_PRIO  // A/B: the second-dispatched half of the waves at priority 1 (MI355X_MICROARCH.md 2-waves item 4)
@@ -481,9 +515,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // small weights into LDS, in the background of the stem
   dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob, T.staged_floats / 4, wave, lane);
   for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
-  if (tid < 2) sm.flag[tid] = 0;
-  if (boards && tid < nbrd) sm.boards[tid] = gld(boards + b0 + tid);
-  __syncthreads();  // the flags before any layer may set one; the boards
+  if (tid < 2) sm.flag[tid] = 0;  // published by the barrier after the stem's MFMAs
 
   const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
   int r[MBW], yx[MBW], brd[MBW];
@@ -507,16 +539,26 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // in fp16, second term 0) or from x split into two fp16 terms -- for a
   // one-hot x the operands, and so the outputs, are bitwise the boards'.
   {
+    // both k-steps' weight fragments and each M block's board (global loads
+    // issued together: one latency, no barrier before the MFMAs)
     const uint4* ws = T.stem16 + (size_t)(nq * 2) * 2 * 64 + lane;
+    uint4 bs2[2][4];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bs2[ks][q] = gld(ws + (size_t)ks * 1024 + q * 64);
+    Board bd[MBW];
+    if (boards) {
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb) bd[mb] = gld(boards + b0 + brd[mb]);
+    }
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      uint4 bs[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bs[q] = gld(ws + (size_t)ks * 1024 + q * 64);
+      const uint4(&bs)[4] = bs2[ks];
       uint4 a[MBW][2];
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb) {
@@ -531,8 +573,8 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
           if (ok) {
             const int q = (py + dy) * W + px + dx;
             if (boards) {
-              const Board& bd = sm.boards[brd[mb]];
-              const uint64_t ow = q < 64 ? bd.own[0] : bd.own[1], op = q < 64 ? bd.opp[0] : bd.opp[1];
+              const uint64_t ow = q < 64 ? bd[mb].own[0] : bd[mb].own[1],
+                             op = q < 64 ? bd[mb].opp[0] : bd[mb].opp[1];
               const bool o = (ow >> (q & 63)) & 1ull, e = (op >> (q & 63)) & 1ull;
               pl = make_float4(o || e ? 0.f : 1.f, o ? 1.f : 0.f, e ? 1.f : 0.f, 1.f);
             } else {
@@ -568,8 +610,10 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   }
   int par = 0;
   // scale state: buffer contents X (block input) and H (conv1 output)
-  bool anyX = store_layer<MBW>(act, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+  bool anyX = store_layer<MBW>(bufX, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
   bool anyH = false;
+  float* red = nullptr;  // the heads' 1x1 partials [TR][16][3] (set by the last block)
+  const int J = T.hidden;  // value head hidden units
   par ^= 1;
   T16_STAMP(21);
 
@@ -584,10 +628,10 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         accr[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
       }
     // conv1 (+ the projection residual into accr), input X
-    k_loop<MBW, 4>(act, T.k1[d], T.k2[d], acc, accr, r, yx, H, W, zrow, nq, lane, mh);
+    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, r, yx, H, W, zX, nq, lane, mh);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
-    __syncthreads();  // every wave is done reading X: H overwrites it
+    if (!dbuf) __syncthreads();  // in place: every wave is done reading X before H overwrites it
     if (d < 4) T16_STAMP(40 + d);
     {
       const float osc = T.s1[d];
@@ -604,7 +648,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         }
       }
     }
-    anyH = store_layer<MBW>(act, r, yx, brd, cq0, yv, sm, par, sm.sc[1], nbrd, err);
+    anyH = store_layer<MBW>(bufH, r, yx, brd, cq0, yv, sm, par, sm.sc[1], nbrd, err);
     par ^= 1;
     if (d < 4) T16_STAMP(3 + 4 * d);
     // the residual was accumulated at X's scale, conv2 runs at H's
@@ -620,13 +664,13 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     }
     // conv2 on H, on top of the residual
-    k_loop<MBW, 0>(act, T.k2[d], nullptr, accr, accr, r, yx, H, W, zrow, nq, lane, mh);
+    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, r, yx, H, W, zH, nq, lane, mh);
     if (d < 4) T16_STAMP(4 + 4 * d);
     if (d < 4) T16_STAMP4(26 + 4 * d);
     const float osc = T.s2[d];
     const float* bb = blob + T.off_b2 + d * 128;
     if (d + 1 < depth) {
-      __syncthreads();  // every wave is done reading H: the block output overwrites it
+      if (!dbuf) __syncthreads();  // in place: every wave is done reading H
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         const float4 bc = *reinterpret_cast<const float4*>(bb + 32 * nq + 16 * nb + 4 * gq);
@@ -638,16 +682,27 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
                                         fmaxf(fmaf(a[2], o, bc.z), 0.f), fmaxf(fmaf(a[3], o, bc.w), 0.f));
         }
       }
-      anyX = store_layer<MBW>(act, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+      anyX = store_layer<MBW>(bufX, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
       par ^= 1;
       if (d < 4) T16_STAMP(5 + 4 * d);
       continue;
     }
     // ------------------------------------------------------------ heads
     // last block: its output goes straight into the 1x1 head convs (policy
-    // F -> 2, value F -> 1, folded BN, ReLU; model.py:68-149): per lane its 8
-    // channels, a fixed xor tree over the four lane groups, the four N
-    // quarters in order through LDS
+    // F -> 2, value F -> 1, folded BN, ReLU; model.py:68-149): per lane the
+    // partial sums over its 8 channels, to LDS as 16 partials per pixel (no
+    // cross-lane step), summed in a fixed order below.  Double-buffered, they
+    // go to X's tile (dead since conv1's barrier) while other waves still
+    // read H; in place, after a barrier.
+    if (dbuf) {
+      red = reinterpret_cast<float*>(bufX);
+      // wv1 into X's tile behind the partials, by the M half that finishes first
+      if (T.wv1_xtile && mh == 0)
+        dma_to_lds<256>(reinterpret_cast<uint4*>(red + TR * 48), T.blob + T.off_wv1, HW * J / 4, nq, lane);
+    } else {
+      __syncthreads();
+      red = reinterpret_cast<float*>(act);
+    }
     const float* wpc = blob + T.off_wpc;
     const float* wvc = blob + T.off_wvc;
     int hr[MBW], hyx[MBW], hb[MBW];  // laundered (see k_loop): addresses recomputed here, not hoisted and spilled
@@ -660,150 +715,179 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
     int hq = 32 * nq + 4 * gq;  // the lane's first channel (N block 0)
     asm volatile("" : "+v"(hq));
+    T16_STAMP4(48);
+    // the lane's 8 channels' bias and head weights, read once (the partial
+    // stores below could alias them, so per M block they would be re-read)
+    float bcv[2][4], wp[2][4][2], wv[2][4];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int c0 = hq + 16 * nb;
+      const float4 bc = *reinterpret_cast<const float4*>(bb + c0);
+      const float4 p01 = *reinterpret_cast<const float4*>(wpc + 2 * c0);      // channels c0, c0+1
+      const float4 p23 = *reinterpret_cast<const float4*>(wpc + 2 * c0 + 4);  // c0+2, c0+3
+      const float4 vv = *reinterpret_cast<const float4*>(wvc + c0);
+      const float bq[4] = {bc.x, bc.y, bc.z, bc.w}, pq[8] = {p01.x, p01.y, p01.z, p01.w, p23.x, p23.y, p23.z, p23.w},
+                  vq[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        bcv[nb][v] = bq[v];
+        wp[nb][v][0] = pq[2 * v];
+        wp[nb][v][1] = pq[2 * v + 1];
+        wv[nb][v] = vq[v];
+      }
+    }
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
+      T16_STAMP4(49 + mb);
+#ifdef AZ_T16_DIAG_NOH1  // diagnostic (wrong outputs): no 1x1 head convs
+      if (hyx[mb] != kNoPixel) red[(hr[mb] * 16 + nq * 4 + gq) * 3] = accr[mb][0][0];
+      continue;
+#endif
       const float o = anyH ? ldexpf(osc, sm.sc[1][hb[mb]]) : osc;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const int c0 = hq + 16 * nb;
-        const float4 bc = *reinterpret_cast<const float4*>(bb + c0);
-        const float4 p01 = *reinterpret_cast<const float4*>(wpc + 2 * c0);      // channels c0, c0+1
-        const float4 p23 = *reinterpret_cast<const float4*>(wpc + 2 * c0 + 4);  // c0+2, c0+3
-        const float4 vv = *reinterpret_cast<const float4*>(wvc + c0);
-        const float wp[4][2] = {{p01.x, p01.y}, {p01.z, p01.w}, {p23.x, p23.y}, {p23.z, p23.w}};
-        const float wv[4] = {vv.x, vv.y, vv.z, vv.w};
-        const float bcv[4] = {bc.x, bc.y, bc.z, bc.w};
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const float yy = fmaxf(fmaf(accr[mb][nb][v], o, bcv[v]), 0.f);
-          a0 = fmaf(yy, wp[v][0], a0);
-          a1 = fmaf(yy, wp[v][1], a1);
-          a2 = fmaf(yy, wv[v], a2);
+          const float yy = fmaxf(fmaf(accr[mb][nb][v], o, bcv[nb][v]), 0.f);
+          a0 = fmaf(yy, wp[nb][v][0], a0);
+          a1 = fmaf(yy, wp[nb][v][1], a1);
+          a2 = fmaf(yy, wv[nb][v], a2);
         }
       }
-      a0 += __shfl_xor(a0, 16);
-      a1 += __shfl_xor(a1, 16);
-      a2 += __shfl_xor(a2, 16);
-      a0 += __shfl_xor(a0, 32);
-      a1 += __shfl_xor(a1, 32);
-      a2 += __shfl_xor(a2, 32);
-      if (gq == 0 && hyx[mb] != kNoPixel) {
-        red[(hr[mb] * 4 + nq) * 3 + 0] = a0;
-        red[(hr[mb] * 4 + nq) * 3 + 1] = a1;
-        red[(hr[mb] * 4 + nq) * 3 + 2] = a2;
+      if (hyx[mb] != kNoPixel) {
+        float* q = red + (hr[mb] * 16 + nq * 4 + gq) * 3;
+        q[0] = a0;
+        q[1] = a1;
+        q[2] = a2;
       }
     }
   }
+  T16_STAMP4(54);
   T16_STAMP(42);
   T16_STAMP4(43);
-  __syncthreads();  // red complete; the activation rows are no longer read
+  if (T.wv1_xtile) __builtin_amdgcn_s_waitcnt(0);  // this wave's wv1 DMA pieces have landed ...
+  __syncthreads();  // ... the partials are complete; no activation row is read any more
   T16_STAMP(18);
 
-  // flattened head features per board (Keras Flatten of NHWC: [p][c]) in the
-  // activation area: pf [bpw][2HW], vf [bpw][HW], logits [bpw][A]
-  float* pf = reinterpret_cast<float*>(act);
-  float* vf = pf + bpw * 2 * HW;
-  float* lg = vf + bpw * HW;
-  const float* hb = blob + T.off_hb;
-  const float bpc0 = hb[0], bpc1 = hb[1], bvc0 = hb[2], bv2 = hb[3];
-  for (int rr = tid; rr < live; rr += NT) {
-    const int b = rr / HW, p = rr - b * HW;
-    float t[3];
+  // head scratch (H's tile, or the in-place tile past the partials): the
+  // flattened features per board (Keras Flatten of NHWC: [p][c]) pf [bpw][2HW]
+  // and, pixel-major for the value dense's reads, vf [HW][8 boards]; logits
+  // lg [bpw][A], policy partials pp [NT], value partials vp [bpw][P][J],
+  // value hidden units hv [bpw][J]
+  const int P = NT / J;
+  float* pf = dbuf ? reinterpret_cast<float*>(bufH) : red + TR * 48;
+  float* vf = pf + ((bpw * 2 * HW + 3) & ~3);  // 16-byte aligned
+  float* lg = vf + kTowerMaxBoards * HW;
+  float* pp = lg + bpw * A;
+  float* vp = pp + NT;
+  float* hv = vp + bpw * P * J;
+  {
+    const float* hbias = blob + T.off_hb;
+    const float bpc0 = hbias[0], bpc1 = hbias[1], bvc0 = hbias[2];
+    for (int i = tid; i < 3 * live; i += NT) {  // (pixel row, output) pairs; 16 partials in order
+      const int rr = i / 3, k = i - 3 * rr;
+      const float* q = red + rr * 48 + k;
+      float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
-      t[k] = ((red[(rr * 4 + 0) * 3 + k] + red[(rr * 4 + 1) * 3 + k]) + red[(rr * 4 + 2) * 3 + k]) +
-             red[(rr * 4 + 3) * 3 + k];
-    pf[b * 2 * HW + 2 * p] = fmaxf(t[0] + bpc0, 0.f);
-    pf[b * 2 * HW + 2 * p + 1] = fmaxf(t[1] + bpc1, 0.f);
-    vf[b * HW + p] = fmaxf(t[2] + bvc0, 0.f);
+      for (int j = 0; j < 16; ++j) t += q[3 * j];
+      const int b = rr / HW, p = rr - b * HW;
+      if (k < 2) pf[b * 2 * HW + 2 * p + k] = fmaxf(t + (k ? bpc1 : bpc0), 0.f);
+      else vf[p * kTowerMaxBoards + b] = fmaxf(t + bvc0, 0.f);
+    }
   }
   __syncthreads();
   T16_STAMP(44);
-  // policy Dense(A) logits, one thread per (board, action); weights in LDS,
-  // reads issued 4 at a time ahead of their FMAs (the chain order is i)
+  // policy Dense(A): 16 threads per logit, each a strided slice of the 2HW
+  // features, then the 16 partials in order; value Dense(J): P threads per
+  // hidden unit, each a strided slice of the pixels for every board, then
+  // the P partials in order
   {
-    const float* wpd = blob + T.off_wpd;
+    const int K = 2 * HW, O = nbrd * A, OP = NT / 16;
     const float* bpd = blob + T.off_bpd;
-    const int K = 2 * HW;
-    for (int idx = tid; idx < nbrd * A; idx += NT) {
-      const int b = idx / A, a = idx - b * A;
-      float s = bpd[a];
-      const float* pb = pf + b * K;
-      int i = 0;
-      for (; i + 4 <= K; i += 4) {
-        const float p0 = pb[i], p1 = pb[i + 1], p2 = pb[i + 2], p3 = pb[i + 3];
-        const float w0 = wpd[i * A + a], w1 = wpd[(i + 1) * A + a], w2 = wpd[(i + 2) * A + a],
-                    w3 = wpd[(i + 3) * A + a];
-        s = fmaf(p0, w0, s);
-        s = fmaf(p1, w1, s);
-        s = fmaf(p2, w2, s);
-        s = fmaf(p3, w3, s);
-      }
-      for (; i < K; ++i) s = fmaf(pb[i], wpd[i * A + a], s);
-      lg[b * A + a] = s;
-    }
-  }
-  T16_STAMP(45);
-  // value Dense(hidden) ReLU -> Dense(1): thread j of each 256-thread group g,
-  // boards g, g + NWM, ...; its weight column read once for all of them
-  {
-    constexpr int NBG = kTowerMaxBoards / NWM;  // boards per group
-    const int j = tid & 255, half = tid >> 8;
-    const int hidden = T.hidden;
     const float* bv1 = blob + T.off_bv1;
     const float* wv2 = blob + T.off_wv2;
-    float sv[NBG];
+    auto policy_part = [&](int base, auto wpd) {
+      const int o = base + tid / 16, pi = tid & 15;
+      float sacc = 0.f;
+      if (o < O) {
+        const int b = o / A, a = o - b * A;
+        const float* pb = pf + b * K;
+        for (int k0 = pi; k0 < K; k0 += 64) {  // 4 features per batch, their reads ahead of the FMAs
+          float xv[4], wv[4];
 #pragma unroll
-    for (int k = 0; k < NBG; ++k) sv[k] = j < hidden ? bv1[j] : 0.f;
-    auto dot = [&](auto wcol) {  // wcol(p) = wv1[p][j]; 4 pixels' reads ahead of their FMAs
-      int p = 0;
-      for (; p + 4 <= HW; p += 4) {
-        const float w0 = wcol(p), w1 = wcol(p + 1), w2 = wcol(p + 2), w3 = wcol(p + 3);
-#pragma unroll
-        for (int k = 0; k < NBG; ++k) {
-          const int b = half + NWM * k;
-          if (b < nbrd) {
-            const float* v = vf + b * HW + p;
-            const float v0 = v[0], v1 = v[1], v2 = v[2], v3 = v[3];
-            sv[k] = fmaf(v0, w0, sv[k]);
-            sv[k] = fmaf(v1, w1, sv[k]);
-            sv[k] = fmaf(v2, w2, sv[k]);
-            sv[k] = fmaf(v3, w3, sv[k]);
+          for (int u = 0; u < 4; ++u) {
+            const int k = k0 + 16 * u;
+            xv[u] = k < K ? pb[k] : 0.f;
+            wv[u] = k < K ? wpd[k * A + a] : 0.f;
           }
-        }
-      }
-      for (; p < HW; ++p) {
-        const float w = wcol(p);
 #pragma unroll
-        for (int k = 0; k < NBG; ++k) {
-          const int b = half + NWM * k;
-          if (b < nbrd) sv[k] = fmaf(vf[b * HW + p], w, sv[k]);
+          for (int u = 0; u < 4; ++u) sacc = fmaf(xv[u], wv[u], sacc);
         }
       }
+      pp[tid] = sacc;
     };
-    if (j < hidden) {
-      if (T.wv1_lds) {
-        const float* wv1 = blob + T.off_wv1;
-        dot([&](int p) { return wv1[p * hidden + j]; });
-      } else {
-        const auto* wv1 = gbl(T.blob + T.off_wv1);
-        dot([&](int p) { return wv1[p * hidden + j]; });
-      }
-    }
-    const float w2 = j < hidden ? wv2[j] : 0.f;
+    auto value_part = [&](auto wv1) {
+      const int j = tid % J, q = tid / J;  // q: wave-uniform for J >= 64
+      if (q >= P) return;
+      float sv[kTowerMaxBoards];
 #pragma unroll
-    for (int k = 0; k < NBG; ++k) {
-      const int b = half + NWM * k;
-      if (b >= nbrd) break;  // wave-uniform
-      const float part = wsum(fmaxf(sv[k], 0.f) * w2);
-      if (lane == 0) sm.vred[b][wave & 3] = part;
+      for (int b = 0; b < kTowerMaxBoards; ++b) sv[b] = 0.f;
+      for (int p0 = q; p0 < HW; p0 += 4 * P) {  // 4 pixels per batch, every read ahead of the FMAs
+        float w[4], v[4][kTowerMaxBoards];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = p0 + u * P;
+          const int pc = p < HW ? p : 0;
+          w[u] = p < HW ? wv1[pc * J + j] : 0.f;
+          // the pixel's 8 boards (past nbrd: stale scratch, never stored)
+          const float4 lo = *reinterpret_cast<const float4*>(vf + pc * kTowerMaxBoards);
+          const float4 hi = *reinterpret_cast<const float4*>(vf + pc * kTowerMaxBoards + 4);
+          v[u][0] = lo.x, v[u][1] = lo.y, v[u][2] = lo.z, v[u][3] = lo.w;
+          v[u][4] = hi.x, v[u][5] = hi.y, v[u][6] = hi.z, v[u][7] = hi.w;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int b = 0; b < kTowerMaxBoards; ++b) sv[b] = fmaf(v[u][b], w[u], sv[b]);
+      }
+#pragma unroll
+      for (int b = 0; b < kTowerMaxBoards; ++b)
+        if (b < nbrd) vp[(b * P + q) * J + j] = sv[b];
+    };
+    for (int base = 0;; base += OP) {  // block-uniform
+      if (T.wpd_lds) policy_part(base, blob + T.off_wpd);
+      else policy_part(base, gbl(T.blob + T.off_wpd));
+      if (base == 0) {
+        if (T.wv1_lds) value_part(blob + T.off_wv1);
+        else if (T.wv1_xtile) value_part(reinterpret_cast<const float*>(bufX) + TR * 48);
+        else value_part(gbl(T.blob + T.off_wv1));
+      }
+      if (base == 0) T16_STAMP(45);
+      __syncthreads();
+      if (base == 0) T16_STAMP(46);
+      if (tid < OP && base + tid < O) {
+        const int o = base + tid, a = o % A;
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t += pp[tid * 16 + j];
+        lg[o] = t + bpd[a];
+      }
+      if (base == 0) {
+        for (int i = tid; i < nbrd * J; i += NT) {
+          const int b = i / J, j = i - b * J;
+          float t = 0.f;
+          for (int q = 0; q < P; ++q) t += vp[(b * P + q) * J + j];
+          hv[i] = fmaxf(t + bv1[j], 0.f) * wv2[j];
+        }
+      }
+      if (base == 0) T16_STAMP(47);
+      __syncthreads();
+      if (base + OP >= O) break;
     }
   }
-  T16_STAMP(46);
-  __syncthreads();
-  T16_STAMP(47);
   // softmax (one wave per board) and tanh
+  const float bv2 = blob[T.off_hb + 3];
   for (int b = wave; b < nbrd; b += NT / 64) {  // wave-uniform
     float m = -INFINITY;
     for (int a = lane; a < A; a += 64) m = fmaxf(m, lg[b * A + a]);
@@ -812,8 +896,10 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     for (int a = lane; a < A; a += 64) z += expf(lg[b * A + a] - m);
     z = wsum(z);
     for (int a = lane; a < A; a += 64) probs[(size_t)(b0 + b) * A + a] = expf(lg[b * A + a] - m) / z;
-    if (lane == 0)
-      values[b0 + b] = tanhf((((sm.vred[b][0] + sm.vred[b][1]) + sm.vred[b][2]) + sm.vred[b][3]) + bv2);
+    float v = 0.f;
+    for (int j = lane; j < J; j += 64) v += hv[b * J + j];
+    v = wsum(v);
+    if (lane == 0) values[b0 + b] = tanhf(v + bv2);
   }
   T16_STAMP(19);
   T16_RSTAMP(23);
@@ -842,10 +928,26 @@ int tower16_boards_per_tile(int HW) {
   return tr ? std::min(tr / HW, kTowerMaxBoards) : 0;
 }
 
-size_t tower16_lds_bytes(int HW, int staged_floats) {
+size_t tower16_lds_bytes(int HW, int staged_floats, bool dbuf) {
   const int tr = tower16_tile_rows(HW);
-  return (size_t)(tr + kZeroRows) * kPitch + sizeof(TowerSmem) + (size_t)tr * 4 * 3 * sizeof(float) +
-         (size_t)staged_floats * sizeof(float);
+  return (size_t)((dbuf ? 2 : 1) * tr + kZeroRows) * kPitch + sizeof(TowerSmem) + (size_t)staged_floats * sizeof(float);
+}
+
+bool tower16_heads_fit(int HW, int A, int hidden, bool dbuf) {
+  // the kernel's head scratch (pf, vf, lg, pp, vp, hv) behind the partials
+  // (in place) or in H's tile (double-buffered), for the larger block size
+  const int tr = tower16_tile_rows(HW), bpw = tower16_boards_per_tile(HW), nt = 512;
+  if (!tr || hidden < 1 || hidden > 256) return false;
+  const int p = nt / hidden;
+  const size_t need = (size_t)bpw * 2 * HW + 3 + (size_t)kTowerMaxBoards * HW + (size_t)bpw * A + nt +
+                      (size_t)bpw * p * hidden + (size_t)bpw * hidden;
+  const size_t have = (size_t)tr * (kPitch / 4) - (dbuf ? 0 : (size_t)tr * 48);
+  return need <= have;
+}
+
+bool tower16_wv1_xtile_fits(int HW, int hidden) {
+  const int tr = tower16_tile_rows(HW);
+  return tr && (HW * hidden) % 4 == 0 && (size_t)tr * 48 * 4 + (size_t)HW * hidden * 4 <= (size_t)tr * kPitch;
 }
 
 void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
@@ -868,12 +970,12 @@ void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
 }
 
 template <int MBT, int NWM>
-static void launch_mbw(const TowerNet* net, int staged, const Board* boards, const float4* x, const int* count,
+static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x, const int* count,
                        int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
                        hipStream_t s) {
   const int bpw = tower16_boards_per_tile(H * W);
   const int grid = (n_max + bpw - 1) / bpw;
-  const size_t bytes = tower16_lds_bytes(H * W, staged);
+  const size_t bytes = tower16_lds_bytes(H * W, staged, dbuf);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBT, NWM>),
@@ -884,7 +986,7 @@ static void launch_mbw(const TowerNet* net, int staged, const Board* boards, con
                                                      err);
 }
 
-void launch_tower16(const TowerNet* net, int staged, const Board* boards, const float4* x, const int* count,
+void launch_tower16(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x, const int* count,
                     int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
                     hipStream_t s) {
   if (n_max <= 0) return;
@@ -892,9 +994,9 @@ void launch_tower16(const TowerNet* net, int staged, const Board* boards, const 
 #define AZ_T16_NWM 2  // wave groups over M: 2 = two waves per SIMD (default), 1 = one (64% vs 80% of the MFMA rate in the K loop)
 #endif
   if (tower16_tile_rows(H * W) == 96)
-    launch_mbw<6, AZ_T16_NWM>(net, staged, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<6, AZ_T16_NWM>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
   else
-    launch_mbw<8, AZ_T16_NWM>(net, staged, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<8, AZ_T16_NWM>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
 }
 
 }  // namespace az

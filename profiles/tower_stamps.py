@@ -24,7 +24,7 @@ def main():
     xx = oracle.full_state(rng.randint(-1, 2, (nb, 6, 7)).astype(np.int8))
     for _ in range(30):
         eng.forward(xx)
-    buf = np.zeros((4096, 48), np.uint64)
+    buf = np.zeros((4096, 64), np.uint64)
     lib = az.load_library()
     lib.az_t16_stamps.argtypes = [ctypes.c_void_p]
     assert lib.az_t16_stamps(buf.ctypes.data) == 0
@@ -44,6 +44,7 @@ def main():
     for i, n in order:
         print(f"  {n:10s} {med[i]:9.0f}  (+{med[i] - prev:7.0f})")
         prev = med[i]
+    print("  wave4 1x1: " + " ".join(f"{med[k]:.0f}" for k in range(48, 56)))
     print(f"  heads: pf/vf {med[44]:.0f}, policy {med[45]:.0f}, value {med[46]:.0f}, barrier {med[47]:.0f}, "
           f"end {med[19]:.0f}; last conv2 wave0 {med[16]:.0f} wave4 {med[38]:.0f}; 1x1 done wave0 {med[42]:.0f} "
           f"wave4 {med[43]:.0f}")
