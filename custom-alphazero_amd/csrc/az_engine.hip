@@ -80,6 +80,13 @@ struct az_engine {
   float* act[3] = {nullptr, nullptr, nullptr};
   float* probs = nullptr;
   float* values = nullptr;
+  // AZ_EVAL_HOST: the callback and its pinned staging buffers (slots leaves)
+  az_eval_fn host_fn = nullptr;
+  void* host_user = nullptr;
+  float* host_x = nullptr;
+  float* host_p = nullptr;
+  float* host_v = nullptr;
+  int32_t* host_n = nullptr;
   double* uniforms = nullptr;
   int32_t* dev_i32 = nullptr;  // scratch for az_tree_reset
   az::Board* dev_boards = nullptr;
@@ -165,6 +172,30 @@ void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
     cells[c] = az::bit(b.own, c) ? 1 : (az::bit(b.opp, c) ? -1 : 0);
 }
 
+// AZ_EVAL_HOST: the leaves' full_state planes to the host, the callback (the
+// reference's self.model(np.expand_dims(board.full_state, 0)), mcts.py:130-137,
+// here over every leaf of the simulation at once), its outputs back to the
+// lane's evaluator slices; synchronous on the lane's stream
+int host_evaluate(az_engine* e, Lane& L, const az::Board* rows, const int32_t* n_rows) {
+  hipStream_t s = L.stream;
+  const int HW = L.g.HW, A = L.g.A;
+  az::launch_encode(rows, n_rows, L.n, HW, L.x, s);
+  AZ_HIP(hipGetLastError());
+  AZ_HIP(hipMemcpyAsync(e->host_n, n_rows, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  const int n = *e->host_n;
+  if (n <= 0) return 0;
+  if (n > L.n) return fail(AZ_E_DEVICE, "host evaluator: leaf count past the lane's slots");
+  AZ_HIP(hipMemcpyAsync(e->host_x, L.x, (size_t)n * HW * 4 * sizeof(float), hipMemcpyDeviceToHost, s));
+  AZ_HIP(hipStreamSynchronize(s));
+  if (e->host_fn(e->host_user, e->host_x, n, e->host_p, e->host_v) != 0)
+    return fail(AZ_E_CALLBACK, "the host evaluator returned an error");
+  AZ_HIP(hipMemcpyAsync(L.probs, e->host_p, (size_t)n * A * sizeof(float), hipMemcpyHostToDevice, s));
+  AZ_HIP(hipMemcpyAsync(L.values, e->host_v, (size_t)n * sizeof(float), hipMemcpyHostToDevice, s));
+  AZ_HIP(hipStreamSynchronize(s));  // the staging buffers are reused by the next lane
+  return 0;
+}
+
 // one simulation for every active slot of a lane (MCTS.search body,
 // mcts.py:171-180), enqueued on the lane's stream
 int simulate(az_engine* e, Lane& L) {
@@ -187,6 +218,8 @@ int simulate(az_engine* e, Lane& L) {
     // the stem reads the queued boards straight (no encode pass; bitwise the same outputs)
     az::launch_forward(e->net, L.x, n_rows, L.n, L.g.H, L.g.W, L.g.A, L.act[0], L.act[1], L.act[2],
                        L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr, rows);
+  } else if (e->cfg.evaluator == AZ_EVAL_HOST) {
+    if (int rc = host_evaluate(e, L, rows, n_rows)) return rc;
   } else {
     az::launch_synth_eval(L.g, rows, n_rows, L.probs, L.values, s);
   }
@@ -235,6 +268,8 @@ int cache_clear(az_engine* e) {
 int ready_to_search(az_engine* e) {
   if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
     return fail(AZ_E_STATE, "network evaluator selected but az_engine_set_weights was not called");
+  if (e->cfg.evaluator == AZ_EVAL_HOST && !e->host_fn)
+    return fail(AZ_E_STATE, "host evaluator selected but az_engine_set_evaluator was not called");
   return 0;
 }
 
@@ -611,7 +646,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
                               "(use AZ_CONV_F16X2_LAYERS or AZ_CONV_DIRECT)");
   if (c.evaluator == AZ_EVAL_NETWORK && (int64_t)c.slots * c.board_height * c.board_width * 512 >= (1ll << 31))
     return fail(AZ_E_INVALID, "slots * H * W * 512 must stay below 2^31 (32-bit activation byte offsets)");
-  if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC)
+  if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC && c.evaluator != AZ_EVAL_HOST)
     return fail(AZ_E_INVALID, "unknown evaluator");
   if (c.evaluator == AZ_EVAL_NETWORK && c.filters != 128)
     return fail(AZ_E_INVALID, "network evaluator supports filters == 128 (ConfigModel.filters)");
@@ -741,6 +776,13 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       (rc = e->alloc(&e->dev_boards, S)))
     return cleanup(rc);
   if ((rc = e->alloc(&e->x, S * g.HW * 4))) return cleanup(rc);
+  if (c.evaluator == AZ_EVAL_HOST) {
+    if (hipHostMalloc(&e->host_x, (size_t)S * g.HW * 4 * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&e->host_p, (size_t)S * A * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&e->host_v, (size_t)S * sizeof(float), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&e->host_n, sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+      return cleanup(fail(AZ_E_HIP, "host evaluator staging allocation failed"));
+  }
   if (c.evaluator == AZ_EVAL_NETWORK) {
     const size_t act = S * g.HW * 128;
     for (int i = 0; i < 3; ++i)
@@ -823,9 +865,20 @@ int az_engine_destroy(az_engine* eng) {
   for (void* p : eng->sample_bufs) (void)hipFree(p);
   for (void* p : eng->owned) (void)hipFree(p);
   if (eng->timer_ref) (void)hipEventDestroy(eng->timer_ref);
+  for (void* q : {(void*)eng->host_x, (void*)eng->host_p, (void*)eng->host_v, (void*)eng->host_n})
+    if (q) (void)hipHostFree(q);
   if (eng->stream) (void)hipStreamDestroy(eng->stream);
   delete eng;
   return 0;
+}
+
+int az_engine_set_evaluator(az_engine* e, az_eval_fn fn, void* user) {
+  if (!e || !fn) return fail(AZ_E_INVALID, "null argument");
+  if (e->cfg.evaluator != AZ_EVAL_HOST) return fail(AZ_E_STATE, "the engine was not created with AZ_EVAL_HOST");
+  if (int rc_ = enter(e)) return rc_;
+  e->host_fn = fn;
+  e->host_user = user;
+  return cache_clear(e);  // cached outputs belong to the previous evaluator
 }
 
 int az_engine_set_weights(az_engine* e, const az_tensor* tensors, int n) {

@@ -79,12 +79,22 @@ __device__ unsigned long long g_t16_stamps[kStampBlocks][kStamps];
   if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) {                           \
     g_t16_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();              \
   }
+// per wave of block 1: [c1 start, c1 end, c2 start, c2 end, HW_ID]
+__device__ unsigned long long g_t16_wstamps[kStampBlocks][8][5];
+#define T16_WSTAMP(d, k)                                                          \
+  if ((d) == 1 && (threadIdx.x & 63) == 0 && blockIdx.x < kStampBlocks) {        \
+    g_t16_wstamps[blockIdx.x][threadIdx.x >> 6][k] = __builtin_amdgcn_s_memtime(); \
+    if ((k) == 0)                                                                 \
+      g_t16_wstamps[blockIdx.x][threadIdx.x >> 6][4] =                            \
+          (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                    \
+  }
 #define T16_STAMP4(k)  /* wave 4 (wave 0's SIMD partner) */                    \
   if (threadIdx.x == 256 && blockIdx.x < kStampBlocks) {                         \
     g_t16_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memtime();                  \
   }
 #else
 #define T16_STAMP4(k)
+#define T16_WSTAMP(d, k)
 #define T16_STAMP(k)
 #define T16_RSTAMP(k)
 #endif
@@ -170,6 +180,7 @@ struct TowerSmem {
   int flag[2];              // overflow seen in the layer being stored (alternating by layer)
   int sc[2][kTowerMaxBoards];  // per-board scale exponent of the two activation buffers' contents
   unsigned bmax[kTowerMaxBoards];  // board maxima (float bits, values >= 0) on the rare rescale path
+  int prog[8];                     // each wave's k-step in the running K loop (AZ_T16_BALANCE)
 };
 
 // store 4 channels (channel quad cq) of activation row r as split16 terms
@@ -296,20 +307,41 @@ template <int MBW, int R>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
                                        t_f4 (&accr)[MBW][2], const int (&r_)[MBW], const int (&yx_)[MBW], int H, int W,
-                                       int zrow, int nq, int lane, int mh) {
+                                       int zrow, int nq, int lane, int mh, int* prog, int wave) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
-#ifndef AZ_T16_NOALTPRIO
+#if defined(AZ_T16_BALANCE)
+  // the wave of a SIMD pair that is behind takes priority 1: each wave posts
+  // its k-step to LDS and reads its partner's (used one k-step later); on a
+  // tie the younger wave (mh = 1) goes first, since age already favours the
+  // older one
+  int pk = 0;
+  const int partner = wave ^ 4;
+  auto turn = [&](int k) {
+    const int seen = __builtin_amdgcn_readfirstlane(pk);
+    if (seen > k || (seen == k && mh)) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    if (lane == 0) prog[wave] = k;
+    pk = prog[partner];
+  };
+#elif !defined(AZ_T16_NOALTPRIO)
   // the two waves of a SIMD (M halves mh = 0, 1) take turns at priority 1,
   // one k-step each, so neither falls a whole phase behind the other (without:
   // the older wave finished its K loop ~7k cycles first and its partner ran
   // the tail alone; with: ~2k, -1 to -2% kernel time)
+#ifndef AZ_T16_ALTSHIFT
+#define AZ_T16_ALTSHIFT 0  // the turns last 2^ALTSHIFT k-steps
+#endif
   auto turn = [&](int k) {
-    if ((k ^ mh) & 1) __builtin_amdgcn_s_setprio(1);
+    if (((k >> AZ_T16_ALTSHIFT) ^ mh) & 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
   };
 #else
   auto turn = [&](int) {};
   (void)mh;
+#endif
+#if !defined(AZ_T16_BALANCE)
+  (void)prog;
+  (void)wave;
 #endif
   constexpr int PF = AZ_T16_PF, NB = PF == 1 ? 2 : 4;
   static_assert(PF >= 1 && PF <= 3, "prefetch depth");
@@ -435,7 +467,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       __builtin_amdgcn_sched_barrier(0);
-      turn(c);
+      turn(R + 4 * t + c);
       // main k-step PF ahead (the prologue or the residual steps fetched 0 .. PF - 1)
       const int ahead = 4 * t + c + PF;
       if (c + PF < 4 || t < 8) load_b(wm + (size_t)ahead * 1024, bq[(c + PF) % NB]);
@@ -516,8 +548,13 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob, T.staged_floats / 4, wave, lane);
   for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 2) sm.flag[tid] = 0;  // published by the barrier after the stem's MFMAs
+  if (tid < 8) sm.prog[tid] = 0;
 
+#ifdef AZ_T16_SWAPMH  // diagnostic: the older waves take the second M half
+  const int mh = (wave >> 2) ^ 1, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
+#else
   const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
+#endif
   int r[MBW], yx[MBW], brd[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
@@ -628,7 +665,9 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         accr[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
       }
     // conv1 (+ the projection residual into accr), input X
-    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, r, yx, H, W, zX, nq, lane, mh);
+    T16_WSTAMP(d, 0);
+    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, r, yx, H, W, zX, nq, lane, mh, sm.prog, wave);
+    T16_WSTAMP(d, 1);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
     if (!dbuf) __syncthreads();  // in place: every wave is done reading X before H overwrites it
@@ -664,7 +703,9 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     }
     // conv2 on H, on top of the residual
-    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, r, yx, H, W, zH, nq, lane, mh);
+    T16_WSTAMP(d, 2);
+    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, r, yx, H, W, zH, nq, lane, mh, sm.prog, wave);
+    T16_WSTAMP(d, 3);
     if (d < 4) T16_STAMP(4 + 4 * d);
     if (d < 4) T16_STAMP4(26 + 4 * d);
     const float osc = T.s2[d];
@@ -911,6 +952,9 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
 }  // namespace az
 extern "C" int az_t16_stamps(unsigned long long* out) {  // [4096][24] of the last launch(es)
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(az::g_t16_stamps), sizeof(az::g_t16_stamps)) == hipSuccess ? 0 : -1;
+}
+extern "C" int az_t16_wstamps(unsigned long long* out) {  // [4096][8][5]
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(az::g_t16_wstamps), sizeof(az::g_t16_wstamps)) == hipSuccess ? 0 : -1;
 }
 namespace az {
 #endif

@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 
 EVAL_NETWORK = 0
 EVAL_SYNTHETIC = 1
+EVAL_HOST = 2  # include/az.h AZ_EVAL_HOST: a Python callable (Engine.set_host_evaluator)
 CONV_F16X2 = 0  # include/az.h AZ_CONV_F16X2 (default)
 CONV_DIRECT = 1
 CONV_F16X2_LAYERS = 2  # AZ_CONV_F16X2_LAYERS: the same arithmetic one layer per launch (A/B runs)
@@ -72,12 +73,26 @@ class Stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
+# az_eval_fn (include/az.h): (user, x [n][H][W][4], n, probs [n][A], values [n]) -> 0 / nonzero
+EVAL_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int32,
+                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float))
+
+
+def _as_numpy(t):
+    """A model output (numpy, torch or TF tensor, list) as a numpy array."""
+    if hasattr(t, "detach"):
+        t = t.detach().cpu()
+    if hasattr(t, "numpy"):
+        t = t.numpy()
+    return np.asarray(t)
+
+
 EXPORTED = (
     "az_abi_version", "az_last_error", "az_engine_create", "az_engine_destroy",
     "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
     "az_selfplay_run", "az_selfplay_results", "az_selfplay_drain", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
-    "az_cache_clear", "az_cache_enable",
+    "az_cache_clear", "az_cache_enable", "az_engine_set_evaluator",
     # include/az_chess.h
     "az_chess_all_moves", "az_chess_legal", "az_chess_encode", "az_chess_play", "az_chess_perft",
     "az_chess_engine_create", "az_chess_engine_destroy", "az_chess_engine_set_weights",
@@ -132,6 +147,7 @@ def load_library():
         "az_pow_table": (ctypes.c_int, [P, P, I64]),
         "az_cache_clear": (ctypes.c_int, [P]),
         "az_cache_enable": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_engine_set_evaluator": (ctypes.c_int, [P, EVAL_FN, P]),
         "az_chess_all_moves": (ctypes.c_int, [P, ctypes.c_int]),
         "az_chess_legal": (ctypes.c_int, [ctypes.c_int, P, ctypes.c_int, P, P, P, P]),
         "az_chess_encode": (ctypes.c_int, [ctypes.c_int, P, P, ctypes.c_int, P]),
@@ -227,6 +243,8 @@ class Engine:
         self._h = handle
         self._L = L
         self._n_games = 0
+        self._host_fn = None     # the EVAL_FN object (kept alive while the engine may call it)
+        self._host_error = None  # an exception the host evaluator raised inside a search
 
     def close(self):
         if getattr(self, "_h", None):
@@ -244,6 +262,38 @@ class Engine:
         """named: iterable of (name, array-like or torch tensor)."""
         arr, n, _keep = tensor_array(named)
         _check(self._L.az_engine_set_weights(self._h, arr, n))
+
+    def set_host_evaluator(self, fn):
+        """EVAL_HOST engines: fn(x) with x [n, H, W, 4] float32 full_state planes
+        returns (probs [n, A], values [n] or [n, 1]) -- the reference's
+        self.model(x) call (mcts.py:130-137), here once per simulation over
+        every leaf that needs an evaluation.  Outputs may be numpy arrays or
+        torch / TF tensors.  An exception inside fn ends the search and is
+        re-raised by the call that ran it."""
+        H, W, A = self.height, self.width, self.action_space
+
+        def cb(_user, xp, n, pp, vp):
+            try:
+                x = np.ctypeslib.as_array(xp, shape=(n, H, W, 4)).copy()
+                p, v = fn(x)
+                p = _as_numpy(p).astype(np.float32, copy=False).reshape(n, A)
+                v = _as_numpy(v).astype(np.float32, copy=False).reshape(n)
+                np.ctypeslib.as_array(pp, shape=(n, A))[:] = p
+                np.ctypeslib.as_array(vp, shape=(n,))[:] = v
+                return 0
+            except BaseException as ex:  # noqa: BLE001 - handed back to the caller below
+                self._host_error = ex
+                return 1
+
+        self._host_fn = EVAL_FN(cb)
+        _check(self._L.az_engine_set_evaluator(self._h, self._host_fn, None))
+
+    def _search_call(self, rc):
+        """_check for calls that can run the host evaluator: its exception first."""
+        if self._host_error is not None:
+            ex, self._host_error = self._host_error, None
+            raise ex
+        _check(rc)
 
     # ------------------------------------------------------------- eval
     def encode(self, boards):
@@ -273,16 +323,16 @@ class Engine:
         snapshot is complete and waits at most for the move before the
         running one (az_selfplay_step with st = NULL)."""
         if not sync:
-            _check(self._L.az_selfplay_step(self._h, int(n_moves), None))
+            self._search_call(self._L.az_selfplay_step(self._h, int(n_moves), None))
             return None
         st = Stats()
-        _check(self._L.az_selfplay_step(self._h, int(n_moves), ctypes.byref(st)))
+        self._search_call(self._L.az_selfplay_step(self._h, int(n_moves), ctypes.byref(st)))
         return st.as_dict()
 
     def selfplay_run(self, first_game, n_games, base_seed):
         st = Stats()
-        _check(self._L.az_selfplay_run(self._h, int(first_game), int(n_games),
-                                       int(base_seed) & 0xFFFFFFFF, ctypes.byref(st)))
+        self._search_call(self._L.az_selfplay_run(self._h, int(first_game), int(n_games),
+                                                  int(base_seed) & 0xFFFFFFFF, ctypes.byref(st)))
         self._n_games = int(n_games)
         return st.as_dict()
 
@@ -338,7 +388,7 @@ class Engine:
         _check(self._L.az_tree_release(self._h, len(slots), _ptr(slots)))
 
     def tree_search(self, n_sims):
-        _check(self._L.az_tree_search(self._h, int(n_sims)))
+        self._search_call(self._L.az_tree_search(self._h, int(n_sims)))
 
     def tree_play(self, uniforms=None, greedy=False, deterministic=False):
         S, A = self.slots, self.action_space

@@ -90,10 +90,15 @@ def _engine_for(model, all_possible_moves) -> az.Engine:
         evaluator = az.EVAL_SYNTHETIC
     elif model is not None and hasattr(model, "engine_weights"):
         evaluator = az.EVAL_NETWORK
+    elif callable(model):
+        # any other model is called as the reference calls it (mcts.py:130-137):
+        # model(x) -> (probabilities, value), here with every leaf of a simulation in x
+        evaluator = az.EVAL_HOST
     else:
         raise TypeError(
-            "MCTS on the MI355X engine needs a custom_alphazero PolicyValueModel (or "
-            "SyntheticEvaluator); HTTP inference and the exact solver are not on the device path")
+            "MCTS on the MI355X engine needs a model (a custom_alphazero PolicyValueModel, "
+            "SyntheticEvaluator or any callable model(x) -> (probabilities, value)); HTTP "
+            "inference and the exact solver are not on the device path")
     A = len(all_possible_moves)
     sims = max(ConfigSelfPlay.mcts_iterations, 1)
     HW = c.board_height * c.board_width
@@ -105,6 +110,8 @@ def _engine_for(model, all_possible_moves) -> az.Engine:
                     arena_edges=max(sims, 1024) * HW * A, max_tree_visits=max(sims, 1024) * HW + 2)
     if evaluator == az.EVAL_NETWORK:
         eng.set_weights(model.engine_weights())
+    elif evaluator == az.EVAL_HOST:
+        eng.set_host_evaluator(model)
     return eng
 
 
@@ -215,10 +222,15 @@ def _chess_engine_for(model):
         evaluator = az.EVAL_SYNTHETIC
     elif model is not None and hasattr(model, "engine_weights"):
         evaluator = az.EVAL_NETWORK
+    elif callable(model):
+        # any other model is called as the reference calls it (mcts.py:130-137):
+        # model(x) -> (probabilities, value), here with every leaf of a simulation in x
+        evaluator = az.EVAL_HOST
     else:
         raise TypeError(
-            "MCTS on the MI355X engine needs a custom_alphazero PolicyValueModel (or "
-            "SyntheticEvaluator); HTTP inference and the exact solver are not on the device path")
+            "MCTS on the MI355X engine needs a model (a custom_alphazero PolicyValueModel, "
+            "SyntheticEvaluator or any callable model(x) -> (probabilities, value)); HTTP "
+            "inference and the exact solver are not on the device path")
     sims = max(SP.mcts_iterations, 1)
     max_plies = max(SP.chess_max_plies, 1)
     # a tree holds at most the visits of its root: sims per search plus the
@@ -231,6 +243,8 @@ def _chess_engine_for(model):
                          arena_edges=160 * sims + 4096)
     if evaluator == az.EVAL_NETWORK:
         eng.set_weights(model.engine_weights())
+    elif evaluator == az.EVAL_HOST:
+        eng.set_host_evaluator(model)
     return eng
 
 

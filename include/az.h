@@ -24,16 +24,19 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 5
+#define AZ_ABI_VERSION 6
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
 #define AZ_E_HIP -2      /* HIP runtime error */
 #define AZ_E_STATE -3    /* call out of order (e.g. no weights) */
 #define AZ_E_DEVICE -4   /* a kernel flagged an error (arena/pow/path overflow, activation range) */
+#define AZ_E_CALLBACK -5 /* the host evaluator (AZ_EVAL_HOST) returned nonzero */
 
 #define AZ_EVAL_NETWORK 0    /* the policy/value network (model/tensorflow/model.py) */
 #define AZ_EVAL_SYNTHETIC 1  /* oracle/synth.py's exact evaluator (parity runs) */
+#define AZ_EVAL_HOST 2       /* a host callback (az_engine_set_evaluator): the reference's
+                                duck-typed self.model(x) seam, mcts/mcts.py:130-137 */
 
 /* az_config.conv_algo */
 #define AZ_CONV_F16X2 0      /* direct implicit GEMM on the fp16 MFMA, fp32-accurate: both operands
@@ -132,6 +135,18 @@ int az_engine_destroy(az_engine* eng);
 /* Replaces PolicyValueModel.load_with_meta / set_weights
  * (model/tensorflow/model.py:190-201): the engine copies and folds them. */
 int az_engine_set_weights(az_engine* eng, const az_tensor* tensors, int n);
+
+/* AZ_EVAL_HOST: the evaluator the search calls once per simulation (and
+ * lane) with the leaves that need an evaluation -- after the transposition
+ * cache and per-simulation dedup, so each board at most once -- as x
+ * [n][H][W][4] f32 full_state planes (connect_n/board.py:83-98); it writes
+ * the model's raw outputs probs [n][A] (before the legal-move mask and
+ * renormalisation, mcts.py:147-150) and values [n], and returns 0 (nonzero:
+ * the search fails with AZ_E_CALLBACK).  Host buffers, valid during the call.
+ * The outputs must be a deterministic function of the board (the cache
+ * relies on it, as the reference's plays_inferences dict does). */
+typedef int32_t (*az_eval_fn)(void* user, const float* x, int32_t n, float* probs, float* values);
+int az_engine_set_evaluator(az_engine* eng, az_eval_fn fn, void* user);
 
 /* Board.full_state + Board.legal_moves_mask for a batch of canonical int8
  * boards [n][H][W] (connect_n/board.py:91-98, :154-155) -> state

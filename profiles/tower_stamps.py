@@ -52,6 +52,19 @@ def main():
         print(f"  b{d}: wave4 c1loop end {med[24 + 4 * d]:.0f} (wave0 {med[2 + 4 * d]:.0f}), after barrier "
               f"{med[40 + d]:.0f}, c1epi end {med[3 + 4 * d]:.0f}; wave4 c2loop end {med[26 + 4 * d]:.0f} "
               f"(wave0 {med[4 + 4 * d]:.0f})")
+    if hasattr(lib, "az_t16_wstamps"):
+        ws = np.zeros((4096, 8, 5), np.uint64)
+        lib.az_t16_wstamps.argtypes = [ctypes.c_void_p]
+        assert lib.az_t16_wstamps(ws.ctypes.data) == 0
+        ws = ws[:nwg].astype(np.int64)
+        t0 = ws[:, :, 0].min(axis=1, keepdims=True)
+        simd = (ws[:, :, 4] >> 4) & 3
+        print("  block 1 per wave (median over workgroups, cycles from the first wave's conv1 start):")
+        for w in range(8):
+            c1s, c1e, c2s, c2e = (np.median(ws[:, w, k] - t0[:, 0]) for k in range(4))
+            sid = np.bincount(simd[:, w], minlength=4).argmax()
+            print(f"    wave {w} simd {sid}: conv1 {c1s:7.0f}..{c1e:7.0f} ({c1e - c1s:6.0f})  "
+                  f"conv2 {c2s:7.0f}..{c2e:7.0f} ({c2e - c2s:6.0f})")
 
 
 if __name__ == "__main__":
