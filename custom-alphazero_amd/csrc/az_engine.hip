@@ -579,18 +579,31 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     tn.off_wpd = put(tb_pdw);
     tn.off_wv1 = put(tb_v1w);
     tn.blob_floats = (int)blob.size();
-    // the largest staging that fits, double-buffered tiles first: the whole
-    // blob, then without wv1, then without wpd too (those then read from L2);
-    // AZ_TOWER_INPLACE=1 forces the single in-place tile (A/B)
+    // the layout: 128/96-row tiles double-buffered, then in place (256-row
+    // tiles in place with AZ_TOWER_TILE=256, A/B: half the weight stream per
+    // FLOP, but 128 x 32 wave tiles spill at two waves per SIMD); per layout
+    // the largest staging that fits: the whole blob, then without wv1, then
+    // without wpd too (those then read from L2).  AZ_TOWER_INPLACE=1 forces
+    // the in-place tile (A/B)
     const char* inplace = getenv("AZ_TOWER_INPLACE");
+    const char* tile = getenv("AZ_TOWER_TILE");
     const bool allow_db = !(inplace && inplace[0] == '1');
+    const bool allow_big = tile && atoi(tile) == 256;
     const int prefix[3] = {tn.blob_floats, tn.off_wv1, tn.off_wpd};
+    struct Layout {
+      int tr;
+      bool db;
+    } layouts[3] = {{allow_big ? tower16_tile_rows(HW, true) : 0, false},
+                    {allow_db ? tower16_tile_rows(HW) : 0, true},
+                    {tower16_tile_rows(HW), false}};
     bool found = false;
-    for (int db = allow_db ? 1 : 0; db >= 0 && !found; --db) {
-      if (!tower16_heads_fit(HW, A, net.hidden, db)) continue;
+    for (int li = 0; li < 3 && !found; ++li) {
+      const Layout L = layouts[li];
+      if (!L.tr || (li == 0 && L.tr != 256) || !tower16_heads_fit(HW, L.tr, A, net.hidden, L.db)) continue;
       for (int i = 0; i < 3 && !found; ++i)
-        if (tower16_lds_bytes(HW, prefix[i], db) <= kTowerLdsMax) {
-          tn.dbuf = db;
+        if (tower16_lds_bytes(HW, L.tr, prefix[i], L.db) <= kTowerLdsMax) {
+          tn.tile_rows = L.tr;
+          tn.dbuf = L.db;
           tn.staged_floats = prefix[i];
           tn.wv1_lds = i == 0;
           tn.wpd_lds = i <= 1;
@@ -598,7 +611,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
         }
     }
     if (!found) return fail(AZ_E_INVALID, "tower: the board's activations and head weights do not fit LDS (use AZ_CONV_F16X2_LAYERS)");
-    tn.wv1_xtile = tn.dbuf && !tn.wv1_lds && tower16_wv1_xtile_fits(HW, net.hidden);
+    tn.wv1_xtile = tn.dbuf && !tn.wv1_lds && tower16_wv1_xtile_fits(HW, tn.tile_rows, net.hidden);
     tn.depth = net.depth;
     tn.hidden = net.hidden;
     if (!net.tower) {
@@ -615,6 +628,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     AZ_HIP(hipMemcpy(net.tower, &tn, sizeof(TowerNet), hipMemcpyHostToDevice));
     net.tower_staged = tn.staged_floats;
     net.tower_dbuf = tn.dbuf != 0;
+    net.tower_rows = tn.tile_rows;
   }
   net.ready = true;
   return 0;

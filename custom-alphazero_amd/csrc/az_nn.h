@@ -33,23 +33,26 @@ struct TowerNet {
   int wv1_xtile;                     // not staged, but DMA'd behind the heads' partials in X's tile (dbuf)
   int dbuf;                          // two activation tiles (else one, updated in place)
   int depth, hidden;
+  int tile_rows;                     // 96, 128 or 256 pixel rows per workgroup tile
 };
-// 0 when the board does not fit a tile (HW > 128); else 96 or 128
-int tower16_tile_rows(int HW);
-int tower16_boards_per_tile(int HW);
+// 0 when the board does not fit a tile (HW > 128); else 96 or 128 (big:
+// 256-row tiles, 16 M blocks, each wave 128 rows x 32 channels -- half the
+// weight stream per FLOP; single tile in place, the LDS holds no second)
+int tower16_tile_rows(int HW, bool big = false);
+int tower16_boards_per_tile(int HW, int tile_rows);
 // LDS of one workgroup: activation rows (one or two tiles + zero rows) +
 // bookkeeping + staged blob floats
-size_t tower16_lds_bytes(int HW, int staged_floats, bool dbuf);
+size_t tower16_lds_bytes(int HW, int tile_rows, int staged_floats, bool dbuf);
 // whether the heads' scratch (features, logits, partials) fits the tiles
-bool tower16_heads_fit(int HW, int A, int hidden, bool dbuf);
+bool tower16_heads_fit(int HW, int tile_rows, int A, int hidden, bool dbuf);
 // whether wv1 [HW][hidden] fits X's tile behind the heads' partials (dbuf)
-bool tower16_wv1_xtile_fits(int HW, int hidden);
+bool tower16_wv1_xtile_fits(int HW, int tile_rows, int hidden);
 constexpr size_t kTowerLdsMax = 160 * 1024;
 // host: folded stem [3][3][4][F] (Keras order) -> the stem16 pack with prescale e
 void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out);
 // boards (self-play: the eval queue's boards) or x ([n][HW][4] one-hot planes,
 // az_forward) -> probs [n][A], values [n]; count (device, may be null -> n_max)
-void launch_tower16(const TowerNet* net, int staged_floats, bool dbuf, const Board* boards, const float4* x, const int* count,
+void launch_tower16(const TowerNet* net, int tile_rows, int staged_floats, bool dbuf, const Board* boards, const float4* x, const int* count,
                     int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
                     hipStream_t s);
 
@@ -64,6 +67,7 @@ struct NetDev {
   TowerNet* tower = nullptr;  // device copy of the tower's view (load_network)
   int tower_staged = 0;       // its blob floats staged in LDS
   bool tower_dbuf = false;    // its activations double-buffered (TowerNet::dbuf)
+  int tower_rows = 0;         // its tile rows (TowerNet::tile_rows)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   float* stem_w = nullptr;  // in_ch == 4: [36][F] (k = tap*4 + c), VALU stem kernels
   float* stem_b = nullptr;  // [F]

@@ -203,18 +203,17 @@ __device__ __forceinline__ float4 scale4(const float4 v, float s) {
 // sc_out holds the exponents).  Contains the barrier that publishes the
 // stores.  `par` alternates per layer (flag[par] is this layer's).
 template <int MBW>
-__device__ __forceinline__ bool store_layer(uint4* act, const int (&r_)[MBW], const int (&yx_)[MBW],
-                                            const int (&brd_)[MBW], int cq0, const float4 (&y)[2 * MBW],
+__device__ __forceinline__ bool store_layer(uint4* act, int r0_, const int (&yx_)[MBW], int cq0, const float4 (&y)[2 * MBW],
                                             TowerSmem& sm, int par, int* sc_out, int nbrd,
                                             unsigned long long* err) {
-  // item mb*2 + nb: row r[mb] (if valid), channel quad cq0 + 4 nb, board brd[mb];
-  // rows and boards laundered (as in k_loop): the addresses derived from them
-  // are recomputed here, not hoisted out of the depth loop and spilled
+  // item mb*2 + nb: row r0 + 16 mb (if valid), channel quad cq0 + 4 nb, board
+  // yx >> 16; rows and boards laundered (as in k_loop): the addresses derived
+  // from them are recomputed here, not hoisted out of the depth loop and spilled
   int row[MBW], brd[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
-    row[mb] = yx_[mb] != kNoPixel ? r_[mb] : -1;
-    brd[mb] = brd_[mb];
+    row[mb] = yx_[mb] != kNoPixel ? r0_ + 16 * mb : -1;
+    brd[mb] = yx_[mb] >> 16;
     asm volatile("" : "+v"(row[mb]), "+v"(brd[mb]));
   }
   float vmax = 0.f;
@@ -306,7 +305,7 @@ __device__ __forceinline__ void mfma_kstep(t_f4 (&C)[MBW][2], const uint4 (&a)[M
 template <int MBW, int R>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
-                                       t_f4 (&accr)[MBW][2], const int (&r_)[MBW], const int (&yx_)[MBW], int H, int W,
+                                       t_f4 (&accr)[MBW][2], int r0_, const int (&yx_)[MBW], int H, int W,
                                        int zrow, int nq, int lane, int mh, int* prog, int wave) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
 #if defined(AZ_T16_BALANCE)
@@ -350,11 +349,13 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   // in the runtime depth loop, and without this the compiler hoists every
   // k-step's LDS address out of it (loop invariant) and spills them
   int r[MBW], yx[MBW];
+  int r0 = r0_;
+  asm volatile("" : "+v"(r0));
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
-    r[mb] = r_[mb];
+    r[mb] = r0 + 16 * mb;
     yx[mb] = yx_[mb];
-    asm volatile("" : "+v"(r[mb]), "+v"(yx[mb]));
+    asm volatile("" : "+v"(yx[mb]));
   }
   const uint4* wm = wmain + (size_t)(nq * 2) * 2 * 64 + lane;
   const uint4* wr = R ? wres + (size_t)(nq * 2) * 2 * 64 + lane + (size_t)36 * 1024 : wmain;
@@ -373,42 +374,49 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   // and term 1 are immediate offsets (+64 c, +256)
   int aaddr[MBW];
   const char* actb = reinterpret_cast<const char*>(act);
-  auto set_own = [&]() {
+  // blocks [lo, hi) to the block input's own rows / to a runtime tap
+  auto set_own = [&](int lo, int hi) {
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
-      aaddr[mb] = (yx[mb] != kNoPixel ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
+      if (mb >= lo && mb < hi) aaddr[mb] = (yx[mb] != kNoPixel ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
   };
-  auto set_tap = [&](int t) {  // runtime tap
+  auto set_tap = [&](int t, int lo, int hi) {
     const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      const int py = yx[mb] >> 8, px = yx[mb] & 255;
+      if (mb < lo || mb >= hi) continue;
+      const int py = (yx[mb] >> 8) & 255, px = yx[mb] & 255;
       const bool ok = py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
       const int sr = r[mb] + dy * W + dx;
       aaddr[mb] = (ok ? sr : zrow + (sr & 7)) * kPitch + gq * 16;
     }
   };
-  // activation fragments, one buffer: an M block's fragments for the next
-  // k-step are read right after its last MFMA of this one, and the other
-  // MBW - 1 blocks' MFMAs hide the LDS latency
-  uint4 aq[MBW][2];
+  // activation fragments in a ring of RING M blocks: after block mb's MFMAs
+  // its slot takes block mb + RING -- of this k-step while that is < MBW, else
+  // block mb + RING - MBW of the next one -- so RING - 1 blocks' MFMAs hide
+  // each read (RING = MBW: every block's read is one k-step ahead).  At a tap
+  // change a block's address moves after its last read of the old tap: blocks
+  // < RING at the start of the tap's last k-step, blocks >= RING at the start
+  // of the next tap's first.
+  constexpr int RING = MBW > 4 ? 4 : MBW;
+  uint4 aq[RING][2];
   auto load_a1 = [&](int chunk, int mb) {
 #ifdef AZ_T16_DIAG_NOA  // diagnostic (wrong outputs): the activation fragments are read once per K loop
     if (chunk > 0) return;
 #endif
     const char* q = actb + aaddr[mb] + 64 * chunk;
-    aq[mb][0] = *reinterpret_cast<const uint4*>(q);
-    aq[mb][1] = *reinterpret_cast<const uint4*>(q + 256);
+    aq[mb % RING][0] = *reinterpret_cast<const uint4*>(q);
+    aq[mb % RING][1] = *reinterpret_cast<const uint4*>(q + 256);
   };
-  // one k-step: per M block its 6 MFMAs (t1*B0 + t0*b1 + t0*B0 per N block,
-  // smallest first), then its reads for the next k-step (next_chunk < 0: none;
-  // the caller moved aaddr to the next tap first when the tap changes)
-  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], int next_chunk) {
+  // one k-step (chunk `chunk` of the current addresses): per M block its 6
+  // MFMAs (t1*B0 + t0*b1 + t0*B0 per N block, smallest first), then the ring
+  // read that follows it (next_chunk < 0: this is the loop's last k-step)
+  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], int chunk, int next_chunk) {
     const t_h8 B0[2] = {__builtin_bit_cast(t_h8, b[0]), __builtin_bit_cast(t_h8, b[2])};
     const t_h8 B1[2] = {__builtin_bit_cast(t_h8, b[1]), __builtin_bit_cast(t_h8, b[3])};
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      const t_h8 a0 = __builtin_bit_cast(t_h8, aq[mb][0]), a1 = __builtin_bit_cast(t_h8, aq[mb][1]);
+      const t_h8 a0 = __builtin_bit_cast(t_h8, aq[mb % RING][0]), a1 = __builtin_bit_cast(t_h8, aq[mb % RING][1]);
 #ifdef AZ_T16_ILV
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a1, C[mb][nb], 0, 0, 0);
@@ -424,42 +432,38 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a0, C[mb][nb], 0, 0, 0);
       }
 #endif
-      if (next_chunk >= 0) load_a1(next_chunk, mb);
+      if (mb + RING < MBW) load_a1(chunk, mb + RING);
+      else if (next_chunk >= 0) load_a1(next_chunk, mb + RING - MBW);
     }
 #ifndef AZ_T16_FREESCHED
     // the order above, kept: the weight loads of the k-step PF ahead first,
-    // then per M block its six MFMAs and its two reads for the next k-step
+    // then per M block its six MFMAs and its two ring reads
     // (left alone, the scheduler bunched the reads and waited for all of
     // them, and for the weight loads just issued, in mid k-step)
     __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);  // VMEM reads
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
       __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);  // MFMA
-      if (next_chunk >= 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS reads
+      if (mb + RING < MBW || next_chunk >= 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS reads
     }
 #endif
   };
 
 #pragma unroll
   for (int k = 0; k < PF; ++k) load_b(bsrc(k), bq[k]);
-  if (R) set_own();
-  else set_tap(0);
+  if (R) set_own(0, MBW);
+  else set_tap(0, 0, MBW);
 #pragma unroll
-  for (int mb = 0; mb < MBW; ++mb) load_a1(0, mb);
+  for (int mb = 0; mb < RING; ++mb) load_a1(0, mb);
   // ---- residual k-steps (static)
 #pragma unroll
   for (int s = 0; s < R; ++s) {
     __builtin_amdgcn_sched_barrier(0);
     turn(s);
     load_b(bsrc(s + PF), bq[(s + PF) % NB]);
-    if (s + 1 == R) {
-      // the next k-step is tap 0's first chunk: the addresses move before the
-      // per-block reads (this k-step's MFMAs read registers only)
-      set_tap(0);
-      kstep(accr, bq[s % NB], 0);
-    } else {
-      kstep(accr, bq[s % NB], s + 1);
-    }
+    // the next k-step is tap 0's first chunk: the ring's low blocks move now
+    if (s + 1 == R) set_tap(0, 0, RING);
+    kstep(accr, bq[s % NB], s, s + 1 == R ? 0 : s + 1);
   }
   // ---- 9 taps x 4 chunks
 #pragma unroll 1
@@ -471,13 +475,15 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
       // main k-step PF ahead (the prologue or the residual steps fetched 0 .. PF - 1)
       const int ahead = 4 * t + c + PF;
       if (c + PF < 4 || t < 8) load_b(wm + (size_t)ahead * 1024, bq[(c + PF) % NB]);
+      // the tap's high blocks (first k-step; tap 0 after the residual steps)
+      if (c == 0 && RING < MBW && (t > 0 || R)) set_tap(t, RING, MBW);
       if (c < 3) {
-        kstep(acc, bq[c % NB], c + 1);
+        kstep(acc, bq[c % NB], c, c + 1);
       } else if (t < 8) {
-        set_tap(t + 1);
-        kstep(acc, bq[c % NB], 0);
+        set_tap(t + 1, 0, RING);
+        kstep(acc, bq[c % NB], c, 0);
       } else {
-        kstep(acc, bq[c % NB], -1);
+        kstep(acc, bq[c % NB], c, -1);
       }
     }
   }
@@ -523,7 +529,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // the other tile, so a wave that finishes its K loop stores its outputs
   // while its SIMD partner still computes, and one barrier per layer
   // publishes them), else one tile updated in place behind a second barrier
-  const bool dbuf = T.dbuf;
+  const bool dbuf = TR <= 128 && T.dbuf;  // 256-row tiles: in place (one tile fills the LDS)
   uint4* const bufX = act;
   uint4* const bufH = dbuf ? act + (TR + kZeroRows) * (kPitch / 16) : act;
   const int zX = TR, zH = dbuf ? -kZeroRows : TR;  // each tile's zero rows, relative to it
@@ -555,15 +561,17 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
 #else
   const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
 #endif
-  int r[MBW], yx[MBW], brd[MBW];
+  // a lane's rows r0 + 16 mb; per M block the row's board-local pixel and its
+  // board, packed (board << 16) | (y << 8) | x (kNoPixel past the boards)
+  const int r0 = mh * MBW * 16 + r16;
+  int yx[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
-    r[mb] = (mh * MBW + mb) * 16 + r16;
-    const bool valid = r[mb] < live;
-    const int b = valid ? r[mb] / HW : 0;
-    brd[mb] = b;
-    const int p = r[mb] - b * HW;
-    yx[mb] = valid ? ((p / W) << 8) | (p - (p / W) * W) : kNoPixel;
+    const int rr = r0 + 16 * mb;
+    const bool valid = rr < live;
+    const int b = valid ? rr / HW : 0;
+    const int p = rr - b * HW;
+    yx[mb] = valid ? (b << 16) | ((p / W) << 8) | (p - (p / W) * W) : kNoPixel;
   }
   const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
   t_f4 acc[MBW][2], accr[MBW][2];
@@ -584,48 +592,63 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int q = 0; q < 4; ++q) bs2[ks][q] = gld(ws + (size_t)ks * 1024 + q * 64);
-    Board bd[MBW];
-    if (boards) {
-#pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) bd[mb] = gld(boards + b0 + brd[mb]);
-    }
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
+    // M blocks in groups of at most 4 (a group's boards and operands in registers)
+    constexpr int SG = MBW <= 4 ? MBW : MBW % 4 == 0 ? 4 : MBW % 3 == 0 ? 3 : 1;
+    static_assert(MBW % SG == 0, "stem groups");
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint4(&bs)[4] = bs2[ks];
-      uint4 a[MBW][2];
+    for (int g0 = 0; g0 < MBW; g0 += SG) {
+      Board bd[SG];
+      if (boards) {
 #pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) {
-        float v[8];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int t = 8 * ks + 2 * gq + h;  // tap of k = 32 ks + 8 gq + 4 h + plane
-          const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
-          const int py = yx[mb] >> 8, px = yx[mb] & 255;
-          const bool ok = t < 9 && py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
-          float4 pl = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (ok) {
-            const int q = (py + dy) * W + px + dx;
-            if (boards) {
-              const uint64_t ow = q < 64 ? bd[mb].own[0] : bd[mb].own[1],
-                             op = q < 64 ? bd[mb].opp[0] : bd[mb].opp[1];
-              const bool o = (ow >> (q & 63)) & 1ull, e = (op >> (q & 63)) & 1ull;
-              pl = make_float4(o || e ? 0.f : 1.f, o ? 1.f : 0.f, e ? 1.f : 0.f, 1.f);
-            } else {
-              pl = gld(x + (size_t)(b0 + brd[mb]) * HW + q);
-            }
-          }
-          v[4 * h + 0] = pl.x;
-          v[4 * h + 1] = pl.y;
-          v[4 * h + 2] = pl.z;
-          v[4 * h + 3] = pl.w;
-        }
-        split_u8(v, a[mb][0], a[mb][1]);
+        for (int i = 0; i < SG; ++i) bd[i] = gld(boards + b0 + (yx[g0 + i] >> 16));
       }
-      mfma_kstep<MBW>(acc, a, bs);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4(&bs)[4] = bs2[ks];
+        const t_h8 B0[2] = {__builtin_bit_cast(t_h8, bs[0]), __builtin_bit_cast(t_h8, bs[2])};
+        const t_h8 B1[2] = {__builtin_bit_cast(t_h8, bs[1]), __builtin_bit_cast(t_h8, bs[3])};
+#pragma unroll
+        for (int i = 0; i < SG; ++i) {
+          const int mb = g0 + i;
+          float v[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int t = 8 * ks + 2 * gq + h;  // tap of k = 32 ks + 8 gq + 4 h + plane
+            const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
+            const int py = (yx[mb] >> 8) & 255, px = yx[mb] & 255;
+            const bool ok = t < 9 && py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
+            float4 pl = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ok) {
+              const int q = (py + dy) * W + px + dx;
+              if (boards) {
+                const uint64_t ow = q < 64 ? bd[i].own[0] : bd[i].own[1],
+                               op = q < 64 ? bd[i].opp[0] : bd[i].opp[1];
+                const bool o = (ow >> (q & 63)) & 1ull, e = (op >> (q & 63)) & 1ull;
+                pl = make_float4(o || e ? 0.f : 1.f, o ? 1.f : 0.f, e ? 1.f : 0.f, 1.f);
+              } else {
+                pl = gld(x + (size_t)(b0 + (yx[mb] >> 16)) * HW + q);
+              }
+            }
+            v[4 * h + 0] = pl.x;
+            v[4 * h + 1] = pl.y;
+            v[4 * h + 2] = pl.z;
+            v[4 * h + 3] = pl.w;
+          }
+          uint4 a0, a1;
+          split_u8(v, a0, a1);
+          // t1*B0 + t0*b1 + t0*B0 per N block, as mfma_kstep
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb) {
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a1), acc[mb][nb], 0, 0, 0);
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], __builtin_bit_cast(t_h8, a0), acc[mb][nb], 0, 0, 0);
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a0), acc[mb][nb], 0, 0, 0);
+          }
+        }
+      }
     }
   }
   __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
@@ -647,7 +670,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   }
   int par = 0;
   // scale state: buffer contents X (block input) and H (conv1 output)
-  bool anyX = store_layer<MBW>(bufX, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+  bool anyX = store_layer<MBW>(bufX, r0, yx, cq0, yv, sm, par, sm.sc[0], nbrd, err);
   bool anyH = false;
   float* red = nullptr;  // the heads' 1x1 partials [TR][16][3] (set by the last block)
   const int J = T.hidden;  // value head hidden units
@@ -666,7 +689,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     // conv1 (+ the projection residual into accr), input X
     T16_WSTAMP(d, 0);
-    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, r, yx, H, W, zX, nq, lane, mh, sm.prog, wave);
+    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, r0, yx, H, W, zX, nq, lane, mh, sm.prog, wave);
     T16_WSTAMP(d, 1);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
@@ -680,21 +703,21 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         const float4 bc = *reinterpret_cast<const float4*>(bb + 32 * nq + 16 * nb + 4 * gq);
 #pragma unroll
         for (int mb = 0; mb < MBW; ++mb) {
-          const float o = anyX ? ldexpf(osc, sm.sc[0][brd[mb]]) : osc;
+          const float o = anyX ? ldexpf(osc, sm.sc[0][yx[mb] >> 16]) : osc;
           const t_f4 a = acc[mb][nb];
           yv[mb * 2 + nb] = make_float4(fmaxf(fmaf(a[0], o, bc.x), 0.f), fmaxf(fmaf(a[1], o, bc.y), 0.f),
                                         fmaxf(fmaf(a[2], o, bc.z), 0.f), fmaxf(fmaf(a[3], o, bc.w), 0.f));
         }
       }
     }
-    anyH = store_layer<MBW>(bufH, r, yx, brd, cq0, yv, sm, par, sm.sc[1], nbrd, err);
+    anyH = store_layer<MBW>(bufH, r0, yx, cq0, yv, sm, par, sm.sc[1], nbrd, err);
     par ^= 1;
     if (d < 4) T16_STAMP(3 + 4 * d);
     // the residual was accumulated at X's scale, conv2 runs at H's
     if (anyX || anyH) {
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb) {
-        const int e = (anyX ? sm.sc[0][brd[mb]] : 0) - (anyH ? sm.sc[1][brd[mb]] : 0);
+        const int e = (anyX ? sm.sc[0][yx[mb] >> 16] : 0) - (anyH ? sm.sc[1][yx[mb] >> 16] : 0);
         if (e) {
           const float f = ldexpf(1.f, e);
 #pragma unroll
@@ -704,7 +727,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
     // conv2 on H, on top of the residual
     T16_WSTAMP(d, 2);
-    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, r, yx, H, W, zH, nq, lane, mh, sm.prog, wave);
+    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, r0, yx, H, W, zH, nq, lane, mh, sm.prog, wave);
     T16_WSTAMP(d, 3);
     if (d < 4) T16_STAMP(4 + 4 * d);
     if (d < 4) T16_STAMP4(26 + 4 * d);
@@ -717,13 +740,13 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         const float4 bc = *reinterpret_cast<const float4*>(bb + 32 * nq + 16 * nb + 4 * gq);
 #pragma unroll
         for (int mb = 0; mb < MBW; ++mb) {
-          const float o = anyH ? ldexpf(osc, sm.sc[1][brd[mb]]) : osc;
+          const float o = anyH ? ldexpf(osc, sm.sc[1][yx[mb] >> 16]) : osc;
           const t_f4 a = accr[mb][nb];
           yv[mb * 2 + nb] = make_float4(fmaxf(fmaf(a[0], o, bc.x), 0.f), fmaxf(fmaf(a[1], o, bc.y), 0.f),
                                         fmaxf(fmaf(a[2], o, bc.z), 0.f), fmaxf(fmaf(a[3], o, bc.w), 0.f));
         }
       }
-      anyX = store_layer<MBW>(bufX, r, yx, brd, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+      anyX = store_layer<MBW>(bufX, r0, yx, cq0, yv, sm, par, sm.sc[0], nbrd, err);
       par ^= 1;
       if (d < 4) T16_STAMP(5 + 4 * d);
       continue;
@@ -749,9 +772,9 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     int hr[MBW], hyx[MBW], hb[MBW];  // laundered (see k_loop): addresses recomputed here, not hoisted and spilled
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      hr[mb] = r[mb];
+      hr[mb] = r0 + 16 * mb;
       hyx[mb] = yx[mb];
-      hb[mb] = brd[mb];
+      hb[mb] = yx[mb] >> 16;
       asm volatile("" : "+v"(hr[mb]), "+v"(hyx[mb]), "+v"(hb[mb]));
     }
     int hq = 32 * nq + 4 * gq;  // the lane's first channel (N block 0)
@@ -959,28 +982,28 @@ extern "C" int az_t16_wstamps(unsigned long long* out) {  // [4096][8][5]
 namespace az {
 #endif
 
-int tower16_tile_rows(int HW) {
-  // 128-row tiles unless 96 rows hold the same boards (more rows per tile, same work per board)
+int tower16_tile_rows(int HW, bool big) {
   if (HW > 128) return 0;
+  // 256-row tiles when they hold at least two boards and no more than the
+  // tile's board limit
+  if (big && HW >= 256 / kTowerMaxBoards + 1) return 256;
+  // 128-row tiles unless 96 rows hold the same boards (more rows per tile, same work per board)
   const int b128 = std::min(128 / HW, kTowerMaxBoards), b96 = std::min(96 / HW, kTowerMaxBoards);
   if (b96 >= 1 && b96 * HW * 128 >= b128 * HW * 96) return 96;  // 96-row tiles are at least as full
   return 128;
 }
 
-int tower16_boards_per_tile(int HW) {
-  const int tr = tower16_tile_rows(HW);
-  return tr ? std::min(tr / HW, kTowerMaxBoards) : 0;
-}
+int tower16_boards_per_tile(int HW, int tr) { return tr ? std::min(tr / HW, kTowerMaxBoards) : 0; }
 
-size_t tower16_lds_bytes(int HW, int staged_floats, bool dbuf) {
-  const int tr = tower16_tile_rows(HW);
+size_t tower16_lds_bytes(int HW, int tr, int staged_floats, bool dbuf) {
+  (void)HW;
   return (size_t)((dbuf ? 2 : 1) * tr + kZeroRows) * kPitch + sizeof(TowerSmem) + (size_t)staged_floats * sizeof(float);
 }
 
-bool tower16_heads_fit(int HW, int A, int hidden, bool dbuf) {
+bool tower16_heads_fit(int HW, int tr, int A, int hidden, bool dbuf) {
   // the kernel's head scratch (pf, vf, lg, pp, vp, hv) behind the partials
   // (in place) or in H's tile (double-buffered), for the larger block size
-  const int tr = tower16_tile_rows(HW), bpw = tower16_boards_per_tile(HW), nt = 512;
+  const int bpw = tower16_boards_per_tile(HW, tr), nt = 512;
   if (!tr || hidden < 1 || hidden > 256) return false;
   const int p = nt / hidden;
   const size_t need = (size_t)bpw * 2 * HW + 3 + (size_t)kTowerMaxBoards * HW + (size_t)bpw * A + nt +
@@ -989,8 +1012,7 @@ bool tower16_heads_fit(int HW, int A, int hidden, bool dbuf) {
   return need <= have;
 }
 
-bool tower16_wv1_xtile_fits(int HW, int hidden) {
-  const int tr = tower16_tile_rows(HW);
+bool tower16_wv1_xtile_fits(int HW, int tr, int hidden) {
   return tr && (HW * hidden) % 4 == 0 && (size_t)tr * 48 * 4 + (size_t)HW * hidden * 4 <= (size_t)tr * kPitch;
 }
 
@@ -1017,9 +1039,9 @@ template <int MBT, int NWM>
 static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x, const int* count,
                        int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
                        hipStream_t s) {
-  const int bpw = tower16_boards_per_tile(H * W);
+  const int bpw = tower16_boards_per_tile(H * W, 16 * MBT);
   const int grid = (n_max + bpw - 1) / bpw;
-  const size_t bytes = tower16_lds_bytes(H * W, staged, dbuf);
+  const size_t bytes = tower16_lds_bytes(H * W, 16 * MBT, staged, dbuf);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBT, NWM>),
@@ -1030,15 +1052,17 @@ static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* 
                                                      err);
 }
 
-void launch_tower16(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x, const int* count,
-                    int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
-                    hipStream_t s) {
+void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, const Board* boards, const float4* x,
+                    const int* count, int n_max, int H, int W, int A, float* probs, float* values,
+                    unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
 #ifndef AZ_T16_NWM
 #define AZ_T16_NWM 2  // wave groups over M: 2 = two waves per SIMD (default), 1 = one (64% vs 80% of the MFMA rate in the K loop)
 #endif
-  if (tower16_tile_rows(H * W) == 96)
+  if (tile_rows == 96)
     launch_mbw<6, AZ_T16_NWM>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
+  else if (tile_rows == 256)
+    launch_mbw<16, 2>(net, staged, false, boards, x, count, n_max, H, W, A, probs, values, err, s);
   else
     launch_mbw<8, AZ_T16_NWM>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
 }
