@@ -612,6 +612,24 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     }
     if (!found) return fail(AZ_E_INVALID, "tower: the board's activations and head weights do not fit LDS (use AZ_CONV_F16X2_LAYERS)");
     tn.wv1_xtile = tn.dbuf && !tn.wv1_lds && tower16_wv1_xtile_fits(HW, tn.tile_rows, net.hidden);
+    // the slot plan: border blocks skip the taps past their edge (AZ_TOWER_PLAN=0: natural order, A/B)
+    {
+      const char* plan = getenv("AZ_TOWER_PLAN");
+      std::vector<int> pix;
+      int skip[2] = {0, 0};
+      if (!(plan && plan[0] == '0') && net.board_h * net.board_w == HW)
+        tower16_slot_plan(net.board_h, net.board_w, tn.tile_rows, pix, skip);
+      tn.slot_pix = nullptr;
+      tn.skip[0] = skip[0];
+      tn.skip[1] = skip[1];
+      if (!pix.empty()) {
+        void* q = nullptr;
+        AZ_HIP(hipMalloc(&q, pix.size() * sizeof(int)));
+        owned.push_back(q);
+        AZ_HIP(hipMemcpy(q, pix.data(), pix.size() * sizeof(int), hipMemcpyHostToDevice));
+        tn.slot_pix = reinterpret_cast<const int*>(q);
+      }
+    }
     tn.depth = net.depth;
     tn.hidden = net.hidden;
     if (!net.tower) {
@@ -803,6 +821,8 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       if ((rc = e->alloc(&e->act[i], act))) return cleanup(rc);
   }
   e->net.depth = c.depth;
+  e->net.board_h = g.H;
+  e->net.board_w = g.W;
   e->net.algo = c.conv_algo == AZ_CONV_F16X2_LAYERS ? AZ_CONV_F16X2 : c.conv_algo;
   e->net.use_tower = c.conv_algo == AZ_CONV_F16X2;
   e->net.err = e->t.stats + az::kStatErrors;

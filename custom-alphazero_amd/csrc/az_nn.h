@@ -34,7 +34,16 @@ struct TowerNet {
   int dbuf;                          // two activation tiles (else one, updated in place)
   int depth, hidden;
   int tile_rows;                     // 96, 128 or 256 pixel rows per workgroup tile
+  // slot plan (tower16_slot_plan; null: natural order, no skips): the pixel
+  // word of each of a full tile's slots, and per M half the blocks each tap
+  // skips (2 bits per tap over the wave's blocks 0 and 1)
+  const int* slot_pix;
+  int skip[2];
 };
+// the slot plan of 128-row tiles: border blocks (16 slots whose pixels all
+// sit on one board edge) skip the three taps that read past that edge; empty
+// vectors when no plan applies (then natural order)
+void tower16_slot_plan(int H, int W, int tile_rows, std::vector<int>& slot_pix, int skip[2]);
 // 0 when the board does not fit a tile (HW > 128); else 96 or 128 (big:
 // 256-row tiles, 16 M blocks, each wave 128 rows x 32 channels -- half the
 // weight stream per FLOP; single tile in place, the LDS holds no second)
@@ -69,6 +78,7 @@ struct NetDev {
   bool tower_dbuf = false;    // its activations double-buffered (TowerNet::dbuf)
   int tower_rows = 0;         // its tile rows (TowerNet::tile_rows)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
+  int board_h = 0, board_w = 0;  // Connect-N board (the tower's slot plan)
   float* stem_w = nullptr;  // in_ch == 4: [36][F] (k = tap*4 + c), VALU stem kernels
   float* stem_b = nullptr;  // [F]
   // in_ch > 4 (chess): the stem is one more 3x3 conv over the zero-padded planes

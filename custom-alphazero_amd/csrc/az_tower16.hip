@@ -42,9 +42,15 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
+#include <type_traits>
 
 #include "az_nn.h"
 #include "az_tree.h"
+
+#ifndef AZ_T16_NWM
+#define AZ_T16_NWM 2  // wave groups over M: 2 = two waves per SIMD (default), 1 = one (-10% isolated, round 3)
+#endif
 
 namespace az {
 
@@ -64,9 +70,16 @@ constexpr float kRange = 32752.f;  // largest |x| a split16 term pair holds
 // its own row has.
 constexpr int kPitch = 544;
 constexpr int kZeroRows = 8;
-// a tile row's board-local pixel, packed (y << 8) | x; rows past the tile's
-// boards get y = x = 127, outside every board, so each tap reads a zero row
-constexpr int kNoPixel = (127 << 8) | 127;
+// A tile slot's pixel word: (board << 16) | (y << 8) | x.  An empty slot (past
+// the tile's boards, or a pad of the slot plan) has y = 127, off every board,
+// so each of its taps reads a zero row; its x holds the LDS bank residue its
+// zero-row reads take.  A slot's LDS row is its pixel's natural row
+// board * HW + y * W + x (the activation image is in natural order whatever
+// order the slots compute in); an empty slot's "row" is its residue.
+__device__ __forceinline__ bool pix_ok(int yx) { return ((yx >> 8) & 255) != 127; }
+__device__ __forceinline__ int pix_row(int yx, int HW, int W) {
+  return pix_ok(yx) ? (yx >> 16) * HW + ((yx >> 8) & 255) * W + (yx & 255) : (yx & 7);
+}
 
 #ifdef AZ_T16_STAMPS  // diagnostic build only: phase clocks of wave 0 per workgroup (az_t16_stamps)
 constexpr int kStampBlocks = 4096, kStamps = 64;
@@ -203,16 +216,17 @@ __device__ __forceinline__ float4 scale4(const float4 v, float s) {
 // sc_out holds the exponents).  Contains the barrier that publishes the
 // stores.  `par` alternates per layer (flag[par] is this layer's).
 template <int MBW>
-__device__ __forceinline__ bool store_layer(uint4* act, int r0_, const int (&yx_)[MBW], int cq0, const float4 (&y)[2 * MBW],
+__device__ __forceinline__ bool store_layer(uint4* act, int HW, int W, const int (&yx_)[MBW], int cq0, const float4 (&y)[2 * MBW],
                                             TowerSmem& sm, int par, int* sc_out, int nbrd,
                                             unsigned long long* err) {
-  // item mb*2 + nb: row r0 + 16 mb (if valid), channel quad cq0 + 4 nb, board
-  // yx >> 16; rows and boards laundered (as in k_loop): the addresses derived
-  // from them are recomputed here, not hoisted out of the depth loop and spilled
+  // item mb*2 + nb: the slot's LDS row (if it holds a pixel), channel quad
+  // cq0 + 4 nb, board yx >> 16; rows and boards laundered (as in k_loop): the
+  // addresses derived from them are recomputed here, not hoisted out of the
+  // depth loop and spilled
   int row[MBW], brd[MBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
-    row[mb] = yx_[mb] != kNoPixel ? r0_ + 16 * mb : -1;
+    row[mb] = pix_ok(yx_[mb]) ? pix_row(yx_[mb], HW, W) : -1;
     brd[mb] = yx_[mb] >> 16;
     asm volatile("" : "+v"(row[mb]), "+v"(brd[mb]));
   }
@@ -302,11 +316,14 @@ __device__ __forceinline__ void mfma_kstep(t_f4 (&C)[MBW][2], const uint4 (&a)[M
 // loop with the chunks unrolled inside: fully unrolled, the two phases made
 // a 110 KB kernel (the instruction cache holds 64 KB).  Ring slots are the
 // k-step mod 4 (R is 0 or 4), so every register index stays static.
+template <int V>
+using IC = std::integral_constant<int, V>;
+
 template <int MBW, int R>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
-                                       t_f4 (&accr)[MBW][2], int r0_, const int (&yx_)[MBW], int H, int W,
-                                       int zrow, int nq, int lane, int mh, int* prog, int wave) {
+                                       t_f4 (&accr)[MBW][2], const int (&yx_)[MBW], int H, int W,
+                                       int zrow, int nq, int lane, int mh, int* prog, int wave, int skw) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
 #if defined(AZ_T16_BALANCE)
   // the wave of a SIMD pair that is behind takes priority 1: each wave posts
@@ -349,13 +366,11 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   // in the runtime depth loop, and without this the compiler hoists every
   // k-step's LDS address out of it (loop invariant) and spills them
   int r[MBW], yx[MBW];
-  int r0 = r0_;
-  asm volatile("" : "+v"(r0));
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
-    r[mb] = r0 + 16 * mb;
     yx[mb] = yx_[mb];
     asm volatile("" : "+v"(yx[mb]));
+    r[mb] = pix_row(yx[mb], H * W, W);
   }
   const uint4* wm = wmain + (size_t)(nq * 2) * 2 * 64 + lane;
   const uint4* wr = R ? wres + (size_t)(nq * 2) * 2 * 64 + lane + (size_t)36 * 1024 : wmain;
@@ -378,7 +393,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   auto set_own = [&](int lo, int hi) {
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
-      if (mb >= lo && mb < hi) aaddr[mb] = (yx[mb] != kNoPixel ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
+      if (mb >= lo && mb < hi) aaddr[mb] = (pix_ok(yx[mb]) ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
   };
   auto set_tap = [&](int t, int lo, int hi) {
     const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
@@ -410,13 +425,18 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   };
   // one k-step (chunk `chunk` of the current addresses): per M block its 6
   // MFMAs (t1*B0 + t0*b1 + t0*B0 per N block, smallest first), then the ring
-  // read that follows it (next_chunk < 0: this is the loop's last k-step)
-  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], int chunk, int next_chunk) {
+  // read that follows it (next_chunk < 0: this is the loop's last k-step).
+  // skc: blocks whose MFMAs this k-step skips (every row's tap is off its
+  // board: they would add exact zeros); skn: blocks the next k-step skips (no
+  // read for them; 0 across a tap change)
+  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], int chunk, int next_chunk, auto skc, auto skn) {
+    constexpr int SKC = decltype(skc)::value, SKN = decltype(skn)::value;
     const t_h8 B0[2] = {__builtin_bit_cast(t_h8, b[0]), __builtin_bit_cast(t_h8, b[2])};
     const t_h8 B1[2] = {__builtin_bit_cast(t_h8, b[1]), __builtin_bit_cast(t_h8, b[3])};
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
       const t_h8 a0 = __builtin_bit_cast(t_h8, aq[mb % RING][0]), a1 = __builtin_bit_cast(t_h8, aq[mb % RING][1]);
+      if (((SKC >> mb) & 1) == 0) {
 #ifdef AZ_T16_ILV
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a1, C[mb][nb], 0, 0, 0);
@@ -432,8 +452,12 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a0, C[mb][nb], 0, 0, 0);
       }
 #endif
-      if (mb + RING < MBW) load_a1(chunk, mb + RING);
-      else if (next_chunk >= 0) load_a1(next_chunk, mb + RING - MBW);
+      }
+      if (mb + RING < MBW) {
+        if (((SKC >> (mb + RING)) & 1) == 0) load_a1(chunk, mb + RING);
+      } else if (next_chunk >= 0 && ((SKN >> (mb + RING - MBW)) & 1) == 0) {
+        load_a1(next_chunk, mb + RING - MBW);
+      }
     }
 #ifndef AZ_T16_FREESCHED
     // the order above, kept: the weight loads of the k-step PF ahead first,
@@ -443,8 +467,10 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     __builtin_amdgcn_sched_group_barrier(0x0020, 4, 0);  // VMEM reads
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);  // MFMA
-      if (mb + RING < MBW || next_chunk >= 0) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS reads
+      if (((SKC >> mb) & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);  // MFMA
+      const bool rd = mb + RING < MBW ? ((SKC >> (mb + RING)) & 1) == 0
+                                      : next_chunk >= 0 && ((SKN >> (mb + RING - MBW)) & 1) == 0;
+      if (rd) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS reads
     }
 #endif
   };
@@ -463,11 +489,11 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     load_b(bsrc(s + PF), bq[(s + PF) % NB]);
     // the next k-step is tap 0's first chunk: the ring's low blocks move now
     if (s + 1 == R) set_tap(0, 0, RING);
-    kstep(accr, bq[s % NB], s, s + 1 == R ? 0 : s + 1);
+    kstep(accr, bq[s % NB], s, s + 1 == R ? 0 : s + 1, IC<0>{}, IC<0>{});
   }
-  // ---- 9 taps x 4 chunks
-#pragma unroll 1
-  for (int t = 0; t < 9; ++t) {
+  // ---- 9 taps x 4 chunks; per tap the blocks it skips (skw: 2 bits per tap,
+  // blocks 0 and 1 of the wave, from the slot plan) select one of four bodies
+  auto tap = [&](int t, auto skc) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       __builtin_amdgcn_sched_barrier(0);
@@ -478,14 +504,22 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
       // the tap's high blocks (first k-step; tap 0 after the residual steps)
       if (c == 0 && RING < MBW && (t > 0 || R)) set_tap(t, RING, MBW);
       if (c < 3) {
-        kstep(acc, bq[c % NB], c, c + 1);
+        kstep(acc, bq[c % NB], c, c + 1, skc, skc);
       } else if (t < 8) {
         set_tap(t + 1, 0, RING);
-        kstep(acc, bq[c % NB], c, 0);
+        kstep(acc, bq[c % NB], c, 0, skc, IC<0>{});
       } else {
-        kstep(acc, bq[c % NB], c, -1);
+        kstep(acc, bq[c % NB], c, -1, skc, IC<0>{});
       }
     }
+  };
+#pragma unroll 1
+  for (int t = 0; t < 9; ++t) {
+    const int m = (skw >> (2 * t)) & 3;  // wave-uniform
+    if (m == 0) tap(t, IC<0>{});
+    else if (m == 1) tap(t, IC<1>{});
+    else if (m == 2) tap(t, IC<2>{});
+    else tap(t, IC<3>{});
   }
 #ifndef AZ_T16_NOALTPRIO
   __builtin_amdgcn_s_setprio(0);
@@ -561,18 +595,27 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
 #else
   const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
 #endif
-  // a lane's rows r0 + 16 mb; per M block the row's board-local pixel and its
-  // board, packed (board << 16) | (y << 8) | x (kNoPixel past the boards)
+  // a lane's slots r0 + 16 mb and their pixel words: the slot plan's
+  // (T.slot_pix, a full tile's boards; the boards past this tile's are
+  // emptied, keeping their rows' bank residues) or the natural order
   const int r0 = mh * MBW * 16 + r16;
   int yx[MBW];
+  const int* plan = T.slot_pix;
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
     const int rr = r0 + 16 * mb;
-    const bool valid = rr < live;
-    const int b = valid ? rr / HW : 0;
-    const int p = rr - b * HW;
-    yx[mb] = valid ? (b << 16) | ((p / W) << 8) | (p - (p / W) * W) : kNoPixel;
+    if (plan) {
+      const int v = *gbl(plan + rr);
+      yx[mb] = pix_ok(v) && (v >> 16) >= nbrd ? (127 << 8) | (pix_row(v, HW, W) & 7) : v;
+    } else {
+      const bool valid = rr < live;
+      const int b = valid ? rr / HW : 0;
+      const int p = rr - b * HW;
+      yx[mb] = valid ? (b << 16) | ((p / W) << 8) | (p - (p / W) * W) : (127 << 8) | (rr & 7);
+    }
   }
+  // this wave's tap skips (2 bits per tap over its blocks 0 and 1)
+  const int skw = T.skip[mh];
   const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
   t_f4 acc[MBW][2], accr[MBW][2];
   float4 yv[2 * MBW];
@@ -670,7 +713,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   }
   int par = 0;
   // scale state: buffer contents X (block input) and H (conv1 output)
-  bool anyX = store_layer<MBW>(bufX, r0, yx, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+  bool anyX = store_layer<MBW>(bufX, HW, W, yx, cq0, yv, sm, par, sm.sc[0], nbrd, err);
   bool anyH = false;
   float* red = nullptr;  // the heads' 1x1 partials [TR][16][3] (set by the last block)
   const int J = T.hidden;  // value head hidden units
@@ -689,7 +732,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     // conv1 (+ the projection residual into accr), input X
     T16_WSTAMP(d, 0);
-    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, r0, yx, H, W, zX, nq, lane, mh, sm.prog, wave);
+    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, yx, H, W, zX, nq, lane, mh, sm.prog, wave, skw);
     T16_WSTAMP(d, 1);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
@@ -710,7 +753,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
         }
       }
     }
-    anyH = store_layer<MBW>(bufH, r0, yx, cq0, yv, sm, par, sm.sc[1], nbrd, err);
+    anyH = store_layer<MBW>(bufH, HW, W, yx, cq0, yv, sm, par, sm.sc[1], nbrd, err);
     par ^= 1;
     if (d < 4) T16_STAMP(3 + 4 * d);
     // the residual was accumulated at X's scale, conv2 runs at H's
@@ -727,7 +770,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
     // conv2 on H, on top of the residual
     T16_WSTAMP(d, 2);
-    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, r0, yx, H, W, zH, nq, lane, mh, sm.prog, wave);
+    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, mh, sm.prog, wave, skw);
     T16_WSTAMP(d, 3);
     if (d < 4) T16_STAMP(4 + 4 * d);
     if (d < 4) T16_STAMP4(26 + 4 * d);
@@ -746,7 +789,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
                                         fmaxf(fmaf(a[2], o, bc.z), 0.f), fmaxf(fmaf(a[3], o, bc.w), 0.f));
         }
       }
-      anyX = store_layer<MBW>(bufX, r0, yx, cq0, yv, sm, par, sm.sc[0], nbrd, err);
+      anyX = store_layer<MBW>(bufX, HW, W, yx, cq0, yv, sm, par, sm.sc[0], nbrd, err);
       par ^= 1;
       if (d < 4) T16_STAMP(5 + 4 * d);
       continue;
@@ -772,7 +815,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     int hr[MBW], hyx[MBW], hb[MBW];  // laundered (see k_loop): addresses recomputed here, not hoisted and spilled
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
-      hr[mb] = r0 + 16 * mb;
+      hr[mb] = pix_row(yx[mb], HW, W);
       hyx[mb] = yx[mb];
       hb[mb] = yx[mb] >> 16;
       asm volatile("" : "+v"(hr[mb]), "+v"(hyx[mb]), "+v"(hb[mb]));
@@ -804,7 +847,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     for (int mb = 0; mb < MBW; ++mb) {
       T16_STAMP4(49 + mb);
 #ifdef AZ_T16_DIAG_NOH1  // diagnostic (wrong outputs): no 1x1 head convs
-      if (hyx[mb] != kNoPixel) red[(hr[mb] * 16 + nq * 4 + gq) * 3] = accr[mb][0][0];
+      if (pix_ok(hyx[mb])) red[(hr[mb] * 16 + nq * 4 + gq) * 3] = accr[mb][0][0];
       continue;
 #endif
       const float o = anyH ? ldexpf(osc, sm.sc[1][hb[mb]]) : osc;
@@ -819,7 +862,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
           a2 = fmaf(yy, wv[nb][v], a2);
         }
       }
-      if (hyx[mb] != kNoPixel) {
+      if (pix_ok(hyx[mb])) {
         float* q = red + (hr[mb] * 16 + nq * 4 + gq) * 3;
         q[0] = a0;
         q[1] = a1;
@@ -1016,6 +1059,112 @@ bool tower16_wv1_xtile_fits(int HW, int tr, int hidden) {
   return tr && (HW * hidden) % 4 == 0 && (size_t)tr * 48 * 4 + (size_t)HW * hidden * 4 <= (size_t)tr * kPitch;
 }
 
+// The slot plan (128-row tiles, 8 waves: M half h = blocks 4h .. 4h + 3).
+// A 3x3 'same' conv tap (dy, dx) reads zeros for every pixel on the board edge
+// it points past; a block whose 16 slots all hold such pixels (or are empty)
+// would add exact zeros for that tap, so it skips the tap's MFMAs and reads.
+// Border blocks: half 0 = [top (y = 0: dy = -1), left (x = 0: dx = -1), 2
+// interior], half 1 = [bottom (dy = +1), right (dx = +1), 2 interior]: each
+// wave skips 6 of its 36 block-taps per conv (C4: 3 boards, 16.7% of the 3x3
+// MFMAs), the two halves alike.  Bank conflicts: a ds_read_b128 lane group
+// reads 8 slots of one term parity ({0-3, 12-15} or {4-11}) at one tap shift;
+// its bank quads are 2 row + slot (mod 16), so the 8 slots' LDS rows must
+// differ mod 8.  Per residue r the pixels with row = r (mod 8) fill 2 slots of
+// each border block (a bipartite matching against the edge classes; corners
+// belong to two), then 2 of each interior block; an interior residue past 8
+// takes a free slot (one 2-way conflict).
+void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int skip[2]) {
+  slot_pix.clear();
+  skip[0] = skip[1] = 0;
+#if AZ_T16_NWM != 2
+  return;  // the plan assumes two M halves of four blocks
+#endif
+  const int HW = H * W, nb = tower16_boards_per_tile(HW, tr);
+  if (tr != 128 || H < 3 || W < 3 || nb < 1) return;
+  auto cls = [&](int b, int y, int x, int c) {
+    (void)b;
+    return c == 0 ? y == 0 : c == 1 ? x == 0 : c == 2 ? y == H - 1 : x == W - 1;
+  };
+  const int border_block[4] = {0, 1, 4, 5}, interior_block[4] = {2, 3, 6, 7};
+  const int S1[8] = {0, 1, 2, 3, 12, 13, 14, 15}, S2[8] = {4, 5, 6, 7, 8, 9, 10, 11};
+  const int kEmpty = 127 << 8;
+  std::vector<int> slot(128, -1);  // pixel word or -1 (free)
+  auto word = [&](int b, int y, int x) { return (b << 16) | (y << 8) | x; };
+  for (int r = 0; r < 8; ++r) {
+    std::vector<int> P;  // natural rows with residue r
+    for (int n = r; n < nb * HW; n += 8) P.push_back(n);
+    // border slots: class c, copy k (0, 1); Kuhn's matching
+    std::vector<int> owner(8, -1);
+    std::function<bool(int, std::vector<char>&)> aug = [&](int pi, std::vector<char>& seen) {
+      const int n = P[pi], b = n / HW, y = (n % HW) / W, x = n % W;
+      for (int sl = 0; sl < 8; ++sl) {
+        if (seen[sl] || !cls(b, y, x, sl / 2)) continue;
+        seen[sl] = 1;
+        if (owner[sl] < 0 || aug(owner[sl], seen)) {
+          owner[sl] = pi;
+          return true;
+        }
+      }
+      return false;
+    };
+    for (int pi = 0; pi < (int)P.size(); ++pi) {
+      std::vector<char> seen(8, 0);
+      aug(pi, seen);
+    }
+    std::vector<char> used(P.size(), 0);
+    for (int sl = 0; sl < 8; ++sl) {
+      const int blk = border_block[sl / 2], pos = (sl & 1) ? S2[r] : S1[r];
+      if (owner[sl] >= 0) {
+        const int n = P[owner[sl]];
+        slot[blk * 16 + pos] = word(n / HW, (n % HW) / W, n % W);
+        used[owner[sl]] = 1;
+      } else {
+        slot[blk * 16 + pos] = kEmpty | r;
+      }
+    }
+    // interior: 2 per block at this residue's positions, in order
+    int k = 0;
+    for (int pi = 0; pi < (int)P.size(); ++pi) {
+      if (used[pi]) continue;
+      if (k >= 8) continue;  // overflow: placed below
+      const int blk = interior_block[k / 2], pos = (k & 1) ? S2[r] : S1[r];
+      const int n = P[pi];
+      slot[blk * 16 + pos] = word(n / HW, (n % HW) / W, n % W);
+      used[pi] = 1;
+      ++k;
+    }
+    for (; k < 8; ++k) slot[interior_block[k / 2] * 16 + ((k & 1) ? S2[r] : S1[r])] = -2 - r;  // free, residue r
+    for (int pi = 0; pi < (int)P.size(); ++pi)
+      if (!used[pi]) slot.push_back(P[pi]);  // overflow natural rows, after the 128 slots
+  }
+  // overflow pixels into free interior slots
+  for (size_t i = 128; i < slot.size(); ++i) {
+    const int n = slot[i];
+    bool placed = false;
+    for (int j = 0; j < 128 && !placed; ++j)
+      if (slot[j] <= -2) {
+        slot[j] = word(n / HW, (n % HW) / W, n % W);
+        placed = true;
+      }
+    if (!placed) return;  // cannot happen: 128 slots >= the tile's pixels
+  }
+  slot.resize(128);
+  int border_pixels[4] = {0, 0, 0, 0};
+  for (int j = 0; j < 128; ++j) {
+    if (slot[j] <= -2) slot[j] = kEmpty | (-2 - slot[j]);
+    for (int c = 0; c < 4; ++c)
+      if (j / 16 == border_block[c] && ((slot[j] >> 8) & 255) != 127) ++border_pixels[c];
+  }
+  for (int c = 0; c < 4; ++c)
+    if (border_pixels[c] < 12) return;  // too few edge pixels for a border block: natural order
+  for (int t = 0; t < 9; ++t) {
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    skip[0] |= ((dy == -1 ? 1 : 0) | (dx == -1 ? 2 : 0)) << (2 * t);
+    skip[1] |= ((dy == 1 ? 1 : 0) | (dx == 1 ? 2 : 0)) << (2 * t);
+  }
+  slot_pix = slot;
+}
+
 void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
   // conv16_pack's fragment layout ([k-step][n-block][term][lane] x 8 fp16) over k = tap*4 + plane
   const int F = 128;
@@ -1056,9 +1205,6 @@ void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, c
                     const int* count, int n_max, int H, int W, int A, float* probs, float* values,
                     unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
-#ifndef AZ_T16_NWM
-#define AZ_T16_NWM 2  // wave groups over M: 2 = two waves per SIMD (default), 1 = one (64% vs 80% of the MFMA rate in the K loop)
-#endif
   if (tile_rows == 96)
     launch_mbw<6, AZ_T16_NWM>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
   else if (tile_rows == 256)

@@ -277,6 +277,27 @@ def test_forward_matches_keras_restatement(shape, conv_algo):
     np.testing.assert_allclose(p.sum(axis=1), 1.0, atol=1e-6)
 
 
+@pytest.mark.parametrize("shape", [(6, 7, True), (5, 5, False), (7, 6, True), (4, 5, True), (9, 9, True)])
+def test_tower_slot_plan_is_bitwise_the_natural_order(shape, monkeypatch):
+    """The slot plan (border blocks skip the taps past their board edge: exact
+    zeros not added) gives the same bits as the natural slot order, full and
+    partial tiles, one-hot and arbitrary inputs."""
+    H, W, grav = shape
+    rng = np.random.RandomState(21)
+    x = oracle.full_state(random_boards(rng, 37, H, W))
+    x[-4:] = rng.rand(4, H, W, 4).astype(np.float32)
+    out = []
+    for plan in ("1", "0"):
+        monkeypatch.setenv("AZ_TOWER_PLAN", plan)
+        eng, _ = make_net_engine(H, W, 4, grav, slots=300, conv_algo=az.CONV_F16X2)
+        out.append(eng.forward(x))
+        out.append(eng.forward(x[:1]))
+        eng.close()
+    for a, b in zip(out[:2], out[2:]):
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+
+
 def _range_weights(S=2.0 ** 18):
     """Weights whose stem output and block-0 conv1 output are S times the
     network's (BN gamma/beta scaled: ReLU is positively homogeneous) while the
