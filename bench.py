@@ -299,7 +299,9 @@ def conv_roofline(args, conv_algo, per_forward, boards_per_launch, avg_ms, busy_
         "flop_per_board": int(direct_flop_per_board),
         "issued": {"achieved": round(issued, 2), "frac": round(issued / peak, 4),
                    "flop_per_board": int(issued_per_board),
-                   "basis": "MFMA FLOP the kernel issues (3 fp16 products per MAC) per launch / avg_launch_ms"},
+                   "basis": ("MFMA FLOP the kernel issues per board (3 fp16 products per MAC; the tower's own count: "
+                             "tile pad rows and stem in, the slot plan's skipped border taps out) x boards per launch "
+                             "/ avg_launch_ms")},
         "busy_union": {"achieved": round(union, 2), "frac": round(union / peak, 4),
                        "basis": "all timed boards' direct FLOP / union of the kernel intervals of all lanes"},
         "launches_per_forward": per_forward,
@@ -679,6 +681,10 @@ def main():
     HW, F = args.height * args.width, 128
     direct_flop = HW * 2 * F * F * 19 * args.depth
     issued = 3 * direct_flop if args.conv_algo != 1 else direct_flop
+    if args.conv_algo == 0 and st1.get("issued_flop_per_board", 0) > 0:
+        # the tower reports what it issues: its tiles' pad rows and stem in,
+        # the slot plan's skipped border taps (exact zeros) out
+        issued = st1["issued_flop_per_board"]
     per_forward = 1 if args.conv_algo == 0 else 2 * args.depth
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     boards_per_launch = local_evals / max(conv_launches / per_forward, 1)

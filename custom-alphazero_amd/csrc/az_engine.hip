@@ -647,6 +647,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     net.tower_staged = tn.staged_floats;
     net.tower_dbuf = tn.dbuf != 0;
     net.tower_rows = tn.tile_rows;
+    net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip);
   }
   net.ready = true;
   return 0;
@@ -1033,6 +1034,7 @@ int az_stats_get(az_engine* e, az_stats* st) {
   }
   st->games_drained = e->drained;
   st->arena_edges = e->g.arena_cap;
+  st->issued_flop_per_board = e->net.issued_flop_per_board;
   return 0;
 }
 

@@ -44,6 +44,9 @@ struct TowerNet {
 // sit on one board edge) skip the three taps that read past that edge; empty
 // vectors when no plan applies (then natural order)
 void tower16_slot_plan(int H, int W, int tile_rows, std::vector<int>& slot_pix, int skip[2]);
+// MFMA FLOP tower16_kernel issues per board: a full tile's stem + 2 depth
+// convs (+ the 1x1 projection k-steps) less the plan's skipped taps, / boards
+double tower16_issued_flop_per_board(int HW, int tile_rows, int depth, const int skip[2]);
 // 0 when the board does not fit a tile (HW > 128); else 96 or 128 (big:
 // 256-row tiles, 16 M blocks, each wave 128 rows x 32 channels -- half the
 // weight stream per FLOP; single tile in place, the LDS holds no second)
@@ -79,6 +82,7 @@ struct NetDev {
   int tower_rows = 0;         // its tile rows (TowerNet::tile_rows)
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   int board_h = 0, board_w = 0;  // Connect-N board (the tower's slot plan)
+  double issued_flop_per_board = 0;  // MFMA FLOP a forward issues per board (tower; az_stats)
   float* stem_w = nullptr;  // in_ch == 4: [36][F] (k = tap*4 + c), VALU stem kernels
   float* stem_b = nullptr;  // [F]
   // in_ch > 4 (chess): the stem is one more 3x3 conv over the zero-padded planes

@@ -492,7 +492,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     kstep(accr, bq[s % NB], s, s + 1 == R ? 0 : s + 1, IC<0>{}, IC<0>{});
   }
   // ---- 9 taps x 4 chunks; per tap the blocks it skips (skw: 2 bits per tap,
-  // blocks 0 and 1 of the wave, from the slot plan) select one of four bodies
+  // blocks 0 and 1 of the wave, from the slot plan) select one of three bodies
   auto tap = [&](int t, auto skc) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -515,11 +515,14 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   };
 #pragma unroll 1
   for (int t = 0; t < 9; ++t) {
-    const int m = (skw >> (2 * t)) & 3;  // wave-uniform
+    // wave-uniform; never 3 (one edge per tap and half).  The dispatch's
+    // shape moves the register allocation: this form spills 7 VGPRs outside
+    // the loops, testing m == 2 first spilled 140 inside them (and ran the
+    // kernel at half speed) -- tests/test_kernel_resources_cpu.py guards it
+    const int m = (skw >> (2 * t)) & 3;
     if (m == 0) tap(t, IC<0>{});
     else if (m == 1) tap(t, IC<1>{});
-    else if (m == 2) tap(t, IC<2>{});
-    else tap(t, IC<3>{});
+    else tap(t, IC<2>{});
   }
 #ifndef AZ_T16_NOALTPRIO
   __builtin_amdgcn_s_setprio(0);
@@ -755,6 +758,12 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
     anyH = store_layer<MBW>(bufH, HW, W, yx, cq0, yv, sm, par, sm.sc[1], nbrd, err);
     par ^= 1;
+    // last block, double-buffered: X's tile is dead from here (conv2 reads H
+    // and the residual sits in accr), so the value dense's wv1 streams into
+    // it behind the heads' partials while conv2 runs (every wave a share)
+    if (dbuf && T.wv1_xtile && d + 1 == depth)
+      dma_to_lds<NT>(reinterpret_cast<uint4*>(reinterpret_cast<float*>(bufX) + TR * 48), T.blob + T.off_wv1,
+                     HW * J / 4, wave, lane);
     if (d < 4) T16_STAMP(3 + 4 * d);
     // the residual was accumulated at X's scale, conv2 runs at H's
     if (anyX || anyH) {
@@ -802,10 +811,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     // go to X's tile (dead since conv1's barrier) while other waves still
     // read H; in place, after a barrier.
     if (dbuf) {
-      red = reinterpret_cast<float*>(bufX);
-      // wv1 into X's tile behind the partials, by the M half that finishes first
-      if (T.wv1_xtile && mh == 0)
-        dma_to_lds<256>(reinterpret_cast<uint4*>(red + TR * 48), T.blob + T.off_wv1, HW * J / 4, nq, lane);
+      red = reinterpret_cast<float*>(bufX);  // (wv1 behind them since the start of this conv2)
     } else {
       __syncthreads();
       red = reinterpret_cast<float*>(act);
@@ -1063,10 +1069,14 @@ bool tower16_wv1_xtile_fits(int HW, int tr, int hidden) {
 // A 3x3 'same' conv tap (dy, dx) reads zeros for every pixel on the board edge
 // it points past; a block whose 16 slots all hold such pixels (or are empty)
 // would add exact zeros for that tap, so it skips the tap's MFMAs and reads.
-// Border blocks: half 0 = [top (y = 0: dy = -1), left (x = 0: dx = -1), 2
-// interior], half 1 = [bottom (dy = +1), right (dx = +1), 2 interior]: each
-// wave skips 6 of its 36 block-taps per conv (C4: 3 boards, 16.7% of the 3x3
-// MFMAs), the two halves alike.  Bank conflicts: a ds_read_b128 lane group
+// Border blocks: half 0 = [top (y = 0: skips dy = -1), bottom (dy = +1), 2
+// interior], half 1 = [left (x = 0: dx = -1), right (dx = +1), 2 interior]:
+// each wave skips 6 of its 36 block-taps per conv (C4: 3 boards, 16.7% of the
+// 3x3 MFMAs), and the two waves of a SIMD (one per half) stay within one
+// block-tap of each other along the tap order, so they share the MFMA pipe
+// evenly to the end of the loop (top/left against bottom/right put half 0's
+// skips in the first taps and half 1's in the last: half 0 finished its loop
+// 8k cycles early and half 1 ran the tail alone, phase stamps).  Bank conflicts: a ds_read_b128 lane group
 // reads 8 slots of one term parity ({0-3, 12-15} or {4-11}) at one tap shift;
 // its bank quads are 2 row + slot (mod 16), so the 8 slots' LDS rows must
 // differ mod 8.  Per residue r the pixels with row = r (mod 8) fill 2 slots of
@@ -1085,7 +1095,11 @@ void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int ski
     (void)b;
     return c == 0 ? y == 0 : c == 1 ? x == 0 : c == 2 ? y == H - 1 : x == W - 1;
   };
+#ifdef AZ_T16_PAIR_TL  // A/B: the first plan (half 0 top + left, half 1 bottom + right)
   const int border_block[4] = {0, 1, 4, 5}, interior_block[4] = {2, 3, 6, 7};
+#else
+  const int border_block[4] = {0, 4, 1, 5}, interior_block[4] = {2, 3, 6, 7};  // T, L, B, R
+#endif
   const int S1[8] = {0, 1, 2, 3, 12, 13, 14, 15}, S2[8] = {4, 5, 6, 7, 8, 9, 10, 11};
   const int kEmpty = 127 << 8;
   std::vector<int> slot(128, -1);  // pixel word or -1 (free)
@@ -1159,10 +1173,30 @@ void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int ski
     if (border_pixels[c] < 12) return;  // too few edge pixels for a border block: natural order
   for (int t = 0; t < 9; ++t) {
     const int dy = t / 3 - 1, dx = t % 3 - 1;
-    skip[0] |= ((dy == -1 ? 1 : 0) | (dx == -1 ? 2 : 0)) << (2 * t);
-    skip[1] |= ((dy == 1 ? 1 : 0) | (dx == 1 ? 2 : 0)) << (2 * t);
+#ifdef AZ_T16_PAIR_TL
+    skip[0] |= ((dy == -1 ? 1 : 0) | (dx == -1 && dy != -1 ? 2 : 0)) << (2 * t);  // 3 -> 1 (the kernel's bodies)
+    skip[1] |= ((dy == 1 ? 1 : 0) | (dx == 1 && dy != 1 ? 2 : 0)) << (2 * t);
+#else
+    skip[0] |= ((dy == -1 ? 1 : 0) | (dy == 1 ? 2 : 0)) << (2 * t);
+    skip[1] |= ((dx == -1 ? 1 : 0) | (dx == 1 ? 2 : 0)) << (2 * t);
+#endif
   }
   slot_pix = slot;
+}
+
+double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2]) {
+  const int bpw = tower16_boards_per_tile(HW, tr);
+  if (!bpw) return 0;
+  const int nwm = tr == 256 ? 2 : AZ_T16_NWM, mbw = tr / 16 / nwm;  // blocks per wave
+  const double mfma = 16.0 * 16 * 32 * 2;                          // FLOP per v_mfma_f32_16x16x32_f16
+  double steps = 0;  // block-k-steps over the tile's waves (4 N quarters per M group)
+  for (int h = 0; h < nwm; ++h) {
+    int skipped = 0;  // block-taps one wave of this M group skips per conv
+    for (int t = 0; t < 9; ++t) skipped += __builtin_popcount((skip[h] >> (2 * t)) & 3);
+    const double per_wave = 2.0 * mbw + depth * ((4.0 + 36) * mbw + 36.0 * mbw - 2.0 * 4 * skipped);
+    steps += 4 * per_wave;
+  }
+  return steps * 6 * mfma / bpw;  // 2 N blocks x 3 products per block-k-step
 }
 
 void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 6
+#define AZ_ABI_VERSION 7
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
@@ -122,6 +122,9 @@ typedef struct az_stats {
     int64_t cache_live_gens;  /* generations a lookup accepts (ages 0 .. n-1; a hit moves the entry
                                  into the current one); entries n+ generations old may be overwritten */
     int64_t arena_edges;      /* tree edges per slot (per half with compaction) this engine allocated */
+    double issued_flop_per_board; /* MFMA FLOP the network forward issues per board (the one-launch
+                                     tower: per full tile after its slot plan's skipped taps, / boards
+                                     per tile; 0 = not reported) */
 } az_stats;
 
 int az_abi_version(void);
