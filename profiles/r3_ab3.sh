@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 3 A/B 3: border blocks paired T/B and L/R per half; stamps; the first pairing (pairtl, T+L | B+R)
+# round 3 A/B: tests, stamps, isolated forward and in-bench games/s against the previous build (prev)
 set -o pipefail
 out=gpurun_out/r3_ab3
 mkdir -p $out
@@ -8,11 +8,11 @@ timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 1
 tail -2 $out/tests.log
 AZ_LIB_PATH=$PWD/profiles/ab_libs/stamps/libaz.so timeout -k 10 120 python profiles/tower_stamps.py 4096 2>&1 | grep -v amdgpu.ids > $out/stamps.txt || exit 1
 head -24 $out/stamps.txt
-for v in base pairtl base pairtl; do
+for v in base prev base prev; do
   bash profiles/tower_ab.sh run $v 2>&1 | grep -v amdgpu.ids | tee -a $out/times.txt || exit 1
 done
 i=0
-for v in base pairtl base pairtl; do
+for v in base prev base prev; do
   i=$((i+1))
   if [ $v = base ]; then lib=custom-alphazero_amd/custom_alphazero/_lib/libaz.so; else lib=profiles/ab_libs/$v/libaz.so; fi
   AZ_LIB_PATH=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-cache-window > $out/b${v}_$i.json 2> $out/b${v}_$i.err || { tail -5 $out/b${v}_$i.err; exit 1; }
