@@ -372,18 +372,26 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     asm volatile("" : "+v"(yx[mb]));
     r[mb] = pix_row(yx[mb], H * W, W);
   }
-  const uint4* wm = wmain + (size_t)(nq * 2) * 2 * 64 + lane;
-  const uint4* wr = R ? wres + (size_t)(nq * 2) * 2 * 64 + lane + (size_t)36 * 1024 : wmain;
   uint4 bq[NB][4];
-  auto load_b = [&](const uint4* p, uint4(&dst)[4]) {
+  // k-step s of the phase (s < R: residual, k-steps 36.. of the conv2 pack)
+  // -> its B fragments, by buffer loads: the pack's base in an SGPR
+  // descriptor, the lane's offset in one VGPR, the k-step's in soffset, the 4
+  // fragments as immediate offsets -- no 64-bit address arithmetic (and its
+  // carry-hazard nop) per k-step
+  const auto rs_m = __builtin_amdgcn_make_buffer_rsrc((void*)wmain, (short)0, 0x7fffffff, 0x00020000);
+  const auto rs_r = __builtin_amdgcn_make_buffer_rsrc((void*)(R ? wres : wmain), (short)0, 0x7fffffff, 0x00020000);
+  const int voff = ((nq * 2) * 2 * 64 + lane) * 16;
+  auto load_bk = [&](int s, uint4(&dst)[4]) {
 #ifdef AZ_T16_DIAG_NOB  // diagnostic (wrong outputs): no weight stream in the loop
-    if (p != wr && p != wm) return;
+    if (s >= PF) return;
 #endif
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = gld(p + q * 64);
+    for (int q = 0; q < 4; ++q) {
+      const auto v = s < R ? __builtin_amdgcn_raw_buffer_load_b128(rs_r, voff + q * 1024, (36 + s) * 16384, 0)
+                           : __builtin_amdgcn_raw_buffer_load_b128(rs_m, voff + q * 1024, (s - R) * 16384, 0);
+      dst[q] = __builtin_bit_cast(uint4, v);
+    }
   };
-  // k-step s of the phase -> its B fragments (s < R: residual)
-  auto bsrc = [&](int s) { return s < R ? wr + (size_t)s * 1024 : wm + (size_t)(s - R) * 1024; };
 
   // per M block: the byte address of the tap row's term-0 slot gq; chunk c
   // and term 1 are immediate offsets (+64 c, +256)
@@ -414,6 +422,13 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   // < RING at the start of the tap's last k-step, blocks >= RING at the start
   // of the next tap's first.
   constexpr int RING = MBW > 4 ? 4 : MBW;
+  // lagged reads (RING = MBW): a block's next fragments are read after the
+  // NEXT block's MFMAs, not right after its own, so the ds_read never
+  // overwrites registers an in-flight MFMA is still reading (the WAR hazard
+  // the compiler pads with s_nop); the last block's read moves to the next
+  // k-step, after its block 0.  With the buffer-load weight stream: +1.6%
+  // games/s (profiles/r3/lag_buf_ab_bench.txt)
+  constexpr bool LAG = RING == MBW && MBW > 1;
   uint4 aq[RING][2];
   auto load_a1 = [&](int chunk, int mb) {
 #ifdef AZ_T16_DIAG_NOA  // diagnostic (wrong outputs): the activation fragments are read once per K loop
@@ -429,7 +444,8 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   // skc: blocks whose MFMAs this k-step skips (every row's tap is off its
   // board: they would add exact zeros); skn: blocks the next k-step skips (no
   // read for them; 0 across a tap change)
-  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], int chunk, int next_chunk, auto skc, auto skn) {
+  auto kstep = [&](t_f4(&C)[MBW][2], const uint4(&b)[4], int chunk, int next_chunk, auto skc, auto skn,
+                   bool first = false) {
     constexpr int SKC = decltype(skc)::value, SKN = decltype(skn)::value;
     const t_h8 B0[2] = {__builtin_bit_cast(t_h8, b[0]), __builtin_bit_cast(t_h8, b[2])};
     const t_h8 B1[2] = {__builtin_bit_cast(t_h8, b[1]), __builtin_bit_cast(t_h8, b[3])};
@@ -453,7 +469,13 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
       }
 #endif
       }
-      if (mb + RING < MBW) {
+      if (LAG) {
+        if (mb == 0) {
+          if (!first && ((SKC >> (MBW - 1)) & 1) == 0) load_a1(chunk, MBW - 1);  // this k-step's, lagged
+        } else if (next_chunk >= 0 && ((SKN >> (mb - 1)) & 1) == 0) {
+          load_a1(next_chunk, mb - 1);
+        }
+      } else if (mb + RING < MBW) {
         if (((SKC >> (mb + RING)) & 1) == 0) load_a1(chunk, mb + RING);
       } else if (next_chunk >= 0 && ((SKN >> (mb + RING - MBW)) & 1) == 0) {
         load_a1(next_chunk, mb + RING - MBW);
@@ -468,7 +490,9 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
       if (((SKC >> mb) & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x0008, 6, 0);  // MFMA
-      const bool rd = mb + RING < MBW ? ((SKC >> (mb + RING)) & 1) == 0
+      const bool rd = LAG ? (mb == 0 ? !first && ((SKC >> (MBW - 1)) & 1) == 0
+                                     : next_chunk >= 0 && ((SKN >> (mb - 1)) & 1) == 0)
+                    : mb + RING < MBW ? ((SKC >> (mb + RING)) & 1) == 0
                                       : next_chunk >= 0 && ((SKN >> (mb + RING - MBW)) & 1) == 0;
       if (rd) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS reads
     }
@@ -476,7 +500,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   };
 
 #pragma unroll
-  for (int k = 0; k < PF; ++k) load_b(bsrc(k), bq[k]);
+  for (int k = 0; k < PF; ++k) load_bk(k, bq[k]);
   if (R) set_own(0, MBW);
   else set_tap(0, 0, MBW);
 #pragma unroll
@@ -486,10 +510,11 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   for (int s = 0; s < R; ++s) {
     __builtin_amdgcn_sched_barrier(0);
     turn(s);
-    load_b(bsrc(s + PF), bq[(s + PF) % NB]);
+    load_bk(s + PF, bq[(s + PF) % NB]);
     // the next k-step is tap 0's first chunk: the ring's low blocks move now
-    if (s + 1 == R) set_tap(0, 0, RING);
-    kstep(accr, bq[s % NB], s, s + 1 == R ? 0 : s + 1, IC<0>{}, IC<0>{});
+    // (lagged: all but the last, whose read of this k-step is still to come)
+    if (s + 1 == R) set_tap(0, 0, LAG ? MBW - 1 : RING);
+    kstep(accr, bq[s % NB], s, s + 1 == R ? 0 : s + 1, IC<0>{}, IC<0>{}, s == 0);
   }
   // ---- 9 taps x 4 chunks; per tap the blocks it skips (skw: 2 bits per tap,
   // blocks 0 and 1 of the wave, from the slot plan) select one of three bodies
@@ -500,16 +525,18 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
       turn(R + 4 * t + c);
       // main k-step PF ahead (the prologue or the residual steps fetched 0 .. PF - 1)
       const int ahead = 4 * t + c + PF;
-      if (c + PF < 4 || t < 8) load_b(wm + (size_t)ahead * 1024, bq[(c + PF) % NB]);
+      if (c + PF < 4 || t < 8) load_bk(R + ahead, bq[(c + PF) % NB]);
       // the tap's high blocks (first k-step; tap 0 after the residual steps)
       if (c == 0 && RING < MBW && (t > 0 || R)) set_tap(t, RING, MBW);
+      if (LAG && c == 0 && (t > 0 || R)) set_tap(t, MBW - 1, MBW);  // its lagged read comes after block 0
+      const bool first = !R && t == 0 && c == 0;
       if (c < 3) {
-        kstep(acc, bq[c % NB], c, c + 1, skc, skc);
+        kstep(acc, bq[c % NB], c, c + 1, skc, skc, first);
       } else if (t < 8) {
-        set_tap(t + 1, 0, RING);
-        kstep(acc, bq[c % NB], c, 0, skc, IC<0>{});
+        set_tap(t + 1, 0, LAG ? MBW - 1 : RING);
+        kstep(acc, bq[c % NB], c, 0, skc, IC<0>{}, first);
       } else {
-        kstep(acc, bq[c % NB], c, -1, skc, IC<0>{});
+        kstep(acc, bq[c % NB], c, -1, skc, IC<0>{}, first);
       }
     }
   };
