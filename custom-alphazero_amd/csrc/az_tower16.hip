@@ -967,33 +967,42 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
       pp[tid] = sacc;
     };
-    auto value_part = [&](auto wv1) {
+    // NBV: the boards a pass covers, 4 when the tile holds at most 4 (C4: 3)
+    // -- the per-board sums are the same either way, the 8-board form spent
+    // 5/8 of its FMAs on boards the tile does not have
+    auto value_part_n = [&](auto wv1, auto nbv) {
+      constexpr int NBV = decltype(nbv)::value;
       const int j = tid % J, q = tid / J;  // q: wave-uniform for J >= 64
       if (q >= P) return;
-      float sv[kTowerMaxBoards];
+      float sv[NBV];
 #pragma unroll
-      for (int b = 0; b < kTowerMaxBoards; ++b) sv[b] = 0.f;
+      for (int b = 0; b < NBV; ++b) sv[b] = 0.f;
       for (int p0 = q; p0 < HW; p0 += 4 * P) {  // 4 pixels per batch, every read ahead of the FMAs
-        float w[4], v[4][kTowerMaxBoards];
+        float w[4], v[4][NBV];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int p = p0 + u * P;
           const int pc = p < HW ? p : 0;
           w[u] = p < HW ? wv1[pc * J + j] : 0.f;
-          // the pixel's 8 boards (past nbrd: stale scratch, never stored)
-          const float4 lo = *reinterpret_cast<const float4*>(vf + pc * kTowerMaxBoards);
-          const float4 hi = *reinterpret_cast<const float4*>(vf + pc * kTowerMaxBoards + 4);
-          v[u][0] = lo.x, v[u][1] = lo.y, v[u][2] = lo.z, v[u][3] = lo.w;
-          v[u][4] = hi.x, v[u][5] = hi.y, v[u][6] = hi.z, v[u][7] = hi.w;
+          // the pixel's boards (past nbrd: stale scratch, never stored)
+#pragma unroll
+          for (int h = 0; h < NBV / 4; ++h) {
+            const float4 f = *reinterpret_cast<const float4*>(vf + pc * kTowerMaxBoards + 4 * h);
+            v[u][4 * h] = f.x, v[u][4 * h + 1] = f.y, v[u][4 * h + 2] = f.z, v[u][4 * h + 3] = f.w;
+          }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int b = 0; b < kTowerMaxBoards; ++b) sv[b] = fmaf(v[u][b], w[u], sv[b]);
+          for (int b = 0; b < NBV; ++b) sv[b] = fmaf(v[u][b], w[u], sv[b]);
       }
 #pragma unroll
-      for (int b = 0; b < kTowerMaxBoards; ++b)
+      for (int b = 0; b < NBV; ++b)
         if (b < nbrd) vp[(b * P + q) * J + j] = sv[b];
+    };
+    auto value_part = [&](auto wv1) {
+      if (nbrd <= 4) value_part_n(wv1, IC<4>{});
+      else value_part_n(wv1, IC<kTowerMaxBoards>{});
     };
     for (int base = 0;; base += OP) {  // block-uniform
       if (T.wpd_lds) policy_part(base, blob + T.off_wpd);
