@@ -1101,54 +1101,59 @@ bool tower16_wv1_xtile_fits(int HW, int tr, int hidden) {
   return tr && (HW * hidden) % 4 == 0 && (size_t)tr * 48 * 4 + (size_t)HW * hidden * 4 <= (size_t)tr * kPitch;
 }
 
-// The slot plan (128-row tiles, 8 waves: M half h = blocks 4h .. 4h + 3).
+// The slot plan (128- and 96-row tiles, 8 waves: M half h = blocks
+// (tr / 32) h ..).
 // A 3x3 'same' conv tap (dy, dx) reads zeros for every pixel on the board edge
 // it points past; a block whose 16 slots all hold such pixels (or are empty)
 // would add exact zeros for that tap, so it skips the tap's MFMAs and reads.
 // Border blocks: half 0 = [top (y = 0: skips dy = -1), bottom (dy = +1), 2
 // interior], half 1 = [left (x = 0: dx = -1), right (dx = +1), 2 interior]:
 // each wave skips 6 of its 36 block-taps per conv (C4: 3 boards, 16.7% of the
-// 3x3 MFMAs), and the two waves of a SIMD (one per half) stay within one
-// block-tap of each other along the tap order, so they share the MFMA pipe
-// evenly to the end of the loop (top/left against bottom/right put half 0's
-// skips in the first taps and half 1's in the last: half 0 finished its loop
-// 8k cycles early and half 1 ran the tail alone, phase stamps).  Bank conflicts: a ds_read_b128 lane group
+// 3x3 MFMAs).  A tile with too few edge pixels for four border blocks (one
+// 9x9 board in a 96-row tile) gets top | bottom only, filled up with pads
+// (11% of the 3x3 MFMAs).  Bank conflicts: a ds_read_b128 lane group
 // reads 8 slots of one term parity ({0-3, 12-15} or {4-11}) at one tap shift;
 // its bank quads are 2 row + slot (mod 16), so the 8 slots' LDS rows must
 // differ mod 8.  Per residue r the pixels with row = r (mod 8) fill 2 slots of
 // each border block (a bipartite matching against the edge classes; corners
 // belong to two), then 2 of each interior block; an interior residue past 8
 // takes a free slot (one 2-way conflict).
-void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int skip[2]) {
-  slot_pix.clear();
-  skip[0] = skip[1] = 0;
-#if AZ_T16_NWM != 2
-  return;  // the plan assumes two M halves of four blocks
-#endif
-  const int HW = H * W, nb = tower16_boards_per_tile(HW, tr);
-  if (tr != 128 || H < 3 || W < 3 || nb < 1) return;
-  auto cls = [&](int b, int y, int x, int c) {
-    (void)b;
+namespace {
+struct PlanBorder {
+  int cls, blk;  // edge class (0 top, 1 left, 2 bottom, 3 right), tile block
+};
+
+// one layout of border blocks: false when a border pad leaves a pixel without
+// a slot or a border block would hold fewer than 8 edge pixels
+bool slot_plan_try(int H, int W, int tr, const std::vector<PlanBorder>& borders, std::vector<int>& slot_pix,
+                   int skip[2]) {
+  const int HW = H * W, nb = tower16_boards_per_tile(HW, tr), nblk = tr / 16, half = nblk / 2;
+  auto cls = [&](int y, int x, int c) {
     return c == 0 ? y == 0 : c == 1 ? x == 0 : c == 2 ? y == H - 1 : x == W - 1;
   };
-#ifdef AZ_T16_PAIR_TL  // A/B: the first plan (half 0 top + left, half 1 bottom + right)
-  const int border_block[4] = {0, 1, 4, 5}, interior_block[4] = {2, 3, 6, 7};
-#else
-  const int border_block[4] = {0, 4, 1, 5}, interior_block[4] = {2, 3, 6, 7};  // T, L, B, R
-#endif
+  const int nbor = (int)borders.size();
+  std::vector<int> interior;
+  for (int k = 0; k < nblk; ++k) {
+    bool b = false;
+    for (const PlanBorder& e : borders) b = b || e.blk == k;
+    if (!b) interior.push_back(k);
+  }
+  const int nint = (int)interior.size();
   const int S1[8] = {0, 1, 2, 3, 12, 13, 14, 15}, S2[8] = {4, 5, 6, 7, 8, 9, 10, 11};
   const int kEmpty = 127 << 8;
-  std::vector<int> slot(128, -1);  // pixel word or -1 (free)
-  auto word = [&](int b, int y, int x) { return (b << 16) | (y << 8) | x; };
+  std::vector<int> slot(tr, -1);  // pixel word, or <= -2: free (residue -2 - v)
+  auto word = [&](int n) { return ((n / HW) << 16) | (((n % HW) / W) << 8) | (n % W); };
+  std::vector<int> overflow;
   for (int r = 0; r < 8; ++r) {
     std::vector<int> P;  // natural rows with residue r
     for (int n = r; n < nb * HW; n += 8) P.push_back(n);
-    // border slots: class c, copy k (0, 1); Kuhn's matching
-    std::vector<int> owner(8, -1);
+    // border slots: border e, copy k (0, 1); Kuhn's matching of the residue's edge pixels
+    const int ns = 2 * nbor;
+    std::vector<int> owner(ns, -1);
     std::function<bool(int, std::vector<char>&)> aug = [&](int pi, std::vector<char>& seen) {
-      const int n = P[pi], b = n / HW, y = (n % HW) / W, x = n % W;
-      for (int sl = 0; sl < 8; ++sl) {
-        if (seen[sl] || !cls(b, y, x, sl / 2)) continue;
+      const int n = P[pi], y = (n % HW) / W, x = n % W;
+      for (int sl = 0; sl < ns; ++sl) {
+        if (seen[sl] || !cls(y, x, borders[sl / 2].cls)) continue;
         seen[sl] = 1;
         if (owner[sl] < 0 || aug(owner[sl], seen)) {
           owner[sl] = pi;
@@ -1158,66 +1163,86 @@ void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int ski
       return false;
     };
     for (int pi = 0; pi < (int)P.size(); ++pi) {
-      std::vector<char> seen(8, 0);
+      std::vector<char> seen(ns, 0);
       aug(pi, seen);
     }
     std::vector<char> used(P.size(), 0);
-    for (int sl = 0; sl < 8; ++sl) {
-      const int blk = border_block[sl / 2], pos = (sl & 1) ? S2[r] : S1[r];
+    for (int sl = 0; sl < ns; ++sl) {
+      const int at = borders[sl / 2].blk * 16 + ((sl & 1) ? S2[r] : S1[r]);
       if (owner[sl] >= 0) {
-        const int n = P[owner[sl]];
-        slot[blk * 16 + pos] = word(n / HW, (n % HW) / W, n % W);
+        slot[at] = word(P[owner[sl]]);
         used[owner[sl]] = 1;
       } else {
-        slot[blk * 16 + pos] = kEmpty | r;
+        slot[at] = kEmpty | r;  // a pad: reads zero rows at its residue
       }
     }
     // interior: 2 per block at this residue's positions, in order
     int k = 0;
     for (int pi = 0; pi < (int)P.size(); ++pi) {
       if (used[pi]) continue;
-      if (k >= 8) continue;  // overflow: placed below
-      const int blk = interior_block[k / 2], pos = (k & 1) ? S2[r] : S1[r];
-      const int n = P[pi];
-      slot[blk * 16 + pos] = word(n / HW, (n % HW) / W, n % W);
-      used[pi] = 1;
-      ++k;
+      if (k < 2 * nint) {
+        slot[interior[k / 2] * 16 + ((k & 1) ? S2[r] : S1[r])] = word(P[pi]);
+        ++k;
+      } else {
+        overflow.push_back(P[pi]);
+      }
     }
-    for (; k < 8; ++k) slot[interior_block[k / 2] * 16 + ((k & 1) ? S2[r] : S1[r])] = -2 - r;  // free, residue r
-    for (int pi = 0; pi < (int)P.size(); ++pi)
-      if (!used[pi]) slot.push_back(P[pi]);  // overflow natural rows, after the 128 slots
+    for (; k < 2 * nint; ++k) slot[interior[k / 2] * 16 + ((k & 1) ? S2[r] : S1[r])] = -2 - r;
   }
-  // overflow pixels into free interior slots
-  for (size_t i = 128; i < slot.size(); ++i) {
-    const int n = slot[i];
+  // overflow pixels into free interior slots (one 2-way bank conflict each)
+  for (int n : overflow) {
     bool placed = false;
-    for (int j = 0; j < 128 && !placed; ++j)
+    for (int j = 0; j < tr && !placed; ++j)
       if (slot[j] <= -2) {
-        slot[j] = word(n / HW, (n % HW) / W, n % W);
+        slot[j] = word(n);
         placed = true;
       }
-    if (!placed) return;  // cannot happen: 128 slots >= the tile's pixels
+    if (!placed) return false;  // the border pads took the slots a pixel needs
   }
-  slot.resize(128);
-  int border_pixels[4] = {0, 0, 0, 0};
-  for (int j = 0; j < 128; ++j) {
+  for (int j = 0; j < tr; ++j)
     if (slot[j] <= -2) slot[j] = kEmpty | (-2 - slot[j]);
-    for (int c = 0; c < 4; ++c)
-      if (j / 16 == border_block[c] && ((slot[j] >> 8) & 255) != 127) ++border_pixels[c];
+  for (const PlanBorder& e : borders) {
+    int px = 0;
+    for (int j = 0; j < 16; ++j) px += ((slot[e.blk * 16 + j] >> 8) & 255) != 127;
+    if (px < 8) return false;
   }
-  for (int c = 0; c < 4; ++c)
-    if (border_pixels[c] < 12) return;  // too few edge pixels for a border block: natural order
-  for (int t = 0; t < 9; ++t) {
-    const int dy = t / 3 - 1, dx = t % 3 - 1;
-#ifdef AZ_T16_PAIR_TL
-    skip[0] |= ((dy == -1 ? 1 : 0) | (dx == -1 && dy != -1 ? 2 : 0)) << (2 * t);  // 3 -> 1 (the kernel's bodies)
-    skip[1] |= ((dy == 1 ? 1 : 0) | (dx == 1 && dy != 1 ? 2 : 0)) << (2 * t);
-#else
-    skip[0] |= ((dy == -1 ? 1 : 0) | (dy == 1 ? 2 : 0)) << (2 * t);
-    skip[1] |= ((dx == -1 ? 1 : 0) | (dx == 1 ? 2 : 0)) << (2 * t);
-#endif
+  skip[0] = skip[1] = 0;
+  for (const PlanBorder& e : borders) {
+    const int h = e.blk / half, bit = e.blk % half;
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const bool past = e.cls == 0 ? dy == -1 : e.cls == 1 ? dx == -1 : e.cls == 2 ? dy == 1 : dx == 1;
+      if (past) skip[h] |= (1 << bit) << (2 * t);
+    }
   }
+  for (int h = 0; h < 2; ++h)  // the kernel's tap bodies skip one block per tap (masks 0, 1, 2)
+    for (int t = 0; t < 9; ++t)
+      if (((skip[h] >> (2 * t)) & 3) == 3) skip[h] &= ~(2 << (2 * t));
   slot_pix = slot;
+  return true;
+}
+}  // namespace
+
+void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int skip[2]) {
+  slot_pix.clear();
+  skip[0] = skip[1] = 0;
+#if AZ_T16_NWM != 2
+  return;  // the plan assumes two M halves
+#endif
+  if ((tr != 128 && tr != 96) || H < 3 || W < 3 || !tower16_boards_per_tile(H * W, tr)) return;
+  const int half = tr / 32;
+  // layouts in order: T, B | L, R; then top | bottom (e.g. one 9x9 board in a
+  // 96-row tile: too few edge pixels for four blocks)
+  const std::vector<std::vector<PlanBorder>> layouts = {
+#ifdef AZ_T16_PAIR_TL  // A/B: the first plan (half 0 top + left, half 1 bottom + right)
+      {{0, 0}, {1, 1}, {2, half}, {3, half + 1}},
+#else
+      {{0, 0}, {2, 1}, {1, half}, {3, half + 1}},
+#endif
+      {{0, 0}, {2, half}}};
+  for (const auto& borders : layouts)
+    if (slot_plan_try(H, W, tr, borders, slot_pix, skip)) return;
+  skip[0] = skip[1] = 0;
 }
 
 double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2]) {
