@@ -631,6 +631,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   const int r0 = mh * MBW * 16 + r16;
   int yx[MBW];
   const int* plan = T.slot_pix;
+  T16_STAMP(56);
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
     const int rr = r0 + 16 * mb;
@@ -724,7 +725,9 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     }
   }
+  T16_STAMP(57);
   __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
+  T16_STAMP(58);
   __syncthreads();                // ... and every wave's: the blob is readable
   T16_STAMP(1);
   {

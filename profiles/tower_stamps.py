@@ -44,6 +44,7 @@ def main():
     for i, n in order:
         print(f"  {n:10s} {med[i]:9.0f}  (+{med[i] - prev:7.0f})")
         prev = med[i]
+    print(f"  stem: before plan {med[56]:.0f}, MFMAs issued {med[57]:.0f}, DMA landed {med[58]:.0f}, barrier {med[1]:.0f}")
     print("  wave4 1x1: " + " ".join(f"{med[k]:.0f}" for k in range(48, 56)))
     print(f"  heads: pf/vf {med[44]:.0f}, policy {med[45]:.0f}, value {med[46]:.0f}, barrier {med[47]:.0f}, "
           f"end {med[19]:.0f}; last conv2 wave0 {med[16]:.0f} wave4 {med[38]:.0f}; 1x1 done wave0 {med[42]:.0f} "
