@@ -833,7 +833,7 @@ static inline int blocks_for(int n) { return (n + 255) / 256; }
 // per-game kernels are latency-bound chains (one lane = one tree): 64-lane
 // blocks spread 4096 games over 64 CUs instead of 16
 #ifndef AZ_GAME_BLOCK
-#define AZ_GAME_BLOCK 256  // 4 waves: the same games/s as 1, tower launches 3% shorter (fewer CUs held by a tree launch); 16: -3% (profiles/r3/game_block_ab_bench.txt)
+#define AZ_GAME_BLOCK 128  // 2 waves: +1% games/s over 4 and 1 (fewer CUs held by a tree launch than 1-wave blocks, less contention per CU than 4); 16: -3% (profiles/r3/game_block_ab_bench.txt, game_block128_ab_bench.txt)
 #endif
 constexpr int kGameBlock = AZ_GAME_BLOCK;
 static_assert(kGameBlock <= kGameBlockMax, "launch bounds");
