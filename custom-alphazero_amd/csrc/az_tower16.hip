@@ -9,19 +9,26 @@
 // neighbours are the zero row), so a tile needs no halo, no layer's output
 // makes an HBM round trip and a forward is one launch instead of eleven.
 // Per-layer work is the split16 scheme of az_conv16.hip: activations
-// x ~= t0 + t1 * 2^-12 and prescaled weights w' = b0 + b1 * 2^-12 as fp16
-// term pairs, three v_mfma_f32_16x16x32_f16 per k-step into one fp32
-// accumulator (t1*b0 + t0*b1 + t0*B0, B0 = 2^12 b0), so every layer is
-// fp32-accurate (network error vs float64 ~1e-7).
+// x ~= t0 + t1 (fp16 terms, t1 unscaled here) and prescaled weights
+// w' = b0 + b1 * 2^-12 as fp16 term pairs, three v_mfma_f32_16x16x32_f16 per
+// k-step into one fp32 accumulator (t1*B0 + t0*b1 + t0*B0, B0 = 2^12 b0), so
+// every layer is fp32-accurate (network error vs float64 ~1e-7).
 //
 // Workgroup = 8 waves (two per SIMD): wave w takes M half w >> 2 (MBW 16-row
 // blocks) and N quarter w & 3 (32 output channels).  The weights are the
 // MFMA's A operand, so a lane's accumulators are 4 consecutive channels of
 // one pixel: an epilogue writes its split16 terms to LDS as 8-byte stores
 // straight from the registers.  B fragments (host-packed, conv16_pack) stream
-// from L2 into registers PF k-steps ahead; activation fragments are read from
-// LDS one k-step ahead (the c16_phys rotation keeps every ds_read_b128 lane
-// group on 16 distinct bank quads for any tap shift).
+// from L2 into registers PF k-steps ahead by buffer loads; activation
+// fragments are read from LDS one k-step ahead, each block's after the next
+// block's MFMAs (34-slot rows keep every ds_read_b128 lane group on 16
+// distinct bank quads for any tap shift).
+//
+// Slot plan (tower16_slot_plan): the tile's slots are ordered so that whole
+// 16-row blocks hold pixels of one board edge; such a border block skips the
+// three taps past its edge (their MFMAs would add exact zeros).  The
+// activation image stays in natural row order; a slot's pixel word names its
+// row.
 //
 // The block's 1x1 projection residual (base_layers.py:95-125) is computed in
 // conv1's phase (4 k-steps on the block input's own rows, into a second
@@ -267,43 +274,6 @@ __device__ __forceinline__ bool store_layer(uint4* act, int HW, int W, const int
   }
   __syncthreads();
   return true;
-}
-
-// one k-step's 6*MBW MFMAs: weights as the A operand, so D = out^T; per
-// (M block, N block): t1*B0 + t0*b1 + t0*B0 (= 2^12 x w' up to the dropped
-// t1*b1), smallest first
-template <int MBW>
-__device__ __forceinline__ void mfma_kstep(t_f4 (&C)[MBW][2], const uint4 (&a)[MBW][2], const uint4 (&b)[4]) {
-  const t_h8 B0[2] = {__builtin_bit_cast(t_h8, b[0]), __builtin_bit_cast(t_h8, b[2])};
-  const t_h8 B1[2] = {__builtin_bit_cast(t_h8, b[1]), __builtin_bit_cast(t_h8, b[3])};
-#ifdef AZ_T16_CHAIN  // A/B: each accumulator's three products back to back
-#pragma unroll
-  for (int mb = 0; mb < MBW; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][1]), C[mb][nb], 0, 0, 0);
-      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
-      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
-    }
-#else
-  // term-major: 2*MBW independent accumulators between an accumulator's
-  // dependent products (the same per-element order, so the same bits)
-#pragma unroll
-  for (int mb = 0; mb < MBW; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][1]), C[mb][nb], 0, 0, 0);
-#pragma unroll
-  for (int mb = 0; mb < MBW; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
-#pragma unroll
-  for (int mb = 0; mb < MBW; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-      C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a[mb][0]), C[mb][nb], 0, 0, 0);
-#endif
 }
 
 #ifndef AZ_T16_PF
@@ -714,7 +684,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
           }
           uint4 a0, a1;
           split_u8(v, a0, a1);
-          // t1*B0 + t0*b1 + t0*B0 per N block, as mfma_kstep
+          // t1*B0 + t0*b1 + t0*B0 per N block, as the K loop's k-step
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb) {
             acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], __builtin_bit_cast(t_h8, a1), acc[mb][nb], 0, 0, 0);
