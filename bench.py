@@ -51,7 +51,6 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16/fp16 MFMA (no 2:1 sparsity)
-BOX_CPU_SHARE = 16              # CPUs one GPU's box grants a job (gpurun); workers stay inside it
 MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
 MAX_PREROLL = 800
 CACHE_TURNOVER_GENS = 2         # cache generations past the live ones before the window (hit rate stationary)
@@ -85,6 +84,9 @@ def parse():
                     help="1: reclaim the subtrees a game has left after every move (az_config.compact)")
     ap.add_argument("--no-cache-window", action="store_true",
                     help="skip the second timed window with the cache bypassed")
+    ap.add_argument("--share-devices", action="store_true",
+                    help="rehearsal: allow more ranks than visible GPUs (ranks share devices; "
+                         "the line reports shared_devices)")
     args = ap.parse_args()
     chess = args.game == "chess"
     for k, c4, ch in (("steps", 30, 3), ("warmup", 5, 2), ("slots", 4096, 256), ("sims", 100, 800)):
@@ -159,14 +161,24 @@ def cpu_baseline(args, weights):
         entries = len(shared)
     games = sum(r[0] for r in res)
     exps = sum(r[1] for r in res)
+    busy = [r[2] for r in res]
+    # each worker's games over its OWN elapsed time, summed over workers: a
+    # worker that finished its last game early does not idle in the
+    # denominator (the pool's wall time waits for the slowest straggler)
+    rate = sum(r[0] / r[2] for r in res if r[2] > 0)
+    erate = sum(r[1] / r[2] for r in res if r[2] > 0)
     return {
-        "value": round(games / wall, 4), "unit": "games/s", "cores": workers,
-        "kind": "port", "expansions_per_s": round(exps / wall, 1),
+        "value": round(rate, 4), "unit": "games/s", "cores": workers,
+        "kind": "port", "expansions_per_s": round(erate, 1),
+        "basis": "sum over workers of games_i / elapsed_i (each worker plays until the budget, then finishes "
+                 "its game); the pool wall-time rate is beside it",
+        "wall_s": round(wall, 2), "busy_s_mean": round(float(np.mean(busy)), 2),
+        "busy_s_max": round(float(np.max(busy)), 2), "value_wall": round(games / wall, 4),
         "cores_reason": why,
         "sample": (f"oracle/refport.py self-play, C4 {args.sims} sims/move, {workers} worker processes "
                    f"x 1 torch-CPU thread, batch-1 forward, one plays_inferences Manager dict shared by "
-                   f"all workers ({entries} entries at the end); {games} games in {wall:.1f}s "
-                   f"({_cpu_model()})"),
+                   f"all workers ({entries} entries at the end); {games} games, worker busy time mean "
+                   f"{np.mean(busy):.1f}s (pool wall {wall:.1f}s) ({_cpu_model()})"),
     }
 
 
@@ -204,12 +216,13 @@ def cpu_configs0(args, weights):
            30_000_000, None)
     t0 = time.perf_counter()
     with ctx.Pool(1) as pool:
-        games, exps, _ = pool.map(refport.baseline_worker, [job])[0]
+        games, exps, busy = pool.map(refport.baseline_worker, [job])[0]
     wall = time.perf_counter() - t0
     return {"config": "BASELINE.json configs[0]: Connect-4 6x7, 25 sims/move, 1 CPU worker",
-            "value": round(games / wall, 4), "unit": "games/s", "expansions_per_s": round(exps / wall, 1),
-            "cores": 1, "kind": "port",
-            "sample": f"oracle/refport.py, {games} games in {wall:.1f}s ({_cpu_model()})"}
+            "value": round(games / busy, 4), "unit": "games/s", "expansions_per_s": round(exps / busy, 1),
+            "cores": 1, "kind": "port", "basis": "games / the worker's own elapsed time",
+            "busy_s": round(busy, 2), "wall_s": round(wall, 2),
+            "sample": f"oracle/refport.py, {games} games in {busy:.1f}s ({_cpu_model()})"}
 
 
 def _device_weights(spec, host_w, rank, world, args, dev):
@@ -325,19 +338,37 @@ def chess_cpu_baseline(args, weights):
                         for i in range(workers)])
     wall = time.perf_counter() - t0
     exps = sum(r[0] for r in res)
-    return {"value": round(exps / wall, 2), "unit": "expansions/s", "cores": workers, "kind": "port",
-            "cores_reason": why,
-            "plies_per_s_est": round(sum(r[1] for r in res) / wall, 4),
+    rate = sum(r[0] / r[2] for r in res if r[2] > 0)
+    return {"value": round(rate, 2), "unit": "expansions/s", "cores": workers, "kind": "port",
+            "basis": "sum over workers of expansions_i / elapsed_i", "wall_s": round(wall, 2),
+            "value_wall": round(exps / wall, 2), "cores_reason": why,
+            "plies_per_s_est": round(sum(r[1] / r[2] for r in res if r[2] > 0), 4),
             "sample": (f"oracle chess MCTS (C tree, reference arithmetic) + torch-CPU network at batch 1 "
                        f"on Board.full_state, {workers} worker processes x 1 thread, {args.sims} sims/move, "
                        f"{exps} expansions in {wall:.1f}s; the reference's own chess path cannot run "
                        f"under MCTS (chess/board.py:178 vs mcts.py:179)")}
 
 
+def check_devices(args, world):
+    """One rank per GPU: refuse (before any GPU call) a world larger than the
+    visible devices, which would stack ranks on one GPU and still print
+    n_gpus = world -- unless --share-devices asks for that rehearsal (then
+    the line says so).  torch.cuda.device_count() does not initialise the
+    GPU on this image."""
+    import torch
+    n = torch.cuda.device_count()
+    if world > n and not args.share_devices:
+        print(f"bench.py: {world} ranks but {n} visible GPU(s); refusing to stack ranks on one device "
+              f"(--share-devices for a rehearsal)", file=sys.stderr)
+        sys.exit(2)
+    return n
+
+
 def _init_dist(args, world, local_rank):
     import torch
     import torch.distributed as dist
-    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    n = check_devices(args, world)
+    dev_index = local_rank % max(n, 1)
     if world > 1:
         torch.cuda.set_device(dev_index)
         dist.init_process_group(args.dist_backend)
@@ -730,6 +761,7 @@ def main():
             "unit": "games/s",
             "n_gpus": world,
             "rank_devices": devices,
+            "shared_devices": len(set(devices)) < len(devices),
             "dist_backend": args.dist_backend if world > 1 else None,
             "steps": args.steps,
             "warmup": args.warmup,

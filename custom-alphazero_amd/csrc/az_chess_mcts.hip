@@ -841,7 +841,8 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
     return az::fail_abi(AZ_E_INVALID, "network evaluator supports filters == 128 (ConfigModel.filters)");
   if (c.conv_algo != AZ_CONV_F16X2 && c.conv_algo != AZ_CONV_DIRECT)
     return az::fail_abi(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2 or AZ_CONV_DIRECT");
-  if (c.max_plies < 0 || c.arena_edges < 0) return az::fail_abi(AZ_E_INVALID, "negative bound");
+  if (c.max_plies < 0 || c.arena_edges < 0 || c.depth < 0 || c.value_hidden < 1)
+    return az::fail_abi(AZ_E_INVALID, "negative bound");
   if ((int64_t)c.slots * 64 * 512 >= (1ll << 31))
     return az::fail_abi(AZ_E_INVALID, "slots * 64 * 512 must stay below 2^31 (32-bit activation byte offsets)");
   int dev_count = 0;
@@ -918,7 +919,9 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
   }
   t.mt_stride = g.slots;
   e->net.depth = c.depth;
-  e->net.algo = c.conv_algo;
+  // depth 0: the fp16x2 chain runs the heads' 1x1 convs inside the last
+  // block's conv2, so a tower without blocks takes the fp32 MFMA path
+  e->net.algo = c.depth == 0 ? AZ_CONV_DIRECT : c.conv_algo;
   e->net.hidden = c.value_hidden;
   e->net.err = t.stats + az::kStatErrors;
   if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));

@@ -114,6 +114,10 @@ struct az_engine {
   unsigned long long* snap_dev = nullptr;   // snap_host's device address
   int64_t batch_first_move = 0;             // moves_issued at az_selfplay_begin
   size_t drain_cap = 0;            // records the two buffers hold
+  // a host evaluator failed mid-simulation (AZ_E_CALLBACK): the leaves it
+  // selected were never expanded, so the trees are one simulation short;
+  // searching refuses until az_selfplay_begin or az_tree_reset starts over
+  bool broken = false;
 
   template <typename T>
   int alloc(T** p, size_t count) {
@@ -219,7 +223,10 @@ int simulate(az_engine* e, Lane& L) {
     az::launch_forward(e->net, L.x, n_rows, L.n, L.g.H, L.g.W, L.g.A, L.act[0], L.act[1], L.act[2],
                        L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr, rows);
   } else if (e->cfg.evaluator == AZ_EVAL_HOST) {
-    if (int rc = host_evaluate(e, L, rows, n_rows)) return rc;
+    if (int rc = host_evaluate(e, L, rows, n_rows)) {
+      e->broken = true;
+      return rc;
+    }
   } else {
     az::launch_synth_eval(L.g, rows, n_rows, L.probs, L.values, s);
   }
@@ -266,6 +273,9 @@ int cache_clear(az_engine* e) {
 }
 
 int ready_to_search(az_engine* e) {
+  if (e->broken)
+    return fail(AZ_E_STATE, "a host evaluator error interrupted a simulation: the trees are incomplete "
+                            "until az_selfplay_begin or az_tree_reset");
   if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
     return fail(AZ_E_STATE, "network evaluator selected but az_engine_set_weights was not called");
   if (e->cfg.evaluator == AZ_EVAL_HOST && !e->host_fn)
@@ -549,7 +559,6 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     }
   }
   if (tower) {
-    if (net.depth > kTowerMaxDepth || net.hidden > 256) return fail(AZ_E_INVALID, "tower: depth/hidden too large");
     TowerNet tn{};
     for (int d = 0; d < net.depth; ++d) {
       tn.k1[d] = reinterpret_cast<const uint4*>(net.k1[d]);
@@ -579,27 +588,18 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     tn.off_wpd = put(tb_pdw);
     tn.off_wv1 = put(tb_v1w);
     tn.blob_floats = (int)blob.size();
-    // the layout: 128/96-row tiles double-buffered, then in place (256-row
-    // tiles in place with AZ_TOWER_TILE=256, A/B: half the weight stream per
-    // FLOP, but 128 x 32 wave tiles spill at two waves per SIMD); per layout
-    // the largest staging that fits: the whole blob, then without wv1, then
-    // without wpd too (those then read from L2).  AZ_TOWER_INPLACE=1 forces
-    // the in-place tile (A/B)
-    const char* inplace = getenv("AZ_TOWER_INPLACE");
-    const char* tile = getenv("AZ_TOWER_TILE");
-    const bool allow_db = !(inplace && inplace[0] == '1');
-    const bool allow_big = tile && atoi(tile) == 256;
+    // the layout: 128/96-row tiles double-buffered, else one tile in place;
+    // per layout the largest staging that fits: the whole blob, then without
+    // wv1, then without wpd too (those then read from L2)
     const int prefix[3] = {tn.blob_floats, tn.off_wv1, tn.off_wpd};
     struct Layout {
       int tr;
       bool db;
-    } layouts[3] = {{allow_big ? tower16_tile_rows(HW, true) : 0, false},
-                    {allow_db ? tower16_tile_rows(HW) : 0, true},
-                    {tower16_tile_rows(HW), false}};
+    } layouts[2] = {{tower16_tile_rows(HW), true}, {tower16_tile_rows(HW), false}};
     bool found = false;
-    for (int li = 0; li < 3 && !found; ++li) {
+    for (int li = 0; li < 2 && !found; ++li) {
       const Layout L = layouts[li];
-      if (!L.tr || (li == 0 && L.tr != 256) || !tower16_heads_fit(HW, L.tr, A, net.hidden, L.db)) continue;
+      if (!L.tr || !tower16_heads_fit(HW, L.tr, A, net.hidden, L.db)) continue;
       for (int i = 0; i < 3 && !found; ++i)
         if (tower16_lds_bytes(HW, L.tr, prefix[i], L.db) <= kTowerLdsMax) {
           tn.tile_rows = L.tr;
@@ -610,14 +610,19 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
           found = true;
         }
     }
-    if (!found) return fail(AZ_E_INVALID, "tower: the board's activations and head weights do not fit LDS (use AZ_CONV_F16X2_LAYERS)");
+    if (!found) {  // the per-layer kernels instead (same arithmetic)
+      net.use_tower = false;
+      if (net.board_w > 16) net.algo = AZ_CONV_DIRECT;
+      net.ready = true;
+      return 0;
+    }
     tn.wv1_xtile = tn.dbuf && !tn.wv1_lds && tower16_wv1_xtile_fits(HW, tn.tile_rows, net.hidden);
-    // the slot plan: border blocks skip the taps past their edge (AZ_TOWER_PLAN=0: natural order, A/B)
+    // the slot plan: border blocks skip the taps past their edge
+    // (az_config.tower_natural_order: natural order, no skips -- bitwise the same outputs)
     {
-      const char* plan = getenv("AZ_TOWER_PLAN");
       std::vector<int> pix;
       int skip[2] = {0, 0};
-      if (!(plan && plan[0] == '0') && net.board_h * net.board_w == HW)
+      if (!net.tower_natural_order && net.board_h * net.board_w == HW)
         tower16_slot_plan(net.board_h, net.board_w, tn.tile_rows, pix, skip);
       tn.slot_pix = nullptr;
       tn.skip[0] = skip[0];
@@ -657,6 +662,14 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
 extern "C" {
 
 int az_abi_version(void) { return AZ_ABI_VERSION; }
+#ifndef AZ_SRC_HASH
+#define AZ_SRC_HASH "unknown"
+#endif
+#ifndef AZ_BUILD_EXTRA
+#define AZ_BUILD_EXTRA "unknown"
+#endif
+const char* az_build_id(void) { return AZ_SRC_HASH; }
+const char* az_build_flags(void) { return AZ_BUILD_EXTRA; }
 const char* az_last_error(void) { return g_last_error.c_str(); }
 
 int az_engine_create(int device, const az_config* cfg, az_engine** out) {
@@ -673,10 +686,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
     return fail(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2, AZ_CONV_DIRECT or AZ_CONV_F16X2_LAYERS");
   if (c.evaluator == AZ_EVAL_NETWORK && c.conv_algo == AZ_CONV_F16X2_LAYERS && c.board_width > 16)
     return fail(AZ_E_INVALID, "AZ_CONV_F16X2_LAYERS supports boards up to 16 columns");
-  if (c.evaluator == AZ_EVAL_NETWORK && c.conv_algo == AZ_CONV_F16X2 &&
-      (c.depth > az::kTowerMaxDepth || c.value_hidden > 256))
-    return fail(AZ_E_INVALID, "AZ_CONV_F16X2 supports depth <= 16 and value_hidden <= 256 "
-                              "(use AZ_CONV_F16X2_LAYERS or AZ_CONV_DIRECT)");
+  if (c.depth < 0 || c.depth > 1024 || c.value_hidden < 1) return fail(AZ_E_INVALID, "need 0 <= depth and value_hidden >= 1");
   if (c.evaluator == AZ_EVAL_NETWORK && (int64_t)c.slots * c.board_height * c.board_width * 512 >= (1ll << 31))
     return fail(AZ_E_INVALID, "slots * H * W * 512 must stay below 2^31 (32-bit activation byte offsets)");
   if (c.evaluator != AZ_EVAL_NETWORK && c.evaluator != AZ_EVAL_SYNTHETIC && c.evaluator != AZ_EVAL_HOST)
@@ -825,7 +835,16 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   e->net.board_h = g.H;
   e->net.board_w = g.W;
   e->net.algo = c.conv_algo == AZ_CONV_F16X2_LAYERS ? AZ_CONV_F16X2 : c.conv_algo;
-  e->net.use_tower = c.conv_algo == AZ_CONV_F16X2;
+  // AZ_CONV_F16X2: the one-launch tower when the network fits it (1 <= depth
+  // <= 16, value_hidden <= 256, the head weights in LDS: load_network),
+  // otherwise quietly the same arithmetic per layer -- or, where the per-layer
+  // kernels do not apply (depth 0: the heads are fused into the last conv2;
+  // boards wider than 16), the fp32 MFMA path; every form within NET_TOL
+  e->net.use_tower = c.conv_algo == AZ_CONV_F16X2 && c.depth >= 1 && c.depth <= az::kTowerMaxDepth &&
+                     c.value_hidden <= 256;
+  e->net.tower_natural_order = c.tower_natural_order != 0;
+  if (c.depth == 0 || (c.conv_algo != AZ_CONV_DIRECT && !e->net.use_tower && c.board_width > 16))
+    e->net.algo = AZ_CONV_DIRECT;
   e->net.err = e->t.stats + az::kStatErrors;
   // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
   int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);
@@ -1093,6 +1112,7 @@ int az_pow_table(az_engine* e, double* out, int64_t n) {
 int az_selfplay_begin(az_engine* e, int64_t first_game, int64_t n_games, uint32_t base_seed) {
   if (!e || n_games < 0 || first_game < 0) return fail(AZ_E_INVALID, "bad arguments");
   int rc;
+  e->broken = false;  // every slot starts a fresh game
   if ((rc = ready_to_search(e))) return rc;
   AZ_HIP(hipSetDevice(e->device));
   if ((rc = sync_all(e))) return rc;  // moves of an earlier batch may still be running (async steps)
@@ -1283,6 +1303,7 @@ int az_tree_reset(az_engine* e, int n, const int32_t* slots, const int8_t* board
   az::launch_slot_set_root(e->g, e->t, e->dev_i32, e->dev_boards, n, e->stream);
   AZ_HIP(hipGetLastError());
   AZ_HIP(hipStreamSynchronize(e->stream));
+  e->broken = false;
   return 0;
 }
 
@@ -1313,6 +1334,7 @@ int az_tree_search(az_engine* e, int n_sims) {
 int az_tree_play(az_engine* e, const double* uniforms, int greedy, int deterministic,
                  int32_t* moves, int32_t* status, double* policy) {
   if (!e || (!deterministic && !uniforms)) return fail(AZ_E_INVALID, "bad arguments");
+  if (e->broken) return ready_to_search(e);
   if (int rc_ = enter(e)) return rc_;
   if (int rc_ = tree_api_ok(e)) return rc_;
   const size_t S = (size_t)e->g.slots;

@@ -50,7 +50,7 @@ double tower16_issued_flop_per_board(int HW, int tile_rows, int depth, const int
 // 0 when the board does not fit a tile (HW > 128); else 96 or 128 (big:
 // 256-row tiles, 16 M blocks, each wave 128 rows x 32 channels -- half the
 // weight stream per FLOP; single tile in place, the LDS holds no second)
-int tower16_tile_rows(int HW, bool big = false);
+int tower16_tile_rows(int HW);
 int tower16_boards_per_tile(int HW, int tile_rows);
 // LDS of one workgroup: activation rows (one or two tiles + zero rows) +
 // bookkeeping + staged blob floats
@@ -76,6 +76,7 @@ struct NetDev {
   int filters = 128, depth = 0, hidden = 256;
   int algo = 0;             // AZ_CONV_F16X2 / AZ_CONV_DIRECT (one algorithm for every forward)
   bool use_tower = false;   // Connect-N, AZ_CONV_F16X2: the whole forward in tower16_kernel (else per layer)
+  bool tower_natural_order = false;  // az_config.tower_natural_order: no slot plan (A/B, bitwise the same)
   TowerNet* tower = nullptr;  // device copy of the tower's view (load_network)
   int tower_staged = 0;       // its blob floats staged in LDS
   bool tower_dbuf = false;    // its activations double-buffered (TowerNet::dbuf)

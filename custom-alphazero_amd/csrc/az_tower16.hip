@@ -55,10 +55,6 @@
 #include "az_nn.h"
 #include "az_tree.h"
 
-#ifndef AZ_T16_NWM
-#define AZ_T16_NWM 2  // wave groups over M: 2 = two waves per SIMD (default), 1 = one (-10% isolated, round 3)
-#endif
-
 namespace az {
 
 typedef _Float16 t_h8 __attribute__((ext_vector_type(8)));
@@ -200,7 +196,6 @@ struct TowerSmem {
   int flag[2];              // overflow seen in the layer being stored (alternating by layer)
   int sc[2][kTowerMaxBoards];  // per-board scale exponent of the two activation buffers' contents
   unsigned bmax[kTowerMaxBoards];  // board maxima (float bits, values >= 0) on the rare rescale path
-  int prog[8];                     // each wave's k-step in the running K loop (AZ_T16_BALANCE)
 };
 
 // store 4 channels (channel quad cq) of activation row r as split16 terms
@@ -276,10 +271,6 @@ __device__ __forceinline__ bool store_layer(uint4* act, int HW, int W, const int
   return true;
 }
 
-#ifndef AZ_T16_PF
-#define AZ_T16_PF 1  // k-steps of B fragments in flight ahead of their MFMAs (1 and 2 measured equal; 1 needs no spill)
-#endif
-
 // One conv phase's K loop: R residual k-steps (the block input's own rows x
 // the 1x1 projection weights, k-steps 36.. of the conv2 pack, into accr),
 // then 9 taps x 4 channel chunks of 32 (into acc).  The taps are a runtime
@@ -293,44 +284,18 @@ template <int MBW, int R>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
                                        t_f4 (&accr)[MBW][2], const int (&yx_)[MBW], int H, int W,
-                                       int zrow, int nq, int lane, int mh, int* prog, int wave, int skw) {
+                                       int zrow, int nq, int lane, int mh, int skw) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
-#if defined(AZ_T16_BALANCE)
-  // the wave of a SIMD pair that is behind takes priority 1: each wave posts
-  // its k-step to LDS and reads its partner's (used one k-step later); on a
-  // tie the younger wave (mh = 1) goes first, since age already favours the
-  // older one
-  int pk = 0;
-  const int partner = wave ^ 4;
-  auto turn = [&](int k) {
-    const int seen = __builtin_amdgcn_readfirstlane(pk);
-    if (seen > k || (seen == k && mh)) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-    if (lane == 0) prog[wave] = k;
-    pk = prog[partner];
-  };
-#elif !defined(AZ_T16_NOALTPRIO)
   // the two waves of a SIMD (M halves mh = 0, 1) take turns at priority 1,
   // one k-step each, so neither falls a whole phase behind the other (without:
   // the older wave finished its K loop ~7k cycles first and its partner ran
   // the tail alone; with: ~2k, -1 to -2% kernel time)
-#ifndef AZ_T16_ALTSHIFT
-#define AZ_T16_ALTSHIFT 0  // the turns last 2^ALTSHIFT k-steps
-#endif
   auto turn = [&](int k) {
-    if (((k >> AZ_T16_ALTSHIFT) ^ mh) & 1) __builtin_amdgcn_s_setprio(1);
+    if ((k ^ mh) & 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
   };
-#else
-  auto turn = [&](int) {};
-  (void)mh;
-#endif
-#if !defined(AZ_T16_BALANCE)
-  (void)prog;
-  (void)wave;
-#endif
-  constexpr int PF = AZ_T16_PF, NB = PF == 1 ? 2 : 4;
-  static_assert(PF >= 1 && PF <= 3, "prefetch depth");
+  // B fragments one k-step ahead of their MFMAs (2 measured equal, 1 needs no spill)
+  constexpr int PF = 1, NB = 2;
   const int gq = lane >> 4;
   // the tap geometry laundered through an empty asm per call: the k-loops sit
   // in the runtime depth loop, and without this the compiler hoists every
@@ -352,9 +317,6 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   const auto rs_r = __builtin_amdgcn_make_buffer_rsrc((void*)(R ? wres : wmain), (short)0, 0x7fffffff, 0x00020000);
   const int voff = ((nq * 2) * 2 * 64 + lane) * 16;
   auto load_bk = [&](int s, uint4(&dst)[4]) {
-#ifdef AZ_T16_DIAG_NOB  // diagnostic (wrong outputs): no weight stream in the loop
-    if (s >= PF) return;
-#endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const auto v = s < R ? __builtin_amdgcn_raw_buffer_load_b128(rs_r, voff + q * 1024, (36 + s) * 16384, 0)
@@ -401,9 +363,6 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   constexpr bool LAG = RING == MBW && MBW > 1;
   uint4 aq[RING][2];
   auto load_a1 = [&](int chunk, int mb) {
-#ifdef AZ_T16_DIAG_NOA  // diagnostic (wrong outputs): the activation fragments are read once per K loop
-    if (chunk > 0) return;
-#endif
     const char* q = actb + aaddr[mb] + 64 * chunk;
     aq[mb % RING][0] = *reinterpret_cast<const uint4*>(q);
     aq[mb % RING][1] = *reinterpret_cast<const uint4*>(q + 256);
@@ -423,21 +382,12 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     for (int mb = 0; mb < MBW; ++mb) {
       const t_h8 a0 = __builtin_bit_cast(t_h8, aq[mb % RING][0]), a1 = __builtin_bit_cast(t_h8, aq[mb % RING][1]);
       if (((SKC >> mb) & 1) == 0) {
-#ifdef AZ_T16_ILV
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a1, C[mb][nb], 0, 0, 0);
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], a0, C[mb][nb], 0, 0, 0);
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a0, C[mb][nb], 0, 0, 0);
-#else
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a1, C[mb][nb], 0, 0, 0);
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1[nb], a0, C[mb][nb], 0, 0, 0);
         C[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0[nb], a0, C[mb][nb], 0, 0, 0);
       }
-#endif
       }
       if (LAG) {
         if (mb == 0) {
@@ -451,7 +401,6 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
         load_a1(next_chunk, mb + RING - MBW);
       }
     }
-#ifndef AZ_T16_FREESCHED
     // the order above, kept: the weight loads of the k-step PF ahead first,
     // then per M block its six MFMAs and its two ring reads
     // (left alone, the scheduler bunched the reads and waited for all of
@@ -466,7 +415,6 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
                                       : next_chunk >= 0 && ((SKN >> (mb + RING - MBW)) & 1) == 0;
       if (rd) __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);  // DS reads
     }
-#endif
   };
 
 #pragma unroll
@@ -521,9 +469,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     else if (m == 1) tap(t, IC<1>{});
     else tap(t, IC<2>{});
   }
-#ifndef AZ_T16_NOALTPRIO
   __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // LDS-DMA of n_u4 16-byte words from global src into LDS dst (both
@@ -563,7 +509,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // the other tile, so a wave that finishes its K loop stores its outputs
   // while its SIMD partner still computes, and one barrier per layer
   // publishes them), else one tile updated in place behind a second barrier
-  const bool dbuf = TR <= 128 && T.dbuf;  // 256-row tiles: in place (one tile fills the LDS)
+  const bool dbuf = T.dbuf;
   uint4* const bufX = act;
   uint4* const bufH = dbuf ? act + (TR + kZeroRows) * (kPitch / 16) : act;
   const int zX = TR, zH = dbuf ? -kZeroRows : TR;  // each tile's zero rows, relative to it
@@ -581,20 +527,12 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   const int zrow = TR;
   T16_RSTAMP(22);
   T16_STAMP(0);
-#ifdef AZ_T16_PRIO  // A/B: the second-dispatched half of the waves at priority 1 (MI355X_MICROARCH.md 2-waves item 4)
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
   // small weights into LDS, in the background of the stem
   dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob, T.staged_floats / 4, wave, lane);
   for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 2) sm.flag[tid] = 0;  // published by the barrier after the stem's MFMAs
-  if (tid < 8) sm.prog[tid] = 0;
 
-#ifdef AZ_T16_SWAPMH  // diagnostic: the older waves take the second M half
-  const int mh = (wave >> 2) ^ 1, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
-#else
   const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
-#endif
   // a lane's slots r0 + 16 mb and their pixel words: the slot plan's
   // (T.slot_pix, a full tile's boards; the boards past this tile's are
   // emptied, keeping their rows' bank residues) or the natural order
@@ -735,7 +673,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     // conv1 (+ the projection residual into accr), input X
     T16_WSTAMP(d, 0);
-    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, yx, H, W, zX, nq, lane, mh, sm.prog, wave, skw);
+    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, yx, H, W, zX, nq, lane, mh, skw);
     T16_WSTAMP(d, 1);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
@@ -779,7 +717,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
     // conv2 on H, on top of the residual
     T16_WSTAMP(d, 2);
-    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, mh, sm.prog, wave, skw);
+    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, mh, skw);
     T16_WSTAMP(d, 3);
     if (d < 4) T16_STAMP(4 + 4 * d);
     if (d < 4) T16_STAMP4(26 + 4 * d);
@@ -852,10 +790,6 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) {
       T16_STAMP4(49 + mb);
-#ifdef AZ_T16_DIAG_NOH1  // diagnostic (wrong outputs): no 1x1 head convs
-      if (pix_ok(hyx[mb])) red[(hr[mb] * 16 + nq * 4 + gq) * 3] = accr[mb][0][0];
-      continue;
-#endif
       const float o = anyH ? ldexpf(osc, sm.sc[1][hb[mb]]) : osc;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
@@ -1040,11 +974,8 @@ extern "C" int az_t16_wstamps(unsigned long long* out) {  // [4096][8][5]
 namespace az {
 #endif
 
-int tower16_tile_rows(int HW, bool big) {
+int tower16_tile_rows(int HW) {
   if (HW > 128) return 0;
-  // 256-row tiles when they hold at least two boards and no more than the
-  // tile's board limit
-  if (big && HW >= 256 / kTowerMaxBoards + 1) return 256;
   // 128-row tiles unless 96 rows hold the same boards (more rows per tile, same work per board)
   const int b128 = std::min(128 / HW, kTowerMaxBoards), b96 = std::min(96 / HW, kTowerMaxBoards);
   if (b96 >= 1 && b96 * HW * 128 >= b128 * HW * 96) return 96;  // 96-row tiles are at least as full
@@ -1199,19 +1130,12 @@ bool slot_plan_try(int H, int W, int tr, const std::vector<PlanBorder>& borders,
 void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int skip[2]) {
   slot_pix.clear();
   skip[0] = skip[1] = 0;
-#if AZ_T16_NWM != 2
-  return;  // the plan assumes two M halves
-#endif
   if ((tr != 128 && tr != 96) || H < 3 || W < 3 || !tower16_boards_per_tile(H * W, tr)) return;
   const int half = tr / 32;
   // layouts in order: T, B | L, R; then top | bottom (e.g. one 9x9 board in a
   // 96-row tile: too few edge pixels for four blocks)
   const std::vector<std::vector<PlanBorder>> layouts = {
-#ifdef AZ_T16_PAIR_TL  // A/B: the first plan (half 0 top + left, half 1 bottom + right)
-      {{0, 0}, {1, 1}, {2, half}, {3, half + 1}},
-#else
       {{0, 0}, {2, 1}, {1, half}, {3, half + 1}},
-#endif
       {{0, 0}, {2, half}}};
   for (const auto& borders : layouts)
     if (slot_plan_try(H, W, tr, borders, slot_pix, skip)) return;
@@ -1221,7 +1145,7 @@ void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int ski
 double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2]) {
   const int bpw = tower16_boards_per_tile(HW, tr);
   if (!bpw) return 0;
-  const int nwm = tr == 256 ? 2 : AZ_T16_NWM, mbw = tr / 16 / nwm;  // blocks per wave
+  const int nwm = 2, mbw = tr / 16 / nwm;  // blocks per wave
   const double mfma = 16.0 * 16 * 32 * 2;                          // FLOP per v_mfma_f32_16x16x32_f16
   double steps = 0;  // block-k-steps over the tile's waves (4 N quarters per M group)
   for (int h = 0; h < nwm; ++h) {
@@ -1274,11 +1198,9 @@ void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, c
                     unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
   if (tile_rows == 96)
-    launch_mbw<6, AZ_T16_NWM>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
-  else if (tile_rows == 256)
-    launch_mbw<16, 2>(net, staged, false, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<6, 2>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
   else
-    launch_mbw<8, AZ_T16_NWM>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<8, 2>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
 }
 
 }  // namespace az

@@ -20,9 +20,12 @@
 
 namespace az {
 
-// threads per block of the per-game kernels (select / expand / play): the
-// launch bound admits up to 4 waves so a launch can be packed onto fewer CUs
-constexpr int kGameBlockMax = 1024;
+// threads per block of the per-game kernels (select / expand / play): 2
+// waves, +1% games/s over 4 and 1 (a tree launch holds fewer of the CUs the
+// other lane's tower needs than 1-wave blocks, less contention per CU than
+// 4); 16 lanes: -3% (profiles/r3/game_block_ab_bench.txt,
+// game_block128_ab_bench.txt).  The launch bound is the block size itself.
+constexpr int kGameBlock = 128;
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ void stat_add(const TreeDev& t, int which, unsigned long long v) {
@@ -283,7 +286,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
 }
 
 // Serial descent, one lane per game (used when the action space exceeds 64).
-__global__ __launch_bounds__(kGameBlockMax) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
+__global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(kGameBlockMax) void select_kernel(GameCfg g, TreeDe
 // sums N and takes the first-maximum UCB by shuffles -- the same float64
 // expressions as the serial loop, so the chosen edge is identical.
 template <int L>
-__global__ __launch_bounds__(kGameBlockMax) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
+__global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = gid / L, j = gid % L;
@@ -526,7 +529,7 @@ __global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, const Board*
 // insert never reuses (kCacheLiveGens < kCacheReuseAge, az_tree.h), so the
 // two halves are independent and share one launch instead of two.
 template <int MAXA, bool INSERT>
-__global__ __launch_bounds__(kGameBlockMax) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
+__global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
                                                      const float* __restrict__ probs,
                                                      const float* __restrict__ values, int exp_blocks) {
   if (INSERT && (int)blockIdx.x >= exp_blocks) {  // block-uniform
@@ -597,7 +600,7 @@ __global__ __launch_bounds__(kGameBlockMax) void expand_kernel(GameCfg g, TreeDe
 // (self_play.py:59-67): greedy one-hot from fullmove_number >= index_move_greedy,
 // else normalised visit counts; one uniform per move even when greedy.
 template <int MAXA>
-__global__ __launch_bounds__(kGameBlockMax) void play_kernel(GameCfg g, TreeDev t, SampleDev smp,
+__global__ __launch_bounds__(kGameBlock) void play_kernel(GameCfg g, TreeDev t, SampleDev smp,
                                                    const double* __restrict__ uniforms,
                                                    int greedy_mode, int deterministic, int refill) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -830,13 +833,6 @@ void launch_drain_pack(const GameCfg& g, const SampleDev& smp, int64_t from, int
 
 // ---------------------------------------------------------------- launchers
 static inline int blocks_for(int n) { return (n + 255) / 256; }
-// per-game kernels are latency-bound chains (one lane = one tree): 64-lane
-// blocks spread 4096 games over 64 CUs instead of 16
-#ifndef AZ_GAME_BLOCK
-#define AZ_GAME_BLOCK 128  // 2 waves: +1% games/s over 4 and 1 (fewer CUs held by a tree launch than 1-wave blocks, less contention per CU than 4); 16: -3% (profiles/r3/game_block_ab_bench.txt, game_block128_ab_bench.txt)
-#endif
-constexpr int kGameBlock = AZ_GAME_BLOCK;
-static_assert(kGameBlock <= kGameBlockMax, "launch bounds");
 static inline int game_blocks(int n) { return (n + kGameBlock - 1) / kGameBlock; }
 
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s) {

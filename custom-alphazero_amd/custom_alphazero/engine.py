@@ -33,7 +33,10 @@ class Config(ctypes.Structure):
         ("value_hidden", ctypes.c_int32), ("bn_epsilon", ctypes.c_double),
         ("arena_edges", ctypes.c_int64), ("max_tree_visits", ctypes.c_int64),
         ("cache_log2", ctypes.c_int32), ("conv_algo", ctypes.c_int32),
-        ("lanes", ctypes.c_int32), ("compact", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4),
+        ("lanes", ctypes.c_int32), ("compact", ctypes.c_int32),
+        ("tower_natural_order", ctypes.c_int32), ("dirichlet_noise", ctypes.c_int32),
+        ("dirichlet_alpha", ctypes.c_double), ("dirichlet_ratio", ctypes.c_double),
+        ("reserved", ctypes.c_int32 * 2),
     ]
 
 
@@ -88,7 +91,7 @@ def _as_numpy(t):
 
 
 EXPORTED = (
-    "az_abi_version", "az_last_error", "az_engine_create", "az_engine_destroy",
+    "az_abi_version", "az_last_error", "az_build_id", "az_build_flags", "az_engine_create", "az_engine_destroy",
     "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
     "az_selfplay_run", "az_selfplay_results", "az_selfplay_drain", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
@@ -126,6 +129,8 @@ def load_library():
     sig = {
         "az_abi_version": (ctypes.c_int, []),
         "az_last_error": (ctypes.c_char_p, []),
+        "az_build_id": (ctypes.c_char_p, []),
+        "az_build_flags": (ctypes.c_char_p, []),
         "az_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(Config), ctypes.POINTER(P)]),
         "az_engine_destroy": (ctypes.c_int, [P]),
         "az_engine_set_weights": (ctypes.c_int, [P, ctypes.POINTER(Tensor), ctypes.c_int]),
@@ -180,6 +185,13 @@ def load_library():
     return L
 
 
+def build_id():
+    """(source hash, extra compile flags) of the loaded libaz (az_build_id /
+    az_build_flags): profiles record the hash, bench.py matches it."""
+    L = load_library()
+    return L.az_build_id().decode(), L.az_build_flags().decode()
+
+
 def _check(rc):
     if rc != 0:
         msg = load_library().az_last_error().decode("utf-8", "replace")
@@ -222,10 +234,13 @@ class Engine:
                  evaluator=EVAL_NETWORK, index_move_greedy=8, exploration_constant=1.5,
                  filters=128, depth=4, value_hidden=256, bn_epsilon=1e-3, arena_edges=0,
                  max_tree_visits=0, device=0, cache_log2=0, conv_algo=CONV_F16X2,
-                 lanes=0, compact=False):
+                 lanes=0, compact=False, tower_natural_order=False, dirichlet_noise=False,
+                 dirichlet_alpha=0.03, dirichlet_ratio=0.25):
         """compact=True reclaims the subtrees a self-play game has left after
         every move (az_config.compact; arena_edges is then per half); keep it
-        off for the tree API (az_tree_*), whose views need the whole tree."""
+        off for the tree API (az_tree_*), whose views need the whole tree.
+        dirichlet_noise: ConfigMCTS.enable_dirichlet_noise (root noise,
+        reference mcts.py:70-85) with dirichlet_alpha / dirichlet_ratio."""
         L = load_library()
         self.height, self.width, self.n, self.gravity = height, width, n, bool(gravity)
         self.action_space = width if gravity else width * height
@@ -237,7 +252,10 @@ class Engine:
                      filters=filters, depth=depth, value_hidden=value_hidden,
                      bn_epsilon=bn_epsilon, arena_edges=arena_edges,
                      max_tree_visits=max_tree_visits, cache_log2=cache_log2, conv_algo=conv_algo,
-                     lanes=lanes, compact=int(bool(compact)))
+                     lanes=lanes, compact=int(bool(compact)),
+                     tower_natural_order=int(bool(tower_natural_order)),
+                     dirichlet_noise=int(bool(dirichlet_noise)), dirichlet_alpha=float(dirichlet_alpha),
+                     dirichlet_ratio=float(dirichlet_ratio))
         handle = ctypes.c_void_p()
         _check(L.az_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
         self._h = handle

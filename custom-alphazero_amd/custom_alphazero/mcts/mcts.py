@@ -81,9 +81,6 @@ class UCTNode:
         return self.edges[int(np.argmax([e.upper_confidence_bound() for e in self.edges]))]
 
 
-_ENGINE_CACHE = {}
-
-
 def _engine_for(model, all_possible_moves) -> az.Engine:
     c = ConfigConnectN
     if isinstance(model, SyntheticEvaluator):
@@ -222,15 +219,12 @@ def _chess_engine_for(model):
         evaluator = az.EVAL_SYNTHETIC
     elif model is not None and hasattr(model, "engine_weights"):
         evaluator = az.EVAL_NETWORK
-    elif callable(model):
-        # any other model is called as the reference calls it (mcts.py:130-137):
-        # model(x) -> (probabilities, value), here with every leaf of a simulation in x
-        evaluator = az.EVAL_HOST
     else:
+        # the chess engine has no host-evaluator seam (az_chess_config.evaluator
+        # is AZ_EVAL_NETWORK or AZ_EVAL_SYNTHETIC): a plain callable model is refused
         raise TypeError(
-            "MCTS on the MI355X engine needs a model (a custom_alphazero PolicyValueModel, "
-            "SyntheticEvaluator or any callable model(x) -> (probabilities, value)); HTTP "
-            "inference and the exact solver are not on the device path")
+            "chess MCTS on the MI355X engine needs a custom_alphazero PolicyValueModel or a "
+            "SyntheticEvaluator (the chess engine has no host-evaluator seam for other callables)")
     sims = max(SP.mcts_iterations, 1)
     max_plies = max(SP.chess_max_plies, 1)
     # a tree holds at most the visits of its root: sims per search plus the
@@ -243,8 +237,6 @@ def _chess_engine_for(model):
                          arena_edges=160 * sims + 4096)
     if evaluator == az.EVAL_NETWORK:
         eng.set_weights(model.engine_weights())
-    elif evaluator == az.EVAL_HOST:
-        eng.set_host_evaluator(model)
     return eng
 
 

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 7
+#define AZ_ABI_VERSION 8
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
@@ -83,7 +83,15 @@ typedef struct az_config {
                                       the free HBM, the most that fits there and at least
                                       8*mcts_iterations*A + H*W*A; overflow is AZ_E_DEVICE).  The tree
                                       API (az_tree_*) does not compact: it refuses such an engine */
-    int32_t reserved[4];
+    int32_t tower_natural_order;   /* 1: the one-launch tower computes its tiles in natural pixel order
+                                      (no slot plan, no skipped edge taps): bitwise the same outputs
+                                      (tests, A/B runs); 0 = the slot plan (default) */
+    int32_t dirichlet_noise;       /* ConfigMCTS.enable_dirichlet_noise (config.py:52): every root
+                                      selection mixes the priors with a fresh Dirichlet draw from the
+                                      game's MT19937 stream (mcts.py:70-85, :115-116) */
+    double dirichlet_alpha;        /* ConfigMCTS.dirichlet_noise_value (config.py:53, 0.03) */
+    double dirichlet_ratio;        /* ConfigMCTS.dirichlet_noise_ratio (config.py:54, 0.25) */
+    int32_t reserved[2];
 } az_config;
 
 /* One named weight tensor in Keras layout ("Weights"). */
@@ -129,6 +137,11 @@ typedef struct az_stats {
 
 int az_abi_version(void);
 const char* az_last_error(void);
+/* Build identity: a hash of the sources libaz was compiled from (profiles
+ * record it, bench.py matches it), and the extra compile flags of a
+ * diagnostic build (empty for the product library). */
+const char* az_build_id(void);
+const char* az_build_flags(void);
 
 /* Replaces constructing PolicyValueModel + MCTS per game
  * (self_play.py:46-57, utils.py:42-48). */
@@ -145,7 +158,10 @@ int az_engine_set_weights(az_engine* eng, const az_tensor* tensors, int n);
  * [n][H][W][4] f32 full_state planes (connect_n/board.py:83-98); it writes
  * the model's raw outputs probs [n][A] (before the legal-move mask and
  * renormalisation, mcts.py:147-150) and values [n], and returns 0 (nonzero:
- * the search fails with AZ_E_CALLBACK).  Host buffers, valid during the call.
+ * the search fails with AZ_E_CALLBACK, and the simulation it interrupted
+ * leaves the trees incomplete: az_selfplay_step, az_tree_search and
+ * az_tree_play then fail with AZ_E_STATE until az_selfplay_begin or
+ * az_tree_reset).  Host buffers, valid during the call.
  * The outputs must be a deterministic function of the board (the cache
  * relies on it, as the reference's plays_inferences dict does). */
 typedef int32_t (*az_eval_fn)(void* user, const float* x, int32_t n, float* probs, float* values);

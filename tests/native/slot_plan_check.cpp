@@ -8,7 +8,7 @@
 
 namespace az {
 void tower16_slot_plan(int H, int W, int tile_rows, std::vector<int>& slot_pix, int skip[2]);
-int tower16_tile_rows(int HW, bool big);
+int tower16_tile_rows(int HW);
 int tower16_boards_per_tile(int HW, int tile_rows);
 }  // namespace az
 
@@ -18,7 +18,7 @@ int main() {
   printf("[");
   for (int H = 3; H <= 11; ++H)
     for (int W = 3; W <= 11; ++W) {
-      const int HW = H * W, tr = az::tower16_tile_rows(HW, false);
+      const int HW = H * W, tr = az::tower16_tile_rows(HW);
       if (!tr) continue;
       const int nb = az::tower16_boards_per_tile(HW, tr), half = tr / 32;
       std::vector<int> pix;

@@ -33,7 +33,23 @@ def test_library_exports_every_declared_symbol():
     for name in header_functions():
         assert hasattr(lib, name), name
     L = az.load_library()
-    assert L.az_abi_version() == 7
+    assert L.az_abi_version() == 8
+
+
+def test_product_library_is_not_a_diagnostic_build():
+    """The shipped libaz.so carries no diagnostic compile flags (EXTRA= in
+    csrc/Makefile: phase stamps, A/B knobs), and its build id is the hash of
+    the sources in this tree (what profiles/ record, bench.py matches)."""
+    import hashlib
+    ident, flags = az.build_id()
+    assert flags == "", flags
+    csrc = os.path.join(REPO, "custom-alphazero_amd", "csrc")
+    names = sorted(f for f in os.listdir(csrc) if f.startswith("az_") and f.endswith((".hip", ".h")))
+    paths = [os.path.join(csrc, f) for f in names] + [os.path.join(REPO, "include", "az.h"),
+                                                      os.path.join(REPO, "include", "az_chess.h"),
+                                                      os.path.join(csrc, "Makefile")]
+    h = hashlib.sha256(b"".join(open(p, "rb").read() for p in paths)).hexdigest()[:16]
+    assert ident == h, (ident, h)
 
 
 def _header_structs():

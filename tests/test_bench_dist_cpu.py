@@ -10,6 +10,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -143,3 +144,17 @@ def test_bench_launch_command_for_n_ranks(monkeypatch):
     assert bench.launch_ranks(argparse.Namespace(gpus=1)) is None
     monkeypatch.setenv("WORLD_SIZE", "4")
     assert bench.launch_ranks(args) is None
+
+
+def test_bench_refuses_more_ranks_than_gpus(monkeypatch):
+    """One rank per GPU: a world larger than the visible devices exits with
+    status 2 before any GPU call (unless --share-devices asks for a
+    rehearsal that shares them)."""
+    import torch
+    bench = _bench()
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    with pytest.raises(SystemExit) as ex:
+        bench.check_devices(argparse.Namespace(share_devices=False), 4)
+    assert ex.value.code == 2
+    assert bench.check_devices(argparse.Namespace(share_devices=True), 4) == 2
+    assert bench.check_devices(argparse.Namespace(share_devices=False), 2) == 2

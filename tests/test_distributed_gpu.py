@@ -119,7 +119,8 @@ def test_bench_two_ranks_gathers_every_rank(outer_launcher):
     brings every rank's window games to rank 0."""
     port = _free_port()
     args = [os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--slots", "512",
-            "--steps", "3", "--warmup", "2", "--cache-log2", "16", "--no-cpu-baseline", "--no-cache-window"]
+            "--steps", "3", "--warmup", "2", "--cache-log2", "16", "--no-cpu-baseline", "--no-cache-window",
+            "--share-devices"]  # two ranks on the box's one GPU (a rehearsal: the line says so)
     cmd = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
             "--master-addr", "127.0.0.1", "--master-port", str(port)] if outer_launcher else [sys.executable]) + args
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
@@ -130,6 +131,7 @@ def test_bench_two_ranks_gathers_every_rank(outer_launcher):
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["dist_backend"] == "gloo" and len(line["rank_devices"]) == 2
+    assert line["shared_devices"] == (len(set(line["rank_devices"])) < 2)
     gather = line["replay_buffer_gather"]
     assert gather is not None and gather["games"] == line["games_timed"] > 0
     assert gather["samples"] >= 7 * gather["games"]

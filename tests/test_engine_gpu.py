@@ -244,12 +244,13 @@ CONV_ALGOS = [az.CONV_F16X2, az.CONV_DIRECT, az.CONV_F16X2_LAYERS]
 
 
 def make_net_engine(H=6, W=7, n=4, grav=True, S=25, slots=256, seed=0, randomize_bn=True, depth=4,
-                    cache_log2=0, conv_algo=az.CONV_F16X2, lanes=0, compact=False):
+                    cache_log2=0, conv_algo=az.CONV_F16X2, lanes=0, compact=False, hidden=256, **kw):
     A = W if grav else W * H
-    spec = weight_spec(H, W, A, depth=depth)
+    spec = weight_spec(H, W, A, depth=depth, hidden=hidden)
     w = init_weights(spec, seed=seed, randomize_bn=randomize_bn)
     eng = az.Engine(H, W, n, grav, S, slots=slots, evaluator=az.EVAL_NETWORK, depth=depth,
-                    cache_log2=cache_log2, conv_algo=conv_algo, lanes=lanes, compact=compact)
+                    value_hidden=hidden, cache_log2=cache_log2, conv_algo=conv_algo, lanes=lanes,
+                    compact=compact, **kw)
     eng.set_weights(w.items())
     return eng, w
 
@@ -277,19 +278,38 @@ def test_forward_matches_keras_restatement(shape, conv_algo):
     np.testing.assert_allclose(p.sum(axis=1), 1.0, atol=1e-6)
 
 
+@pytest.mark.parametrize("depth,hidden", [(0, 256), (1, 256), (17, 64), (2, 300)])
+def test_forward_outside_the_tower_falls_back(depth, hidden):
+    """the default conv_algo accepts any depth and value head
+    size.  Networks the one-launch tower does not hold (depth 0 -- its heads
+    run inside the last block --, depth > 16, value_hidden > 256) run the
+    per-layer kernels instead, within NET_TOL of the float64 restatement."""
+    eng, w = make_net_engine(6, 7, 4, True, slots=64, depth=depth, hidden=hidden)
+    rng = np.random.RandomState(3)
+    x = oracle.full_state(random_boards(rng, 20, 6, 7))
+    p, v = eng.forward(x)
+    rp, rv = keras_ref.forward(w, x, depth=depth)
+    assert np.abs(p - rp).max() < NET_TOL, np.abs(p - rp).max()
+    assert np.abs(v - rv).max() < NET_TOL, np.abs(v - rv).max()
+    eng.selfplay_run(0, 2, 1)
+    assert eng.stats()["errors"] == 0
+    eng.close()
+
+
 @pytest.mark.parametrize("shape", [(6, 7, True), (5, 5, False), (7, 6, True), (4, 5, True), (9, 9, True)])
-def test_tower_slot_plan_is_bitwise_the_natural_order(shape, monkeypatch):
+def test_tower_slot_plan_is_bitwise_the_natural_order(shape):
     """The slot plan (border blocks skip the taps past their board edge: exact
-    zeros not added) gives the same bits as the natural slot order, full and
-    partial tiles, one-hot and arbitrary inputs."""
+    zeros not added) gives the same bits as the natural slot order
+    (az_config.tower_natural_order), full and partial tiles, one-hot and
+    arbitrary inputs."""
     H, W, grav = shape
     rng = np.random.RandomState(21)
     x = oracle.full_state(random_boards(rng, 37, H, W))
     x[-4:] = rng.rand(4, H, W, 4).astype(np.float32)
     out = []
-    for plan in ("1", "0"):
-        monkeypatch.setenv("AZ_TOWER_PLAN", plan)
-        eng, _ = make_net_engine(H, W, 4, grav, slots=300, conv_algo=az.CONV_F16X2)
+    for natural in (False, True):
+        eng, _ = make_net_engine(H, W, 4, grav, slots=300, conv_algo=az.CONV_F16X2,
+                                 tower_natural_order=natural)
         out.append(eng.forward(x))
         out.append(eng.forward(x[:1]))
         eng.close()
