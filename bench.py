@@ -289,12 +289,29 @@ def conv_roofline(args, conv_algo, per_forward, boards_per_launch, avg_ms, busy_
     achieved = per_launch * direct_flop_per_board / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
     issued = per_launch * issued_per_board / (avg_ms * 1e-3) / 1e12 if avg_ms else 0.0
     union = boards_total * direct_flop_per_board / (busy_ms * 1e-3) / 1e12 if busy_ms else 0.0
-    traffic = None
-    if os.path.exists(pmc_file):  # PMC bytes/board (rocprofv3 FETCH_SIZE/WRITE_SIZE) x live batch
+    # PMC (rocprofv3 FETCH_SIZE / WRITE_SIZE / SQ_VALU_MFMA_BUSY_CYCLES passes, profiles/pmc_fold.py):
+    # bytes per board x the live batch, and the MFMA-busy fraction -- only when
+    # the profile measured THIS build (its az_build_id), else null with the reason
+    from custom_alphazero import engine as az
+    build, _flags = az.build_id()
+    traffic = mfma_busy = None
+    pmc_note = f"no PMC profile {os.path.relpath(pmc_file, REPO)}"
+    if os.path.exists(pmc_file):
         with open(pmc_file) as fp:
             tj = json.load(fp)
-        if pmc_key in tj:
-            traffic = int(tj[pmc_key]["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+        if pmc_key not in tj:
+            pmc_note = f"{os.path.relpath(pmc_file, REPO)} holds no [{pmc_key}] entry"
+        elif tj.get("build_id") != build:
+            pmc_note = (f"{os.path.relpath(pmc_file, REPO)} measured build {tj.get('build_id')}, this libaz is "
+                        f"{build}: traffic and mfma_busy not reported")
+        else:
+            e = tj[pmc_key]
+            traffic = int(e["mean_hbm_bytes_per_board_per_launch"] * boards_per_launch)
+            mfma_busy = round(e["mfma_busy"], 4) if e.get("mfma_busy") is not None else None
+            pmc_note = (f"{os.path.relpath(pmc_file, REPO)} [{pmc_key}], build {build}: "
+                        f"{e['mean_hbm_bytes_per_board_per_launch']:.0f} HBM bytes per board at "
+                        f"{e['boards_per_launch']} boards per launch (x live boards/launch here); mfma_busy = "
+                        f"SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) of that launch")
     return {
         "kernel": conv_kernel_name(conv_algo, chess),
         "bound": "mfma",
@@ -303,8 +320,10 @@ def conv_roofline(args, conv_algo, per_forward, boards_per_launch, avg_ms, busy_
         "unit": "TFLOP/s",
         "frac": round(achieved / peak, 4),
         "traffic": traffic,
-        "traffic_unit": f"HBM bytes per launch (PMC bytes/board, {os.path.relpath(pmc_file, REPO)} [{pmc_key}], "
-                        f"x live boards/launch)",
+        "traffic_unit": "HBM bytes per launch",
+        "mfma_busy": mfma_busy,
+        "pmc": pmc_note,
+        "build_id": build,
         "dtype": dtype,
         "achieved_basis": (f"direct-convolution FLOP per launch ({int(direct_flop_per_board)} per board x "
                            f"boards_per_launch / {per_forward} launch(es) per forward) / avg_launch_ms (HIP events "
@@ -430,7 +449,7 @@ def chess_main(args):
     avg_ms = st1["conv_ms"] / max(launches, 1)
     roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, avg_ms, st1["conv_busy_ms"],
                          local_evals, launches, direct_flop, issued,
-                         os.path.join(REPO, "profiles", "r3", "pmc_chess_traffic.json"),
+                         os.path.join(REPO, "profiles", "r4", "pmc_chess.json"),
                          "f16x2" if args.conv_algo != 1 else "direct", chess=True)
     if rank == 0:
         line = {
@@ -719,7 +738,7 @@ def main():
     per_forward = 1 if args.conv_algo == 0 else 2 * args.depth
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     boards_per_launch = local_evals / max(conv_launches / per_forward, 1)
-    pmc = os.path.join(REPO, "profiles", "r3", "pmc_conv_traffic.json")
+    pmc = os.path.join(REPO, "profiles", "r4", "pmc_tower.json")
     pmc_key = {0: "tower16", 1: "direct", 2: "f16x2"}[args.conv_algo]
     roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, conv_avg_ms, busy_ms, local_evals,
                          conv_launches, direct_flop, issued, pmc, pmc_key)

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Fold rocprofv3 --pmc passes over profiles/conv_bench.py into the per-board
+HBM traffic and the MFMA-busy fraction of the forward's dominant kernel,
+stamped with the libaz build they measured (az_build_id): bench.py prints a
+profile's traffic / mfma_busy only for the same build.
+
+Usage: pmc_fold.py <dir with fetch/ write/ sq/ passes> <boards per launch> <kernel substring> <key>
+
+Corrections per MI355X_MICROARCH.md (HBM/rocprofv3 section): FETCH_SIZE and
+WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of 16 B/lane
+streaming reads -> x2.  SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-busy cycles
+summed over the SIMDs; kernel cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the
+8 XCDs) -> mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles)."""
+import csv
+import glob
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "custom-alphazero_amd"))
+
+
+def per_dispatch(d, counter, pat):
+    vals = []
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter and pat in r["Kernel_Name"]:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def mean(v):
+    return sum(v) / len(v) if v else None
+
+
+def main():
+    d, B, pat, key = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    from custom_alphazero import engine as az
+    build, flags = az.build_id()
+    fetch = mean(per_dispatch(f"{d}/fetch", "FETCH_SIZE", pat))
+    write = mean(per_dispatch(f"{d}/write", "WRITE_SIZE", pat))
+    busy = mean(per_dispatch(f"{d}/sq", "SQ_VALU_MFMA_BUSY_CYCLES", pat))
+    grbm = mean(per_dispatch(f"{d}/sq", "GRBM_GUI_ACTIVE", pat))
+    mfma = mean(per_dispatch(f"{d}/sq", "SQ_INSTS_MFMA", pat))
+    out = {
+        "build_id": build, "build_flags": flags,
+        "source": f"rocprofv3 --pmc, separate passes (FETCH_SIZE; WRITE_SIZE; SQ_VALU_MFMA_BUSY_CYCLES + "
+                  f"SQ_INSTS_MFMA + GRBM_GUI_ACTIVE), profiles/conv_bench.py at B={B} boards per launch, "
+                  f"kernel '{pat}'",
+        "correction": "fetch bytes = 2 x FETCH_SIZE KiB x 1024 (gfx950, 16 B/lane streams); write = WRITE_SIZE KiB "
+                      "x 1024; kernel cycles = GRBM_GUI_ACTIVE / 8; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / "
+                      "(1024 SIMDs x kernel cycles)",
+        key: {
+            "boards_per_launch": B,
+            "hbm_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
+            "mean_hbm_bytes_per_board_per_launch":
+                (2 * fetch + write) * 1024 / B if fetch is not None and write is not None else None,
+            "mfma_busy": busy / (1024 * grbm / 8) if busy and grbm else None,
+            "sq_valu_mfma_busy_cycles": busy, "grbm_gui_active": grbm, "sq_insts_mfma": mfma,
+            "kernel_cycles": grbm / 8 if grbm else None,
+        },
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -158,3 +158,24 @@ def test_bench_refuses_more_ranks_than_gpus(monkeypatch):
     assert ex.value.code == 2
     assert bench.check_devices(argparse.Namespace(share_devices=True), 4) == 2
     assert bench.check_devices(argparse.Namespace(share_devices=False), 2) == 2
+
+
+def test_roofline_traffic_only_from_the_same_build(tmp_path):
+    """the line's PMC traffic and MFMA-busy fraction come
+    from a profile that recorded the libaz build it measured; a profile of
+    another build yields null with the reason."""
+    import json
+    from custom_alphazero import engine as az
+    bench = _bench()
+    build, _ = az.build_id()
+    entry = {"boards_per_launch": 672, "mean_hbm_bytes_per_board_per_launch": 1000.0, "mfma_busy": 0.5}
+    f = tmp_path / "pmc.json"
+    args = argparse.Namespace()
+    for bid, want in ((build, 672 * 1000), ("0123456789abcdef", None)):
+        f.write_text(json.dumps({"build_id": bid, "tower16": entry}))
+        r = bench.conv_roofline(args, 0, 1, 672.0, 0.2, 10.0, 6720, 10, 104.6e6, 270.5e6, str(f), "tower16")
+        assert r["traffic"] == want, r["pmc"]
+        assert r["mfma_busy"] == (0.5 if want else None)
+        assert r["build_id"] == build
+    r = bench.conv_roofline(args, 0, 1, 672.0, 0.2, 10.0, 6720, 10, 104.6e6, 270.5e6, str(tmp_path / "no"), "tower16")
+    assert r["traffic"] is None and "no PMC profile" in r["pmc"]
