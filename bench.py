@@ -542,6 +542,30 @@ def launch_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
+def tree_arena(args, st):
+    """The tree memory the engine chose and what the window used of it."""
+    A, HW = args.width, args.height * args.width
+    safe = args.sims * HW * A + A
+    if not args.compact:
+        return {"compact": False, "edges_per_slot": st["arena_edges"],
+                "bytes_total": 32 * args.slots * st["arena_edges"],
+                "rule": f"a static run of {st['arena_edges']} edges per slot (S*H*W*A + A = {safe}: the whole game)"}
+    pool, high = st["arena_pool_edges"], st["arena_pool_high"]
+    proof = st["arena_edges"] >= safe
+    return {
+        "compact": True, "pool_edges_total": pool, "bytes_total": 32 * pool,
+        "pool_edges_per_half_per_slot": st["arena_edges"], "overflow_proof": proof,
+        "high_water_edges_per_lane_half": high, "max_retained_edges": st["max_retained"],
+        "rule": (f"pooled arenas: each lane owns two halves of {st['arena_edges']} edges x its slots; a slot takes "
+                 f"{16 * A}-edge chunks of the current half as it expands, and after every move compaction copies "
+                 f"each slot's kept subtree (Cheney scan) into the other half, which becomes the current one. "
+                 + (f"{st['arena_edges']} >= S*H*W*A + A = {safe} per slot: no game can overflow it"
+                    if proof else
+                    f"{st['arena_edges']} < S*H*W*A + A = {safe} per slot (the 40%-of-free-HBM cap bound it): the "
+                    f"slots share the pool, overflow raises a device error (none in this run)")),
+    }
+
+
 def check_device(eng, where):
     """The engine's device error word after a window of asynchronous steps
     (az_selfplay_step without stats returns before the kernels finish): a
@@ -824,16 +848,7 @@ def main():
                 "semantics": "reference plays_inferences (mcts.py:122-143): board -> network output, shared "
                              "by all games on the GPU, emptied when weights change; bit-identical results",
             } if args.cache_log2 else None),
-            "tree_arena": {
-                "compact": bool(args.compact),
-                "edges_per_slot": (2 if args.compact else 1) * st1["arena_edges"],
-                "bytes_total": 32 * args.slots * (2 if args.compact else 1) * st1["arena_edges"],
-                "max_retained_edges": st1["max_retained"] if args.compact else None,
-                "rule": ("after every move the chosen child's subtree is copied into the other half of the "
-                         "slot's arena (Cheney scan); each half holds one move's search plus the reused subtree, "
-                         "sized S*H*W*A + A (no game can overflow it) when that fits 40% of the free HBM"
-                         if args.compact else "whole game tree kept (S*H*W*A edges per slot)"),
-            },
+            "tree_arena": tree_arena(args, st1),
             "cache_off": off,
             "roofline_tree": roofline_tree,
             "roofline": roof,

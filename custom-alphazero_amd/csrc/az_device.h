@@ -21,8 +21,8 @@ struct GameCfg {
   int greedy_ply;               // index_move_greedy (config.py:55)
   double c_puct;                // exploration_constant (config.py:51)
   int slots;                    // concurrent game slots on this device
-  int arena_cap;                // edges per slot (per half with compaction)
-  int halves;                   // 2: the live tree alternates between two halves (compaction), else 1
+  int arena_cap;                // halves == 1: edges per slot (a static arena per slot)
+  int halves;                   // 2: pooled arenas with compaction (TreeDev::pool_*), else 1
   int max_depth;                // path buffer per slot (= HW)
   int pow_len;                  // entries of the pow(n, 0.5) table
 };

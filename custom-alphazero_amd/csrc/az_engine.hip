@@ -62,6 +62,7 @@ struct Lane {
   az::ConvTimer timer;
   az::ConvTimer tree_timer;  // select and expand launches (bench.py roofline_tree)
   hipEvent_t move_done[4] = {nullptr, nullptr, nullptr, nullptr};  // end of move m on this lane, m mod 4
+  int64_t pool_cap = 0;        // compacted self-play: edges per pool half (TreeDev::pool_cap)
 };
 
 struct az_engine {
@@ -378,8 +379,9 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
   L->g.slots = n;
   az::TreeDev t = e->t;
   const size_t f = (size_t)first;
-  t.edges += f * g.halves * g.arena_cap;
-  if (t.half) t.half += f;
+  if (g.halves == 1) t.edges += f * g.arena_cap;  // pooled: the lane's own pool (alloc_pool)
+  if (t.arena_end) t.arena_end += f;
+  if (t.slot_live) t.slot_live += f;
   t.root_board += f;
   t.root_first += f;
   t.root_n += f;
@@ -419,6 +421,22 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
   for (int i = 0; i < 3; ++i) L->act[i] = e->act[i] ? e->act[i] + f * g.HW * 128 : nullptr;
   L->probs = e->probs + f * g.A;
   L->values = e->values + f;
+  return 0;
+}
+
+// compacted self-play: the lane's two pool halves of `cap` edges and their counters
+int alloc_pool(az_engine* e, Lane* L, int64_t cap) {
+  int rc;
+  az::Edge* halves = nullptr;
+  unsigned long long* tops = nullptr;
+  if ((rc = e->alloc(&halves, 2 * (size_t)cap)) || (rc = e->alloc(&tops, 2))) return rc;
+  AZ_HIP(hipMemset(tops, 0, 2 * sizeof(unsigned long long)));
+  L->pool_cap = cap;
+  L->t.pool_cap = (int32_t)cap;
+  L->t.edges = halves;
+  L->t.dst_edges = halves + cap;
+  L->t.pool_top = tops;
+  L->t.dst_top = tops + 1;
   return 0;
 }
 
@@ -715,18 +733,19 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   g.slots = c.slots;
   g.max_depth = g.HW + 1;
   const int64_t visits = c.max_tree_visits > 0 ? c.max_tree_visits : (int64_t)c.mcts_iterations * g.HW + 2;
-  // compaction keeps one move's search plus the reused subtree per half: 8 S A
-  // covers a chosen child holding up to 7/8 of the root's visits move after
-  // move (the retained high-water mark is reported as az_stats.max_retained)
-  g.halves = c.compact ? 2 : 1;
   // a slot's tree holds at most mcts_iterations * H*W expansions of <= A edges
-  // (one game), so a half of that size cannot overflow.  Compacted, each half
-  // holds one move's search plus the subtree kept -- measured a few thousand
-  // edges at configs[1] with random weights, but a trained network that keeps
-  // most visits on the chosen child grows the kept subtree toward the game's
-  // whole search -- so the default is the safe size whenever two such halves
-  // per slot fit in 40% of the free HBM, else the most that does (at least
-  // 8 S A + H W A; an overflow is reported as kErrArena, never overrun).
+  // (one game): `safe` edges per slot can never overflow.
+  //  * uncompacted (tree API): a static run of arena_edges (default safe) per slot;
+  //  * compacted self-play (az_config.compact): pooled arenas (az_tree.h) -- per
+  //    lane two halves of arena_edges x the lane's slots, arena_edges (an
+  //    average per slot) defaulting to safe when two such halves per slot fit
+  //    in 40% of the free HBM, else the most that does (at least 8 S A + H W A).
+  //    A slot holds what it uses -- one move's search plus its kept subtree,
+  //    a few thousand edges at configs[1] -- so the pool is shared: a game
+  //    whose kept subtree grows toward the whole game's search (a peaked
+  //    network) takes the room other slots leave.  Overflow is kErrArena,
+  //    never an overrun.
+  g.halves = c.compact ? 2 : 1;
   const int64_t safe = (int64_t)c.mcts_iterations * g.HW * A + A;
   int64_t arena = c.arena_edges > 0 ? c.arena_edges : safe;
   if (c.arena_edges <= 0 && c.compact) {
@@ -736,9 +755,9 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       arena = std::min(safe, std::max(fit, (int64_t)8 * c.mcts_iterations * A + (int64_t)g.HW * A));
     }
   }
-  if (visits > (1 << 30) || arena > (1 << 30)) {
+  if (visits > (1 << 30) || arena > (1 << 30) || (c.compact && arena < 2 * az::kPoolChunkA * A)) {
     delete e;
-    return fail(AZ_E_INVALID, "tree bounds too large");
+    return fail(AZ_E_INVALID, "tree bounds too large (or a pooled arena below two chunks per slot)");
   }
   g.pow_len = (int)visits;
   g.arena_cap = (int)arena;
@@ -753,9 +772,11 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   if (c.lanes < 0) return cleanup(fail(AZ_E_INVALID, "lanes must be >= 0"));
   const size_t S = (size_t)g.slots;
   az::TreeDev& t = e->t;
-  t.half = nullptr;
-  if (g.halves > 1 && (rc = e->alloc(&t.half, S))) return cleanup(rc);
-  if ((rc = e->alloc(&t.edges, S * g.halves * (size_t)g.arena_cap)) || (rc = e->alloc(&t.root_board, S)) ||
+  t.edges = nullptr;
+  t.arena_end = t.slot_live = nullptr;
+  if (g.halves == 1 && (rc = e->alloc(&t.edges, S * (size_t)g.arena_cap))) return cleanup(rc);
+  if (g.halves > 1 && ((rc = e->alloc(&t.arena_end, S)) || (rc = e->alloc(&t.slot_live, S)))) return cleanup(rc);
+  if ((rc = e->alloc(&t.root_board, S)) ||
       (rc = e->alloc(&t.root_first, S)) || (rc = e->alloc(&t.root_n, S)) ||
       (rc = e->alloc(&t.root_value, S)) || (rc = e->alloc(&t.arena_top, S)) ||
       (rc = e->alloc(&t.ply, S)) || (rc = e->alloc(&t.game_id, S)) ||
@@ -869,6 +890,10 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
           return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
     }
   }
+  if (g.halves > 1)  // pooled arenas, one pool per lane (whose indices stay below 2^31)
+    for (Lane* L : e->lanes)
+      if ((rc = alloc_pool(e, L, std::min<int64_t>((int64_t)g.arena_cap * L->n, (1ll << 31) - 1))))
+        return cleanup(rc);
   if (nl == 1)
     for (hipEvent_t& ev : e->whole.move_done)
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
@@ -1053,6 +1078,11 @@ int az_stats_get(az_engine* e, az_stats* st) {
   }
   st->games_drained = e->drained;
   st->arena_edges = e->g.arena_cap;
+  if (e->g.halves > 1) {
+    st->arena_pool_edges = 0;
+    for (Lane* L : e->lanes) st->arena_pool_edges += 2 * L->pool_cap;
+    st->arena_pool_high = (int64_t)h[az::kStatPoolHigh];
+  }
   st->issued_flop_per_board = e->net.issued_flop_per_board;
   return 0;
 }
@@ -1147,6 +1177,11 @@ int az_selfplay_begin(az_engine* e, int64_t first_game, int64_t n_games, uint32_
   AZ_HIP(hipMemcpyAsync(e->t.stats, st, sizeof(st), hipMemcpyHostToDevice, e->stream));
   az::launch_slot_init(e->g, e->t, smp, first_wave, e->stream);
   AZ_HIP(hipGetLastError());
+  if (e->g.halves > 1)  // every slot starts with no chunk: the pools are empty
+    for (Lane* L : e->lanes) {
+      AZ_HIP(hipMemsetAsync(L->t.pool_top, 0, sizeof(unsigned long long), e->stream));
+      AZ_HIP(hipMemsetAsync(L->t.dst_top, 0, sizeof(unsigned long long), e->stream));
+    }
   AZ_HIP(hipStreamSynchronize(e->stream));
   e->sp_first = first_game;
   e->sp_n = n_games;
@@ -1175,6 +1210,10 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
           if (O != L) AZ_HIP(hipStreamWaitEvent(L->stream, O->move_done[(m - 1) % 4], 0));
       az::launch_play(L->g, L->t, e->smp, nullptr, -1, 0, 1, L->stream);
       az::launch_compact(L->g, L->t, L->stream);
+      if (L->g.halves > 1) {  // the kept trees are in the other half now: it is the current one
+        std::swap(L->t.edges, L->t.dst_edges);
+        std::swap(L->t.pool_top, L->t.dst_top);
+      }
       az::launch_move_end(e->move_arrive + m % 4, (int)e->lanes.size(), e->smp.done_count,
                           e->snap_dev + m % 4, L->stream);
       AZ_HIP(hipEventRecord(L->move_done[m % 4], L->stream));
@@ -1378,13 +1417,13 @@ int az_tree_export(az_engine* e, int slot, double* prior, double* w, int32_t* n,
   if (!e || slot < 0 || slot >= e->g.slots) return fail(AZ_E_INVALID, "bad arguments");
   if (int rc_ = enter(e)) return rc_;
   AZ_HIP(hipStreamSynchronize(e->stream));
-  int32_t top, half = 0;
+  if (int rc_ = tree_api_ok(e)) return rc_;
+  int32_t top;
   AZ_HIP(hipMemcpy(&top, e->t.arena_top + slot, 4, hipMemcpyDeviceToHost));
-  if (e->g.halves > 1) AZ_HIP(hipMemcpy(&half, e->t.half + slot, 4, hipMemcpyDeviceToHost));
   std::vector<az::Edge> h(top);
   if (top)
-    AZ_HIP(hipMemcpy(h.data(), e->t.edges + ((size_t)slot * e->g.halves + half) * e->g.arena_cap,
-                     top * sizeof(az::Edge), hipMemcpyDeviceToHost));
+    AZ_HIP(hipMemcpy(h.data(), e->t.edges + (size_t)slot * e->g.arena_cap, top * sizeof(az::Edge),
+                     hipMemcpyDeviceToHost));
   for (int i = 0; i < top; ++i) {
     if (prior) prior[i] = h[i].prior;
     if (w) w[i] = h[i].W;

@@ -33,7 +33,8 @@ enum : int {
   kStatCacheInserts = 9,
   kStatPathEdges = 10,   // edges on the selected paths (sum of select depths)
   kStatMaxRetained = 11, // compaction: most edges kept (atomicMax)
-  kStatCount = 12        // (kStatCacheInserts counts since engine creation; CacheDev::ctl since a clear)
+  kStatPoolHigh = 12,    // pooled arenas: most edges a lane's half held at a move's end (atomicMax)
+  kStatCount = 13        // (kStatCacheInserts counts since engine creation; CacheDev::ctl since a clear)
 };
 enum : unsigned long long {
   kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16,
@@ -41,14 +42,33 @@ enum : unsigned long long {
 };
 
 // All device state of a forest (struct of arrays over slots).
+//
+// Arenas.  halves == 1 (the tree API, uncompacted self-play): slot s owns the
+// static run edges[s * arena_cap, (s + 1) * arena_cap); edge indices are
+// relative to it.  halves == 2 (compacted self-play): every lane owns a POOL
+// of two halves of pool_cap edges; a move's search allocates from the
+// current half (`edges`, bump counter `pool_top`) in chunks of kPoolChunkA * A
+// edges per slot, and compaction copies each slot's kept subtree into the
+// other half (`dst_edges`, `dst_top`), reserving the slot's live edge count
+// there in one bump.  After a lane's compaction the current half is empty:
+// its counter resets and the halves swap (host side, the next launches'
+// views).  Edge indices are pool-half indices.  The pool is shared by the
+// lane's slots, so one game whose kept subtree grows large (a peaked
+// network) borrows what other slots do not use; overflow raises kErrArena.
+constexpr int kPoolChunkA = 16;
 struct TreeDev {
-  Edge* edges;                 // [slots][halves][arena_cap]
-  int32_t* half;               // [slots] half holding the live tree (halves == 2)
+  Edge* edges;                 // halves == 1: [slots][arena_cap]; 2: the lane's current pool half
+  int32_t* arena_end;          // [slots] pool: end of the slot's current chunk
+  int32_t* slot_live;          // [slots] pool: edges of the slot's tree in the current half
+  unsigned long long* pool_top;  // pool: the current half's bump counter
+  Edge* dst_edges;             // pool: the other half (compaction target) ...
+  unsigned long long* dst_top;   // ... and its counter
+  int32_t pool_cap;            // pool: edges per half
   Board* root_board;           // [slots]
   int32_t* root_first;         // [slots]
   int32_t* root_n;             // [slots]
   float* root_value;           // [slots]
-  int32_t* arena_top;          // [slots]
+  int32_t* arena_top;          // [slots] next free edge (static: of the slot's run; pool: of the half)
   int32_t* ply;                // [slots] (Board.fullmove_number)
   int64_t* game_id;            // [slots], -1 = idle
   int32_t* path;               // [slots][max_depth]
@@ -160,13 +180,15 @@ size_t drain_record_bytes(const GameCfg& g);
 void launch_drain_pack(const GameCfg& g, const SampleDev& smp, int64_t from, int n, uint8_t* out,
                        hipStream_t s);
 
-// the live arena of slot s
+// the base edge indices of slot s are relative to
 AZ_HD Edge* slot_edges(const GameCfg& g, const TreeDev& t, int s) {
-  return t.edges + ((size_t)s * g.halves + (g.halves > 1 ? t.half[s] : 0)) * g.arena_cap;
+  return g.halves > 1 ? t.edges : t.edges + (size_t)s * g.arena_cap;
 }
 
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s);
-// self-play tree reuse (halves == 2): the new root's subtree into the other half
+// self-play tree reuse (halves == 2): the new root's subtree into the other
+// pool half; then the current half's counter is reset (its high-water mark to
+// kStatPoolHigh) -- the host swaps the halves for the next move
 void launch_compact(const GameCfg& g, const TreeDev& t, hipStream_t s);
 // end of a lane's move: the last of n_lanes lanes to arrive stores the
 // games-finished count into *snap (pinned host memory) and resets *arrive

@@ -143,7 +143,10 @@ __device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gi
   t.root_n[s] = 0;
   t.root_value[s] = 0.f;
   t.arena_top[s] = 0;
-  if (g.halves > 1) t.half[s] = 0;
+  if (g.halves > 1) {  // pooled: no chunk yet (the first expansion takes one)
+    t.arena_end[s] = 0;
+    t.slot_live[s] = 0;
+  }
   t.ply[s] = 0;
   t.path_len[s] = 0;
   t.slot_expansions[s] = 0;
@@ -559,8 +562,29 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
   const int nm = moves_order(g, b, moves);
   const float sum = pairwise_sum_f32(masked, nl);
   Edge* E = slot_edges(g, t, s);
-  const int first = t.arena_top[s];
-  if (first + nm > g.arena_cap) {
+  int first = t.arena_top[s];
+  if (g.halves > 1) {
+    // pooled arena: the run goes into the slot's current chunk, or a new one
+    // of kPoolChunkA * A edges bumped off the lane's half (one atomic per wave)
+    int end = t.arena_end[s];
+    if (first + nm > end) {
+      const int ch = kPoolChunkA * g.A;
+      const unsigned long long m = __ballot(1);
+      const int leader = __ffsll((long long)m) - 1;
+      const int rank = __popcll(m & ((1ull << lane_id()) - 1));
+      unsigned long long base = 0;
+      if (lane_id() == leader) base = atomicAdd(t.pool_top, (unsigned long long)__popcll(m) * ch);
+      base = __shfl(base, leader) + (unsigned long long)rank * ch;
+      if (base + ch > (unsigned long long)t.pool_cap) {
+        flag_error(t, kErrArena);
+        return;
+      }
+      first = (int)base;
+      end = first + ch;
+      t.arena_end[s] = end;
+    }
+    t.slot_live[s] += nm;
+  } else if (first + nm > g.arena_cap) {
     flag_error(t, kErrArena);
     return;
   }
@@ -691,56 +715,65 @@ __global__ __launch_bounds__(kGameBlock) void play_kernel(GameCfg g, TreeDev t, 
 
 // Tree reuse with reclamation (halves == 2), after play_kernel: the new
 // root's subtree -- the nodes MCTS.play keeps by moving current_root to the
-// chosen child (mcts.py:207) -- is copied into the slot's other arena half by
+// chosen child (mcts.py:207) -- is copied into the lane's other pool half by
 // a Cheney scan, one wave per slot: the root's edge run first, then for each
 // scanned edge with an expanded child that child's run, placed by a
 // prefix sum over the wave's 64 edges (BFS order; edges before `scan` point
-// into the new half).  Everything else the game has left is dropped, so the
-// arena holds one move's search plus what it reuses.  Edge values are copied
-// bit for bit: the next search sees the same tree.
+// into the new half).  The destination is one bump of the slot's live edge
+// count (a bound on the kept subtree); the next move's expansions fill its
+// unused tail before taking chunks.  Everything else the game has left is
+// dropped.  Edge values are copied bit for bit: the next search sees the same
+// tree.
 __global__ __launch_bounds__(64) void compact_kernel(GameCfg g, TreeDev t) {
   const int s = blockIdx.x, lane = threadIdx.x;
   if (t.game_id[s] < 0) return;
-  const int h = t.half[s];
-  const Edge* E = t.edges + ((size_t)s * 2 + h) * g.arena_cap;
-  Edge* D = t.edges + ((size_t)s * 2 + (1 - h)) * g.arena_cap;
+  const Edge* E = t.edges;
   const int first = t.root_first[s], n = t.root_n[s];
   if (n <= 0) {  // a fresh game (refilled slot) or a terminal root: nothing to keep
     if (lane == 0) {
-      t.half[s] = 1 - h;
       t.arena_top[s] = 0;
+      t.arena_end[s] = 0;
+      t.slot_live[s] = 0;
       t.root_first[s] = 0;
     }
     return;
   }
-  for (int j = lane; j < n; j += 64) D[j] = E[first + j];
-  __syncthreads();
+  const int need = t.slot_live[s];
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(t.dst_top, (unsigned long long)need);
+  base = __shfl(base, 0);
+  const bool room = base + (unsigned long long)need <= (unsigned long long)t.pool_cap;
+  Edge* D = t.dst_edges + (room ? base : 0);
   int top = n, scan = 0;
-  bool overflow = false;
-  while (scan < top) {
+  bool overflow = !room || n > need;
+  if (!overflow) {
+    for (int j = lane; j < n; j += 64) D[j] = E[first + j];
+    __syncthreads();
+  }
+  while (!overflow && scan < top) {
     const int top0 = top;
     const int j = scan + lane;
     Edge e;
-    int need = 0;
+    int need_j = 0;
     if (j < top0) {
       e = D[j];
-      if (e.child >= 0) need = e.child_n;
+      if (e.child >= 0) need_j = e.child_n;
     }
-    int incl = need;
+    int incl = need_j;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const int o = __shfl_up(incl, off, 64);
       if (lane >= off) incl += o;
     }
     const int total = __shfl(incl, 63, 64);
-    if (top0 + total > g.arena_cap) {
+    if (top0 + total > need) {
       overflow = true;
       break;
     }
-    if (need) {
-      const int nf = top0 + incl - need;
-      for (int k = 0; k < need; ++k) D[nf + k] = E[e.child + k];
-      e.child = nf;
+    if (need_j) {
+      const int nf = top0 + incl - need_j;
+      for (int k = 0; k < need_j; ++k) D[nf + k] = E[e.child + k];
+      e.child = (int)base + nf;  // a pool-half index
       D[j] = e;
     }
     top = top0 + total;
@@ -748,13 +781,25 @@ __global__ __launch_bounds__(64) void compact_kernel(GameCfg g, TreeDev t) {
     __syncthreads();
   }
   if (lane == 0) {
-    if (overflow) flag_error(t, kErrArena);
-    t.half[s] = 1 - h;
-    t.arena_top[s] = overflow ? 0 : top;
-    t.root_first[s] = 0;
-    if (overflow) t.root_n[s] = 0;
+    if (overflow) {
+      flag_error(t, kErrArena);
+      t.root_n[s] = 0;
+      top = 0;
+    }
+    t.root_first[s] = (int)base;
+    t.arena_top[s] = (int)base + top;
+    t.arena_end[s] = overflow ? (int)base : (int)base + need;
+    t.slot_live[s] = top;
     atomicMax(t.stats + kStatMaxRetained, (unsigned long long)top);
   }
+}
+
+// after a lane's compaction nothing lives in its current half: record how
+// full it got and empty it (the host swaps the halves for the next move)
+__global__ void pool_flip_kernel(TreeDev t) {
+  if (threadIdx.x != 0) return;
+  atomicMax(t.stats + kStatPoolHigh, *t.pool_top);
+  *t.pool_top = 0;
 }
 
 // First n_first slots get games first_game .. first_game+n_first-1; the rest idle.
@@ -881,7 +926,9 @@ void launch_play(const GameCfg& g, const TreeDev& t, const SampleDev& smp, const
 }
 
 void launch_compact(const GameCfg& g, const TreeDev& t, hipStream_t s) {
-  if (g.halves > 1 && g.slots > 0) compact_kernel<<<g.slots, 64, 0, s>>>(g, t);
+  if (g.halves <= 1) return;
+  if (g.slots > 0) compact_kernel<<<g.slots, 64, 0, s>>>(g, t);
+  pool_flip_kernel<<<1, 64, 0, s>>>(t);
 }
 
 // Every lane's play kernel for move m + 1 waits for the other lanes' move m

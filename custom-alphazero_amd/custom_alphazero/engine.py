@@ -70,6 +70,7 @@ class Stats(ctypes.Structure):
         ("cache_capacity", ctypes.c_int64), ("games_drained", ctypes.c_int64),
         ("max_retained", ctypes.c_int64), ("cache_live_gens", ctypes.c_int64),
         ("arena_edges", ctypes.c_int64), ("issued_flop_per_board", ctypes.c_double),
+        ("arena_pool_edges", ctypes.c_int64), ("arena_pool_high", ctypes.c_int64),
     ]
 
     def as_dict(self):

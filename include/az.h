@@ -64,7 +64,9 @@ typedef struct az_config {
     int32_t depth;                 /* ConfigModel.depth (config.py:63) */
     int32_t value_hidden;          /* ValueHead hidden_dim (model/tensorflow/model.py:110) */
     double bn_epsilon;             /* Keras BatchNormalization epsilon (1e-3) */
-    int64_t arena_edges;           /* tree edges per slot; 0 = mcts_iterations*H*W*A */
+    int64_t arena_edges;           /* tree edges per slot (compact: the average per slot of a lane's
+                                      pooled halves); 0 = mcts_iterations*H*W*A + A, no game can
+                                      overflow it */
     int64_t max_tree_visits;       /* bound on visits through one node; 0 = mcts_iterations*H*W */
     int32_t cache_log2;            /* transposition cache entries = 2^cache_log2 (the reference's
                                       plays_inferences, mcts/mcts.py:122-143); 0 = off, else 4..30
@@ -76,13 +78,16 @@ typedef struct az_config {
     int32_t lanes;                 /* self-play slot groups searched on separate HIP streams
                                       (0 = auto: 2 when slots >= 512); results do not depend on it */
     int32_t compact;               /* 1: after every self-play move the chosen child's subtree is
-                                      copied into the other half of the slot's arena (the subtrees
-                                      the game has left are reclaimed, mcts.py:207); arena_edges is
-                                      then per half (0 = mcts_iterations*H*W*A + A, a half no game
-                                      can overflow, or, when two such halves per slot exceed 40% of
-                                      the free HBM, the most that fits there and at least
-                                      8*mcts_iterations*A + H*W*A; overflow is AZ_E_DEVICE).  The tree
-                                      API (az_tree_*) does not compact: it refuses such an engine */
+                                      copied into the other half of the lane's pooled arena (the
+                                      subtrees the game has left are reclaimed, mcts.py:207).  Each
+                                      lane (slot group) owns two halves of arena_edges x its slots
+                                      edges; a slot takes 16*A-edge chunks of the current half as it
+                                      expands, so the slots share the room (0 = the overflow-proof
+                                      size S*H*W*A + A per slot, or, when two such halves per slot
+                                      exceed 40% of the free HBM, the most that fits there and at
+                                      least 8*mcts_iterations*A + H*W*A; overflow is AZ_E_DEVICE).
+                                      The tree API (az_tree_*) does not compact: it refuses such an
+                                      engine */
     int32_t tower_natural_order;   /* 1: the one-launch tower computes its tiles in natural pixel order
                                       (no slot plan, no skipped edge taps): bitwise the same outputs
                                       (tests, A/B runs); 0 = the slot plan (default) */
@@ -129,10 +134,13 @@ typedef struct az_stats {
                                  before the next search) since engine creation */
     int64_t cache_live_gens;  /* generations a lookup accepts (ages 0 .. n-1; a hit moves the entry
                                  into the current one); entries n+ generations old may be overwritten */
-    int64_t arena_edges;      /* tree edges per slot (per half with compaction) this engine allocated */
+    int64_t arena_edges;      /* tree edges per slot this engine allocated (compact: per half, the
+                                 average over a lane's pool) */
     double issued_flop_per_board; /* MFMA FLOP the network forward issues per board (the one-launch
                                      tower: per full tile after its slot plan's skipped taps, / boards
                                      per tile; 0 = not reported) */
+    int64_t arena_pool_edges; /* compact: edges of every lane's two pool halves (0 uncompacted) */
+    int64_t arena_pool_high;  /* compact: most edges one lane's half held at a move's end */
 } az_stats;
 
 int az_abi_version(void);

@@ -453,15 +453,19 @@ def test_abi_error_behaviour():
 
 
 def test_compaction_bounds_the_arena_and_reports_overflow():
-    """With compact, a slot's arena holds one move's search plus the reused
-    subtree: 8*S*A + H*W*A edges per half against S*H*W*A without (5.9k vs
-    29.4k at S=100); the high-water mark is reported and stays inside; an
-    arena too small for a search is a device error, not a wrong tree."""
+    """With compact, the slots of a lane share a pooled arena of two halves:
+    a slot holds one move's search plus its kept subtree (a few thousand
+    edges here, against S*H*W*A + A = 29.4k for a whole game at S=100); the
+    retained and pool high-water marks are reported and stay inside; a pool
+    too small for a search is a device error, not a wrong tree; results equal
+    the uncompacted engine's bit for bit."""
     eng = az.Engine(6, 7, 4, True, 100, slots=64, evaluator=az.EVAL_SYNTHETIC, compact=True)
     eng.selfplay_run(0, 128, 3)
     st = eng.stats()
     assert st["errors"] == 0 and st["games_done"] == 128
     assert 0 < st["max_retained"] <= 8 * 100 * 7 + 42 * 7
+    assert st["arena_pool_edges"] == 2 * 64 * st["arena_edges"]
+    assert 0 < st["arena_pool_high"] <= 64 * (st["max_retained"] + 100 * 7 + 16 * 7)
     r = eng.selfplay_results()
     eng.close()
     ref = az.Engine(6, 7, 4, True, 100, slots=64, evaluator=az.EVAL_SYNTHETIC)
@@ -475,3 +479,41 @@ def test_compaction_bounds_the_arena_and_reports_overflow():
     with pytest.raises(az.AzError, match="arena-overflow"):
         small.selfplay_run(0, 8, 3)
     small.close()
+
+
+def _peaked(x):
+    """A host evaluator that puts nearly all prior on one action picked by a
+    hash of the board, value 0: PUCT then spends almost every simulation
+    below that child, and the played (greedy) move keeps nearly the whole
+    search -- the kept subtree grows move after move toward the game's
+    whole search."""
+    n = len(x)
+    cells = np.arange(1, x.shape[1] * x.shape[2] + 1)
+    own = x[..., 1].reshape(n, -1) @ cells
+    opp = x[..., 2].reshape(n, -1) @ cells
+    a = (3 * own + 7 * opp).astype(np.int64) % x.shape[2]
+    p = np.full((n, x.shape[2]), 1e-4, np.float32)
+    p[np.arange(n), a] = 1.0
+    return p, np.zeros(n, np.float32)
+
+
+@pytest.mark.timeout(300)
+def test_pooled_arena_holds_a_peaked_network():
+    """A peaked evaluator over full games: compaction keeps trees of tens of
+    thousands of edges per slot (far past the 8*S*A + H*W*A halves round 2
+    sized), the pooled arena holds them with no device error, and every game
+    equals the uncompacted engine's bit for bit."""
+    S, slots = 200, 32
+    out = []
+    for compact in (True, False):
+        eng = az.Engine(6, 7, 4, True, S, slots=slots, evaluator=az.EVAL_HOST, compact=compact)
+        eng.set_host_evaluator(_peaked)
+        st = eng.selfplay_run(0, slots, 17)
+        assert st["errors"] == 0 and st["games_done"] == slots
+        out.append((eng.selfplay_results(), eng.stats()))
+        eng.close()
+    (r, st), (rr, _) = out
+    assert st["max_retained"] > 8 * S * 7 + 42 * 7, st["max_retained"]
+    for k in ("lengths", "moves", "expansions", "results"):
+        np.testing.assert_array_equal(r[k], rr[k])
+    np.testing.assert_array_equal(r["policies"].view(np.uint64), rr["policies"].view(np.uint64))

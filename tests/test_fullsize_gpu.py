@@ -110,16 +110,21 @@ def test_c4_fullsize_game_replays_on_oracle(c4_games, g):
 @pytest.mark.parametrize("cfg", [
     dict(H=9, W=9, n=5, S=200, slots=8192, first=0, replay=(8191,)),        # configs[2]
     dict(H=6, W=7, n=4, S=400, slots=4096, first=7 * 4096, replay=(4095,)),  # configs[3], rank 7
-], ids=["c5_9x9_s200_8192", "c4_s400_shard7"])
+    dict(H=6, W=7, n=4, S=400, slots=16384, first=16384, replay=(0, 16383)),  # configs[3] over 2 GPUs, rank 1
+], ids=["c5_9x9_s200_8192", "c4_s400_shard7", "c4_s400_2gpu_shard1"])
 @pytest.mark.timeout(400)  # configs[2] plays ~80M expansions (about 90 s)
 def test_connect_n_fullsize_configs(cfg):
-    """BASELINE configs[2] and one rank's shard of configs[3] at full size:
-    rules and policies for every game, sampled games replayed on the oracle
-    (a shard's game i uses seed base + first + i, as bench.py's ranks do)."""
+    """BASELINE configs[2] and one rank's shard of configs[3] at full size --
+    8 ranks (4096 games each) and 2 ranks (16384 games each, the largest
+    shard configs[3] names): rules and policies for every game, sampled games
+    replayed on the oracle (a shard's game i uses seed base + first + i, as
+    bench.py's ranks do); the pooled arenas hold every tree (no device error)."""
     H, W, n, S = cfg["H"], cfg["W"], cfg["n"], cfg["S"]
     eng, _ = make_net_engine(H, W, n, True, S=S, slots=cfg["slots"], seed=13, cache_log2=25, compact=True)
     try:
         games = selfplay_games(eng, cfg["first"], cfg["slots"], base_seed=C4_SEED)
+        st = eng.stats()
+        assert st["errors"] == 0 and 0 < st["arena_pool_high"] <= st["arena_pool_edges"] // 2
         check_rules_and_policies(games, H, W, n)
         for g in cfg["replay"]:
             replay_on_oracle(eng, games[g], H, W, n, S, C4_SEED + cfg["first"] + g)
