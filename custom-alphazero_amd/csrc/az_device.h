@@ -25,7 +25,17 @@ struct GameCfg {
   int halves;                   // 2: pooled arenas with compaction (TreeDev::pool_*), else 1
   int max_depth;                // path buffer per slot (= HW)
   int pow_len;                  // entries of the pow(n, 0.5) table
+  int noise;                    // ConfigMCTS.enable_dirichlet_noise (config.py:52): root Dirichlet noise
+  double noise_alpha;           // dirichlet_noise_value (config.py:53)
+  double noise_ratio;           // dirichlet_noise_ratio (config.py:54)
 };
+
+// Edge::action carries the action index in its low 14 bits; kPrior64 marks
+// the edges of an expansion whose priors came from normalize_probabilities'
+// float64 uniform branch (mcts/utils.py:13-14) -- the reference's noisy-prior
+// arithmetic depends on the priors' dtype (mcts.py:72-76)
+constexpr int kActMask = 0x3fff;
+constexpr int kPrior64 = 0x4000;
 
 // ----------------------------------------------------------------- board
 // Canonical board: `own` = stones of the side to move (+1 in the reference's

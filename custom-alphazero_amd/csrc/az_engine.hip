@@ -732,6 +732,14 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   g.c_puct = c.exploration_constant;
   g.slots = c.slots;
   g.max_depth = g.HW + 1;
+  g.noise = c.dirichlet_noise != 0;
+  g.noise_alpha = c.dirichlet_alpha;
+  g.noise_ratio = c.dirichlet_ratio;
+  if (g.noise && !(c.dirichlet_alpha > 0.0 && c.dirichlet_alpha <= 1.0 && std::isfinite(c.dirichlet_ratio))) {
+    delete e;
+    return fail(AZ_E_INVALID, "Dirichlet noise needs 0 < dirichlet_alpha <= 1 (the reference's 0.03) and a "
+                              "finite dirichlet_ratio");
+  }
   const int64_t visits = c.max_tree_visits > 0 ? c.max_tree_visits : (int64_t)c.mcts_iterations * g.HW + 2;
   // a slot's tree holds at most mcts_iterations * H*W expansions of <= A edges
   // (one game): `safe` edges per slot can never overflow.
@@ -1360,6 +1368,9 @@ int az_tree_release(az_engine* e, int n, const int32_t* slots) {
 
 int az_tree_search(az_engine* e, int n_sims) {
   if (!e || n_sims < 0) return fail(AZ_E_INVALID, "bad arguments");
+  if (e->g.noise)  // its draws come from each game's own stream, which self-play owns
+    return fail(AZ_E_INVALID, "Dirichlet root noise runs in self-play (az_selfplay_*); the tree API "
+                              "engine must be created with dirichlet_noise = 0");
   int rc;
   if ((rc = ready_to_search(e))) return rc;
   if (int rc_ = enter(e)) return rc_;
@@ -1430,7 +1441,7 @@ int az_tree_export(az_engine* e, int slot, double* prior, double* w, int32_t* n,
     if (n) n[i] = h[i].N;
     if (child) child[i] = h[i].child;
     if (child_n) child_n[i] = h[i].child_n;
-    if (action) action[i] = h[i].action;
+    if (action) action[i] = h[i].action & az::kActMask;
     if (child_value) child_value[i] = h[i].child_value;
   }
   return 0;

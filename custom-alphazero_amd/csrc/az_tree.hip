@@ -16,6 +16,7 @@
 //   prior = float32 pairwise sum + float32 divide, or float64 1/n uniform
 //   W    += v in path order leaf->root with v negated per level (mcts.py:163-168)
 //   move  = cumsum / last / searchsorted-right on one legacy random_sample
+#include "az_random.h"
 #include "az_tree.h"
 
 namespace az {
@@ -288,7 +289,33 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   }
 }
 
+// ---------------------------------------------------- Dirichlet root noise
+// get_best_edge_with_noise (mcts.py:70-85), used by select at the current
+// root when ConfigMCTS.enable_dirichlet_noise is set (:113-116): a fresh
+// np.random.dirichlet(alpha * ones(k)) from the game's MT19937 stream per
+// root selection (az_random.h), mixed into the priors as numpy computes
+// (1 - ratio) * priors + ratio * noise -- the first product in the priors'
+// dtype (float32, or float64 after the uniform branch: kPrior64), the rest
+// float64 -- and the UCB with that prior; np.argmax treats NaN as the maximum.
+struct SlotMt {  // the slot's MT19937 words, one at a time
+  const TreeDev* t;
+  int s;
+  __device__ uint32_t operator()() { return mt_next(*t, t->mt_stride, s); }
+};
+__device__ __forceinline__ double noisy_prior(const GameCfg& g, const Edge& e, double d) {
+  const double kept = (e.action & kPrior64) ? (1.0 - g.noise_ratio) * e.prior
+                                            : (double)((float)(1.0 - g.noise_ratio) * (float)e.prior);
+  return kept + g.noise_ratio * d;
+}
+// np.argmax order: NaN above every number, then value, then the lower index
+__device__ __forceinline__ bool argmax_before(double v, int i, double bv, int bi) {
+  if (bv != bv) return v != v && i < bi;
+  if (v != v) return true;
+  return v > bv || (v == bv && i < bi);
+}
+
 // Serial descent, one lane per game (used when the action space exceeds 64).
+template <bool NOISE>
 __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -309,14 +336,34 @@ __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t
     const double sq = t.powtab[sum];
     int best = 0;
     double best_v = 0.0;
-    for (int i = 0; i < cnt; ++i) {
-      const Edge e = E[first + i];
-      const double q = e.N ? e.W / (double)e.N : 0.0;
-      const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
-      const double ucb = q + u;
-      if (i == 0 || ucb > best_v) {
-        best = i;
-        best_v = ucb;
+    if (NOISE && depth == 0) {
+      double gam[kMaxActions], acc = 0.0;
+      SlotMt r{&t, s};
+      for (int i = 0; i < cnt; ++i) {
+        gam[i] = legacy_standard_gamma(r, g.noise_alpha);
+        acc = acc + gam[i];
+      }
+      const double invacc = 1 / acc;
+      for (int i = 0; i < cnt; ++i) {
+        const Edge e = E[first + i];
+        const double q = e.N ? e.W / (double)e.N : 0.0;
+        const double u = g.c_puct * noisy_prior(g, e, gam[i] * invacc) * sq / (double)(1 + e.N);
+        const double ucb = q + u;
+        if (i == 0 || argmax_before(ucb, i, best_v, best)) {
+          best = i;
+          best_v = ucb;
+        }
+      }
+    } else {
+      for (int i = 0; i < cnt; ++i) {
+        const Edge e = E[first + i];
+        const double q = e.N ? e.W / (double)e.N : 0.0;
+        const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
+        const double ucb = q + u;
+        if (i == 0 || ucb > best_v) {
+          best = i;
+          best_v = ucb;
+        }
       }
     }
     if (depth >= g.max_depth) {
@@ -325,7 +372,7 @@ __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t
     }
     const Edge& e = E[first + best];
     path[depth++] = first + best;
-    status = play_bb(g, mk, b, e.action);
+    status = play_bb(g, mk, b, e.action & kActMask);
     if (status < 0) {
       flag_error(t, kErrIllegal);
       return;
@@ -340,7 +387,7 @@ __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t
 // Lane j loads edge j (contiguous, one 32-byte record per lane), the group
 // sums N and takes the first-maximum UCB by shuffles -- the same float64
 // expressions as the serial loop, so the chosen edge is identical.
-template <int L>
+template <int L, bool NOISE>
 __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -409,26 +456,58 @@ __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, Tre
     AZ_SEL_PHASE(ph_load);
     double best_v = -INFINITY;
     int best = L;
-    if (mine) {
-      const double q = e.N ? e.W / (double)e.N : 0.0;
-      const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
-      best_v = q + u;
-      best = j;
-    }
+    if (NOISE && depth == 0) {
+      // the group walks the root's k gamma draws in order; its first lane
+      // (the slot's RNG owner) draws, each lane keeps its edge's
+      double acc = 0.0, gj = 0.0;
+      for (int k = 0; k < cnt; ++k) {  // group-uniform
+        double gv = 0.0;
+        if (j == 0) {
+          SlotMt r{&t, s};
+          gv = legacy_standard_gamma(r, g.noise_alpha);
+        }
+        gv = __shfl(gv, 0, L);
+        if (k == j) gj = gv;
+        acc = acc + gv;
+      }
+      const double invacc = 1 / acc;
+      if (mine) {
+        const double q = e.N ? e.W / (double)e.N : 0.0;
+        const double u = g.c_puct * noisy_prior(g, e, gj * invacc) * sq / (double)(1 + e.N);
+        best_v = q + u;
+        best = j;
+      }
 #pragma unroll
-    for (int off = L / 2; off > 0; off >>= 1) {
-      const double ov = __shfl_xor(best_v, off, L);
-      const int oj = __shfl_xor(best, off, L);
-      if (ov > best_v || (ov == best_v && oj < best)) {  // np.argmax: first maximum
-        best_v = ov;
-        best = oj;
+      for (int off = L / 2; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(best_v, off, L);
+        const int oj = __shfl_xor(best, off, L);
+        if (argmax_before(ov, oj, best_v, best)) {
+          best_v = ov;
+          best = oj;
+        }
+      }
+    } else {
+      if (mine) {
+        const double q = e.N ? e.W / (double)e.N : 0.0;
+        const double u = g.c_puct * e.prior * sq / (double)(1 + e.N);
+        best_v = q + u;
+        best = j;
+      }
+#pragma unroll
+      for (int off = L / 2; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(best_v, off, L);
+        const int oj = __shfl_xor(best, off, L);
+        if (ov > best_v || (ov == best_v && oj < best)) {  // np.argmax: first maximum
+          best_v = ov;
+          best = oj;
+        }
       }
     }
     if (depth >= g.max_depth) {
       if (j == 0) flag_error(t, kErrPath);
       return;
     }
-    const int action = __shfl(mine ? (int)e.action : 0, best, L);
+    const int action = __shfl(mine ? (int)(e.action & kActMask) : 0, best, L);
     const int child = __shfl(mine ? e.child : 0, best, L);
     const int child_n = __shfl(mine ? (int)e.child_n : 0, best, L);
     sum_next = __shfl(mine ? e.N : 0, best, L) - 1;
@@ -597,7 +676,7 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     e.N = 0;
     e.child = kNoChild;
     e.child_n = 0;
-    e.action = (int16_t)moves[k];
+    e.action = (int16_t)(moves[k] | (sum == 0.0f ? kPrior64 : 0));
     e.child_value = 0.f;
     E[first + k] = e;
   }
@@ -669,10 +748,11 @@ __global__ __launch_bounds__(kGameBlock) void play_kernel(GameCfg g, TreeDev t, 
     for (int i = 0; i < cnt; ++i)
       if (cdf[i] / last <= u) k = i + 1;
   }
-  const Edge chosen = E[first + k];
+  Edge chosen = E[first + k];
+  chosen.action &= kActMask;
   double* lp = t.last_policy + (size_t)s * g.A;
   for (int a = 0; a < g.A; ++a) lp[a] = 0.0;
-  for (int i = 0; i < cnt; ++i) lp[E[first + i].action] = pr[i];
+  for (int i = 0; i < cnt; ++i) lp[E[first + i].action & kActMask] = pr[i];
   const int64_t gid = t.game_id[s];
   const bool record = smp.n_games > 0 && gid >= smp.first_game && gid < smp.first_game + smp.n_games;
   if (record) {
@@ -883,12 +963,22 @@ static inline int game_blocks(int n) { return (n + kGameBlock - 1) / kGameBlock;
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s) {
   const int lanes = g.A <= 8 ? 8 : g.A <= 16 ? 16 : g.A <= 32 ? 32 : g.A <= 64 ? 64 : 1;
   const int blocks = (int)(((int64_t)g.slots * lanes + kGameBlock - 1) / kGameBlock);
+  if (g.noise) {  // the root-noise instantiations (the default path carries none of their code)
+    switch (lanes) {
+      case 8: select_group_kernel<8, true><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+      case 16: select_group_kernel<16, true><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+      case 32: select_group_kernel<32, true><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+      case 64: select_group_kernel<64, true><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+      default: select_kernel<true><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c); break;
+    }
+    return;
+  }
   switch (lanes) {
-    case 8: select_group_kernel<8><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
-    case 16: select_group_kernel<16><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
-    case 32: select_group_kernel<32><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
-    case 64: select_group_kernel<64><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
-    default: select_kernel<<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c); break;
+    case 8: select_group_kernel<8, false><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    case 16: select_group_kernel<16, false><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    case 32: select_group_kernel<32, false><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    case 64: select_group_kernel<64, false><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
+    default: select_kernel<false><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c); break;
   }
 }
 

@@ -95,14 +95,15 @@ class ConfigPath:
     model_success = "MODEL_SAVED_SUCCESSFULLY"
 
 
-def check_mcts_config():
-    """Refuse MCTS settings this engine does not implement instead of
-    silently ignoring them: Dirichlet root noise (mcts.py:70-85, used by
-    select at :113-116) is disabled in the reference (config.py:52) and not
-    built here (its numpy gamma/log/pow draws are outside the
-    parity scope)."""
-    if ConfigMCTS.enable_dirichlet_noise:
+def check_mcts_config(path: str = "tree"):
+    """Refuse MCTS settings an engine path does not implement instead of
+    silently ignoring them.  Dirichlet root noise (mcts.py:70-85, used by
+    select at :113-116; disabled in the reference, config.py:52) runs in
+    Connect-N self-play (path "selfplay": self_play.play / play_game), whose
+    games own their np.random streams on the device (MT19937 seeded like
+    self_play.py:45).  The single-tree MCTS API, the arena and chess draw
+    from the caller's np.random instead and refuse it."""
+    if ConfigMCTS.enable_dirichlet_noise and path != "selfplay":
         raise NotImplementedError(
-            "ConfigMCTS.enable_dirichlet_noise=True is not supported by the MI355X engine "
-            "(root Dirichlet noise, reference mcts.py:70-85, is disabled in the reference's config)")
-
+            "ConfigMCTS.enable_dirichlet_noise=True runs in Connect-N self-play (self_play.play / "
+            "play_game) on the MI355X engine; the MCTS tree API, the arena and chess do not draw it")

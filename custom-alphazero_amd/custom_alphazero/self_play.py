@@ -39,9 +39,17 @@ def alternating_rewards(result: int, length: int) -> np.ndarray:
 def play_game(process_id: int, all_possible_moves: List[Move], mcts_iterations: int, run_id: str,
               plays_inferences: Optional[Dict[str, Tuple[np.ndarray, float]]] = None,
               model=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray, MCTS]:
-    np.random.seed(int((process_id + 1) * time.time()) % (2 ** 32 - 1))
+    seed = int((process_id + 1) * time.time()) % (2 ** 32 - 1)
+    np.random.seed(seed)
     if model is None:
         model = best_saved_model(run_id)
+    if ConfigMCTS.enable_dirichlet_noise and ConfigGeneral.game != "chess":
+        # root noise draws from the game's own stream: the game runs on the
+        # batched engine as game 0 of a one-game batch seeded like this
+        # process (MT19937(seed): the same stream np.random.seed(seed) starts)
+        states, policies, rewards, records = play(run_id, plays_inferences, model=model, n_games=1,
+                                                  base_seed=seed, sims=mcts_iterations)
+        return states, policies, rewards, records[0]
     if ConfigGeneral.game == "chess":
         # one game on the chess engine, seeded like the reference's process seed
         seed = int(np.random.randint(0, 2 ** 31 - 1))
@@ -83,23 +91,26 @@ _ENGINES = {}
 _CACHE_OWNER = {"dict": None}
 
 
-def _batched_engine(model, n_slots):
-    check_mcts_config()
+def _batched_engine(model, n_slots, sims=None):
+    check_mcts_config("selfplay")
     c = ConfigConnectN
     synthetic = isinstance(model, SyntheticEvaluator)
-    key = (c.board_height, c.board_width, c.n, c.gravity, ConfigSelfPlay.mcts_iterations, n_slots,
+    sims = int(sims or ConfigSelfPlay.mcts_iterations)
+    noise = (bool(ConfigMCTS.enable_dirichlet_noise), ConfigMCTS.dirichlet_noise_value,
+             ConfigMCTS.dirichlet_noise_ratio)
+    key = (c.board_height, c.board_width, c.n, c.gravity, sims, n_slots,
            synthetic, ConfigMCTS.index_move_greedy, ConfigMCTS.exploration_constant,
-           ConfigModel.depth, ConfigSelfPlay.cache_log2, ConfigSelfPlay.lanes)
+           ConfigModel.depth, ConfigSelfPlay.cache_log2, ConfigSelfPlay.lanes, noise)
     eng = _ENGINES.get(key)
     if eng is None:
-        eng = az.Engine(c.board_height, c.board_width, c.n, c.gravity,
-                        ConfigSelfPlay.mcts_iterations, slots=n_slots,
+        eng = az.Engine(c.board_height, c.board_width, c.n, c.gravity, sims, slots=n_slots,
                         evaluator=az.EVAL_SYNTHETIC if synthetic else az.EVAL_NETWORK,
                         index_move_greedy=ConfigMCTS.index_move_greedy,
                         exploration_constant=ConfigMCTS.exploration_constant,
                         filters=ConfigModel.filters, depth=ConfigModel.depth,
                         value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon,
-                        cache_log2=ConfigSelfPlay.cache_log2, lanes=ConfigSelfPlay.lanes, compact=True)
+                        cache_log2=ConfigSelfPlay.cache_log2, lanes=ConfigSelfPlay.lanes, compact=True,
+                        dirichlet_noise=noise[0], dirichlet_alpha=noise[1], dirichlet_ratio=noise[2])
         eng.weights_key = None
         _ENGINES.clear()
         _ENGINES[key] = eng
@@ -118,7 +129,7 @@ _CHESS_ENGINES = {}
 
 
 def _chess_engine(model, n_slots, sims):
-    check_mcts_config()
+    check_mcts_config("chess")
     synthetic = isinstance(model, SyntheticEvaluator)
     key = (sims, n_slots, synthetic, ConfigMCTS.index_move_greedy, ConfigMCTS.exploration_constant,
            ConfigModel.depth, ConfigSelfPlay.chess_max_plies)
@@ -178,7 +189,7 @@ def play_chess(model, n_games: int, base_seed: int, first_game: int = 0, sims: O
 
 def play(run_id: str, plays_inferences: Optional[Dict[str, Tuple[np.ndarray, float]]] = None,
          model=None, n_games: Optional[int] = None, base_seed: Optional[int] = None,
-         first_game: int = 0):
+         first_game: int = 0, sims: Optional[int] = None):
     """Batched self-play.  Returns (states [M,H,W,4] f32, policies [M,A] f64,
     rewards [M] int64, records) concatenated in game order like the reference
     (self_play.py:112-118); with ConfigGeneral.game == "chess" the chess
@@ -192,7 +203,7 @@ def play(run_id: str, plays_inferences: Optional[Dict[str, Tuple[np.ndarray, flo
         base_seed = int(time.time()) % (2 ** 32 - 1)
     if ConfigGeneral.game == "chess":
         return play_chess(model, n_games, base_seed, first_game)
-    eng = _batched_engine(model, min(n_games, ConfigSelfPlay.concurrent_games))
+    eng = _batched_engine(model, min(n_games, ConfigSelfPlay.concurrent_games), sims)
     if ConfigSelfPlay.cache_log2 and (plays_inferences is None
                                       or plays_inferences is not _CACHE_OWNER["dict"]):
         eng.cache_clear()

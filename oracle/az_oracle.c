@@ -240,6 +240,59 @@ int orc_choice(const double* p, int n, double u) {
     return idx;
 }
 
+/* ------------------------------------------------ Dirichlet root noise */
+/* numpy legacy RandomState.dirichlet (mtrand.pyx) over legacy_standard_gamma
+ * (legacy-distributions.c), as np.random.dirichlet runs in the reference
+ * (mcts.py:70-85 with ConfigMCTS.enable_dirichlet_noise, config.py:52-54):
+ * libm log / pow through volatile pointers, exactly the calls numpy makes. */
+static double (*volatile orc_log_fn)(double) = log;
+
+static double orc_std_exponential(orc_mt* s) { return -orc_log_fn(1.0 - orc_mt_uniform(s)); }
+
+/* 0 < shape <= 1 (Johnk / Best rejection of the legacy sampler) */
+double orc_legacy_gamma(orc_mt* s, double shape) {
+    if (shape == 1.0) return orc_std_exponential(s);
+    for (;;) {
+        double U = orc_mt_uniform(s);
+        double V = orc_std_exponential(s);
+        if (U <= 1.0 - shape) {
+            double X = orc_pow_fn(U, 1. / shape);
+            if (X <= V) return X;
+        } else {
+            double Y = -orc_log_fn((1 - U) / shape);
+            double X = orc_pow_fn(1.0 - shape + shape * Y, 1. / shape);
+            if (X <= (V + Y)) return X;
+        }
+    }
+}
+
+/* dirichlet(alpha * ones(k)): gammas, acc, invacc = 1 / acc, d = g * invacc */
+void orc_dirichlet(orc_mt* s, double alpha, int k, double* out) {
+    double acc = 0.0;
+    for (int j = 0; j < k; ++j) {
+        out[j] = orc_legacy_gamma(s, alpha);
+        acc = acc + out[j];
+    }
+    double invacc = 1 / acc;
+    for (int j = 0; j < k; ++j) out[j] = out[j] * invacc;
+}
+
+/* test helper: n draws of dirichlet(alpha * ones(k)) from MT19937(seed) */
+void orc_dirichlet_draws(uint32_t seed, double alpha, int k, int n, double* out) {
+    orc_mt s;
+    orc_mt_seed(&s, seed);
+    for (int i = 0; i < n; ++i) orc_dirichlet(&s, alpha, k, out + (size_t)i * k);
+}
+
+/* the noise setting of the next orc_play_game calls (ConfigMCTS) */
+static int orc_noise_on = 0;
+static double orc_noise_alpha = 0.03, orc_noise_ratio = 0.25;
+void orc_set_noise(int on, double alpha, double ratio) {
+    orc_noise_on = on;
+    orc_noise_alpha = alpha;
+    orc_noise_ratio = ratio;
+}
+
 /* test helpers exposed for the numeric fixtures */
 double orc_seed_uniform(uint32_t seed, int k) {
     orc_mt s;
@@ -384,6 +437,7 @@ typedef struct {
 typedef struct {
     int first, count;  /* edges; count == 0 -> leaf */
     int status;        /* 0 ongoing, 1 win for the mover into it, 2 draw */
+    int prior64;       /* priors from normalize_probabilities' float64 uniform branch */
 } orc_node;
 
 typedef struct {
@@ -396,6 +450,7 @@ typedef struct {
     int root;
     int64_t expansions, terminal_visits, max_depth;
     int error;
+    orc_mt* rng;  /* the game's np.random stream (root noise draws) */
 } orc_tree;
 
 static int orc_new_node(orc_tree* t, const int8_t* board, int status) {
@@ -408,6 +463,7 @@ static int orc_new_node(orc_tree* t, const int8_t* board, int status) {
     t->nodes[id].first = 0;
     t->nodes[id].count = 0;
     t->nodes[id].status = status;
+    t->nodes[id].prior64 = 0;
     memcpy(t->boards + (size_t)id * (size_t)(t->g.H * t->g.W), board, (size_t)(t->g.H * t->g.W));
     return id;
 }
@@ -428,6 +484,34 @@ static int orc_best_edge(const orc_tree* t, const orc_node* node) {
     return best;
 }
 
+/* get_best_edge_with_noise (mcts.py:70-85): priors as the reference holds
+ * them (a float32 array, or float64 from the uniform branch), noisy =
+ * (1 - ratio) * priors (in the priors' dtype, numpy legacy promotion) +
+ * ratio * dirichlet (float64), UCB with the noisy prior, np.argmax (first
+ * maximum; a NaN counts as the maximum, the first NaN wins). */
+static int orc_best_edge_noise(orc_tree* t, const orc_node* node) {
+    const orc_edge* e = t->edges + node->first;
+    double d[ORC_MAX_ACTIONS];
+    orc_dirichlet(t->rng, orc_noise_alpha, node->count, d);
+    int64_t sum = 0;
+    for (int i = 0; i < node->count; ++i) sum += e[i].N;
+    double sq = orc_pow_half(sum);
+    int best = 0;
+    double best_v = 0.0;
+    for (int i = 0; i < node->count; ++i) {
+        double kept = node->prior64 ? (1 - orc_noise_ratio) * e[i].prior
+                                    : (double)((float)(1 - orc_noise_ratio) * (float)e[i].prior);
+        double noisy = kept + orc_noise_ratio * d[i];
+        double q = e[i].N ? e[i].W / (double)e[i].N : 0.0;
+        double u = t->g.c_puct * noisy * sq / (double)(1 + e[i].N);
+        double ucb = q + u;
+        if (i == 0) { best = 0; best_v = ucb; continue; }
+        if (best_v != best_v) continue;                       /* a NaN already holds the max */
+        if (ucb != ucb || ucb > best_v) { best = i; best_v = ucb; }
+    }
+    return best;
+}
+
 /* evaluate_and_expand: returns the leaf's value (side to move at the leaf) */
 static double orc_expand(orc_tree* t, int node_id) {
     const orc_game* g = &t->g;
@@ -439,7 +523,7 @@ static double orc_expand(orc_tree* t, int node_id) {
     double priors[ORC_MAX_ACTIONS];
     int nl = orc_mask_order(g, board, legal);
     for (int i = 0; i < nl; ++i) masked[i] = probs[legal[i]];
-    orc_normalize_f32(masked, nl, priors);
+    const int prior64 = orc_normalize_f32(masked, nl, priors);
     int nm = orc_moves(g, board, moves);
     if (t->n_edges + nm > t->cap_edges) {
         while (t->n_edges + nm > t->cap_edges) t->cap_edges = t->cap_edges ? 2 * t->cap_edges : 4096;
@@ -461,6 +545,7 @@ static double orc_expand(orc_tree* t, int node_id) {
     t->n_edges += nm;
     t->nodes[node_id].first = first;  /* node pointer may have moved */
     t->nodes[node_id].count = nm;
+    t->nodes[node_id].prior64 = prior64;
     t->expansions++;
     return (double)value;
 }
@@ -470,7 +555,9 @@ static void orc_search(orc_tree* t, int sims) {
     for (int s = 0; s < sims; ++s) {
         int depth = 0, node = t->root;
         while (t->nodes[node].count) {
-            int k = orc_best_edge(t, t->nodes + node);
+            /* select (mcts.py:111-120): the noisy choice at the current root */
+            int k = orc_noise_on && node == t->root ? orc_best_edge_noise(t, t->nodes + node)
+                                                    : orc_best_edge(t, t->nodes + node);
             int e = t->nodes[node].first + k;
             path[depth++] = e;
             node = t->edges[e].child;
@@ -523,6 +610,7 @@ int orc_play_game(int H, int W, int n, int gravity, int sims, uint32_t seed, int
     if (HW > ORC_MAX_CELLS || A > ORC_MAX_ACTIONS) return -1;
     orc_mt rng;
     orc_mt_seed(&rng, seed);
+    t.rng = &rng;
     int8_t board[ORC_MAX_CELLS];
     memset(board, 0, sizeof(board));
     t.root = orc_new_node(&t, board, 0);

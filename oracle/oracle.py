@@ -64,6 +64,10 @@ def lib():
         L.orc_table_misses.restype = ctypes.c_int64
         L.orc_table_misses.argtypes = [P]
         L.orc_play_game.restype = ctypes.c_int
+        L.orc_set_noise.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        L.orc_set_noise.restype = None
+        L.orc_dirichlet_draws.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_int, ctypes.c_int, P]
+        L.orc_dirichlet_draws.restype = None
         L.orc_play_game.argtypes = (
             [ctypes.c_int] * 5 + [ctypes.c_uint32, ctypes.c_int, P, EVAL_CB, P]
             + [P] * 10 + [ctypes.POINTER(GameOut)])
@@ -152,13 +156,31 @@ class EvalTable:
             self.handle = None
 
 
+def dirichlet_draws(seed, alpha, k, n):
+    """n draws of np.random.dirichlet(alpha * ones(k)) from a legacy stream
+    seeded `seed` (the C restatement, libm log/pow as numpy calls them)."""
+    out = np.zeros((n, k), np.float64)
+    lib().orc_dirichlet_draws(int(seed) & 0xFFFFFFFF, float(alpha), int(k), int(n), _ptr(out))
+    return out
+
+
 def play_game(height, width, n, gravity, sims, seed, evaluator="synth", table=None,
-              callback=None):
+              callback=None, noise=None):
     """One reference self-play game (self_play.py:37-82) on the C oracle.
 
     evaluator: "synth" (oracle/synth.py), "table" (EvalTable), or "callback"
     (python callable board[H,W] int8 -> (probs[A] f32, value f32)).
+    noise: None, or (alpha, ratio) -- ConfigMCTS.enable_dirichlet_noise with
+    dirichlet_noise_value / dirichlet_noise_ratio (mcts.py:70-85).
     """
+    lib().orc_set_noise(int(noise is not None), *(noise if noise is not None else (0.03, 0.25)))
+    try:
+        return _play_game(height, width, n, gravity, sims, seed, evaluator, table, callback)
+    finally:
+        lib().orc_set_noise(0, 0.03, 0.25)
+
+
+def _play_game(height, width, n, gravity, sims, seed, evaluator, table, callback):
     A = action_space(width, height, gravity)
     T = height * width
     o = {

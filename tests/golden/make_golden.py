@@ -115,8 +115,12 @@ def _counting_expand(self, node):
 ref_mcts.MCTS.evaluate_and_expand = _counting_expand
 
 
-def run_games(name, height, width, n, gravity, sims, seeds):
+def run_games(name, height, width, n, gravity, sims, seeds, noise=False):
+    """noise: ConfigMCTS.enable_dirichlet_noise = True for these games (the
+    reference's root Dirichlet noise, mcts.py:70-85, drawn from the game's
+    np.random stream at every root selection)."""
     set_game(height, width, n, gravity)
+    ref_config.ConfigMCTS.enable_dirichlet_noise = bool(noise)
     all_moves = Board.get_all_possible_moves()
     A = len(all_moves)
     rec = {k: [] for k in (
@@ -177,6 +181,9 @@ def run_games(name, height, width, n, gravity, sims, seeds):
         state=np.concatenate(rec["state"]),
         reward=np.concatenate(rec["reward"]),
     )
+    out.update(dirichlet_noise=bool(noise), dirichlet_alpha=ref_config.ConfigMCTS.dirichlet_noise_value,
+               dirichlet_ratio=ref_config.ConfigMCTS.dirichlet_noise_ratio)
+    ref_config.ConfigMCTS.enable_dirichlet_noise = False
     np.savez_compressed(os.path.join(OUT, f"mcts_{name}.npz"), **out)
     print(f"mcts_{name}: {len(seeds)} games, plies={out['game_len'].tolist()}, "
           f"expansions={out['expansions'].tolist()}")
@@ -287,4 +294,10 @@ if __name__ == "__main__":
         run_games("nograv_5x5_s25", 5, 5, 4, False, 25, [500, 501, 502, 503])
         run_games("c4_s1", 6, 7, 4, True, 1, [10, 11])
         run_games("c4_s2", 6, 7, 4, True, 2, [20, 21])
+    if "mcts" in which or "noise" in which:
+        # Dirichlet root noise on (config.py:52-54 with enable_dirichlet_noise = True)
+        run_games("c4_s25_noise", 6, 7, 4, True, 25, list(range(30, 38)), noise=True)
+        run_games("c4_s100_noise", 6, 7, 4, True, 100, [130, 131, 132], noise=True)
+        run_games("c5_9x9_s50_noise", 9, 9, 5, True, 50, [930, 931], noise=True)
+        run_games("nograv_5x5_s25_noise", 5, 5, 4, False, 25, [530, 531, 532], noise=True)
     print(f"done in {time.time() - t0:.1f}s")

@@ -115,12 +115,16 @@ def test_reference_weight_hash_matches_legacy_numpy(golden_dir):
     assert content_hash([w2[n] for n in names]) != content_hash([w[n] for n in names])
 
 
-def test_dirichlet_noise_is_refused():
+def test_dirichlet_noise_paths():
+    """Root Dirichlet noise (mcts.py:70-85) runs in Connect-N self-play; the
+    single-tree MCTS API, the arena and chess refuse it rather than ignore it."""
     from custom_alphazero.config import ConfigMCTS, check_mcts_config
     check_mcts_config()
     ConfigMCTS.enable_dirichlet_noise = True
     try:
-        with pytest.raises(NotImplementedError):
-            check_mcts_config()
+        check_mcts_config("selfplay")
+        for path in ("tree", "chess", "arena"):
+            with pytest.raises(NotImplementedError):
+                check_mcts_config(path)
     finally:
         ConfigMCTS.enable_dirichlet_noise = False

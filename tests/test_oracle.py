@@ -120,6 +120,40 @@ def test_oracle_selfplay_matches_reference(golden, name):
         check_game_against_golden(z, g, got)
 
 
+NOISE_FIXTURES = ["c4_s25_noise", "c4_s100_noise", "c5_9x9_s50_noise", "nograv_5x5_s25_noise"]
+
+
+def noise_of(z):
+    return (float(z["dirichlet_alpha"]), float(z["dirichlet_ratio"])) if bool(z["dirichlet_noise"]) else None
+
+
+@pytest.mark.parametrize("name", NOISE_FIXTURES)
+def test_oracle_selfplay_with_dirichlet_noise_matches_reference(golden, name):
+    """the reference's root Dirichlet noise (mcts.py:70-85,
+    enable_dirichlet_noise = True) -- every root selection draws
+    np.random.dirichlet(0.03 * ones(k)) from the game's stream and mixes it
+    into the priors at 0.25 -- restated in the C oracle; visit counts, W,
+    priors, moves and policies bitwise the reference's (fixtures generated by
+    the reference itself, tests/golden/make_golden.py)."""
+    z = golden("mcts_" + name)
+    assert bool(z["dirichlet_noise"])
+    H, W, n, grav, S = (int(z[k]) for k in ("height", "width", "n", "gravity", "sims"))
+    for g, seed in enumerate(z["seed"]):
+        got = oracle.play_game(H, W, n, bool(grav), S, int(seed), noise=noise_of(z))
+        check_game_against_golden(z, g, got)
+
+
+def test_oracle_dirichlet_is_numpys_legacy_sampler():
+    """The oracle's Dirichlet restatement draws exactly what numpy's legacy
+    RandomState.dirichlet draws from the same seed (this interpreter's numpy
+    keeps the legacy sampler for RandomState; both call libm log / pow)."""
+    for seed, k, alpha in ((0, 7, 0.03), (5, 7, 0.03), (99, 9, 0.03), (7, 25, 0.03), (3, 4, 0.5), (11, 3, 1.0)):
+        rs = np.random.RandomState(seed)
+        ref = np.stack([rs.dirichlet(np.ones(k) * alpha) for _ in range(200)])
+        got = oracle.dirichlet_draws(seed, alpha, k, 200)
+        np.testing.assert_array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
 def test_table_evaluator_replays_synthetic():
     """The replay (table) evaluator gives the same game as the one it recorded."""
     rec = []
