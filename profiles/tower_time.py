@@ -20,7 +20,7 @@ def main():
     spec = weight_spec(6, 7, 7, depth=4)
     w = init_weights(spec, seed=0, randomize_bn=True)
     out = []
-    for nb in (673, 1346, 4096):
+    for nb in [int(v) for v in os.environ.get("AZ_BATCHES", "673,1346,4096").split(",")]:
         xx = oracle.full_state(rng.randint(-1, 2, (nb, 6, 7)).astype(np.int8))
         eng = az.Engine(6, 7, 4, True, 25, slots=max(nb, 2048), evaluator=az.EVAL_NETWORK, depth=4,
                         conv_algo=algo)
