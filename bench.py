@@ -259,9 +259,14 @@ def _reduce(values, op, world, args, dev):
     return t.tolist()
 
 
-def conv_kernel_name(conv_algo, chess=False):
+def conv_kernel_name(conv_algo, chess=False, tower=False):
     if conv_algo == 1:
         return "conv3x3_mfma (fp32 MFMA implicit-GEMM 3x3 conv, fused BN/ReLU/residual), one launch per conv"
+    if conv_algo == 0 and chess and tower:
+        return ("tower16_kernel, input-row form (one launch per lane-simulation: the 118-plane stem conv and the "
+                "residual tower's 8 3x3 convs as implicit GEMMs on the 16x16x32 fp16 MFMA -- fp32-accurate, both "
+                "operands as two fp16 terms, 3 products per k-step -- activations double-buffered in LDS, 1x1 "
+                "projection residuals, head 1x1 convs; the 1880-logit dense heads follow in their own kernels)")
     if conv_algo == 0 and not chess:
         return ("tower16_kernel (the whole forward in one launch per lane-simulation: the stem and the "
                 "residual tower's 8 3x3 convs as implicit GEMMs on the 16x16x32 fp16 MFMA -- fp32-accurate, both operands "
@@ -273,7 +278,7 @@ def conv_kernel_name(conv_algo, chess=False):
 
 
 def conv_roofline(args, conv_algo, per_forward, boards_per_launch, avg_ms, busy_ms, boards_total, launches,
-                  direct_flop_per_board, issued_per_board, pmc_file, pmc_key, chess=False):
+                  direct_flop_per_board, issued_per_board, pmc_file, pmc_key, chess=False, tower=False):
     """roofline of the dominant kernel (the residual tower's convs: the whole
     forward in one tower16_kernel launch, or one conv per launch).
     achieved = ALGORITHMIC FLOP per launch -- the direct convolution's
@@ -313,7 +318,7 @@ def conv_roofline(args, conv_algo, per_forward, boards_per_launch, avg_ms, busy_
                         f"{e['boards_per_launch']} boards per launch (x live boards/launch here); mfma_busy = "
                         f"SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) of that launch")
     return {
-        "kernel": conv_kernel_name(conv_algo, chess),
+        "kernel": conv_kernel_name(conv_algo, chess, tower),
         "bound": "mfma",
         "achieved": round(achieved, 2),
         "peak": peak,
@@ -442,15 +447,21 @@ def chess_main(args):
     (elapsed,) = _reduce([elapsed], dist.ReduceOp.MAX if world > 1 else None, world, args, dev)
     F, HW = 128, 64
     direct_flop = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
-    issued = 3 * direct_flop if args.conv_algo == 0 else direct_flop  # fp16x2: 3 products per MAC
+    issued = 3 * direct_flop if args.conv_algo != 1 else direct_flop  # fp16x2: 3 products per MAC
     launches = st1["conv_launches"]
-    per_forward = 2 * args.depth
+    tower = st1.get("issued_flop_per_board", 0) > 0  # the one-launch tower (input-row form)
+    per_forward = 1 if tower else 2 * args.depth
+    if tower:  # the launch also runs the stem conv (118 planes -> F, 3x3): its direct FLOP count too;
+        # issued: the tower's own count (stem over the padded planes in, the slot plan's skipped taps out)
+        direct_flop += HW * 2 * 118 * 9 * F
+        issued = st1["issued_flop_per_board"]
     boards_per_launch = local_evals / max(launches / per_forward, 1)
     avg_ms = st1["conv_ms"] / max(launches, 1)
     roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, avg_ms, st1["conv_busy_ms"],
                          local_evals, launches, direct_flop, issued,
                          os.path.join(REPO, "profiles", "r4", "pmc_chess.json"),
-                         "f16x2" if args.conv_algo != 1 else "direct", chess=True)
+                         ("tower16_rows" if tower else "f16x2") if args.conv_algo != 1 else "direct", chess=True,
+                         tower=tower)
     if rank == 0:
         line = {
             "metric": f"MCTS node-expansions/s (Chess, {args.sims} sims/move)",

@@ -839,8 +839,8 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
     return az::fail_abi(AZ_E_INVALID, "unknown evaluator");
   if (c.evaluator == AZ_EVAL_NETWORK && c.filters != 128)
     return az::fail_abi(AZ_E_INVALID, "network evaluator supports filters == 128 (ConfigModel.filters)");
-  if (c.conv_algo != AZ_CONV_F16X2 && c.conv_algo != AZ_CONV_DIRECT)
-    return az::fail_abi(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2 or AZ_CONV_DIRECT");
+  if (c.conv_algo != AZ_CONV_F16X2 && c.conv_algo != AZ_CONV_DIRECT && c.conv_algo != AZ_CONV_F16X2_LAYERS)
+    return az::fail_abi(AZ_E_INVALID, "conv_algo must be AZ_CONV_F16X2, AZ_CONV_DIRECT or AZ_CONV_F16X2_LAYERS");
   if (c.max_plies < 0 || c.arena_edges < 0 || c.depth < 0 || c.value_hidden < 1)
     return az::fail_abi(AZ_E_INVALID, "negative bound");
   if ((int64_t)c.slots * 64 * 512 >= (1ll << 31))
@@ -921,7 +921,12 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
   e->net.depth = c.depth;
   // depth 0: the fp16x2 chain runs the heads' 1x1 convs inside the last
   // block's conv2, so a tower without blocks takes the fp32 MFMA path
-  e->net.algo = c.depth == 0 ? AZ_CONV_DIRECT : c.conv_algo;
+  e->net.algo = c.depth == 0 ? AZ_CONV_DIRECT : (c.conv_algo == AZ_CONV_F16X2_LAYERS ? AZ_CONV_F16X2 : c.conv_algo);
+  // AZ_CONV_F16X2: the stem, the tower and the heads' 1x1 convs in one launch
+  // (tower16_kernel's input-row form) when the network fits it, else the
+  // per-layer conv16 chain (AZ_CONV_F16X2_LAYERS forces the chain)
+  e->net.use_tower = c.conv_algo == AZ_CONV_F16X2 && c.depth >= 1 && c.depth <= az::kTowerMaxDepth;
+  e->net.board_h = e->net.board_w = 8;
   e->net.hidden = c.value_hidden;
   e->net.err = t.stats + az::kStatErrors;
   if (c.lanes < 0) return cleanup(az::fail_abi(AZ_E_INVALID, "lanes must be >= 0"));
@@ -1051,6 +1056,7 @@ int az_chess_stats(az_chess_engine* e, az_stats* st) {
   st->plies = (int64_t)h[az::kStatPlies];
   st->errors = (int64_t)h[az::kStatErrors];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
+  st->issued_flop_per_board = e->net.use_tower && e->net.tower ? e->net.issued_flop_per_board : 0.0;
   st->active_slots = std::count_if(gid.begin(), gid.end(), [](int64_t v) { return v >= 0; });
   // conv-busy time = union of the timed conv intervals over all lanes
   std::vector<az::ConvTimer*> timers = {&e->timer};

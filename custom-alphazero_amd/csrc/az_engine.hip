@@ -461,12 +461,14 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
   int rc;
   if ((rc = fold_unit(m, "stem", 3, in_ch, F, eps, w, b))) return rc;
   // host copies for the one-launch tower (tower16_kernel): its stem pack and the small-weight blob
-  const bool tower = in_ch == 4 && net.use_tower;
+  // (in_ch > 4, chess: the input-row form, whose stem is the conv16 pack stem_k)
+  const bool tower = net.use_tower && (in_ch == 4 || HW == 64);
+  const bool rows_tower = tower && in_ch > 4;
   std::vector<float> tb_b1, tb_b2, tb_stemb(b.begin(), b.end()), tb_pcw, tb_vcw, tb_hb(4, 0.f), tb_pdw, tb_pdb,
       tb_v1w, tb_v1b, tb_v2w;
   uint16_t* stem16 = nullptr;
   float stem_s = 1.f;
-  if (tower) {
+  if (tower && !rows_tower) {
     const int e = conv16_prescale(w.data(), w.size(), nullptr, 0);
     std::vector<uint16_t> pack;
     tower16_stem_pack(w.data(), e, pack);
@@ -586,6 +588,8 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     }
     tn.stem16 = reinterpret_cast<const uint4*>(stem16);
     tn.stem_s = stem_s;
+    tn.stem_k = rows_tower ? reinterpret_cast<const uint4*>(net.stem_k) : nullptr;
+    tn.stem_ks = net.stem_scale;
     // the small-weight blob (TowerNet), every part padded to a multiple of 4 floats
     std::vector<float> blob;
     auto put = [&](const std::vector<float>& v) {
@@ -609,7 +613,8 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     // the layout: 128/96-row tiles double-buffered, else one tile in place;
     // per layout the largest staging that fits: the whole blob, then without
     // wv1, then without wpd too (those then read from L2)
-    const int prefix[3] = {tn.blob_floats, tn.off_wv1, tn.off_wpd};
+    // (the input-row form runs no dense head: the biases and 1x1 head weights only)
+    const int prefix[3] = {rows_tower ? tn.off_bpd : tn.blob_floats, tn.off_wv1, tn.off_wpd};
     struct Layout {
       int tr;
       bool db;
@@ -617,14 +622,15 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     bool found = false;
     for (int li = 0; li < 2 && !found; ++li) {
       const Layout L = layouts[li];
-      if (!L.tr || !tower16_heads_fit(HW, L.tr, A, net.hidden, L.db)) continue;
-      for (int i = 0; i < 3 && !found; ++i)
+      if (!L.tr || (!rows_tower && !tower16_heads_fit(HW, L.tr, A, net.hidden, L.db))) continue;
+      if (rows_tower && (L.tr != 128 || tower16_lds_bytes(HW, L.tr, prefix[0], L.db) > kTowerLdsMax)) continue;
+      for (int i = 0; i < (rows_tower ? 1 : 3) && !found; ++i)
         if (tower16_lds_bytes(HW, L.tr, prefix[i], L.db) <= kTowerLdsMax) {
           tn.tile_rows = L.tr;
           tn.dbuf = L.db;
           tn.staged_floats = prefix[i];
-          tn.wv1_lds = i == 0;
-          tn.wpd_lds = i <= 1;
+          tn.wv1_lds = i == 0 && !rows_tower;
+          tn.wpd_lds = i <= 1 && !rows_tower;
           found = true;
         }
     }
@@ -634,7 +640,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       net.ready = true;
       return 0;
     }
-    tn.wv1_xtile = tn.dbuf && !tn.wv1_lds && tower16_wv1_xtile_fits(HW, tn.tile_rows, net.hidden);
+    tn.wv1_xtile = !rows_tower && tn.dbuf && !tn.wv1_lds && tower16_wv1_xtile_fits(HW, tn.tile_rows, net.hidden);
     // the slot plan: border blocks skip the taps past their edge
     // (az_config.tower_natural_order: natural order, no skips -- bitwise the same outputs)
     {
@@ -670,7 +676,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     net.tower_staged = tn.staged_floats;
     net.tower_dbuf = tn.dbuf != 0;
     net.tower_rows = tn.tile_rows;
-    net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip);
+    net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip, rows_tower);
   }
   net.ready = true;
   return 0;

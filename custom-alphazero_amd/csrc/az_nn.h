@@ -19,6 +19,8 @@ struct TowerNet {
   float s2[kTowerMaxDepth];
   const uint4* stem16;               // the stem as 2 k-steps over k = tap*4 + plane (tower16_stem_pack)
   float stem_s;                      // its 2^(e - 12)
+  const uint4* stem_k;               // input-row stem (chess, 118 planes padded to F): a conv16 pack, 36 k-steps
+  float stem_ks;                     // its 2^(e - 12)
   // small weights, one contiguous float blob; a prefix of it is copied into
   // LDS at kernel start (offsets in floats, each a multiple of 4): folded
   // biases b1[depth][F], b2[depth][F] (+ the residual's), stem bias [F]; head
@@ -46,7 +48,7 @@ struct TowerNet {
 void tower16_slot_plan(int H, int W, int tile_rows, std::vector<int>& slot_pix, int skip[2]);
 // MFMA FLOP tower16_kernel issues per board: a full tile's stem + 2 depth
 // convs (+ the 1x1 projection k-steps) less the plan's skipped taps, / boards
-double tower16_issued_flop_per_board(int HW, int tile_rows, int depth, const int skip[2]);
+double tower16_issued_flop_per_board(int HW, int tile_rows, int depth, const int skip[2], bool rows_stem = false);
 // 0 when the board does not fit a tile (HW > 128); else 96 or 128 (big:
 // 256-row tiles, 16 M blocks, each wave 128 rows x 32 channels -- half the
 // weight stream per FLOP; single tile in place, the LDS holds no second)
@@ -67,6 +69,15 @@ void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out);
 void launch_tower16(const TowerNet* net, int tile_rows, int staged_floats, bool dbuf, const Board* boards, const float4* x, const int* count,
                     int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
                     hipStream_t s);
+// the input-row form (chess): rows [n][HW] of 512 B split16 (t0 of F
+// channels, t1 x 2^12; az_nn's store_act4) -> the stem, the residual tower
+// and the heads' 1x1 convs; per pixel float4 (relu(p0), relu(p1), relu(v), 0)
+// into feat [n * HW] for the dense heads' kernels (policy_dense_kernel,
+// heads_tail_kernel).  first_chunk: input channel chunks (32) below it are
+// known zero and skipped (chess self-play: planes 0-63)
+void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged_floats, bool dbuf, const void* rows,
+                         int first_chunk, const int* count, int n_max, int H, int W, float4* feat,
+                         unsigned long long* err, hipStream_t s);
 
 // Folded (BatchNorm-in) weights resident in HBM, packed for the kernels (not
 // Keras layouts).  AZ_CONV_F16X2 (default): conv16_kernel packs (fp16 term

@@ -663,6 +663,22 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
     if (timer) timer->end(s, 1);
     return;
   }
+  if (f16 && net.use_tower && net.in_ch > 4 && net.tower && HW == 64 && A > kMaxActions) {
+    // chess: the stem, the tower and the heads' 1x1 convs in one launch
+    // (features into act_a), then the dense heads as below
+    if (timer) timer->begin(s);
+    launch_tower16_rows(net.tower, net.tower_rows, net.tower_staged, net.tower_dbuf, x, stem_first_chunk, count,
+                        n_max, H, W, static_cast<float4*>(act_a), net.err, s);
+    if (timer) timer->end(s, 1);
+    HeadWeights hw{net.pc_w, net.pc_b, net.vc_w, net.vc_b, net.pd_w,
+                   net.pd_b, net.v1_w, net.v1_b, net.v2_w, net.v2_b};
+    const float4* feat = static_cast<const float4*>(act_a);
+    policy_dense_kernel<128><<<dim3((A + 63) / 64, (n_max + 31) / 32), 256, 0, s>>>(feat, net.pd_wt, net.pd_b, count,
+                                                                                 n_max, HW, A, probs);
+    heads_tail_kernel<<<std::min(n_max, 2048), kTailThreads, 0, s>>>(feat, hw, count, n_max, HW, A, net.hidden, probs,
+                                                                     values);
+    return;
+  }
   Conv16Args ca;
   ca.count = count;
   ca.n_max = n_max;

@@ -487,17 +487,22 @@ __device__ __forceinline__ void dma_to_lds(uint4* dst, const float* src, int n_u
   }
 }
 
-// MBT 16-row M blocks per tile (8: 128 rows, 6: 96); NWM wave groups over M:
-// 2 = 8 waves, two per SIMD, each MBT/2 blocks; 1 = 4 waves, one per SIMD,
-// each all MBT blocks of its 32 output channels
-template <int MBT, int NWM>
+// MBT 16-row M blocks per tile (8: 128 rows, 6: 96); NWM wave groups over M
+// (2 = 8 waves, two per SIMD, each MBT/2 blocks).  ROWS: the input-row form
+// (chess, launch_tower16_rows): the stem is a 3x3 conv over F (padded) input
+// channels read from split16 rows, and the kernel ends with the heads' 1x1
+// convs (per pixel float4 features into feat) -- the dense heads (1880
+// logits) run in their own kernels
+template <int MBT, int NWM, bool ROWS>
 __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet* __restrict__ net,
                                                                const Board* __restrict__ boards,
                                                                const float4* __restrict__ x,
+                                                               const uint4* __restrict__ rows,
                                                                const int* __restrict__ count, int n_static,
                                                                int H, int W, int A, int bpw,
                                                                float* __restrict__ probs,
                                                                float* __restrict__ values,
+                                                               float4* __restrict__ feat,
                                                                unsigned long long* __restrict__ err) {
   constexpr int MBW = MBT / NWM;  // M blocks per wave
   constexpr int TR = 16 * MBT;    // tile rows
@@ -560,6 +565,35 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   float4 yv[2 * MBW];
 
   // ---------------------------------------------------------------- stem
+  if constexpr (ROWS) {
+    // input rows -> H's tile (512 B split16 per pixel: t0 copied, t1 from the
+    // rows' x 2^12 scale to the tower's unscaled term), then the stem conv
+    // (F -> F over the padded input channels) as a K loop into X
+    const uint4* src = rows + (size_t)b0 * HW * 32;
+    char* dst = reinterpret_cast<char*>(bufH);
+#pragma unroll 4
+    for (int i = tid; i < live * 32; i += NT) {
+      uint4 v = gld(src + i);
+      if ((i & 31) >= 16) {
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const az_h2 h = __builtin_bit_cast(az_h2, w[k]);
+          w[k] = pk_f16((float)h[0] * 0x1p-12f, (float)h[1] * 0x1p-12f);
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *reinterpret_cast<uint4*>(dst + (i >> 5) * kPitch + (i & 31) * 16) = v;
+    }
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
+    __syncthreads();                // ... every wave's, and the input rows
+    k_loop<MBW, 0>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, mh, skw);
+    if (!dbuf) __syncthreads();  // in place: every wave is done reading the input before X overwrites it
+  } else {
   // conv3x3 4 -> F + folded BN + ReLU on the MFMA: k = tap*4 + plane (36 of
   // two 32-wide k-steps), the im2col operand built in registers from the
   // boards' bits (one-hot planes [empty, own, opp, 1], board.py:83-98: exact
@@ -637,9 +671,10 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
   T16_STAMP(58);
   __syncthreads();                // ... and every wave's: the blob is readable
+  }  // !ROWS
   T16_STAMP(1);
   {
-    const float osc = T.stem_s;
+    const float osc = ROWS ? T.stem_ks : T.stem_s;
     const float* bb = blob + T.off_stemb;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
@@ -816,6 +851,24 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   if (T.wv1_xtile) __builtin_amdgcn_s_waitcnt(0);  // this wave's wv1 DMA pieces have landed ...
   __syncthreads();  // ... the partials are complete; no activation row is read any more
   T16_STAMP(18);
+  if constexpr (ROWS) {
+    // per pixel (policy 0, policy 1, value) = 16 partials in order + folded
+    // bias, ReLU: the dense heads read them (az_nn.hip policy_dense_kernel,
+    // heads_tail_kernel)
+    const float* hbias = blob + T.off_hb;
+    const float bpc0 = hbias[0], bpc1 = hbias[1], bvc0 = hbias[2];
+    for (int rr = tid; rr < live; rr += NT) {
+      const float* q = red + rr * 48;
+      float t[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) t[k] += q[3 * j + k];
+      feat[(size_t)b0 * HW + rr] =
+          make_float4(fmaxf(t[0] + bpc0, 0.f), fmaxf(t[1] + bpc1, 0.f), fmaxf(t[2] + bvc0, 0.f), 0.f);
+    }
+    return;
+  }
 
   // head scratch (H's tile, or the in-place tile past the partials): the
   // flattened features per board (Keras Flatten of NHWC: [p][c]) pf [bpw][2HW]
@@ -1142,7 +1195,7 @@ void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int ski
   skip[0] = skip[1] = 0;
 }
 
-double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2]) {
+double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2], bool rows_stem) {
   const int bpw = tower16_boards_per_tile(HW, tr);
   if (!bpw) return 0;
   const int nwm = 2, mbw = tr / 16 / nwm;  // blocks per wave
@@ -1151,7 +1204,9 @@ double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2
   for (int h = 0; h < nwm; ++h) {
     int skipped = 0;  // block-taps one wave of this M group skips per conv
     for (int t = 0; t < 9; ++t) skipped += __builtin_popcount((skip[h] >> (2 * t)) & 3);
-    const double per_wave = 2.0 * mbw + depth * ((4.0 + 36) * mbw + 36.0 * mbw - 2.0 * 4 * skipped);
+    // stem: 2 k-steps (4 one-hot planes), or a 36-k-step conv over the input rows (its skips too)
+    const double stem = rows_stem ? 36.0 * mbw - 4.0 * skipped : 2.0 * mbw;
+    const double per_wave = stem + depth * ((4.0 + 36) * mbw + 36.0 * mbw - 2.0 * 4 * skipped);
     steps += 4 * per_wave;
   }
   return steps * 6 * mfma / bpw;  // 2 N blocks x 3 products per block-k-step
@@ -1176,21 +1231,21 @@ void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
     }
 }
 
-template <int MBT, int NWM>
-static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x, const int* count,
-                       int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
-                       hipStream_t s) {
+template <int MBT, int NWM, bool ROWS>
+static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x,
+                       const uint4* rows, const int* count, int n_max, int H, int W, int A, float* probs,
+                       float* values, float4* feat, unsigned long long* err, hipStream_t s) {
   const int bpw = tower16_boards_per_tile(H * W, 16 * MBT);
   const int grid = (n_max + bpw - 1) / bpw;
   const size_t bytes = tower16_lds_bytes(H * W, 16 * MBT, staged, dbuf);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBT, NWM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBT, NWM, ROWS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTowerLdsMax);
     attr = true;
   }
-  tower16_kernel<MBT, NWM><<<grid, NWM * 256, bytes, s>>>(net, boards, x, count, n_max, H, W, A, bpw, probs, values,
-                                                     err);
+  tower16_kernel<MBT, NWM, ROWS><<<grid, NWM * 256, bytes, s>>>(net, boards, x, rows, count, n_max, H, W, A, bpw,
+                                                                probs, values, feat, err);
 }
 
 void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, const Board* boards, const float4* x,
@@ -1198,9 +1253,20 @@ void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, c
                     unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
   if (tile_rows == 96)
-    launch_mbw<6, 2>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<6, 2, false>(net, staged, dbuf, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr,
+                            err, s);
   else
-    launch_mbw<8, 2>(net, staged, dbuf, boards, x, count, n_max, H, W, A, probs, values, err, s);
+    launch_mbw<8, 2, false>(net, staged, dbuf, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr,
+                            err, s);
+}
+
+void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged, bool dbuf, const void* rows,
+                         int first_chunk, const int* count, int n_max, int H, int W, float4* feat,
+                         unsigned long long* err, hipStream_t s) {
+  (void)first_chunk;  // every chunk is computed (the zero ones add exact zeros)
+  if (n_max <= 0 || tile_rows != 128) return;
+  launch_mbw<8, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
+                         0, nullptr, nullptr, feat, err, s);
 }
 
 }  // namespace az

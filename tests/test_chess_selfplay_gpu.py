@@ -86,16 +86,17 @@ def _states(n, seed):
     return x.astype(np.float32)
 
 
-@pytest.mark.parametrize("algo", ["f16x2", "direct"])
+@pytest.mark.parametrize("algo", ["f16x2", "direct", "f16x2_layers"])
 def test_chess_forward_matches_keras_restatement(chess_net, algo):
-    """Both tower/stem algorithms (AZ_CONV_F16X2, AZ_CONV_DIRECT) against the
-    float64 restatement, and batch invariant."""
+    """Every algorithm -- the one-launch tower (AZ_CONV_F16X2: stem, tower and
+    head 1x1 convs in one kernel), fp32 direct, the per-layer fp16x2 chain --
+    against the float64 restatement, and batch invariant."""
     import keras_ref
     from custom_alphazero import engine as az
     eng, w = chess_net
-    if algo == "direct":
+    if algo != "f16x2":
         eng = _engine(mcts_iterations=16, slots=64, evaluator=az.EVAL_NETWORK, max_plies=12,
-                      conv_algo=az.CONV_DIRECT)
+                      conv_algo=az.CONV_DIRECT if algo == "direct" else az.CONV_F16X2_LAYERS)
         eng.set_weights(w.items())
     x = _states(96, seed=21)  # more than one engine chunk (64 slots)
     probs, values = eng.forward(x)
@@ -105,8 +106,66 @@ def test_chess_forward_matches_keras_restatement(chess_net, algo):
     # batch invariance (the replay parity below depends on it)
     p1, v1 = eng.forward(x[5:6])
     assert np.array_equal(p1[0], probs[5]) and v1[0] == values[5]
-    if algo == "direct":
+    if algo != "f16x2":
         eng.close()
+
+
+def test_chess_tower_reports_its_launch():
+    """The chess forward is one tower launch per simulation (plus the dense
+    heads): the conv timer sees one launch per forward, and the engine
+    reports the tower's issued MFMA FLOP per board."""
+    from custom_alphazero import engine as az
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    eng = _engine(mcts_iterations=8, slots=64, evaluator=az.EVAL_NETWORK, max_plies=4)
+    eng.set_weights(init_weights(weight_spec(8, 8, 1880, in_channels=118), seed=1).items())
+    eng.timer(True)
+    eng.forward(_states(64, seed=2))
+    st = eng.stats()
+    eng.timer(False)
+    assert st["conv_launches"] == 1 and st["issued_flop_per_board"] > 3 * 64 * 2 * 128 * 128 * 19 * 4 * 0.8
+    eng.close()
+
+
+def _chess_range_weights(S=2.0 ** 18):
+    """The same function as seed-7 weights with the stem's and block 0 conv1's
+    outputs S times larger (BN gamma/beta scaled; ReLU is positively
+    homogeneous) and the next convs' kernels divided by S: activations far
+    past the fp16 split range (|x| > 32752)."""
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    w = init_weights(weight_spec(8, 8, 1880, depth=2, in_channels=118), seed=7, randomize_bn=True)
+    for u in ("stem", "block0.conv1"):
+        w[u + ".gamma"] = (w[u + ".gamma"] * S).astype(np.float32)
+        w[u + ".beta"] = (w[u + ".beta"] * S).astype(np.float32)
+    for u in ("block0.conv1", "block0.res", "block0.conv2"):
+        w[u + ".kernel"] = (w[u + ".kernel"] / S).astype(np.float32)
+    return w
+
+
+def test_chess_activation_range_is_rescaled_not_failed():
+    """activations past the fp16 split range.  The chess
+    tower stores such a board's layer at a power-of-two scale: the forward
+    stays within NET_TOL of the float64 restatement and self-play completes
+    (the per-layer chain reports a device error instead)."""
+    import keras_ref
+    from custom_alphazero import engine as az
+    w = _chess_range_weights()
+    x = _states(40, seed=9)
+    stem = keras_ref.inner(np.asarray(x, np.float64), w, "stem", 1e-3)
+    assert stem.max() > 32752 * 4
+    rp, rv = keras_ref.forward(w, x, depth=2)
+    eng = _engine(mcts_iterations=8, slots=64, evaluator=az.EVAL_NETWORK, max_plies=6, depth=2)
+    eng.set_weights(w.items())
+    p, v = eng.forward(x)
+    assert np.abs(p - rp).max() < NET_TOL and np.abs(v - rv).max() < NET_TOL
+    st = eng.selfplay_run(0, 8, 5)
+    assert st["errors"] == 0 and st["games_done"] == 8
+    eng.close()
+    lay = _engine(mcts_iterations=8, slots=64, evaluator=az.EVAL_NETWORK, max_plies=6, depth=2,
+                  conv_algo=az.CONV_F16X2_LAYERS)
+    lay.set_weights(w.items())
+    with pytest.raises(az.AzError, match="activation-range"):
+        lay.selfplay_run(0, 8, 5)
+    lay.close()
 
 
 def test_chess_selfplay_network_replays_on_oracle(chess_net):
