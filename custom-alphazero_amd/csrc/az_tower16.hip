@@ -280,11 +280,18 @@ __device__ __forceinline__ bool store_layer(uint4* act, int HW, int W, const int
 template <int V>
 using IC = std::integral_constant<int, V>;
 
-template <int MBW, int R>
+// res_shift: the residual k-steps read the own rows res_shift rows from
+// `act` (conv2 of the double-buffered tower reads X's rows beside H's taps);
+// mid() runs between the residual k-steps and the taps.
+struct NoMid {
+  __device__ void operator()() const {}
+};
+template <int MBW, int R, typename Mid = NoMid>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
                                        t_f4 (&accr)[MBW][2], const int (&yx_)[MBW], int H, int W,
-                                       int zrow, int nq, int lane, int mh, int skw) {
+                                       int zrow, int nq, int lane, int mh, int skw, int res_shift = 0,
+                                       Mid mid = Mid{}) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
   // the two waves of a SIMD (M halves mh = 0, 1) take turns at priority 1,
   // one k-step each, so neither falls a whole phase behind the other (without:
@@ -333,7 +340,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   auto set_own = [&](int lo, int hi) {
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
-      if (mb >= lo && mb < hi) aaddr[mb] = (pix_ok(yx[mb]) ? r[mb] : zrow + (r[mb] & 7)) * kPitch + gq * 16;
+      if (mb >= lo && mb < hi) aaddr[mb] = (pix_ok(yx[mb]) ? r[mb] + res_shift : zrow + (r[mb] & 7)) * kPitch + gq * 16;
   };
   auto set_tap = [&](int t, int lo, int hi) {
     const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
@@ -434,6 +441,7 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     if (s + 1 == R) set_tap(0, 0, LAG ? MBW - 1 : RING);
     kstep(accr, bq[s % NB], s, s + 1 == R ? 0 : s + 1, IC<0>{}, IC<0>{}, s == 0);
   }
+  if (R) mid();
   // ---- 9 taps x 4 chunks; per tap the blocks it skips (skw: 2 bits per tap,
   // blocks 0 and 1 of the wave, from the slot plan) select one of three bodies
   auto tap = [&](int t, auto skc) {
@@ -493,7 +501,7 @@ __device__ __forceinline__ void dma_to_lds(uint4* dst, const float* src, int n_u
 // channels read from split16 rows, and the kernel ends with the heads' 1x1
 // convs (per pixel float4 features into feat) -- the dense heads (1880
 // logits) run in their own kernels
-template <int MBT, int NWM, bool ROWS>
+template <int MBT, int NWM, bool ROWS, bool DB>
 __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet* __restrict__ net,
                                                                const Board* __restrict__ boards,
                                                                const float4* __restrict__ x,
@@ -514,7 +522,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // the other tile, so a wave that finishes its K loop stores its outputs
   // while its SIMD partner still computes, and one barrier per layer
   // publishes them), else one tile updated in place behind a second barrier
-  const bool dbuf = T.dbuf;
+  constexpr bool dbuf = DB;
   uint4* const bufX = act;
   uint4* const bufH = dbuf ? act + (TR + kZeroRows) * (kPitch / 16) : act;
   const int zX = TR, zH = dbuf ? -kZeroRows : TR;  // each tile's zero rows, relative to it
@@ -561,7 +569,12 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // this wave's tap skips (2 bits per tap over its blocks 0 and 1)
   const int skw = T.skip[mh];
   const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
-  t_f4 acc[MBW][2], accr[MBW][2];
+  // double-buffered: one accumulator set (conv2 runs the block's 1x1
+  // projection residual first, from X, which nothing overwrites before its
+  // epilogue); in place: the residual is taken in conv1's phase (X is then
+  // overwritten by conv1's output) into a second set accr
+  t_f4 acc[MBW][2], accr_[MBW][2];
+  auto& accr = DB ? acc : accr_;
   float4 yv[2 * MBW];
 
   // ---------------------------------------------------------------- stem
@@ -704,11 +717,12 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
-        accr[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
+        accr_[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
       }
-    // conv1 (+ the projection residual into accr), input X
+    // conv1, input X (in place: + the projection residual into accr)
     T16_WSTAMP(d, 0);
-    k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr, yx, H, W, zX, nq, lane, mh, skw);
+    if constexpr (DB) k_loop<MBW, 0>(bufX, T.k1[d], nullptr, acc, acc, yx, H, W, zX, nq, lane, mh, skw);
+    else k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr_, yx, H, W, zX, nq, lane, mh, skw);
     T16_WSTAMP(d, 1);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
@@ -731,28 +745,41 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
     anyH = store_layer<MBW>(bufH, HW, W, yx, cq0, yv, sm, par, sm.sc[1], nbrd, err);
     par ^= 1;
-    // last block, double-buffered: X's tile is dead from here (conv2 reads H
-    // and the residual sits in accr), so the value dense's wv1 streams into
-    // it behind the heads' partials while conv2 runs (every wave a share)
-    if (dbuf && T.wv1_xtile && d + 1 == depth)
-      dma_to_lds<NT>(reinterpret_cast<uint4*>(reinterpret_cast<float*>(bufX) + TR * 48), T.blob + T.off_wv1,
-                     HW * J / 4, wave, lane);
     if (d < 4) T16_STAMP(3 + 4 * d);
     // the residual was accumulated at X's scale, conv2 runs at H's
-    if (anyX || anyH) {
+    auto rescale = [&]() {
+      if (anyX || anyH) {
 #pragma unroll
-      for (int mb = 0; mb < MBW; ++mb) {
-        const int e = (anyX ? sm.sc[0][yx[mb] >> 16] : 0) - (anyH ? sm.sc[1][yx[mb] >> 16] : 0);
-        if (e) {
-          const float f = ldexpf(1.f, e);
+        for (int mb = 0; mb < MBW; ++mb) {
+          const int e = (anyX ? sm.sc[0][yx[mb] >> 16] : 0) - (anyH ? sm.sc[1][yx[mb] >> 16] : 0);
+          if (e) {
+            const float f = ldexpf(1.f, e);
 #pragma unroll
-          for (int nb = 0; nb < 2; ++nb) accr[mb][nb] *= f;
+            for (int nb = 0; nb < 2; ++nb) accr[mb][nb] *= f;
+          }
         }
       }
-    }
-    // conv2 on H, on top of the residual
+    };
     T16_WSTAMP(d, 2);
-    k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, mh, skw);
+    if constexpr (DB) {
+      // conv2: the 1x1 projection residual from X's rows, then (once every
+      // wave is past them: X's tile is dead from here) the taps on H; the last
+      // block streams the value dense's wv1 into X's tile behind the heads'
+      // partials while the taps run (every wave a share).  The same sums in
+      // the same order as the in-place form: bitwise the same outputs
+      auto mid = [&]() {
+        rescale();
+        __syncthreads();
+        if (T.wv1_xtile && d + 1 == depth)
+          dma_to_lds<NT>(reinterpret_cast<uint4*>(reinterpret_cast<float*>(bufX) + TR * 48), T.blob + T.off_wv1,
+                         HW * J / 4, wave, lane);
+      };
+      k_loop<MBW, 4>(bufH, T.k2[d], T.k2[d], acc, acc, yx, H, W, zH, nq, lane, mh, skw, -(TR + kZeroRows), mid);
+    } else {
+      rescale();
+      // conv2 on H, on top of the residual
+      k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, mh, skw);
+    }
     T16_WSTAMP(d, 3);
     if (d < 4) T16_STAMP(4 + 4 * d);
     if (d < 4) T16_STAMP4(26 + 4 * d);
@@ -1231,21 +1258,30 @@ void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
     }
 }
 
+template <int MBT, int NWM, bool ROWS, bool DB>
+static void launch_db(const TowerNet* net, int staged, const Board* boards, const float4* x, const uint4* rows,
+                      const int* count, int n_max, int H, int W, int A, float* probs, float* values, float4* feat,
+                      unsigned long long* err, hipStream_t s) {
+  const int bpw = tower16_boards_per_tile(H * W, 16 * MBT);
+  const int grid = (n_max + bpw - 1) / bpw;
+  const size_t bytes = tower16_lds_bytes(H * W, 16 * MBT, staged, DB);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBT, NWM, ROWS, DB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTowerLdsMax);
+    attr = true;
+  }
+  tower16_kernel<MBT, NWM, ROWS, DB><<<grid, NWM * 256, bytes, s>>>(net, boards, x, rows, count, n_max, H, W, A,
+                                                                    bpw, probs, values, feat, err);
+}
 template <int MBT, int NWM, bool ROWS>
 static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x,
                        const uint4* rows, const int* count, int n_max, int H, int W, int A, float* probs,
                        float* values, float4* feat, unsigned long long* err, hipStream_t s) {
-  const int bpw = tower16_boards_per_tile(H * W, 16 * MBT);
-  const int grid = (n_max + bpw - 1) / bpw;
-  const size_t bytes = tower16_lds_bytes(H * W, 16 * MBT, staged, dbuf);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_kernel<MBT, NWM, ROWS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTowerLdsMax);
-    attr = true;
-  }
-  tower16_kernel<MBT, NWM, ROWS><<<grid, NWM * 256, bytes, s>>>(net, boards, x, rows, count, n_max, H, W, A, bpw,
-                                                                probs, values, feat, err);
+  if (dbuf)
+    launch_db<MBT, NWM, ROWS, true>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat, err, s);
+  else
+    launch_db<MBT, NWM, ROWS, false>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat, err, s);
 }
 
 void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, const Board* boards, const float4* x,

@@ -31,13 +31,14 @@ def test_tower_kernel_register_budget(tmp_path):
         m = re.search(r"VGPRs Spill: (\d+)", line)
         if m and name:
             spills[name] = int(m.group(1))
-    t128 = [v for k, v in spills.items() if "tower16_kernelILi8ELi2ELb0E" in k]
-    t96 = [v for k, v in spills.items() if "tower16_kernelILi6ELi2ELb0E" in k]
-    rows = [v for k, v in spills.items() if "tower16_kernelILi8ELi2ELb1E" in k]  # chess: input-row form
-    assert t128 and t96 and rows, spills
-    assert t128[0] <= 8, spills
-    assert t96[0] == 0, spills
-    assert rows[0] <= 8, spills
+    # <tile blocks, wave groups, input-row form (chess), double-buffered>
+    t128 = [v for k, v in spills.items() if "tower16_kernelILi8ELi2ELb0ELb1E" in k]
+    t96 = [v for k, v in spills.items() if "tower16_kernelILi6ELi2ELb0ELb1E" in k]
+    rows = [v for k, v in spills.items() if "tower16_kernelILi8ELi2ELb1ELb1E" in k]
+    inplace = [v for k, v in spills.items() if "tower16_kernel" in k and "Lb0EEEv" in k]
+    assert t128 and t96 and rows and len(inplace) == 3, spills
+    assert t128[0] == 0 and t96[0] == 0 and rows[0] == 0, spills  # the forms every config runs
+    assert max(inplace) <= 8, spills  # the in-place fallback (LDS too small for two tiles)
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
