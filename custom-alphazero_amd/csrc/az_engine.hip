@@ -676,7 +676,8 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     net.tower_staged = tn.staged_floats;
     net.tower_dbuf = tn.dbuf != 0;
     net.tower_rows = tn.tile_rows;
-    net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip, rows_tower);
+    // (chess: as self-play runs it, the stem's known-zero input chunks 0-1 skipped)
+    net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip, rows_tower, 2);
   }
   net.ready = true;
   return 0;

@@ -48,7 +48,9 @@ struct TowerNet {
 void tower16_slot_plan(int H, int W, int tile_rows, std::vector<int>& slot_pix, int skip[2]);
 // MFMA FLOP tower16_kernel issues per board: a full tile's stem + 2 depth
 // convs (+ the 1x1 projection k-steps) less the plan's skipped taps, / boards
-double tower16_issued_flop_per_board(int HW, int tile_rows, int depth, const int skip[2], bool rows_stem = false);
+// (rows_stem: the input-row stem, stem_chunks of its 4 input chunks computed)
+double tower16_issued_flop_per_board(int HW, int tile_rows, int depth, const int skip[2], bool rows_stem = false,
+                                     int stem_chunks = 4);
 // 0 when the board does not fit a tile (HW > 128); else 96 or 128 (big:
 // 256-row tiles, 16 M blocks, each wave 128 rows x 32 channels -- half the
 // weight stream per FLOP; single tile in place, the LDS holds no second)

@@ -286,13 +286,16 @@ using IC = std::integral_constant<int, V>;
 struct NoMid {
   __device__ void operator()() const {}
 };
-template <int MBW, int R, typename Mid = NoMid>
+// C0: input channel chunks below it are known zero and skipped (each tap
+// runs chunks C0..3; the chess stem in self-play, planes 0-63)
+template <int MBW, int R, int C0 = 0, typename Mid = NoMid>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
                                        t_f4 (&accr)[MBW][2], const int (&yx_)[MBW], int H, int W,
                                        int zrow, int nq, int lane, int mh, int skw, int res_shift = 0,
                                        Mid mid = Mid{}) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
+  static_assert(C0 == 0 || (R == 0 && C0 == 2), "skipped chunks: the stem only, an even count");
   // the two waves of a SIMD (M halves mh = 0, 1) take turns at priority 1,
   // one k-step each, so neither falls a whole phase behind the other (without:
   // the older wave finished its K loop ~7k cycles first and its partner ran
@@ -425,11 +428,11 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   };
 
 #pragma unroll
-  for (int k = 0; k < PF; ++k) load_bk(k, bq[k]);
+  for (int k = 0; k < PF; ++k) load_bk(C0 + k, bq[(C0 + k) % NB]);
   if (R) set_own(0, MBW);
   else set_tap(0, 0, MBW);
 #pragma unroll
-  for (int mb = 0; mb < RING; ++mb) load_a1(0, mb);
+  for (int mb = 0; mb < RING; ++mb) load_a1(C0, mb);
   // ---- residual k-steps (static)
 #pragma unroll
   for (int s = 0; s < R; ++s) {
@@ -446,21 +449,21 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   // blocks 0 and 1 of the wave, from the slot plan) select one of three bodies
   auto tap = [&](int t, auto skc) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = C0; c < 4; ++c) {
       __builtin_amdgcn_sched_barrier(0);
       turn(R + 4 * t + c);
-      // main k-step PF ahead (the prologue or the residual steps fetched 0 .. PF - 1)
-      const int ahead = 4 * t + c + PF;
+      // main k-step PF ahead (the prologue or the residual steps fetched the first PF)
+      const int ahead = c + PF < 4 ? 4 * t + c + PF : 4 * (t + 1) + C0 + (c + PF - 4);
       if (c + PF < 4 || t < 8) load_bk(R + ahead, bq[(c + PF) % NB]);
       // the tap's high blocks (first k-step; tap 0 after the residual steps)
-      if (c == 0 && RING < MBW && (t > 0 || R)) set_tap(t, RING, MBW);
-      if (LAG && c == 0 && (t > 0 || R)) set_tap(t, MBW - 1, MBW);  // its lagged read comes after block 0
-      const bool first = !R && t == 0 && c == 0;
+      if (c == C0 && RING < MBW && (t > 0 || R)) set_tap(t, RING, MBW);
+      if (LAG && c == C0 && (t > 0 || R)) set_tap(t, MBW - 1, MBW);  // its lagged read comes after block 0
+      const bool first = !R && t == 0 && c == C0;
       if (c < 3) {
         kstep(acc, bq[c % NB], c, c + 1, skc, skc, first);
       } else if (t < 8) {
         set_tap(t + 1, 0, LAG ? MBW - 1 : RING);
-        kstep(acc, bq[c % NB], c, 0, skc, IC<0>{}, first);
+        kstep(acc, bq[c % NB], c, C0, skc, IC<0>{}, first);
       } else {
         kstep(acc, bq[c % NB], c, -1, skc, IC<0>{}, first);
       }
@@ -510,7 +513,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
                                                                int H, int W, int A, int bpw,
                                                                float* __restrict__ probs,
                                                                float* __restrict__ values,
-                                                               float4* __restrict__ feat,
+                                                               float4* __restrict__ feat, int first_chunk,
                                                                unsigned long long* __restrict__ err) {
   constexpr int MBW = MBT / NWM;  // M blocks per wave
   constexpr int TR = 16 * MBT;    // tile rows
@@ -604,7 +607,8 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
     __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
     __syncthreads();                // ... every wave's, and the input rows
-    k_loop<MBW, 0>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, mh, skw);
+    if (first_chunk == 2) k_loop<MBW, 0, 2>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, mh, skw);
+    else k_loop<MBW, 0>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, mh, skw);
     if (!dbuf) __syncthreads();  // in place: every wave is done reading the input before X overwrites it
   } else {
   // conv3x3 4 -> F + folded BN + ReLU on the MFMA: k = tap*4 + plane (36 of
@@ -1222,7 +1226,7 @@ void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int ski
   skip[0] = skip[1] = 0;
 }
 
-double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2], bool rows_stem) {
+double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2], bool rows_stem, int stem_chunks) {
   const int bpw = tower16_boards_per_tile(HW, tr);
   if (!bpw) return 0;
   const int nwm = 2, mbw = tr / 16 / nwm;  // blocks per wave
@@ -1232,7 +1236,7 @@ double tower16_issued_flop_per_board(int HW, int tr, int depth, const int skip[2
     int skipped = 0;  // block-taps one wave of this M group skips per conv
     for (int t = 0; t < 9; ++t) skipped += __builtin_popcount((skip[h] >> (2 * t)) & 3);
     // stem: 2 k-steps (4 one-hot planes), or a 36-k-step conv over the input rows (its skips too)
-    const double stem = rows_stem ? 36.0 * mbw - 4.0 * skipped : 2.0 * mbw;
+    const double stem = rows_stem ? 9.0 * stem_chunks * mbw - stem_chunks * skipped : 2.0 * mbw;
     const double per_wave = stem + depth * ((4.0 + 36) * mbw + 36.0 * mbw - 2.0 * 4 * skipped);
     steps += 4 * per_wave;
   }
@@ -1261,7 +1265,7 @@ void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
 template <int MBT, int NWM, bool ROWS, bool DB>
 static void launch_db(const TowerNet* net, int staged, const Board* boards, const float4* x, const uint4* rows,
                       const int* count, int n_max, int H, int W, int A, float* probs, float* values, float4* feat,
-                      unsigned long long* err, hipStream_t s) {
+                      int first_chunk, unsigned long long* err, hipStream_t s) {
   const int bpw = tower16_boards_per_tile(H * W, 16 * MBT);
   const int grid = (n_max + bpw - 1) / bpw;
   const size_t bytes = tower16_lds_bytes(H * W, 16 * MBT, staged, DB);
@@ -1272,16 +1276,18 @@ static void launch_db(const TowerNet* net, int staged, const Board* boards, cons
     attr = true;
   }
   tower16_kernel<MBT, NWM, ROWS, DB><<<grid, NWM * 256, bytes, s>>>(net, boards, x, rows, count, n_max, H, W, A,
-                                                                    bpw, probs, values, feat, err);
+                                                                    bpw, probs, values, feat, first_chunk, err);
 }
 template <int MBT, int NWM, bool ROWS>
 static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x,
                        const uint4* rows, const int* count, int n_max, int H, int W, int A, float* probs,
-                       float* values, float4* feat, unsigned long long* err, hipStream_t s) {
+                       float* values, float4* feat, int first_chunk, unsigned long long* err, hipStream_t s) {
   if (dbuf)
-    launch_db<MBT, NWM, ROWS, true>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat, err, s);
+    launch_db<MBT, NWM, ROWS, true>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat,
+                                    first_chunk, err, s);
   else
-    launch_db<MBT, NWM, ROWS, false>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat, err, s);
+    launch_db<MBT, NWM, ROWS, false>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat,
+                                     first_chunk, err, s);
 }
 
 void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, const Board* boards, const float4* x,
@@ -1289,20 +1295,19 @@ void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, c
                     unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
   if (tile_rows == 96)
-    launch_mbw<6, 2, false>(net, staged, dbuf, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr,
+    launch_mbw<6, 2, false>(net, staged, dbuf, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr, 0,
                             err, s);
   else
-    launch_mbw<8, 2, false>(net, staged, dbuf, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr,
+    launch_mbw<8, 2, false>(net, staged, dbuf, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr, 0,
                             err, s);
 }
 
 void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged, bool dbuf, const void* rows,
                          int first_chunk, const int* count, int n_max, int H, int W, float4* feat,
                          unsigned long long* err, hipStream_t s) {
-  (void)first_chunk;  // every chunk is computed (the zero ones add exact zeros)
   if (n_max <= 0 || tile_rows != 128) return;
   launch_mbw<8, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
-                         0, nullptr, nullptr, feat, err, s);
+                         0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s);
 }
 
 }  // namespace az
