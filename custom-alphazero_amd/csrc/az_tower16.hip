@@ -778,6 +778,10 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
           dma_to_lds<NT>(reinterpret_cast<uint4*>(reinterpret_cast<float*>(bufX) + TR * 48), T.blob + T.off_wv1,
                          HW * J / 4, wave, lane);
       };
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};  // conv1's sums are stored
       k_loop<MBW, 4>(bufH, T.k2[d], T.k2[d], acc, acc, yx, H, W, zH, nq, lane, mh, skw, -(TR + kZeroRows), mid);
     } else {
       rescale();
