@@ -752,6 +752,9 @@ int check_errors(az_chess_engine* e) {
   if (err & az::kErrPath) m += " path-overflow";
   if (err & az::kErrIllegal) m += " illegal-move";
   if (err & az::kErrNoRoot) m += " play-before-search";
+  if (err & az::kErrActRange)
+    m += " activation-range(a non-finite activation, or |x| > 32752 in the per-layer fp16x2 convs: "
+         "use conv_algo=AZ_CONV_F16X2 or AZ_CONV_DIRECT)";
   // play on a slot without a searched root changes nothing: that flag is
   // cleared once reported (the others mean a broken tree and stay)
   if (err == az::kErrNoRoot) AZC_HIP(hipMemset(e->t.stats + az::kStatErrors, 0, sizeof(err)));

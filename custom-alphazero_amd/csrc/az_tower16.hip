@@ -554,7 +554,10 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // emptied, keeping their rows' bank residues) or the natural order
   const int r0 = mh * MBW * 16 + r16;
   int yx[MBW];
-  const int* plan = T.slot_pix;
+  // (the plan is for the TowerNet's tile height: a smaller tile of the same
+  // boards -- chess's 64-row tiles -- runs in natural order, the same bits)
+  const bool planned = 16 * MBT == T.tile_rows;
+  const int* plan = planned ? T.slot_pix : nullptr;
   T16_STAMP(56);
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
@@ -570,7 +573,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
   }
   // this wave's tap skips (2 bits per tap over its blocks 0 and 1)
-  const int skw = T.skip[mh];
+  const int skw = planned ? T.skip[mh] : 0;
   const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
   // double-buffered: one accumulator set (conv2 runs the block's 1x1
   // projection residual first, from X, which nothing overwrites before its
@@ -1310,8 +1313,15 @@ void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged, bool db
                          int first_chunk, const int* count, int n_max, int H, int W, float4* feat,
                          unsigned long long* err, hipStream_t s) {
   if (n_max <= 0 || tile_rows != 128) return;
-  launch_mbw<8, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
-                         0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s);
+  // a launch of fewer than 512 boards (chess self-play: 128 per lane) in
+  // 2-board tiles would hold under a quarter of the 256 CUs: one board per
+  // 64-row tile then (MI355X has 256 CUs; the same sums, bitwise)
+  if (n_max < 512)
+    launch_mbw<4, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
+                           0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s);
+  else
+    launch_mbw<8, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
+                           0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s);
 }
 
 }  // namespace az
