@@ -575,21 +575,25 @@ def _peaked(x):
 
 @pytest.mark.timeout(300)
 def test_pooled_arena_holds_a_peaked_network():
-    """A peaked evaluator over full games: compaction keeps trees of tens of
-    thousands of edges per slot (far past the 8*S*A + H*W*A halves round 2
-    sized), the pooled arena holds them with no device error, and every game
-    equals the uncompacted engine's bit for bit."""
-    S, slots = 200, 32
+    """A peaked evaluator over full games keeps large subtrees: some slots
+    hold more than the per-slot average the pool was sized with (4000
+    edges per half here: round 3's per-slot halves of that size would have
+    overflowed, kErrArena), while the slots together fit -- the pooled halves
+    are shared.  Every game equals the uncompacted engine's bit for bit."""
+    S, slots, per_slot = 200, 32, 4000
     out = []
     for compact in (True, False):
-        eng = az.Engine(6, 7, 4, True, S, slots=slots, evaluator=az.EVAL_HOST, compact=compact)
+        eng = az.Engine(6, 7, 4, True, S, slots=slots, evaluator=az.EVAL_HOST, compact=compact,
+                        arena_edges=per_slot if compact else 0)
         eng.set_host_evaluator(_peaked)
         st = eng.selfplay_run(0, slots, 17)
         assert st["errors"] == 0 and st["games_done"] == slots
         out.append((eng.selfplay_results(), eng.stats()))
         eng.close()
     (r, st), (rr, _) = out
-    assert st["max_retained"] > 8 * S * 7 + 42 * 7, st["max_retained"]
+    assert st["arena_pool_edges"] == 2 * slots * per_slot
+    assert st["max_retained"] > per_slot, st["max_retained"]  # one slot past the per-slot share
+    assert st["arena_pool_high"] <= slots * per_slot
     for k in ("lengths", "moves", "expansions", "results"):
         np.testing.assert_array_equal(r[k], rr[k])
     np.testing.assert_array_equal(r["policies"].view(np.uint64), rr["policies"].view(np.uint64))
