@@ -23,7 +23,7 @@ def main():
     for nb in [int(v) for v in os.environ.get("AZ_BATCHES", "673,1346,4096").split(",")]:
         xx = oracle.full_state(rng.randint(-1, 2, (nb, 6, 7)).astype(np.int8))
         eng = az.Engine(6, 7, 4, True, 25, slots=max(nb, 2048), evaluator=az.EVAL_NETWORK, depth=4,
-                        conv_algo=algo)
+                        conv_algo=algo, tower_natural_order=os.environ.get("AZ_NATURAL") == "1")
         eng.set_weights(w.items())
         eng.forward(xx)
         eng.timer(True)
