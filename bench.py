@@ -774,7 +774,10 @@ def main():
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     boards_per_launch = local_evals / max(conv_launches / per_forward, 1)
     pmc = os.path.join(REPO, "profiles", "r4", "pmc_tower.json")
+    # the PMC entry of this board shape (profiles/r4/collect_pmc.sh: 6x7 "tower16", 9x9 "tower16_9x9")
     pmc_key = {0: "tower16", 1: "direct", 2: "f16x2"}[args.conv_algo]
+    if (args.height, args.width) != (6, 7):
+        pmc_key += f"_{args.height}x{args.width}"
     roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, conv_avg_ms, busy_ms, local_evals,
                          conv_launches, direct_flop, issued, pmc, pmc_key)
 

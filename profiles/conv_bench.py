@@ -2,6 +2,7 @@
 """Forward-pass microbenchmark: az_forward on B random Connect-4 boards, the
 conv kernels timed with the engine's HIP events (same method as bench.py).
 Usage: python3 profiles/conv_bench.py [B] [reps] [algo: 0 one-launch tower, 1 fp32 direct, 2 fp16x2 per layer]
+[H W] (default 6 7; the 9x9 Connect-5 board of configs[2]: 9 9)
 TFLOP/s are direct-convolution (algorithmic) FLOP per second."""
 import os
 import sys
@@ -16,9 +17,9 @@ from custom_alphazero.model.weights import init_weights, weight_spec  # noqa: E4
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-H, W = 6, 7
+H, W = (int(sys.argv[4]), int(sys.argv[5])) if len(sys.argv) > 5 else (6, 7)
 algo = int(sys.argv[3]) if len(sys.argv) > 3 else az.CONV_F16X2
-eng = az.Engine(H, W, 4, True, 1, slots=B, evaluator=az.EVAL_NETWORK, conv_algo=algo)
+eng = az.Engine(H, W, 4 if (H, W) == (6, 7) else 5, True, 1, slots=B, evaluator=az.EVAL_NETWORK, conv_algo=algo)
 eng.set_weights(init_weights(weight_spec(H, W, W), seed=0).items())
 rng = np.random.RandomState(0)
 b = rng.randint(-1, 2, (B, H, W)).astype(np.int8)

@@ -36,6 +36,7 @@ def mean(v):
 
 def main():
     d, B, pat, key = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    script = sys.argv[5] if len(sys.argv) > 5 else "profiles/conv_bench.py"
     from custom_alphazero import engine as az
     build, flags = az.build_id()
     fetch = mean(per_dispatch(f"{d}/fetch", "FETCH_SIZE", pat))
@@ -46,7 +47,7 @@ def main():
     out = {
         "build_id": build, "build_flags": flags,
         "source": f"rocprofv3 --pmc, separate passes (FETCH_SIZE; WRITE_SIZE; SQ_VALU_MFMA_BUSY_CYCLES + "
-                  f"SQ_INSTS_MFMA + GRBM_GUI_ACTIVE), profiles/conv_bench.py at B={B} boards per launch, "
+                  f"SQ_INSTS_MFMA + GRBM_GUI_ACTIVE), {script} at B={B} boards per launch, "
                   f"kernel '{pat}'",
         "correction": "fetch bytes = 2 x FETCH_SIZE KiB x 1024 (gfx950, 16 B/lane streams); write = WRITE_SIZE KiB "
                       "x 1024; kernel cycles = GRBM_GUI_ACTIVE / 8; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / "
