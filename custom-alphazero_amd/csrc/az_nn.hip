@@ -691,9 +691,6 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
   // wins, 3207 vs 3137 games/s in-bench (profiles/r2/hw_queues.txt)
   const long rows_max = (long)n_max * HW;
   ca.mb = rows_max <= 24576 ? 2 : (rows_max <= 65536 ? 3 : 4);
-#ifdef AZ_FORCE_MB  // A/B builds (profiles/ab_libs.sh)
-  ca.mb = AZ_FORCE_MB;
-#endif
   ca.err = net.err;
   if (net.in_ch > 4) {
     // chess: 118 input planes zero-padded to F, the stem is one more 3x3 conv;

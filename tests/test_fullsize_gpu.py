@@ -16,10 +16,11 @@ import numpy as np
 import pytest
 
 import chess_oracle as C
+import keras_ref
 import oracle
 from custom_alphazero import engine as az
 from test_chess_selfplay_gpu import _compare
-from test_engine_gpu import make_net_engine, selfplay_games
+from test_engine_gpu import NET_TOL, make_net_engine, selfplay_games
 
 pytestmark = pytest.mark.gpu
 
@@ -105,6 +106,55 @@ def test_c4_fullsize_game_replays_on_oracle(c4_games, g):
     outputs."""
     eng, games = c4_games[25]
     replay_on_oracle(eng, games[g], C4["H"], C4["W"], C4["n"], C4["S"], C4_SEED + g)
+
+
+def playout_boards(rng, k, H, W):
+    """k gravity positions reached by random play from the empty board (0 to
+    H*W - 1 plies, the side to move as +1), as int8 [k, H, W]."""
+    b = np.zeros((k, H, W), np.int8)
+    plies = rng.randint(0, H * W, k)
+    for t in range(H * W - 1):
+        live = np.nonzero(plies > t)[0]
+        if not len(live):
+            break
+        b[live] *= -1  # the mover's stones become the opponent's
+        height = (b[live] != 0).sum(axis=1)  # stones per column
+        for i, row in zip(live, height):
+            cols = np.nonzero(row < H)[0]
+            c = cols[rng.randint(len(cols))]
+            b[i, H - 1 - row[c], c] = -1  # the stone of the player who just moved
+    return b
+
+
+def forward_vs_keras(H, W, n, x, seed):
+    eng, w = make_net_engine(H, W, n, True, slots=len(x), seed=seed)
+    try:
+        p, v = eng.forward(x)
+    finally:
+        eng.close()
+    rp, rv = keras_ref.forward(w, x, depth=4)
+    assert np.abs(p - rp).max() < NET_TOL, np.abs(p - rp).max()
+    assert np.abs(v - rv).max() < NET_TOL, np.abs(v - rv).max()
+
+
+@pytest.mark.parametrize("B", [672, 4096])
+def test_c4_forward_at_bench_batches_matches_keras(c4_games, B):
+    """The tower at the bench's launch sizes (672 boards: one lane's live
+    batch in bench.py; 4096: 1366 tiles, more than five per CU) on positions
+    the bench workload's own games reach (every ply of the 4096 self-play
+    games above), within NET_TOL of the float64 Keras restatement -- not only
+    the 37-board random fills of test_engine_gpu.py."""
+    pos = np.concatenate([g["boards"] for g in c4_games[25][1]])
+    rng = np.random.RandomState(B)
+    forward_vs_keras(6, 7, 4, oracle.full_state(pos[rng.choice(len(pos), B, replace=False)]), seed=11)
+
+
+def test_c5_9x9_forward_at_bench_batch_matches_keras():
+    """configs[2]'s launch size (3443 boards: one lane's live batch in
+    bench.py, one 9x9 board per 96-row tile) on random-playout positions,
+    within NET_TOL of the float64 Keras restatement."""
+    rng = np.random.RandomState(9)
+    forward_vs_keras(9, 9, 5, oracle.full_state(playout_boards(rng, 3443, 9, 9)), seed=13)
 
 
 @pytest.mark.parametrize("cfg", [
