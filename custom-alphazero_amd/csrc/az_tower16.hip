@@ -14,8 +14,15 @@
 // k-step into one fp32 accumulator (t1*B0 + t0*b1 + t0*B0, B0 = 2^12 b0), so
 // every layer is fp32-accurate (network error vs float64 ~1e-7).
 //
-// Workgroup = 8 waves (two per SIMD): wave w takes M half w >> 2 (MBW 16-row
-// blocks) and N quarter w & 3 (32 output channels).  The weights are the
+// Workgroup = 8 waves (two per SIMD): wave w takes M half w & 1 (MBW 16-row
+// blocks) and N quarter w >> 1 (32 output channels).  The two waves loading
+// one N quarter's weight fragments are then w and w ^ 1: a workgroup's waves
+// go to the SIMDs in the order 0, 2, 1, 3, so they sit on different SIMDs
+// and are both the older (waves 0-3) or both the younger (4-7) wave of their
+// SIMD -- they run in step and the second request for a fragment finds it in
+// the CU's L1 (round 4: 975 vs 1008 us per 4096-board forward, +3.2%
+// games/s, profiles/r4/shape_runs/ab_pairl1.txt; with M half w >> 2 the pair
+// shared a SIMD, the younger ran ~6 k-steps behind and missed L1).  The weights are the
 // MFMA's A operand, so a lane's accumulators are 4 consecutive channels of
 // one pixel: an epilogue writes its split16 terms to LDS as 8-byte stores
 // straight from the registers.  B fragments (host-packed, conv16_pack) stream
@@ -292,18 +299,13 @@ template <int MBW, int R, int C0 = 0, typename Mid = NoMid>
 __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                        const uint4* __restrict__ wres, t_f4 (&acc)[MBW][2],
                                        t_f4 (&accr)[MBW][2], const int (&yx_)[MBW], int H, int W,
-                                       int zrow, int nq, int lane, int mh, int skw, int res_shift = 0,
+                                       int zrow, int nq, int lane, int skw, int res_shift = 0,
                                        Mid mid = Mid{}) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
   static_assert(C0 == 0 || (R == 0 && C0 == 2), "skipped chunks: the stem only, an even count");
-  // the two waves of a SIMD (M halves mh = 0, 1) take turns at priority 1,
-  // one k-step each, so neither falls a whole phase behind the other (without:
-  // the older wave finished its K loop ~7k cycles first and its partner ran
-  // the tail alone; with: ~2k, -1 to -2% kernel time)
-  auto turn = [&](int k) {
-    if ((k ^ mh) & 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-  };
+  // (no SIMD-pair priority scheme: an s_setprio under a per-wave branch
+  // executed on both paths, so round 3's alternating turn was a no-op; made
+  // wave-uniform it cost 4%, profiles/r4/kloop_diag_r4.md)
   // B fragments one k-step ahead of their MFMAs (2 measured equal, 1 needs no spill)
   constexpr int PF = 1, NB = 2;
   const int gq = lane >> 4;
@@ -437,7 +439,6 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #pragma unroll
   for (int s = 0; s < R; ++s) {
     __builtin_amdgcn_sched_barrier(0);
-    turn(s);
     load_bk(s + PF, bq[(s + PF) % NB]);
     // the next k-step is tap 0's first chunk: the ring's low blocks move now
     // (lagged: all but the last, whose read of this k-step is still to come)
@@ -451,7 +452,6 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #pragma unroll
     for (int c = C0; c < 4; ++c) {
       __builtin_amdgcn_sched_barrier(0);
-      turn(R + 4 * t + c);
       // main k-step PF ahead (the prologue or the residual steps fetched the first PF)
       const int ahead = c + PF < 4 ? 4 * t + c + PF : 4 * (t + 1) + C0 + (c + PF - 4);
       if (c + PF < 4 || t < 8) load_bk(R + ahead, bq[(c + PF) % NB]);
@@ -480,7 +480,6 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     else if (m == 1) tap(t, IC<1>{});
     else tap(t, IC<2>{});
   }
-  __builtin_amdgcn_s_setprio(0);
 }
 
 // LDS-DMA of n_u4 16-byte words from global src into LDS dst (both
@@ -548,7 +547,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 2) sm.flag[tid] = 0;  // published by the barrier after the stem's MFMAs
 
-  const int mh = wave >> 2, nq = wave & 3, r16 = lane & 15, gq = lane >> 4;
+  const int mh = wave & 1, nq = wave >> 1, r16 = lane & 15, gq = lane >> 4;
   // a lane's slots r0 + 16 mb and their pixel words: the slot plan's
   // (T.slot_pix, a full tile's boards; the boards past this tile's are
   // emptied, keeping their rows' bank residues) or the natural order
@@ -610,8 +609,8 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
     __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
     __syncthreads();                // ... every wave's, and the input rows
-    if (first_chunk == 2) k_loop<MBW, 0, 2>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, mh, skw);
-    else k_loop<MBW, 0>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, mh, skw);
+    if (first_chunk == 2) k_loop<MBW, 0, 2>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, skw);
+    else k_loop<MBW, 0>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, skw);
     if (!dbuf) __syncthreads();  // in place: every wave is done reading the input before X overwrites it
   } else {
   // conv3x3 4 -> F + folded BN + ReLU on the MFMA: k = tap*4 + plane (36 of
@@ -728,8 +727,8 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     // conv1, input X (in place: + the projection residual into accr)
     T16_WSTAMP(d, 0);
-    if constexpr (DB) k_loop<MBW, 0>(bufX, T.k1[d], nullptr, acc, acc, yx, H, W, zX, nq, lane, mh, skw);
-    else k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr_, yx, H, W, zX, nq, lane, mh, skw);
+    if constexpr (DB) k_loop<MBW, 0>(bufX, T.k1[d], nullptr, acc, acc, yx, H, W, zX, nq, lane, skw);
+    else k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr_, yx, H, W, zX, nq, lane, skw);
     T16_WSTAMP(d, 1);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
@@ -785,11 +784,11 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};  // conv1's sums are stored
-      k_loop<MBW, 4>(bufH, T.k2[d], T.k2[d], acc, acc, yx, H, W, zH, nq, lane, mh, skw, -(TR + kZeroRows), mid);
+      k_loop<MBW, 4>(bufH, T.k2[d], T.k2[d], acc, acc, yx, H, W, zH, nq, lane, skw, -(TR + kZeroRows), mid);
     } else {
       rescale();
       // conv2 on H, on top of the residual
-      k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, mh, skw);
+      k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, skw);
     }
     T16_WSTAMP(d, 3);
     if (d < 4) T16_STAMP(4 + 4 * d);
