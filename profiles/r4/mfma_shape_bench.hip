@@ -26,7 +26,8 @@ template <int SHAPE, int FL = 0, int MBW0 = 4>
 __global__ __launch_bounds__(512, 1) void kbench(const uint4* __restrict__ w, float* __restrict__ out, int W) {
   extern __shared__ __attribute__((aligned(16))) uint4 act[];
   constexpr int PITCH = SHAPE == 0 ? 544 : 528;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, mh = wave >> 2, nq = wave & 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, mh = (FL & 128) ? wave & 1 : wave >> 2,
+            nq = (FL & 128) ? wave >> 1 : wave & 3;
   for (int i = tid; i < (TR + 16) * PITCH / 16; i += 512) {
     const unsigned v = (unsigned)(i * 2654435761u);
     act[i] = make_uint4(v & 0x3bff3bff, (v >> 3) & 0x3bff3bff, (v >> 7) & 0x3bff3bff, (v >> 11) & 0x3bff3bff);
@@ -259,6 +260,79 @@ __global__ __launch_bounds__(512, 1) void kbench(const uint4* __restrict__ w, fl
     }
     for (int mb = 0; mb < MBW; ++mb)
       for (int nb = 0; nb < 2; ++nb) sink += acc[mb][nb][0] + acc[mb][nb][1] + acc[mb][nb][2] + acc[mb][nb][3];
+  } else if constexpr (SHAPE == 3) {
+    // M quarters x N halves: wave = 2 blocks of 16 rows x 4 N blocks (64
+    // channels); the 4 waves of an N half load the same fragments and are all
+    // the older (0-3) or all the younger (4-7) wave of their SIMD
+    constexpr int MBW = 2, NBW = 4;
+    const int mq = wave & 3, nh = wave >> 2;
+    f4 acc[MBW][NBW];
+    for (int mb = 0; mb < MBW; ++mb)
+      for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = f4{0, 0, 0, 0};
+    const int voff = ((nh * NBW) * 2 * 64 + lane) * 16, gq = lane >> 4, r16 = lane & 15;
+    for (int cv = 0; cv < CONVS; ++cv) {
+      uint4 bq[2][2 * NBW];
+      uint4 aq[2][MBW][2];
+      int ad[MBW];
+      auto load_b = [&](int ks, uint4(&d)[2 * NBW]) {
+#pragma unroll
+        for (int q = 0; q < 2 * NBW; ++q)
+          d[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + q * 1024, (cv * 40 + ks) * 16384, 0));
+      };
+      auto set_tap = [&](int t) {
+        const int sh = (t / 3 - 1) * W + (t % 3 - 1);
+#pragma unroll
+        for (int mb = 0; mb < MBW; ++mb) {
+          int r = mq * 32 + mb * 16 + r16;
+          asm volatile("" : "+v"(r));
+          ad[mb] = ((r + sh) & 127) * PITCH + gq * 16;
+        }
+      };
+      load_b(0, bq[0]);
+      set_tap(0);
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb) {
+        aq[0][mb][0] = *reinterpret_cast<const uint4*>(actb + ad[mb]);
+        aq[0][mb][1] = *reinterpret_cast<const uint4*>(actb + ad[mb] + 256);
+      }
+#pragma unroll 1
+      for (int t = 0; t < 9; ++t) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int ks = 4 * t + c;
+          if (!(FL & 1) && ks + 1 < 36) load_b(ks + 1, bq[(c + 1) & 1]);
+          const int nc = (c + 1) & 3;
+          if (c == 3 && t < 8) set_tap(t + 1);
+#pragma unroll
+          for (int mb = 0; mb < MBW; ++mb) {
+            const h8 a0 = __builtin_bit_cast(h8, aq[c & 1][mb][0]), a1 = __builtin_bit_cast(h8, aq[c & 1][mb][1]);
+#pragma unroll
+            for (int nb = 0; nb < NBW; ++nb) {
+              const h8 B0 = __builtin_bit_cast(h8, bq[c & 1][2 * nb]), B1 = __builtin_bit_cast(h8, bq[c & 1][2 * nb + 1]);
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0, a1, acc[mb][nb], 0, 0, 0);
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B1, a0, acc[mb][nb], 0, 0, 0);
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(B0, a0, acc[mb][nb], 0, 0, 0);
+            }
+            if (!(FL & 2) && ks + 1 < 36) {
+              aq[(c + 1) & 1][mb][0] = *reinterpret_cast<const uint4*>(actb + ad[mb] + 64 * nc);
+              aq[(c + 1) & 1][mb][1] = *reinterpret_cast<const uint4*>(actb + ad[mb] + 64 * nc + 256);
+            }
+          }
+          if (!(FL & 3)) {
+          __builtin_amdgcn_sched_group_barrier(0x0020, 2 * NBW, 0);
+#pragma unroll
+          for (int mb = 0; mb < MBW; ++mb) {
+            __builtin_amdgcn_sched_group_barrier(0x0008, 3 * NBW, 0);
+            __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);
+          }
+          }
+        }
+      }
+      __syncthreads();
+    }
+    for (int mb = 0; mb < MBW; ++mb)
+      for (int nb = 0; nb < NBW; ++nb) sink += acc[mb][nb][0] + acc[mb][nb][1] + acc[mb][nb][2] + acc[mb][nb][3];
   } else if constexpr (SHAPE == 2) {
     constexpr int MBW = 8;
     f4 acc[MBW];
@@ -428,6 +502,10 @@ int main(int argc, char** argv) {
   };
   for (int round = 0; round < 2; ++round) {
     run("16x16x32", kbench<0, 0>, 512);
+    run("16x16x32 pairs in step (product)", kbench<0, 128>, 512);
+    run("M quarters x N halves", kbench<3, 0>, 512);
+    run("M quarters x N halves no-B", kbench<3, 1>, 512);
+    run("pairs in step no-B", kbench<0, 129>, 512);
     run("16x16x32 term-major (dbuf A)", kbench<0, 8>, 512);
     run("term-major ring (product regs)", kbench<0, 32>, 512);
     run("term-major ring pf2", kbench<0, 48>, 512);
