@@ -562,18 +562,23 @@ def tree_arena(args, st):
                 "bytes_total": 32 * args.slots * st["arena_edges"],
                 "rule": f"a static run of {st['arena_edges']} edges per slot (S*H*W*A + A = {safe}: the whole game)"}
     pool, high = st["arena_pool_edges"], st["arena_pool_high"]
-    proof = st["arena_edges"] >= safe
+    # the per-slot average the pools actually hold (a lane's half is also
+    # capped at 2^31 - 1 edges, its indices' range, below arena_edges x slots)
+    per_slot = pool // (2 * args.slots)
+    proof = per_slot >= safe
     return {
         "compact": True, "pool_edges_total": pool, "bytes_total": 32 * pool,
-        "pool_edges_per_half_per_slot": st["arena_edges"], "overflow_proof": proof,
+        "pool_edges_per_half_per_slot": per_slot, "arena_edges_requested": st["arena_edges"],
+        "overflow_proof": proof,
         "high_water_edges_per_lane_half": high, "max_retained_edges": st["max_retained"],
-        "rule": (f"pooled arenas: each lane owns two halves of {st['arena_edges']} edges x its slots; a slot takes "
+        "rule": (f"pooled arenas: each lane owns two halves of {per_slot} edges x its slots; a slot takes "
                  f"{16 * A}-edge chunks of the current half as it expands, and after every move compaction copies "
                  f"each slot's kept subtree (Cheney scan) into the other half, which becomes the current one. "
-                 + (f"{st['arena_edges']} >= S*H*W*A + A = {safe} per slot: no game can overflow it"
+                 + (f"{per_slot} >= S*H*W*A + A = {safe} per slot: no game can overflow it"
                     if proof else
-                    f"{st['arena_edges']} < S*H*W*A + A = {safe} per slot (the 40%-of-free-HBM cap bound it): the "
-                    f"slots share the pool, overflow raises a device error (none in this run)")),
+                    f"{per_slot} < S*H*W*A + A = {safe} per slot (bound by the 40%-of-free-HBM cap or a lane "
+                    f"half's 2^31-edge index range): the slots share the pool, overflow raises a device error "
+                    f"(none in this run)")),
     }
 
 

@@ -179,3 +179,20 @@ def test_roofline_traffic_only_from_the_same_build(tmp_path):
         assert r["build_id"] == build
     r = bench.conv_roofline(args, 0, 1, 672.0, 0.2, 10.0, 6720, 10, 104.6e6, 270.5e6, str(tmp_path / "no"), "tower16")
     assert r["traffic"] is None and "no PMC profile" in r["pmc"]
+
+
+def test_tree_arena_rule_states_the_pool_it_holds():
+    """the line's arena rule is the size the pools hold --
+    per slot, the pools' edges over both halves and all slots, not the
+    requested average (a lane half is also capped at 2^31 - 1 edges)."""
+    bench = _bench()
+    args = argparse.Namespace(width=7, height=6, sims=100, slots=4096, compact=True)
+    safe = 100 * 42 * 7 + 7
+    st = dict(arena_edges=safe, arena_pool_edges=2 * 4096 * safe, arena_pool_high=10, max_retained=5)
+    r = bench.tree_arena(args, st)
+    assert r["overflow_proof"] and r["pool_edges_per_half_per_slot"] == safe and "no game can overflow" in r["rule"]
+    capped = dict(st, arena_pool_edges=2 * 2 * ((1 << 31) - 1))  # two lanes, each half at the index cap
+    args.slots, args.sims = 65536, 400
+    r = bench.tree_arena(args, capped)
+    assert not r["overflow_proof"] and r["pool_edges_per_half_per_slot"] == 2 * ((1 << 31) - 1) // 65536
+    assert "share the pool" in r["rule"]
