@@ -141,3 +141,16 @@ def test_chess_kernels_fail_loudly_without_gpu():
         b.moves
     with pytest.raises(az.AzError, match="no HIP device"):
         K.encode(np.zeros((1, 8), K.POS_DTYPE), np.ones((1, 8), np.uint8))
+
+
+def test_integration_stub_matches_the_header():
+    """INTEGRATION.md's ctypes stub (what a maintainer would paste into the
+    reference) declares az_config and az_tensor field for field as
+    include/az.h does."""
+    doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    hdr = _header_structs()
+    for name in ("az_config", "az_tensor"):
+        m = re.search(r"class %s\(ctypes\.Structure\):\s*_fields_ = \[(.*?)\]\n" % name, doc, re.S)
+        assert m, name
+        fields = re.findall(r'\("(\w+)"', m.group(1))
+        assert fields == hdr[name], (name, fields, hdr[name])
