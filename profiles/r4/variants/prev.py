@@ -1,5 +1,11 @@
-# the committed tower (git HEAD) beside the working tree's other sources: the
-# A/B base for an uncommitted tower change
+# every csrc source at git HEAD: the A/B base for uncommitted product changes
+import os
 import subprocess
-src = subprocess.check_output(["git", "-C", "/root/repo", "show", "HEAD:custom-alphazero_amd/csrc/az_tower16.hip"])
-open("az_tower16.hip", "wb").write(src)
+for f in os.listdir("."):
+    if f.endswith((".hip", ".h")) or f == "Makefile":
+        try:
+            src = subprocess.check_output(["git", "-C", "/root/repo", "show", f"HEAD:custom-alphazero_amd/csrc/{f}"],
+                                          stderr=subprocess.DEVNULL)
+        except subprocess.CalledProcessError:
+            continue  # new in the working tree
+        open(f, "wb").write(src)
