@@ -303,9 +303,15 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
                                        Mid mid = Mid{}) {
   static_assert(R == 0 || R == 4, "ring slots = k-step mod NB, NB divides 4");
   static_assert(C0 == 0 || (R == 0 && C0 == 2), "skipped chunks: the stem only, an even count");
-  // (no SIMD-pair priority scheme: an s_setprio under a per-wave branch
-  // executed on both paths, so round 3's alternating turn was a no-op; made
-  // wave-uniform it cost 4%, profiles/r4/kloop_diag_r4.md)
+  // SIMD-pair priority by phase: each SIMD runs one of waves 0-3 (older)
+  // and one of 4-7 (younger); the older wins the MFMA pipe by default and
+  // finishes ~8k cycles ahead, after which its partner runs alone.  The
+  // younger wave takes priority 1 for the residual steps and taps 0-5, the
+  // older for taps 6-8, so both reach the barrier closer together (round 4:
+  // 929-938 vs 964-970 us per 4096-board forward, +1.9% games/s,
+  // profiles/r4/shape_runs/ab_prio2.txt).  The wave index goes through
+  // readfirstlane so each s_setprio sits under a scalar branch (under a
+  // per-lane branch both paths execute: round 3's per-k-step turn was a no-op)
   // B fragments one k-step ahead of their MFMAs (2 measured equal, 1 needs no spill)
   constexpr int PF = 1, NB = 2;
   const int gq = lane >> 4;
@@ -435,6 +441,12 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   else set_tap(0, 0, MBW);
 #pragma unroll
   for (int mb = 0; mb < RING; ++mb) load_a1(C0, mb);
+  const bool young = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= 256;
+  auto prio = [&](bool hi) {
+    if (hi) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  };
+  prio(young);
   // ---- residual k-steps (static)
 #pragma unroll
   for (int s = 0; s < R; ++s) {
@@ -476,10 +488,12 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
     // the loops, testing m == 2 first spilled 140 inside them (and ran the
     // kernel at half speed) -- tests/test_kernel_resources_cpu.py guards it
     const int m = (skw >> (2 * t)) & 3;
+    if (t == 6) prio(!young);
     if (m == 0) tap(t, IC<0>{});
     else if (m == 1) tap(t, IC<1>{});
     else tap(t, IC<2>{});
   }
+  __builtin_amdgcn_s_setprio(0);
 }
 
 // LDS-DMA of n_u4 16-byte words from global src into LDS dst (both
