@@ -22,7 +22,7 @@ constexpr int TR = 128, CONVS = 8;
 
 __device__ unsigned long long g_clk[4];
 
-template <int SHAPE, int FL = 0, int MBW0 = 4>
+template <int SHAPE, int FL = 0, int MBW0 = 4, int TU = 1>
 __global__ __launch_bounds__(512, 1) void kbench(const uint4* __restrict__ w, float* __restrict__ out, int W) {
   extern __shared__ __attribute__((aligned(16))) uint4 act[];
   constexpr int PITCH = SHAPE == 0 ? 544 : 528;
@@ -175,7 +175,8 @@ __global__ __launch_bounds__(512, 1) void kbench(const uint4* __restrict__ w, fl
     for (int mb = 0; mb < MBW; ++mb) acc[mb][0] = acc[mb][1] = f4{0, 0, 0, 0};
     const int voff = ((nq * 2) * 2 * 64 + lane) * 16, gq = lane >> 4, r16 = lane & 15;
     for (int cv = 0; cv < CONVS; ++cv) {
-      uint4 bq[2][4];
+      constexpr int PFB = (FL & 512) ? 2 : 1, NBB = 2 * PFB;
+      uint4 bq[NBB][4];
       uint4 aq[2][MBW][2];
       int ad[MBW];
       auto load_b = [&](int ks, uint4(&d)[4]) {
@@ -193,22 +194,23 @@ __global__ __launch_bounds__(512, 1) void kbench(const uint4* __restrict__ w, fl
         }
       };
       load_b(0, bq[0]);
+      if (PFB == 2) load_b(1, bq[1]);
       set_tap(0);
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb) {
         aq[0][mb][0] = *reinterpret_cast<const uint4*>(actb + ad[mb]);
         aq[0][mb][1] = *reinterpret_cast<const uint4*>(actb + ad[mb] + 256);
       }
-#pragma unroll 1
+#pragma unroll TU
       for (int t = 0; t < 9; ++t) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           __builtin_amdgcn_sched_barrier(0);
           const int ks = 4 * t + c;
-          if (!(FL & 1) && ks + 1 < 36) load_b(ks + 1, bq[(c + 1) & 1]);
+          if (!(FL & 1) && ks + PFB < 36) load_b(ks + PFB, bq[(c + PFB) % NBB]);
           const int nc = (c + 1) & 3;
           if (c == 3 && t < 8) set_tap(t + 1);
-          const uint4(&b)[4] = bq[c & 1];
+          const uint4(&b)[4] = bq[c % NBB];
           const h8 B0[2] = {__builtin_bit_cast(h8, b[0]), __builtin_bit_cast(h8, b[2])};
           const h8 B1[2] = {__builtin_bit_cast(h8, b[1]), __builtin_bit_cast(h8, b[3])};
 #pragma unroll
@@ -503,6 +505,10 @@ int main(int argc, char** argv) {
   for (int round = 0; round < 2; ++round) {
     run("16x16x32", kbench<0, 0>, 512);
     run("16x16x32 pairs in step (product)", kbench<0, 128>, 512);
+    run("pairs, taps unrolled by 3", kbench<0, 128, 4, 3>, 512);
+    run("pairs, taps unrolled by 9", kbench<0, 128, 4, 9>, 512);
+    run("pairs, PF2", kbench<0, 128 | 512>, 512);
+    run("pairs, PF2, unrolled by 3", kbench<0, 128 | 512, 4, 3>, 512);
     run("M quarters x N halves", kbench<3, 0>, 512);
     run("M quarters x N halves no-B", kbench<3, 1>, 512);
     run("pairs in step no-B", kbench<0, 129>, 512);
