@@ -6,8 +6,9 @@ collectives -- the weight broadcast and the replay-buffer gather on the
 rank's GPU (custom_alphazero.distributed, self_play.py:96-118 in the
 reference) -- would otherwise run only on the driver's multi-GPU node.  Here
 a one-rank nccl group drives them through RCCL on cuda:0: the broadcast
-weights are the host weights bit for bit, and the games gathered through
-RCCL are one engine's games bit for bit.
+weights are the host weights bit for bit, bench.py's broadcast and
+all-reduces (their multi-rank branches) run on the device, and the games
+gathered through RCCL are one engine's games bit for bit.
 """
 import os
 import socket
@@ -32,7 +33,7 @@ def _free_port():
 
 
 def _paths():
-    for p in (os.path.join(REPO, "custom-alphazero_amd"), os.path.join(REPO, "tests")):
+    for p in (os.path.join(REPO, "custom-alphazero_amd"), REPO):
         if p not in sys.path:
             sys.path.insert(0, p)
 
@@ -59,6 +60,19 @@ def _worker(rank, port, outdir):
     for (n, t) in named:  # on the rank's GPU (collective_device under nccl), unchanged
         assert t.device == dev, n
         np.testing.assert_array_equal(t.cpu().numpy(), host[n].astype(np.float32), err_msg=n)
+    # bench.py's own multi-rank branches (taken when world > 1) on the same group
+    import argparse
+    import bench
+    a = argparse.Namespace(dist_backend="nccl")
+    bnamed, flat = bench._device_weights(spec, host, 0, 2, a, dev)
+    assert flat.device == dev
+    for (n, t) in bnamed:
+        np.testing.assert_array_equal(t.cpu().numpy().reshape(host[n].shape), host[n], err_msg=n)
+    assert bench._reduce([1.5, 2.0], dist.ReduceOp.SUM, 2, a, dev) == [1.5, 2.0]
+    assert bench._reduce([3.0], dist.ReduceOp.MAX, 2, a, dev) == [3.0]
+    devices = [None]
+    dist.all_gather_object(devices, 0)
+    assert devices == [0]
     eng = az.Engine(H, W, N, True, S, slots=8, evaluator=az.EVAL_NETWORK, compact=True)
     eng.set_weights(named)
     g = D.selfplay_sharded(D.engine_runner(eng), N_GAMES, BASE_SEED)  # gather: RCCL all_gather on cuda:0
