@@ -14,6 +14,7 @@ import numpy as np
 
 from custom_alphazero import engine as az
 from custom_alphazero.config import ConfigConnectN, ConfigModel, ConfigPath
+from custom_alphazero.model.tf_checkpoint import load_keras_weights, save_keras_weights
 from custom_alphazero.model.weights import (content_hash, init_weights, keras_order, reference_hash,
                                             weight_spec)
 
@@ -116,8 +117,11 @@ class PolicyValueModel:
     # ------------------------------------------------------------ persistence
     def save_with_meta(self, path):
         os.makedirs(path, exist_ok=True)
-        np.savez(os.path.join(path, ConfigPath.model_prefix + ".npz"),
-                 **dict(zip(self.weight_names, self.get_weights())))
+        # the reference's files: Model.save_weights(path/model) in TensorFlow's
+        # checkpoint format (model.py:203-204; model/tf_checkpoint.py)
+        shapes = dict(self.spec)
+        save_keras_weights(os.path.join(path, ConfigPath.model_prefix), self.spec,
+                           {n: w.reshape(shapes[n]) for n, w in zip(self.weight_names, self.get_weights())})
         # `hash` is the reference's (sum of md5(str(w)), model.py:172-177): it
         # depends on numpy's str() of an array, so a checkpoint moved between
         # numpy versions may not reproduce it; `content_hash` (md5 of the raw
@@ -131,8 +135,13 @@ class PolicyValueModel:
     def load_with_meta(self, path):
         if not os.path.exists(os.path.join(path, ConfigPath.model_success)):
             raise AssertionError(f"No verification file of the model found at {path}!")
-        with np.load(os.path.join(path, ConfigPath.model_prefix + ".npz"), allow_pickle=False) as z:
-            self.set_weights([z[name] for name in self.weight_names])
+        prefix = os.path.join(path, ConfigPath.model_prefix)
+        if os.path.exists(prefix + ".index"):  # Model.load_weights (model.py:194): a TF checkpoint
+            w = load_keras_weights(prefix, self.spec)
+            self.set_weights([w[name] for name in self.weight_names])
+        else:  # the .npz this package's earlier builds wrote
+            with np.load(prefix + ".npz", allow_pickle=False) as z:
+                self.set_weights([z[name] for name in self.weight_names])
         with open(os.path.join(path, ConfigPath.model_meta)) as fp:
             meta = json.load(fp)
         self.steps = int(meta.get("steps", 0))

@@ -126,6 +126,11 @@ def test_model_save_load_roundtrip(tmp_path, game_cfg, golden):
     a = PolicyValueModel((6, 7, 4), 7, seed=1)
     a.steps = 12
     a.save_with_meta(str(tmp_path))
+    # the reference's files: Model.save_weights(path/model) -> a TF checkpoint
+    # (model.py:203-204), read back here without TensorFlow
+    for f in ("model.index", "model.data-00000-of-00001", "checkpoint", "meta.json",
+              "MODEL_SAVED_SUCCESSFULLY"):
+        assert (tmp_path / f).exists(), f
     b = PolicyValueModel((6, 7, 4), 7, seed=2)
     assert not a.is_equal(b)
     b.load_with_meta(str(tmp_path))
