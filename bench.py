@@ -698,14 +698,17 @@ def main():
                    "boards": np.zeros((0, args.height * args.width, args.height, args.width), np.int8),
                    "policies": np.zeros((0, args.height * args.width, A)),
                    "moves": np.zeros((0, args.height * args.width), np.int32)}
-        g = D.gather_games(res, device=None if args.dist_backend == "gloo" else dev)
+        gstats = {}
+        g = D.gather_games(res, device=None if args.dist_backend == "gloo" else dev, stats=gstats)
         gt = time.perf_counter() - t_g
         if rank == 0:
             gather = {"games": int(len(g["lengths"])), "samples": int(len(g["moves"])),
-                      "bytes": int(g["boards"].nbytes + g["policies"].nbytes + g["moves"].nbytes),
+                      "bytes": gstats["wire_bytes"],
+                      "bytes_note": "what rank 0 received from the other ranks (its own games stay put)",
                       "seconds": round(gt, 4),
-                      "how": f"compact int8 boards + f64 policies + int16 moves, all_gather over "
-                             f"{args.dist_backend} after the timed window (distributed.gather_games)"}
+                      "how": f"compact int8 boards + f64 policies + int16 moves + per-game counts; a gather "
+                             f"of the sizes, then each rank sends its blob to rank 0 only (point-to-point "
+                             f"over {args.dist_backend}) after the timed window (distributed.gather_games)"}
 
     # ---- tree kernels (select + expand: latency/HBM-bound) timed with HIP
     # events in a short window of their own (4 more events per simulation),

@@ -9,7 +9,8 @@ remain, both over torch.distributed ("nccl" = RCCL over xGMI on MI355X,
   * broadcast_weights: rank 0's weights, flattened into ONE buffer (~5 MB for
     the 128x4 net), one broadcast -- the analogue of every worker loading the
     best model from disk (utils.py:64-78);
-  * gather_games: each rank's finished games to rank 0 in global game order,
+  * gather_games: each rank's finished games to rank 0 only, in global game
+    order (a gather of the sizes, then point-to-point sends to rank 0),
     shipped compact (canonical int8 boards, float64 policies, int16 moves, one
     result per game) and expanded to full_state only on rank 0 -- the
     analogue of joblib's result return (self_play.py:112-118).
@@ -80,36 +81,48 @@ def _pack(results: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
                 expansions=results["expansions"].astype(np.int64))
 
 
-def gather_games(results: Dict[str, np.ndarray], device=None, dst: int = 0):
-    """Gather every rank's compact games to `dst` (padded all-gather of one
-    byte buffer per rank).  Returns the concatenated dict on `dst`, None elsewhere."""
+def gather_games(results: Dict[str, np.ndarray], device=None, dst: int = 0, stats=None):
+    """Gather every rank's compact games to `dst` only: the per-rank sizes by
+    one `gather` of three int64s, then each other rank `send`s its byte blob
+    (exact length, no padding) and `dst` `recv`s them in rank order -- under
+    nccl both are RCCL point-to-point transfers between the ranks' GPUs over
+    xGMI; no rank but `dst` receives or holds another rank's games.  Returns
+    the concatenated dict on `dst`, None elsewhere; `stats` (a dict) gets
+    `wire_bytes`, the bytes `dst` received from the other ranks."""
     import torch
     import torch.distributed as dist
 
     packed = _pack(results)
     order = ("lengths", "results", "expansions", "boards", "policies", "moves")
     blob = b"".join(np.ascontiguousarray(packed[k]).tobytes() for k in order)
-    header = np.array([len(packed["lengths"]), len(packed["moves"])], np.int64)
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
     device = collective_device(device)
-    sizes = torch.tensor([len(blob), *header.tolist()], dtype=torch.int64, device=device)
-    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-    dist.all_gather(all_sizes, sizes)
-    max_len = max(int(s[0]) for s in all_sizes)
-    buf = torch.zeros(max(max_len, 1), dtype=torch.uint8)
-    if blob:
-        buf[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-    buf = buf.to(device)
-    bufs = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf)
-    if dist.get_rank() != dst:
+    sizes = torch.tensor([len(blob), len(packed["lengths"]), len(packed["moves"])], dtype=torch.int64,
+                         device=device)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)] if rank == dst else None
+    dist.gather(sizes, gather_list=all_sizes, dst=dst)
+    if rank != dst:
+        if blob:
+            dist.send(torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device), dst=dst)
         return None
+    all_sizes = [[int(v) for v in t.cpu().tolist()] for t in all_sizes]
+    bufs, reqs = [], []
+    for r in range(world):
+        if r == dst or all_sizes[r][0] == 0:
+            bufs.append(None)
+            continue
+        bufs.append(torch.empty(all_sizes[r][0], dtype=torch.uint8, device=device))
+        reqs.append(dist.irecv(bufs[r], src=r))
+    for q in reqs:
+        q.wait()
+    if stats is not None:
+        stats["wire_bytes"] = int(sum(all_sizes[r][0] for r in range(world) if r != dst))
     board_shape = packed["boards"].shape[1:]
     A = packed["policies"].shape[1]
     parts: List[Dict[str, np.ndarray]] = []
     for r in range(world):
-        raw = bufs[r].cpu().numpy().tobytes()
-        n_games, n_samples = int(all_sizes[r][1]), int(all_sizes[r][2])
+        raw = blob if r == dst else (bufs[r].cpu().numpy().tobytes() if bufs[r] is not None else b"")
+        n_games, n_samples = all_sizes[r][1], all_sizes[r][2]
         spec = [("lengths", np.int64, (n_games,)), ("results", np.int8, (n_games,)),
                 ("expansions", np.int64, (n_games,)),
                 ("boards", np.int8, (n_samples,) + tuple(board_shape)),

@@ -18,8 +18,9 @@ UNPINNED against a file TensorFlow wrote (only crc32c is pinned, to the RFC
   size, masked crc32c of the bytes).  Snappy-compressed blocks are read;
   blocks are written uncompressed (a reader accepts either).
 * `<prefix>.data-00000-of-00001` -- the tensors' bytes back to back
-  (little-endian; a string tensor is varint64 lengths, a masked crc32c of
-  them, then the bytes).
+  (little-endian; a string tensor is varint64 lengths, the masked crc32c
+  of those lengths as uint32 words, then the bytes; its entry checksum runs
+  on over the masked checksum and the bytes, as TF's WriteStringTensor).
 * `_CHECKPOINTABLE_OBJECT_GRAPH` -- a TrackableObjectGraph proto (scalar
   string tensor): the object tree from the model, whose variables'
   checkpoint keys are their attribute paths.  For the reference's
@@ -368,11 +369,15 @@ def read_checkpoint(prefix):
             fh = files[sid]
             fh.seek(e["offset"])
             raw = fh.read(e["size"])
+            if e["dtype"] == DT_STRING:
+                val, crc = _decode_strings(raw, e["shape"], key.decode())
+                if e["crc32c"] is not None and crc != e["crc32c"]:
+                    raise ValueError(f"{key.decode()}: data checksum mismatch")
+                out[key.decode()] = val
+                continue
             if e["crc32c"] is not None and crc32c(raw) != e["crc32c"]:
                 raise ValueError(f"{key.decode()}: data checksum mismatch")
-            if e["dtype"] == DT_STRING:
-                out[key.decode()] = _decode_strings(raw, e["shape"])
-            elif e["dtype"] in DT:
+            if e["dtype"] in DT:
                 out[key.decode()] = np.frombuffer(raw, DT[e["dtype"]]).reshape(e["shape"]).copy()
             else:
                 raise ValueError(f"{key.decode()}: dtype {e['dtype']} not supported")
@@ -382,23 +387,43 @@ def read_checkpoint(prefix):
     return out
 
 
-def _decode_strings(raw, shape):
+# A string tensor's bytes (TF tensor_bundle.cc WriteStringTensor /
+# ReadStringTensor): the varint64 lengths, a masked crc32c, then the strings.
+# The masked crc32c covers the lengths as fixed-width little-endian integers
+# (uint32, or uint64 for a length past UINT32_MAX), NOT their varint bytes;
+# the entry's crc32c continues that same checksum over the 4 masked-checksum
+# bytes and then the string bytes.
+def _length_words(lens):
+    return b"".join(struct.pack("<I", n) if n <= 0xFFFFFFFF else struct.pack("<Q", n) for n in lens)
+
+
+def _decode_strings(raw, shape, key="string tensor"):
+    """-> (value, the entry crc32c TF computes while reading it)."""
     n = int(np.prod(shape)) if shape else 1
     pos, lens = 0, []
     for _ in range(n):
         ln, pos = _read_varint(raw, pos)
         lens.append(ln)
-    pos += 4  # masked crc32c of the lengths
+    words = _length_words(lens)
+    stored = bytes(raw[pos:pos + 4])
+    if len(stored) != 4 or struct.unpack("<I", stored)[0] != mask(crc32c(words)):
+        raise ValueError(f"{key}: string lengths checksum mismatch")
+    pos += 4
     out = []
     for ln in lens:
         out.append(bytes(raw[pos:pos + ln]))
         pos += ln
-    return out[0] if not shape else out
+    if pos != len(raw):
+        raise ValueError(f"{key}: string tensor size mismatch")
+    crc = crc32c(words + stored + b"".join(out))
+    return (out[0] if not shape else out), crc
 
 
 def _encode_string(b):
-    lens = _varint(len(b))
-    return lens + struct.pack("<I", mask(crc32c(lens))) + b
+    """One scalar string -> (its bytes in the data file, its entry crc32c)."""
+    words = _length_words([len(b)])
+    stored = struct.pack("<I", mask(crc32c(words)))
+    return _varint(len(b)) + stored + b, crc32c(words + stored + b)
 
 
 def write_checkpoint(prefix, tensors):
@@ -412,14 +437,15 @@ def write_checkpoint(prefix, tensors):
         for key in sorted(tensors):
             t = tensors[key]
             if isinstance(t, (bytes, bytearray)):
-                raw, dtype, shape = _encode_string(bytes(t)), DT_STRING, ()
+                (raw, crc), dtype, shape = _encode_string(bytes(t)), DT_STRING, ()
             else:
                 a = np.asarray(t)  # (ascontiguousarray would make a scalar 1-D)
                 if a.dtype not in NP_DT:
                     raise ValueError(f"{key}: dtype {a.dtype} not supported")
                 raw, dtype, shape = a.astype(a.dtype.newbyteorder("<")).tobytes(), NP_DT[a.dtype], a.shape
+                crc = crc32c(raw)
             f.write(raw)
-            entries.append((key.encode(), _entry_proto(dtype, shape, off, len(raw), crc32c(raw))))
+            entries.append((key.encode(), _entry_proto(dtype, shape, off, len(raw), crc)))
             off += len(raw)
     header = _pb_varint(1, 1) + _pb_bytes(3, _pb_varint(1, 1))  # num_shards 1, little endian, version 1
     write_table(prefix + ".index", [(b"", header)] + entries)

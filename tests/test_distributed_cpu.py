@@ -38,7 +38,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, n_games=N_GAMES):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -55,25 +55,35 @@ def _worker(rank, world, port, outdir):
     got = D.broadcast_weights(named)
     assert torch.equal(got[0][1], torch.arange(6, dtype=torch.float32).reshape(2, 3))
     assert torch.equal(got[1][1], torch.full((4,), 7.0))
-    g = D.selfplay_sharded(oracle_runner, N_GAMES, BASE_SEED)
+    first, count = D.shard(n_games, world, rank)
+    stats = {}
+    g = D.gather_games(oracle_runner(first, count, BASE_SEED), stats=stats)
     if rank == 0:
         states, policies, rewards = D.to_samples(g)
         np.savez(os.path.join(outdir, f"world{world}.npz"), states=states, policies=policies,
-                 rewards=rewards, lengths=g["lengths"], moves=g["moves"])
+                 rewards=rewards, lengths=g["lengths"], moves=g["moves"], wire=stats["wire_bytes"])
+    else:
+        assert g is None  # only rank 0 receives
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_sharded_selfplay_gloo(tmp_path, world):
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+@pytest.mark.parametrize("world,n_games", [(1, N_GAMES), (2, N_GAMES), (3, 2)])
+def test_sharded_selfplay_gloo(tmp_path, world, n_games):
+    """(3, 2): rank 2's shard is empty (it sends nothing)."""
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), n_games), nprocs=world,
                        start_method="spawn")
     got = np.load(tmp_path / f"world{world}.npz")
     # every game, in global order, equals the single-engine reference run
-    ref = oracle_runner(0, N_GAMES, BASE_SEED)
+    ref = oracle_runner(0, n_games, BASE_SEED)
     np.testing.assert_array_equal(got["lengths"], ref["lengths"])
+    # rank 0 received exactly the other ranks' compact games (8+1+8 B per game,
+    # 1 + 8*A + 2 B per sample), nothing of its own
+    c0 = n_games // world + (1 if n_games % world else 0)
+    rest_t = int(ref["lengths"][c0:].sum())
+    assert int(got["wire"]) == 17 * (n_games - c0) + (H * W + 8 * W + 2) * rest_t
     off = 0
-    for g in range(N_GAMES):
+    for g in range(n_games):
         t = int(ref["lengths"][g])
         np.testing.assert_array_equal(got["moves"][off:off + t], ref["moves"][g, :t])
         np.testing.assert_array_equal(got["policies"][off:off + t], ref["policies"][g, :t])

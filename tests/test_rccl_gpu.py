@@ -75,7 +75,7 @@ def _worker(rank, port, outdir):
     assert devices == [0]
     eng = az.Engine(H, W, N, True, S, slots=8, evaluator=az.EVAL_NETWORK, compact=True)
     eng.set_weights(named)
-    g = D.selfplay_sharded(D.engine_runner(eng), N_GAMES, BASE_SEED)  # gather: RCCL all_gather on cuda:0
+    g = D.selfplay_sharded(D.engine_runner(eng), N_GAMES, BASE_SEED)  # gather: RCCL gather (+ point-to-point for other ranks) on cuda:0
     eng.close()
     np.savez(os.path.join(outdir, "rccl.npz"), **g)
     dist.barrier()

@@ -34,6 +34,59 @@ def test_crc32c_chunked_path_equals_bytewise():
         assert T.unmask(T.mask(v)) == v
 
 
+def _crc32c_bitwise(data, crc=0):
+    """CRC-32C bit by bit (an implementation independent of the module's tables);
+    `crc` continues an earlier result (crc32c::Extend)."""
+    crc ^= 0xFFFFFFFF
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+    return crc ^ 0xFFFFFFFF
+
+
+def _mask_hand(c):
+    return ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+def test_string_tensor_follows_tensorflow_layout():
+    """TF's WriteStringTensor (tensor_bundle.cc): varint64 lengths, then the
+    masked crc32c of the lengths taken as little-endian uint32 words, then the
+    bytes; the entry crc32c is that length crc extended over the 4 masked
+    bytes and the string bytes.  Hand-assembled here for a 200-byte scalar
+    (a 2-byte varint length, so the varint and uint32 forms differ) and a
+    3-element vector."""
+    s = bytes(range(200))
+    lcrc = _crc32c_bitwise(struct.pack("<I", 200))
+    masked = struct.pack("<I", _mask_hand(lcrc))
+    raw = bytes([0xC8, 0x01]) + masked + s
+    entry_crc = _crc32c_bitwise(s, _crc32c_bitwise(masked, lcrc))
+    assert T._encode_string(s) == (raw, entry_crc)
+    assert T._decode_strings(raw, ()) == (s, entry_crc)
+    vec = [b"ab", b"", b"x" * 130]
+    lw = struct.pack("<III", 2, 0, 130)
+    lcrc = _crc32c_bitwise(lw)
+    masked = struct.pack("<I", _mask_hand(lcrc))
+    raw = bytes([2, 0, 0x82, 0x01]) + masked + b"".join(vec)
+    assert T._decode_strings(raw, (3,)) == (vec, _crc32c_bitwise(b"".join(vec), _crc32c_bitwise(masked, lcrc)))
+    bad = bytearray(raw)
+    bad[4] ^= 1
+    with pytest.raises(ValueError, match="lengths checksum"):
+        T._decode_strings(bytes(bad), (3,))
+
+
+def test_checkpoint_string_entry_carries_the_tensorflow_crc(tmp_path):
+    prefix = str(tmp_path / "model")
+    g = b"\x0a\x05hello" * 30
+    T.write_checkpoint(prefix, {T.OBJECT_GRAPH_KEY: g, "v": np.arange(3, dtype=np.float32)})
+    rows = dict(T.read_table(prefix + ".index"))
+    e = T._parse_entry(rows[T.OBJECT_GRAPH_KEY.encode()])
+    lcrc = _crc32c_bitwise(struct.pack("<I", len(g)))
+    masked = struct.pack("<I", _mask_hand(lcrc))
+    assert e["crc32c"] == _crc32c_bitwise(g, _crc32c_bitwise(masked, lcrc))
+    assert T.read_checkpoint(prefix)[T.OBJECT_GRAPH_KEY] == g
+
+
 def test_snappy_literals_and_overlapping_copies():
     # "abcd" literal, then a 1-byte-offset copy of 8 from offset 4 (overlaps
     # its own output), then a 2-byte-offset copy of 3 from offset 12
