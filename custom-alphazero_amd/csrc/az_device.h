@@ -28,6 +28,7 @@ struct GameCfg {
   int noise;                    // ConfigMCTS.enable_dirichlet_noise (config.py:52): root Dirichlet noise
   double noise_alpha;           // dirichlet_noise_value (config.py:53)
   double noise_ratio;           // dirichlet_noise_ratio (config.py:54)
+  int rng_skip;                 // MT19937 words a game's stream discards after seeding (az_config.rng_skip)
 };
 
 // Edge::action carries the action index in its low 14 bits; kPrior64 marks

@@ -89,6 +89,8 @@ struct az_engine {
   float* host_v = nullptr;
   int32_t* host_n = nullptr;
   double* uniforms = nullptr;
+  double* noise_buf = nullptr;  // az_tree_search_noise: the caller's root-noise rows
+  size_t noise_cap = 0;
   int32_t* dev_i32 = nullptr;  // scratch for az_tree_reset
   az::Board* dev_boards = nullptr;
   std::vector<void*> owned;
@@ -142,6 +144,7 @@ int check_device_errors(az_engine* e) {
     if (err & az::kErrPath) m += " path-overflow";
     if (err & az::kErrIllegal) m += " illegal-move";
     if (err & az::kErrNoRoot) m += " play-before-search";
+    if (err & az::kErrNoise) m += " root-noise-rows-exhausted(pass a row per root selection)";
     if (err & az::kErrActRange)
       m += " activation-range(a non-finite activation, or |x| > 32752 in the per-layer fp16x2 convs: "
            "use conv_algo=AZ_CONV_F16X2 or AZ_CONV_DIRECT)";
@@ -742,6 +745,11 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   g.noise = c.dirichlet_noise != 0;
   g.noise_alpha = c.dirichlet_alpha;
   g.noise_ratio = c.dirichlet_ratio;
+  g.rng_skip = c.rng_skip;
+  if (c.rng_skip < 0) {
+    delete e;
+    return fail(AZ_E_INVALID, "rng_skip must be >= 0");
+  }
   if (g.noise && !(c.dirichlet_alpha > 0.0 && c.dirichlet_alpha <= 1.0 && std::isfinite(c.dirichlet_ratio))) {
     delete e;
     return fail(AZ_E_INVALID, "Dirichlet noise needs 0 < dirichlet_alpha <= 1 (the reference's 0.03) and a "
@@ -1375,15 +1383,46 @@ int az_tree_release(az_engine* e, int n, const int32_t* slots) {
 
 int az_tree_search(az_engine* e, int n_sims) {
   if (!e || n_sims < 0) return fail(AZ_E_INVALID, "bad arguments");
-  if (e->g.noise)  // its draws come from each game's own stream, which self-play owns
-    return fail(AZ_E_INVALID, "Dirichlet root noise runs in self-play (az_selfplay_*); the tree API "
-                              "engine must be created with dirichlet_noise = 0");
+  if (e->g.noise)  // the tree API's noise is drawn by the caller from numpy's global stream
+    return fail(AZ_E_INVALID, "this engine mixes Dirichlet root noise: search it with az_tree_search_noise "
+                              "(the caller's np.random.dirichlet draws)");
   int rc;
   if ((rc = ready_to_search(e))) return rc;
   if (int rc_ = enter(e)) return rc_;
   if (int rc_ = tree_api_ok(e)) return rc_;
   for (int s = 0; s < n_sims; ++s)
     if ((rc = simulate(e, e->whole))) return rc;
+  AZ_HIP(hipStreamSynchronize(e->stream));
+  return check_device_errors(e);
+}
+
+int az_tree_search_noise(az_engine* e, int n_sims, const double* noise, int rows) {
+  if (!e || n_sims < 0 || rows < 0 || (rows > 0 && !noise)) return fail(AZ_E_INVALID, "bad arguments");
+  if (!e->g.noise)
+    return fail(AZ_E_INVALID, "az_tree_search_noise needs an engine created with dirichlet_noise = 1");
+  int rc;
+  if ((rc = ready_to_search(e))) return rc;
+  if (int rc_ = enter(e)) return rc_;
+  if (int rc_ = tree_api_ok(e)) return rc_;
+  const size_t S = (size_t)e->g.slots, n = S * (size_t)std::max(rows, 1) * e->g.A;
+  az::TreeDev& t = e->whole.t;
+  if (n > e->noise_cap) {  // grown on demand, kept for the next searches
+    double* buf = nullptr;
+    if ((rc = e->alloc(&buf, n))) return rc;
+    e->noise_buf = buf;
+    e->noise_cap = n;
+  }
+  if (!t.noise_cur && (rc = e->alloc(&t.noise_cur, S))) return rc;
+  if (rows) AZ_HIP(hipMemcpyAsync(e->noise_buf, noise, S * rows * e->g.A * sizeof(double), hipMemcpyHostToDevice,
+                                  e->stream));
+  AZ_HIP(hipMemsetAsync(t.noise_cur, 0, S * sizeof(int32_t), e->stream));
+  t.noise_in = e->noise_buf;
+  t.noise_rows = rows;
+  rc = 0;
+  for (int s = 0; s < n_sims && !rc; ++s) rc = simulate(e, e->whole);
+  t.noise_in = nullptr;  // self-play keeps drawing on the device
+  t.noise_rows = 0;
+  if (rc) return rc;
   AZ_HIP(hipStreamSynchronize(e->stream));
   return check_device_errors(e);
 }

@@ -38,7 +38,8 @@ enum : int {
 };
 enum : unsigned long long {
   kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16,
-  kErrActRange = 32  // a conv16 activation beyond the split16 range (|x| > 32752)
+  kErrActRange = 32,  // a conv16 activation beyond the split16 range (|x| > 32752)
+  kErrNoise = 64      // the tree API's host-drawn root noise ran out of rows
 };
 
 // All device state of a forest (struct of arrays over slots).
@@ -100,6 +101,12 @@ struct TreeDev {
   int32_t* last_move;          // [slots] action played (-1 none)
   int32_t* last_status;        // [slots] 0 ongoing / 1 win / 2 draw
   double* last_policy;         // [slots][A]
+  // tree API root noise drawn by the host (az_tree_search_noise): slot s's
+  // r-th root selection of the search mixes noise_in[(s * noise_rows + r) * A + i]
+  // into edge i's prior; null: self-play draws on the device from the slot's MT19937
+  const double* noise_in;
+  int32_t* noise_cur;          // [slots] rows consumed
+  int32_t noise_rows;
 };
 
 // Transposition cache = the reference's plays_inferences (mcts/mcts.py:122-143,

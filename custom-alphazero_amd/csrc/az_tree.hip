@@ -155,6 +155,9 @@ __device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gi
   t.last_move[s] = -1;
   t.last_status[s] = kOngoing;
   mt_seed(t, t.mt_stride, s, seed);
+  // the reference's play_game draws np.random.rand(1, H, W, 4) building its
+  // model between the seed and the game (az_config.rng_skip)
+  for (int k = 0; k < g.rng_skip; ++k) (void)mt_next(t, t.mt_stride, s);
 }
 
 // ------------------------------------------------------------------- select
@@ -292,8 +295,10 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
 // ---------------------------------------------------- Dirichlet root noise
 // get_best_edge_with_noise (mcts.py:70-85), used by select at the current
 // root when ConfigMCTS.enable_dirichlet_noise is set (:113-116): a fresh
-// np.random.dirichlet(alpha * ones(k)) from the game's MT19937 stream per
-// root selection (az_random.h), mixed into the priors as numpy computes
+// np.random.dirichlet(alpha * ones(k)) per root selection -- in self-play
+// from the game's MT19937 stream on the device (az_random.h), in the tree
+// API drawn by the host from numpy's global stream (TreeDev::noise_in) --
+// mixed into the priors as numpy computes
 // (1 - ratio) * priors + ratio * noise -- the first product in the priors'
 // dtype (float32, or float64 after the uniform branch: kPrior64), the rest
 // float64 -- and the UCB with that prior; np.argmax treats NaN as the maximum.
@@ -338,16 +343,26 @@ __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t
     double best_v = 0.0;
     if (NOISE && depth == 0) {
       double gam[kMaxActions], acc = 0.0;
-      SlotMt r{&t, s};
-      for (int i = 0; i < cnt; ++i) {
-        gam[i] = legacy_standard_gamma(r, g.noise_alpha);
-        acc = acc + gam[i];
+      const double* hn = nullptr;  // tree API: the host's normalised draw
+      if (t.noise_in) {
+        const int row = t.noise_cur[s]++;
+        if (row >= t.noise_rows) {
+          flag_error(t, kErrNoise);
+          return;
+        }
+        hn = t.noise_in + ((size_t)s * t.noise_rows + row) * g.A;
+      } else {
+        SlotMt r{&t, s};
+        for (int i = 0; i < cnt; ++i) {
+          gam[i] = legacy_standard_gamma(r, g.noise_alpha);
+          acc = acc + gam[i];
+        }
       }
       const double invacc = 1 / acc;
       for (int i = 0; i < cnt; ++i) {
         const Edge e = E[first + i];
         const double q = e.N ? e.W / (double)e.N : 0.0;
-        const double u = g.c_puct * noisy_prior(g, e, gam[i] * invacc) * sq / (double)(1 + e.N);
+        const double u = g.c_puct * noisy_prior(g, e, hn ? hn[i] : gam[i] * invacc) * sq / (double)(1 + e.N);
         const double ucb = q + u;
         if (i == 0 || argmax_before(ucb, i, best_v, best)) {
           best = i;
@@ -457,23 +472,37 @@ __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, Tre
     double best_v = -INFINITY;
     int best = L;
     if (NOISE && depth == 0) {
-      // the group walks the root's k gamma draws in order; its first lane
-      // (the slot's RNG owner) draws, each lane keeps its edge's
-      double acc = 0.0, gj = 0.0;
-      for (int k = 0; k < cnt; ++k) {  // group-uniform
-        double gv = 0.0;
-        if (j == 0) {
-          SlotMt r{&t, s};
-          gv = legacy_standard_gamma(r, g.noise_alpha);
+      double dj = 0.0;  // this lane's edge's noise component
+      if (t.noise_in) {
+        // tree API: the host drew the vector from numpy's global stream
+        int row = 0;
+        if (j == 0) row = t.noise_cur[s]++;
+        row = __shfl(row, 0, L);
+        if (row >= t.noise_rows) {
+          if (j == 0) flag_error(t, kErrNoise);
+          return;
         }
-        gv = __shfl(gv, 0, L);
-        if (k == j) gj = gv;
-        acc = acc + gv;
+        if (mine) dj = t.noise_in[((size_t)s * t.noise_rows + row) * g.A + j];
+      } else {
+        // the group walks the root's k gamma draws in order; its first lane
+        // (the slot's RNG owner) draws, each lane keeps its edge's
+        double acc = 0.0, gj = 0.0;
+        for (int k = 0; k < cnt; ++k) {  // group-uniform
+          double gv = 0.0;
+          if (j == 0) {
+            SlotMt r{&t, s};
+            gv = legacy_standard_gamma(r, g.noise_alpha);
+          }
+          gv = __shfl(gv, 0, L);
+          if (k == j) gj = gv;
+          acc = acc + gv;
+        }
+        const double invacc = 1 / acc;
+        dj = gj * invacc;
       }
-      const double invacc = 1 / acc;
       if (mine) {
         const double q = e.N ? e.W / (double)e.N : 0.0;
-        const double u = g.c_puct * noisy_prior(g, e, gj * invacc) * sq / (double)(1 + e.N);
+        const double u = g.c_puct * noisy_prior(g, e, dj) * sq / (double)(1 + e.N);
         best_v = q + u;
         best = j;
       }

@@ -99,11 +99,13 @@ def check_mcts_config(path: str = "tree"):
     """Refuse MCTS settings an engine path does not implement instead of
     silently ignoring them.  Dirichlet root noise (mcts.py:70-85, used by
     select at :113-116; disabled in the reference, config.py:52) runs in
-    Connect-N self-play (path "selfplay": self_play.play / play_game), whose
-    games own their np.random streams on the device (MT19937 seeded like
-    self_play.py:45).  The single-tree MCTS API, the arena and chess draw
-    from the caller's np.random instead and refuse it."""
-    if ConfigMCTS.enable_dirichlet_noise and path != "selfplay":
+    Connect-N self-play (path "selfplay": self_play.play / play_game, whose
+    games own their np.random streams on the device, MT19937 seeded like
+    self_play.py:45) and in the Connect-N tree API and arena (path "tree":
+    the caller's np.random.dirichlet draws, az_tree_search_noise).  Chess
+    (path "chess") has no root noise: the reference's chess MCTS cannot run
+    (chess/board.py:178 vs mcts.py:179), so there is no behaviour to match."""
+    if ConfigMCTS.enable_dirichlet_noise and path == "chess":
         raise NotImplementedError(
-            "ConfigMCTS.enable_dirichlet_noise=True runs in Connect-N self-play (self_play.play / "
-            "play_game) on the MI355X engine; the MCTS tree API, the arena and chess do not draw it")
+            "ConfigMCTS.enable_dirichlet_noise=True is not implemented for chess on the MI355X engine "
+            "(Connect-N self-play, MCTS and the arena draw it)")

@@ -36,7 +36,7 @@ class Config(ctypes.Structure):
         ("lanes", ctypes.c_int32), ("compact", ctypes.c_int32),
         ("tower_natural_order", ctypes.c_int32), ("dirichlet_noise", ctypes.c_int32),
         ("dirichlet_alpha", ctypes.c_double), ("dirichlet_ratio", ctypes.c_double),
-        ("reserved", ctypes.c_int32 * 2),
+        ("rng_skip", ctypes.c_int32), ("reserved", ctypes.c_int32 * 1),
     ]
 
 
@@ -94,7 +94,7 @@ def _as_numpy(t):
 EXPORTED = (
     "az_abi_version", "az_last_error", "az_build_id", "az_build_flags", "az_engine_create", "az_engine_destroy",
     "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
-    "az_selfplay_run", "az_selfplay_results", "az_selfplay_drain", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_play",
+    "az_selfplay_run", "az_selfplay_results", "az_selfplay_drain", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_search_noise", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
     "az_cache_clear", "az_cache_enable", "az_engine_set_evaluator",
     # include/az_chess.h
@@ -145,6 +145,7 @@ def load_library():
         "az_tree_reset": (ctypes.c_int, [P, ctypes.c_int, P, P]),
         "az_tree_release": (ctypes.c_int, [P, ctypes.c_int, P]),
         "az_tree_search": (ctypes.c_int, [P, ctypes.c_int]),
+        "az_tree_search_noise": (ctypes.c_int, [P, ctypes.c_int, P, ctypes.c_int]),
         "az_tree_play": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, P, P, P]),
         "az_tree_info": (ctypes.c_int, [P, ctypes.c_int, P, P]),
         "az_tree_export": (ctypes.c_int, [P, ctypes.c_int, P, P, P, P, P, P, P]),
@@ -236,12 +237,16 @@ class Engine:
                  filters=128, depth=4, value_hidden=256, bn_epsilon=1e-3, arena_edges=0,
                  max_tree_visits=0, device=0, cache_log2=0, conv_algo=CONV_F16X2,
                  lanes=0, compact=False, tower_natural_order=False, dirichlet_noise=False,
-                 dirichlet_alpha=0.03, dirichlet_ratio=0.25):
+                 dirichlet_alpha=0.03, dirichlet_ratio=0.25, rng_skip=None):
         """compact=True reclaims the subtrees a self-play game has left after
         every move (az_config.compact; arena_edges is then per half); keep it
         off for the tree API (az_tree_*), whose views need the whole tree.
         dirichlet_noise: ConfigMCTS.enable_dirichlet_noise (root noise,
-        reference mcts.py:70-85) with dirichlet_alpha / dirichlet_ratio."""
+        reference mcts.py:70-85) with dirichlet_alpha / dirichlet_ratio.
+        rng_skip: MT19937 words a self-play game's stream discards after
+        seeding; None = the reference play_game's model construction
+        (np.random.rand(1, H, W, 4): 2 H W 4 words), so game g of a batch is
+        the reference's play_game under np.random.seed(base_seed + g)."""
         L = load_library()
         self.height, self.width, self.n, self.gravity = height, width, n, bool(gravity)
         self.action_space = width if gravity else width * height
@@ -256,7 +261,8 @@ class Engine:
                      lanes=lanes, compact=int(bool(compact)),
                      tower_natural_order=int(bool(tower_natural_order)),
                      dirichlet_noise=int(bool(dirichlet_noise)), dirichlet_alpha=float(dirichlet_alpha),
-                     dirichlet_ratio=float(dirichlet_ratio))
+                     dirichlet_ratio=float(dirichlet_ratio),
+                     rng_skip=2 * height * width * 4 if rng_skip is None else int(rng_skip))
         handle = ctypes.c_void_p()
         _check(L.az_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
         self._h = handle
@@ -406,8 +412,17 @@ class Engine:
         slots = np.ascontiguousarray(slots, np.int32)
         _check(self._L.az_tree_release(self._h, len(slots), _ptr(slots)))
 
-    def tree_search(self, n_sims):
-        self._search_call(self._L.az_tree_search(self._h, int(n_sims)))
+    def tree_search(self, n_sims, noise=None):
+        """noise (engines made with dirichlet_noise): [slots, rows, A] float64,
+        row r of slot s the np.random.dirichlet vector its r-th root selection
+        mixes in (az_tree_search_noise)."""
+        if noise is None:
+            self._search_call(self._L.az_tree_search(self._h, int(n_sims)))
+            return
+        noise = np.ascontiguousarray(noise, np.float64)
+        if noise.ndim != 3 or noise.shape[0] != self.slots or noise.shape[2] != self.action_space:
+            raise ValueError(f"noise must be [slots={self.slots}, rows, A={self.action_space}], got {noise.shape}")
+        self._search_call(self._L.az_tree_search_noise(self._h, int(n_sims), _ptr(noise), int(noise.shape[1])))
 
     def tree_play(self, uniforms=None, greedy=False, deterministic=False):
         S, A = self.slots, self.action_space

@@ -9,7 +9,9 @@
   other engine's copy idle).  With deterministic=True the per-game results are
   those of the sequential loop; with stochastic play each game draws from its
   own RandomState(seed + game) instead of the shared np.random stream (the
-  only difference; the draw count per move is the reference's).
+  only difference; the draw count per move is the reference's).  Dirichlet
+  root noise (ConfigMCTS.enable_dirichlet_noise) is drawn the same way: the
+  search's root-noise vectors, then play's draw, from the game's stream.
 The exact-solver scoring path needs the refused c4solver binary (SURVEY.md
 section 8c) and raises NotImplementedError.
 """
@@ -22,7 +24,7 @@ from custom_alphazero.config import (ConfigConnectN, ConfigMCTS, ConfigModel, Co
                                      ConfigServing, check_mcts_config)
 from custom_alphazero.connect_n.board import Board
 from custom_alphazero.connect_n.move import Move
-from custom_alphazero.mcts.mcts import MCTS
+from custom_alphazero.mcts.mcts import MCTS, root_noise_rows
 from custom_alphazero.mcts.utils import normalize_probabilities
 
 get_all_possible_moves = Board.get_all_possible_moves
@@ -59,16 +61,20 @@ def _single_game_evaluation(current_model, previous_model, game_index: int,
         mcts = MCTS(board=Board(), all_possible_moves=all_possible_moves, concurrency=False,
                     model=model, plays_inferences={})
         while not mcts.board.is_game_over():
-            mcts.search(ConfigSelfPlay.mcts_iterations)
             greedy = mcts.board.fullmove_number > ConfigMCTS.index_move_greedy
-            if rng is not np.random and not deterministic:
-                # the shim draws from np.random; route this game's stream through it
+            if rng is not np.random and (not deterministic or ConfigMCTS.enable_dirichlet_noise):
+                # the shim draws (root noise in search, the move in play) from
+                # np.random; route this game's stream through it
                 state = np.random.get_state()
                 np.random.set_state(rng.get_state())
-                mcts.play(greedy, deterministic=deterministic)
-                rng.set_state(np.random.get_state())
-                np.random.set_state(state)
+                try:
+                    mcts.search(ConfigSelfPlay.mcts_iterations)
+                    mcts.play(greedy, deterministic=deterministic)
+                finally:
+                    rng.set_state(np.random.get_state())
+                    np.random.set_state(state)
             else:
+                mcts.search(ConfigSelfPlay.mcts_iterations)
                 mcts.play(greedy, deterministic=deterministic)
             if not mcts.board.is_game_over():
                 model = previous_model if mcts.model is current_model else current_model
@@ -112,7 +118,9 @@ def _arena_engine(model, n_slots: int) -> az.Engine:
                     exploration_constant=ConfigMCTS.exploration_constant,
                     filters=ConfigModel.filters, depth=ConfigModel.depth,
                     value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon,
-                    lanes=1)
+                    lanes=1, dirichlet_noise=ConfigMCTS.enable_dirichlet_noise,
+                    dirichlet_alpha=ConfigMCTS.dirichlet_noise_value,
+                    dirichlet_ratio=ConfigMCTS.dirichlet_noise_ratio)
     eng.set_weights(model.engine_weights())
     return eng
 
@@ -158,7 +166,17 @@ def evaluate_two_models_batched(model, other_model, n_games: Optional[int] = Non
                     eng.tree_release(stale)
                 eng.tree_reset(idx, np.stack([boards[g].array for g in idx]))
                 active[s] = set(idx)
-                eng.tree_search(ConfigSelfPlay.mcts_iterations)
+                sims = ConfigSelfPlay.mcts_iterations
+                if ConfigMCTS.enable_dirichlet_noise:
+                    # each move's MCTS starts on an unexpanded root (evaluate.py:64-83):
+                    # sims - 1 root selections draw from the game's stream, before play's draw
+                    rows = max(sims - 1, 0)
+                    noise = np.zeros((n, max(rows, 1), A))
+                    for g in idx:
+                        noise[g] = root_noise_rows(rngs[g], len(boards[g].moves), rows, A)
+                    eng.tree_search(sims, noise=noise)
+                else:
+                    eng.tree_search(sims)
                 u = None
                 if not deterministic:
                     u = np.zeros(n)

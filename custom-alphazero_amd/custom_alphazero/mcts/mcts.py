@@ -81,6 +81,17 @@ class UCTNode:
         return self.edges[int(np.argmax([e.upper_confidence_bound() for e in self.edges]))]
 
 
+def root_noise_rows(rng, k: int, rows: int, A: int) -> np.ndarray:
+    """`rows` root-noise vectors as get_best_edge_with_noise draws them
+    (mcts.py:74-78: rng.dirichlet(ones(k) * dirichlet_noise_value) for the
+    root's k edges), padded to the action space: [max(rows, 1), A]."""
+    out = np.zeros((max(rows, 1), A), np.float64)
+    alpha = np.ones(k) * ConfigMCTS.dirichlet_noise_value
+    for r in range(rows):
+        out[r, :k] = rng.dirichlet(alpha)
+    return out
+
+
 def _engine_for(model, all_possible_moves) -> az.Engine:
     c = ConfigConnectN
     if isinstance(model, SyntheticEvaluator):
@@ -104,7 +115,10 @@ def _engine_for(model, all_possible_moves) -> az.Engine:
                     exploration_constant=ConfigMCTS.exploration_constant,
                     filters=ConfigModel.filters, depth=ConfigModel.depth,
                     value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon,
-                    arena_edges=max(sims, 1024) * HW * A, max_tree_visits=max(sims, 1024) * HW + 2)
+                    arena_edges=max(sims, 1024) * HW * A, max_tree_visits=max(sims, 1024) * HW + 2,
+                    dirichlet_noise=ConfigMCTS.enable_dirichlet_noise,
+                    dirichlet_alpha=ConfigMCTS.dirichlet_noise_value,
+                    dirichlet_ratio=ConfigMCTS.dirichlet_noise_ratio)
     if evaluator == az.EVAL_NETWORK:
         eng.set_weights(model.engine_weights())
     elif evaluator == az.EVAL_HOST:
@@ -142,7 +156,19 @@ class MCTS:
         check_mcts_config()
         if self.board.is_game_over():
             return
-        self._engine.tree_search(int(iterations_number))
+        n = int(iterations_number)
+        if not ConfigMCTS.enable_dirichlet_noise:
+            self._engine.tree_search(n)
+            return
+        # get_best_edge_with_noise (mcts.py:70-85): every select whose root
+        # has edges draws np.random.dirichlet from the global stream -- all n
+        # selections, or n - 1 when the first one expands the root (:111-120);
+        # nothing else in a search draws, so drawing them up front takes the
+        # same words in the same order
+        expanded = self._engine.tree_export(0)["root_n"] > 0
+        rows = n if expanded else max(n - 1, 0)
+        noise = root_noise_rows(np.random, len(self.board.moves), rows, len(self.all_possible_moves))
+        self._engine.tree_search(n, noise=noise[None])
 
     def play(self, greedy: bool = False, return_details: bool = False,
              deterministic: bool = False) -> Union[Tuple[np.ndarray, np.ndarray, np.ndarray, Move], Board]:
@@ -268,7 +294,7 @@ class ChessMCTS(MCTS):
         self.path_cache = []
 
     def search(self, iterations_number: int):
-        check_mcts_config()
+        check_mcts_config("chess")
         if self.board.is_game_over():
             return
         self._engine.tree_search(int(iterations_number))

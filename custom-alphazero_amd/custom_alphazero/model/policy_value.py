@@ -39,6 +39,12 @@ class PolicyValueModel:
         self._engine = None
         self._engine_version = -1
         self._version = 0
+        # the reference's constructor runs a dummy forward on
+        # np.random.rand(1, *input_dim) (model/tensorflow/model.py:167-169):
+        # the same draws from numpy's global stream, so a caller seeding
+        # np.random before building the model (self_play.play_game) sees the
+        # reference's stream afterwards
+        np.random.rand(1, *self.input_dim)
 
     # ------------------------------------------------------------ weights
     def engine_weights(self):

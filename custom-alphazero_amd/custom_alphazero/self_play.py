@@ -7,7 +7,9 @@
 * play(...) is the batched path: ConfigSelfPlay.games_per_call games run on
   the device at once (ConfigSelfPlay.concurrent_games trees in flight, slots
   refilled as games end), replacing the reference's one-game-per-process
-  joblib fan-out (self_play.py:98-110).  Game g is seeded MT19937(base_seed+g).
+  joblib fan-out (self_play.py:98-110).  Game g is the reference's play_game
+  under np.random.seed(base_seed + g): MT19937(base_seed + g) past the
+  2 H W 4 words its model construction draws (az_config.rng_skip).
 """
 import json
 import os
@@ -42,11 +44,17 @@ def play_game(process_id: int, all_possible_moves: List[Move], mcts_iterations: 
     seed = int((process_id + 1) * time.time()) % (2 ** 32 - 1)
     np.random.seed(seed)
     if model is None:
-        model = best_saved_model(run_id)
+        model = best_saved_model(run_id)  # its constructor draws np.random.rand(1, *input_dim)
+    elif ConfigGeneral.game != "chess":
+        # a caller's model: take the draws the reference's model construction
+        # makes at this point (model/tensorflow/model.py:167-169)
+        c = ConfigConnectN
+        np.random.rand(1, c.board_height, c.board_width, 4)
     if ConfigMCTS.enable_dirichlet_noise and ConfigGeneral.game != "chess":
         # root noise draws from the game's own stream: the game runs on the
         # batched engine as game 0 of a one-game batch seeded like this
-        # process (MT19937(seed): the same stream np.random.seed(seed) starts)
+        # process -- MT19937(seed) past the model construction's 2 H W 4 words
+        # (az_config.rng_skip), the stream np.random holds here
         states, policies, rewards, records = play(run_id, plays_inferences, model=model, n_games=1,
                                                   base_seed=seed, sims=mcts_iterations)
         return states, policies, rewards, records[0]

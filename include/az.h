@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 8
+#define AZ_ABI_VERSION 9
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */
@@ -92,11 +92,18 @@ typedef struct az_config {
                                       (no slot plan, no skipped edge taps): bitwise the same outputs
                                       (tests, A/B runs); 0 = the slot plan (default) */
     int32_t dirichlet_noise;       /* ConfigMCTS.enable_dirichlet_noise (config.py:52): every root
-                                      selection mixes the priors with a fresh Dirichlet draw from the
-                                      game's MT19937 stream (mcts.py:70-85, :115-116) */
+                                      selection mixes the priors with a fresh Dirichlet draw
+                                      (mcts.py:70-85, :115-116) -- in self-play from the game's
+                                      MT19937 stream, in the tree API the caller's draws
+                                      (az_tree_search_noise) */
     double dirichlet_alpha;        /* ConfigMCTS.dirichlet_noise_value (config.py:53, 0.03) */
     double dirichlet_ratio;        /* ConfigMCTS.dirichlet_noise_ratio (config.py:54, 0.25) */
-    int32_t reserved[2];
+    int32_t rng_skip;              /* MT19937 words each self-play game's stream discards after seeding
+                                      (ABI 9): the reference's play_game seeds np.random, then builds
+                                      the model, whose constructor draws np.random.rand(1, H, W, 4)
+                                      (self_play.py:45-47, model/tensorflow/model.py:167-169): 2*H*W*4
+                                      words.  0 = none */
+    int32_t reserved[1];
 } az_config;
 
 /* One named weight tensor in Keras layout ("Weights"). */
@@ -223,6 +230,15 @@ int az_tree_reset(az_engine* eng, int n, const int32_t* slots, const int8_t* boa
  * engine per model and hand each game to the engine whose model moves. */
 int az_tree_release(az_engine* eng, int n, const int32_t* slots);
 int az_tree_search(az_engine* eng, int n_sims);
+/* az_tree_search on an engine created with dirichlet_noise = 1 (ABI 9): the
+ * reference draws np.random.dirichlet(alpha * ones(k)) from numpy's global
+ * stream at every root selection of MCTS.select (mcts.py:70-85, :113-116),
+ * so the caller draws them: noise [slots][rows][A] float64, row r of slot s
+ * the normalised vector of its r-th root selection in this search (component
+ * i for root edge i; a search on an unexpanded root makes n_sims - 1 root
+ * selections, on an expanded one n_sims).  Fails with AZ_E_DEVICE
+ * (root-noise-rows-exhausted) when a slot needs more rows. */
+int az_tree_search_noise(az_engine* eng, int n_sims, const double* noise, int rows);
 /* MCTS.play(greedy, deterministic) (mcts.py:182-222) on every active slot:
  * uniforms [slots] are the np.random.random_sample draws np.random.choice
  * would consume (ignored when deterministic); outputs per slot: moves

@@ -591,6 +591,11 @@ typedef struct {
  *   at the moment each move was played), policy[T][A] (float64), boards[T][H*W]
  *   (the canonical root board before each move), rewards[T] (int64).
  */
+/* MT19937 words each game's stream discards after seeding; -1 = the
+ * reference play_game's model-construction draws, 2 * H * W * 4 */
+static int orc_rng_skip = -1;
+void orc_set_rng_skip(int words) { orc_rng_skip = words; }
+
 int orc_play_game(int H, int W, int n, int gravity, int sims, uint32_t seed, int eval_kind,
                   orc_table* table, orc_eval_cb cb, void* cb_ctx, int32_t* moves, uint8_t* greedy,
                   int32_t* n_edges, int32_t* edge_action, double* edge_prior, int64_t* edge_n,
@@ -610,6 +615,11 @@ int orc_play_game(int H, int W, int n, int gravity, int sims, uint32_t seed, int
     if (HW > ORC_MAX_CELLS || A > ORC_MAX_ACTIONS) return -1;
     orc_mt rng;
     orc_mt_seed(&rng, seed);
+    /* self_play.play_game seeds np.random, then builds the model, whose
+     * constructor runs a dummy forward on np.random.rand(1, H, W, 4)
+     * (model/tensorflow/model.py:167-169): 2 words per double */
+    const int skip = orc_rng_skip >= 0 ? orc_rng_skip : 2 * HW * 4;
+    for (int i = 0; i < skip; ++i) (void)orc_mt_next(&rng);
     t.rng = &rng;
     int8_t board[ORC_MAX_CELLS];
     memset(board, 0, sizeof(board));

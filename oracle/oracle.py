@@ -66,6 +66,8 @@ def lib():
         L.orc_play_game.restype = ctypes.c_int
         L.orc_set_noise.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double]
         L.orc_set_noise.restype = None
+        L.orc_set_rng_skip.argtypes = [ctypes.c_int]
+        L.orc_set_rng_skip.restype = None
         L.orc_dirichlet_draws.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_int, ctypes.c_int, P]
         L.orc_dirichlet_draws.restype = None
         L.orc_play_game.argtypes = (
@@ -165,19 +167,23 @@ def dirichlet_draws(seed, alpha, k, n):
 
 
 def play_game(height, width, n, gravity, sims, seed, evaluator="synth", table=None,
-              callback=None, noise=None):
+              callback=None, noise=None, rng_skip=None):
     """One reference self-play game (self_play.py:37-82) on the C oracle.
 
     evaluator: "synth" (oracle/synth.py), "table" (EvalTable), or "callback"
     (python callable board[H,W] int8 -> (probs[A] f32, value f32)).
     noise: None, or (alpha, ratio) -- ConfigMCTS.enable_dirichlet_noise with
     dirichlet_noise_value / dirichlet_noise_ratio (mcts.py:70-85).
+    rng_skip: MT19937 words discarded after seeding; None = the reference
+    play_game's model construction, np.random.rand(1, H, W, 4) (2 H W 4).
     """
     lib().orc_set_noise(int(noise is not None), *(noise if noise is not None else (0.03, 0.25)))
+    lib().orc_set_rng_skip(-1 if rng_skip is None else int(rng_skip))
     try:
         return _play_game(height, width, n, gravity, sims, seed, evaluator, table, callback)
     finally:
         lib().orc_set_noise(0, 0.03, 0.25)
+        lib().orc_set_rng_skip(-1)
 
 
 def _play_game(height, width, n, gravity, sims, seed, evaluator, table, callback):

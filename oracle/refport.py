@@ -252,6 +252,9 @@ class PortMCTS:
 def play_game(height, width, n, gravity, sims, seed, evaluator, greedy_ply=8, cache=None):
     """self_play.play_game (self_play.py:37-82) with an explicit seed."""
     np.random.seed(int(seed) % (2 ** 32 - 1))
+    # best_saved_model -> PolicyValueModel.__init__'s dummy forward on
+    # np.random.rand(1, *input_dim) (model/tensorflow/model.py:167-169)
+    np.random.rand(1, height, width, 4)
     A = width if gravity else width * height
     mcts = PortMCTS(PortBoard(height, width, n, gravity), evaluator, {} if cache is None else cache)
     states, policies, moves = [], [], []

@@ -45,11 +45,15 @@ class _Tensor:
 
 
 class StubPolicyValueModel:
-    """Stand-in for model/tensorflow/model.py:152-188 (call signature only)."""
+    """Stand-in for model/tensorflow/model.py:152-188: the call signature, and
+    the constructor's one use of numpy's global stream -- its dummy forward on
+    np.random.rand(1, *input_dim) (model.py:167-169), which play_game runs
+    between np.random.seed and the game (self_play.py:45-47)."""
 
     def __init__(self, input_dim, action_space):
         self.input_dim = input_dim
         self.action_space = action_space
+        np.random.rand(1, *self.input_dim).astype("float32")
 
     def __call__(self, x):
         x = np.asarray(x)

@@ -116,15 +116,27 @@ def test_reference_weight_hash_matches_legacy_numpy(golden_dir):
 
 
 def test_dirichlet_noise_paths():
-    """Root Dirichlet noise (mcts.py:70-85) runs in Connect-N self-play; the
-    single-tree MCTS API, the arena and chess refuse it rather than ignore it."""
+    """Root Dirichlet noise (mcts.py:70-85) runs in Connect-N self-play, the
+    MCTS tree API and the arena; chess refuses it rather than ignore it."""
     from custom_alphazero.config import ConfigMCTS, check_mcts_config
     check_mcts_config()
     ConfigMCTS.enable_dirichlet_noise = True
     try:
-        check_mcts_config("selfplay")
-        for path in ("tree", "chess", "arena"):
-            with pytest.raises(NotImplementedError):
-                check_mcts_config(path)
+        for path in ("selfplay", "tree"):
+            check_mcts_config(path)
+        with pytest.raises(NotImplementedError):
+            check_mcts_config("chess")
     finally:
         ConfigMCTS.enable_dirichlet_noise = False
+
+
+def test_root_noise_rows_are_numpys_dirichlet_draws():
+    """The tree API's host-drawn root noise: rng.dirichlet(0.03 * ones(k)) per
+    row, in order, padded to the action space (mcts.py:74-78)."""
+    from custom_alphazero.mcts.mcts import root_noise_rows
+    rows = root_noise_rows(np.random.RandomState(3), 5, 4, 7)
+    rs = np.random.RandomState(3)
+    for r in range(4):
+        np.testing.assert_array_equal(rows[r, :5], rs.dirichlet(np.ones(5) * 0.03))
+    assert not rows[:, 5:].any()
+    assert root_noise_rows(np.random.RandomState(3), 5, 0, 7).shape == (1, 7)

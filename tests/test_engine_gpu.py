@@ -19,7 +19,7 @@ NET_TOL = 1e-5  # north_star: value/policy outputs within 1e-5 (fp32)
 
 def synth_engine(z, slots, cache_log2=0, lanes=0, compact=False):
     H, W, n, grav, S = (int(z[k]) for k in ("height", "width", "n", "gravity", "sims"))
-    noise = bool(z["dirichlet_noise"]) if "dirichlet_noise" in z else False
+    noise = bool(z["dirichlet_noise"])
     kw = dict(dirichlet_noise=True, dirichlet_alpha=float(z["dirichlet_alpha"]),
               dirichlet_ratio=float(z["dirichlet_ratio"])) if noise else {}
     return az.Engine(H, W, n, bool(grav), S, slots=slots, evaluator=az.EVAL_SYNTHETIC,
@@ -137,20 +137,34 @@ def test_selfplay_dirichlet_noise_network_replays_on_oracle():
     eng.close()
 
 
-def test_tree_api_refuses_noise():
+def test_tree_api_noise_needs_the_callers_draws():
+    """A noisy engine's tree search takes the caller's np.random.dirichlet
+    rows (az_tree_search_noise): a plain search is refused, too few rows
+    fail loudly, the device never draws for the tree API."""
     eng = az.Engine(6, 7, 4, True, 10, slots=1, evaluator=az.EVAL_SYNTHETIC, dirichlet_noise=True)
     eng.tree_reset([0], np.zeros((1, 6, 7), np.int8))
-    with pytest.raises(az.AzError, match="self-play"):
+    with pytest.raises(az.AzError, match="az_tree_search_noise"):
         eng.tree_search(5)
+    with pytest.raises(az.AzError, match="root-noise-rows-exhausted"):
+        eng.tree_search(5, noise=np.full((1, 3, 7), 1 / 7))  # an unexpanded root makes 4 selections
     eng.close()
+    plain = az.Engine(6, 7, 4, True, 10, slots=1, evaluator=az.EVAL_SYNTHETIC)
+    plain.tree_reset([0], np.zeros((1, 6, 7), np.int8))
+    with pytest.raises(az.AzError, match="dirichlet_noise = 1"):
+        plain.tree_search(5, noise=np.full((1, 5, 7), 1 / 7))
+    plain.close()
 
 
-@pytest.mark.parametrize("name", ["c4_s25", "c4_s100", "c5_9x9_s50", "nograv_5x5_s25", "c4_s1"])
+@pytest.mark.parametrize("name", ["c4_s25", "c4_s100", "c5_9x9_s50", "nograv_5x5_s25", "c4_s1"] + NOISE_FIXTURES)
 def test_tree_api_edges_match_reference(golden, name):
-    """MCTS.search/play through the tree API: root edge N, W, prior bit-exact."""
+    """MCTS.search/play through the tree API: root edge N, W, prior bit-exact.
+    Noisy fixtures: every root selection's np.random.dirichlet vector is drawn
+    here from the game's stream, before play's draw, as the reference's
+    select does (mcts.py:70-85, 111-120), and passed to the search."""
     z = golden("mcts_" + name)
     H, W, S = int(z["height"]), int(z["width"]), int(z["sims"])
     A = int(z["action_space"])
+    noisy = bool(z["dirichlet_noise"])
     off = 0
     for g, seed in enumerate(z["seed"][:3]):
         eng = synth_engine(z, 1)
@@ -158,7 +172,16 @@ def test_tree_api_edges_match_reference(golden, name):
         rng = np.random.RandomState(int(seed))
         T = int(z["game_len"][g])
         for ply in range(T):
-            eng.tree_search(S)
+            if noisy:
+                before = eng.tree_export(0)
+                rows = S if before["root_n"] > 0 else S - 1
+                k = int(z["n_edges"][off + ply])
+                noise = np.zeros((1, max(rows, 1), A))
+                for r in range(rows):
+                    noise[0, r, :k] = rng.dirichlet(np.ones(k) * float(z["dirichlet_alpha"]))
+                eng.tree_search(S, noise=noise)
+            else:
+                eng.tree_search(S)
             t = eng.tree_export(0)
             k, f = t["root_n"], t["root_first"]
             gi = off + ply
