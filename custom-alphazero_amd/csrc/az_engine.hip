@@ -217,8 +217,7 @@ int simulate(az_engine* e, Lane& L) {
   if (L.tree_timer.enabled) L.tree_timer.end(s, 1);
   const az::Board* rows = L.t.eval_board;
   const int32_t* n_rows = L.t.eval_count;
-  if (e->cache.enabled) {
-    az::launch_dedup_resolve(L.g, L.t, s);
+  if (e->cache.enabled) {  // the select launch resolved its duplicate boards (dedup_tail)
     rows = L.t.nn_board;
     n_rows = L.t.nn_count;
   }
@@ -410,8 +409,9 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
     size_t cap = 1024;
     while (cap < 4 * (size_t)n) cap <<= 1;
     if ((rc = e->alloc(&t.eval_count, 8)) || (rc = e->alloc(&t.step_tag, cap)) ||
-        (rc = e->alloc(&t.step_row, cap)))
+        (rc = e->alloc(&t.step_row, cap)) || (rc = e->alloc(&t.sel_done, 1)))
       return rc;
+    AZ_HIP(hipMemset(t.sel_done, 0, sizeof(uint32_t)));
     AZ_HIP(hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)));
     AZ_HIP(hipMemset(t.eval_count, 0, 8 * sizeof(int32_t)));
     set_counts(t, t.eval_count, 0);
@@ -809,6 +809,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       (rc = e->alloc(&t.eval_src, S)) || (rc = e->alloc(&t.miss_q, S)) ||
       (rc = e->alloc(&t.nn_board, S)) ||
       (rc = e->alloc(&t.eval_count, 8)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
+      (rc = e->alloc(&t.sel_done, 1)) ||
       (rc = e->alloc(&t.last_move, S)) || (rc = e->alloc(&t.last_status, S)) ||
       (rc = e->alloc(&t.last_policy, S * A)))
     return cleanup(rc);
@@ -855,6 +856,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   }
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(t.eval_count, 0, 8 * sizeof(int32_t)) != hipSuccess ||
+      hipMemset(t.sel_done, 0, sizeof(uint32_t)) != hipSuccess ||
       hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
     return cleanup(fail(AZ_E_HIP, "memset failed"));
   // evaluator buffers (batch = slots)

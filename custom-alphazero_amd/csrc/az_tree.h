@@ -91,6 +91,7 @@ struct TreeDev {
   // simulation (epoch parity): the select kernel zeroes the other block, the
   // next simulation's, so no memset launch sits between simulations
   int32_t* next_counts;        // [4] the block the next simulation uses
+  uint32_t* sel_done;          // [1] select blocks finished (the last one resolves the dedup, 0 after)
   uint64_t* step_tag;          // [step_cap] per-simulation dedup table: (epoch << 32) | fp32
   int32_t* step_row;           // [step_cap] evaluator row of the tag's owner
   uint32_t step_mask;          // step_cap - 1
@@ -203,7 +204,6 @@ void launch_move_end(int32_t* arrive, int n_lanes, const unsigned long long* don
                      unsigned long long* snap, hipStream_t s);
 // cache on: misses are deduplicated inside select (step tag table); this
 // resolves the ones whose tag matched, by full-board compare
-void launch_dedup_resolve(const GameCfg& g, const TreeDev& t, hipStream_t s);
 void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* count, float* probs,
                        float* values, hipStream_t s);
 void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const float* probs,

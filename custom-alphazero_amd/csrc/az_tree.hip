@@ -261,7 +261,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   // miss: one evaluator row per distinct board in this simulation.  Tag =
   // (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
   // empty, so the table needs no clearing.  A tag match is only a candidate:
-  // dedup_resolve compares the full boards after this kernel.
+  // the launch's last block (dedup_tail) compares the full boards.
   wave_count(t.miss_count);
   const uint64_t tag = ((uint64_t)t.epoch << 32) | (uint32_t)(h >> 32);
   uint32_t slot = (uint32_t)h & t.step_mask;
@@ -321,7 +321,7 @@ __device__ __forceinline__ bool argmax_before(double v, int i, double bv, int bi
 
 // Serial descent, one lane per game (used when the action space exceeds 64).
 template <bool NOISE>
-__global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
+__device__ __forceinline__ void select_body(const GameCfg& g, const TreeDev& t, const CacheDev& c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
@@ -403,7 +403,7 @@ __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t
 // sums N and takes the first-maximum UCB by shuffles -- the same float64
 // expressions as the serial loop, so the chosen edge is identical.
 template <int L, bool NOISE>
-__global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
+__device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDev& t, const CacheDev& c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = gid / L, j = gid % L;
@@ -565,22 +565,49 @@ __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, Tre
 // ----------------------------------------------------------- dedup resolve
 // Misses whose step tag matched an owner's: same board -> share the owner's
 // evaluator row; a fingerprint collision (different board) -> its own row.
-__global__ __launch_bounds__(256) void dedup_resolve_kernel(GameCfg g, TreeDev t) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) atomicAdd(t.stats + kStatNNEvals, (unsigned long long)*t.nn_count);
-  if (i >= *t.dup_count) return;
-  const int q = t.dup_q[i];
-  const uint32_t slot = (uint32_t)t.eval_src[q] & 0x7fffffffu;
-  const int row = t.step_row[slot];
-  const Board b = t.eval_board[q];
-  if (same_board(t.nn_board[row], b)) {
-    t.eval_src[q] = -(row + 1);
-  } else {
-    const int r2 = atomicAdd(t.nn_count, 1);
-    t.nn_board[r2] = b;
-    t.eval_src[q] = -(r2 + 1);
-    atomicAdd(t.stats + kStatNNEvals, 1ull);
+// Run by the select launch's last block to finish (every block fences its
+// writes, then counts itself done; the block that completes the count sees
+// all of them): no launch of its own between select and the network (round
+// 4: a separate kernel, 24,000 launches, 4.3% of the kernel time).
+__device__ __forceinline__ void dedup_tail(const TreeDev& t, const CacheDev& c) {
+  if (!c.enabled) return;  // uniform
+  __shared__ int last;
+  __threadfence();  // this thread's eval_src / nn_board / step_row / dup_q stores, device-wide
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(t.sel_done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;  // block-uniform
+  __threadfence();
+  const int n = __hip_atomic_load(t.dup_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int q = t.dup_q[i];
+    const uint32_t slot = (uint32_t)t.eval_src[q] & 0x7fffffffu;
+    const int row = t.step_row[slot];
+    const Board b = t.eval_board[q];
+    if (same_board(t.nn_board[row], b)) {
+      t.eval_src[q] = -(row + 1);
+    } else {
+      const int r2 = atomicAdd(t.nn_count, 1);
+      t.nn_board[r2] = b;
+      t.eval_src[q] = -(r2 + 1);
+    }
   }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(t.stats + kStatNNEvals, (unsigned long long)*t.nn_count);
+    *t.sel_done = 0;  // the lane's next select launch counts from zero
+  }
+}
+
+template <bool NOISE>
+__global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
+  select_body<NOISE>(g, t, c);
+  dedup_tail(t, c);
+}
+template <int L, bool NOISE>
+__global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
+  select_group_body<L, NOISE>(g, t, c);
+  dedup_tail(t, c);
 }
 
 // ------------------------------------------------------------ cache insert
@@ -1009,10 +1036,6 @@ void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStr
     case 64: select_group_kernel<64, false><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;
     default: select_kernel<false><<<game_blocks(g.slots), kGameBlock, 0, s>>>(g, t, c); break;
   }
-}
-
-void launch_dedup_resolve(const GameCfg& g, const TreeDev& t, hipStream_t s) {
-  dedup_resolve_kernel<<<blocks_for(g.slots), 256, 0, s>>>(g, t);
 }
 
 void launch_synth_eval(const GameCfg& g, const Board* boards, const int32_t* count, float* probs,
