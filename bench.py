@@ -80,6 +80,11 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
     ap.add_argument("--cache-log2", type=int, default=25,
                     help="transposition cache (the reference's plays_inferences) entries = 2^N; 0 = off")
+    ap.add_argument("--arena-edges", default="bounded",
+                    help="tree edges per slot, the average of a lane's pooled halves: 'bounded' (default, "
+                         "8*S*A + H*W*A: ~5x the high-water mark measured at configs[1] and configs[3]), "
+                         "'proof' (S*H*W*A + A, no game can overflow, capped at 40%% of free HBM) or a number; "
+                         "an overflow is a device error, never an overrun")
     ap.add_argument("--compact", type=int, default=1,
                     help="1: reclaim the subtrees a game has left after every move (az_config.compact)")
     ap.add_argument("--no-cache-window", action="store_true",
@@ -553,6 +558,20 @@ def launch_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
+def arena_edges_arg(args):
+    """az_config.arena_edges for --arena-edges: 0 lets the engine choose the
+    overflow-proof size ('proof'); 'bounded' sizes the pools from the measured
+    high-water mark (round 4: a lane half held at most 2.09 M of 60.2 M edges
+    at configs[1], 1,020 per slot; 38.9 M of 963 M at configs[3]'s 16384-game
+    shard, 4,750 per slot): 8*S*A + H*W*A per slot, 5.8x / 4.8x those."""
+    if not args.compact or args.arena_edges == "proof":
+        return 0
+    A, HW = args.width, args.height * args.width
+    if args.arena_edges == "bounded":
+        return 8 * args.sims * A + HW * A
+    return int(args.arena_edges)
+
+
 def tree_arena(args, st):
     """The tree memory the engine chose and what the window used of it."""
     A, HW = args.width, args.height * args.width
@@ -566,19 +585,23 @@ def tree_arena(args, st):
     # capped at 2^31 - 1 edges, its indices' range, below arena_edges x slots)
     per_slot = pool // (2 * args.slots)
     proof = per_slot >= safe
+    lanes = args.lanes or (2 if args.slots >= 512 else 1)  # az_config.lanes = 0: auto
+    half = pool // (2 * lanes)
     return {
-        "compact": True, "pool_edges_total": pool, "bytes_total": 32 * pool,
+        "compact": True, "sizing": args.arena_edges, "pool_edges_total": pool, "bytes_total": 32 * pool,
         "pool_edges_per_half_per_slot": per_slot, "arena_edges_requested": st["arena_edges"],
         "overflow_proof": proof,
-        "high_water_edges_per_lane_half": high, "max_retained_edges": st["max_retained"],
+        "high_water_edges_per_lane_half": high, "lane_half_edges": half,
+        "high_water_fraction": round(high / max(1, half), 4), "max_retained_edges": st["max_retained"],
         "rule": (f"pooled arenas: each lane owns two halves of {per_slot} edges x its slots; a slot takes "
                  f"{16 * A}-edge chunks of the current half as it expands, and after every move compaction copies "
                  f"each slot's kept subtree (Cheney scan) into the other half, which becomes the current one. "
                  + (f"{per_slot} >= S*H*W*A + A = {safe} per slot: no game can overflow it"
                     if proof else
-                    f"{per_slot} < S*H*W*A + A = {safe} per slot (bound by the 40%-of-free-HBM cap or a lane "
-                    f"half's 2^31-edge index range): the slots share the pool, overflow raises a device error "
-                    f"(none in this run)")),
+                    f"{per_slot} < S*H*W*A + A = {safe} per slot ({args.arena_edges}: "
+                    + ("8*S*A + H*W*A, ~5x the measured high-water mark" if args.arena_edges == "bounded"
+                       else "a request, the 40%-of-free-HBM cap or a lane half's 2^31-edge index range")
+                    + "): the slots share the pool, overflow raises a device error (none in this run)")),
     }
 
 
@@ -634,7 +657,7 @@ def main():
     eng = az.Engine(args.height, args.width, args.n, True, args.sims, slots=args.slots,
                     evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index,
                     cache_log2=args.cache_log2, lanes=args.lanes, conv_algo=args.conv_algo,
-                    compact=bool(args.compact))
+                    compact=bool(args.compact), arena_edges=arena_edges_arg(args))
     eng.set_weights(named)
     tree_steps = 3
     total_moves = MAX_PREROLL + 2 * args.steps + tree_steps + args.warmup

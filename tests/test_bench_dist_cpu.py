@@ -186,7 +186,8 @@ def test_tree_arena_rule_states_the_pool_it_holds():
     per slot, the pools' edges over both halves and all slots, not the
     requested average (a lane half is also capped at 2^31 - 1 edges)."""
     bench = _bench()
-    args = argparse.Namespace(width=7, height=6, sims=100, slots=4096, compact=True)
+    args = argparse.Namespace(width=7, height=6, sims=100, slots=4096, compact=True, lanes=0,
+                              arena_edges="proof")
     safe = 100 * 42 * 7 + 7
     st = dict(arena_edges=safe, arena_pool_edges=2 * 4096 * safe, arena_pool_high=10, max_retained=5)
     r = bench.tree_arena(args, st)
@@ -196,3 +197,22 @@ def test_tree_arena_rule_states_the_pool_it_holds():
     r = bench.tree_arena(args, capped)
     assert not r["overflow_proof"] and r["pool_edges_per_half_per_slot"] == 2 * ((1 << 31) - 1) // 65536
     assert "share the pool" in r["rule"]
+
+
+def test_bounded_arena_is_sized_from_the_measured_high_water_mark():
+    """--arena-edges bounded (the default) asks for
+    8*S*A + H*W*A edges per slot -- 5,894 at configs[1], ~5.8x the 1,020 per
+    slot a lane half held at its high-water mark in round 4 -- instead of
+    the overflow-proof 29,407; the line states the pool and the fraction the
+    window's high-water mark used."""
+    bench = _bench()
+    args = argparse.Namespace(width=7, height=6, sims=100, slots=4096, compact=True, lanes=0,
+                              arena_edges="bounded")
+    assert bench.arena_edges_arg(args) == 8 * 100 * 7 + 42 * 7 == 5894
+    assert bench.arena_edges_arg(argparse.Namespace(**dict(vars(args), arena_edges="proof"))) == 0
+    assert bench.arena_edges_arg(argparse.Namespace(**dict(vars(args), arena_edges="1234"))) == 1234
+    st = dict(arena_edges=5894, arena_pool_edges=2 * 4096 * 5894, arena_pool_high=2_090_000, max_retained=2485)
+    r = bench.tree_arena(args, st)
+    assert not r["overflow_proof"] and r["sizing"] == "bounded"
+    assert r["lane_half_edges"] == 2048 * 5894 and r["high_water_fraction"] == round(2_090_000 / (2048 * 5894), 4)
+    assert "measured high-water mark" in r["rule"]
