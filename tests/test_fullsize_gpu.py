@@ -283,3 +283,42 @@ def test_chess_fullsize_game_replays_on_oracle(chess_games, g):
 
     ref = C.play_game(CHESS["sims"], CHESS_SEED + g, CHESS["plies"], callback=cb)
     _compare(r, g, ref, "fullsize")
+
+
+CHESS_END = dict(sims=800, slots=8, plies=512)
+
+
+@pytest.mark.timeout(600)
+def test_chess_games_to_termination_at_800_sims():
+    """configs[4]'s 800 sims/move played from the opening
+    to the end -- 8 games, every one finishing by the rules (checkmate,
+    stalemate, insufficient material, the 75-move rule) or at the 512-ply
+    cap the reference lacks -- with rules and policies checked at every ply
+    and the shortest rule-terminated game replayed bit for bit on the oracle
+    (its network outputs: the engine's own batch-1 forward)."""
+    from custom_alphazero.model.weights import init_weights, weight_spec
+    w = init_weights(weight_spec(8, 8, 1880, in_channels=118), seed=7)
+    eng = az.ChessEngine(mcts_iterations=CHESS_END["sims"], slots=CHESS_END["slots"],
+                         evaluator=az.EVAL_NETWORK, max_plies=CHESS_END["plies"])
+    try:
+        eng.set_weights(w.items())
+        st = eng.selfplay_run(0, CHESS_END["slots"], CHESS_SEED)
+        assert st["errors"] == 0 and st["games_done"] == CHESS_END["slots"]
+        r = eng.selfplay_results()
+        check_chess_games(r, CHESS_END["slots"], CHESS_END["plies"])
+        lengths = r["lengths"][:CHESS_END["slots"]]
+        terms = r["terminations"][:CHESS_END["slots"]]
+        ended = [g for g in range(CHESS_END["slots"]) if terms[g] != 5]
+        assert ended, (lengths.tolist(), terms.tolist())  # some game ends by the rules
+        print(f"chess to termination: lengths {lengths.tolist()}, terminations {terms.tolist()}")
+
+        def cb(pos, initial):
+            x = C.full_state(*C.reference_history(pos, bool(initial)), pos)[None].astype(np.float32)
+            p, v = eng.forward(x)
+            return p[0], float(v[0])
+
+        g = min(ended, key=lambda k: int(lengths[k]))
+        ref = C.play_game(CHESS_END["sims"], CHESS_SEED + g, CHESS_END["plies"], callback=cb)
+        _compare(r, g, ref, "to-termination")
+    finally:
+        eng.close()
