@@ -147,8 +147,8 @@ typedef struct az_stats {
                                      tower: per full tile after its slot plan's skipped taps, / boards
                                      per tile; 0 = not reported).  Chess (az_chess_stats): the
                                      self-play forward's, whose stem skips the always-zero history
-                                     planes 0-63; az_chess_forward runs every plane and issues
-                                     2 x 9 x 3 x 16384 x 4 more per board */
+                                     planes 0-63; az_chess_forward runs every plane: 18 more
+                                     k-steps of 96 MFMAs (28.3 MFLOP) per board */
     int64_t arena_pool_edges; /* compact: edges of every lane's two pool halves (0 uncompacted) */
     int64_t arena_pool_high;  /* compact: most edges one lane's half held at a move's end */
 } az_stats;
