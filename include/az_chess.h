@@ -115,6 +115,12 @@ typedef struct az_chess_config {
                                      128 slots, else 1); results do not depend on it */
     int32_t reserved[6];
 } az_chess_config;
+/* Scope: no Dirichlet root noise (ConfigMCTS.enable_dirichlet_noise,
+ * mcts.py:70-85) in the chess engine.  The reference's chess MCTS cannot run
+ * a search at all (chess/board.py:178's get_result signature vs mcts.py:179),
+ * so there is no noisy chess behaviour to match; the Python layer refuses
+ * the flag for chess (config.check_mcts_config("chess")) instead of
+ * ignoring it.  Connect-N has it in self-play and in the tree API (az.h). */
 
 /* Termination of a finished self-play game: AZ_CHESS_* above, or this */
 #define AZ_CHESS_MAX_PLIES 5
