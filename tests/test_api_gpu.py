@@ -62,6 +62,65 @@ def test_play_game_api_matches_reference(golden, game_cfg, monkeypatch, name):
         monkeypatch.undo()
 
 
+@pytest.fixture
+def noise_on():
+    from custom_alphazero.config import ConfigMCTS
+    ConfigMCTS.enable_dirichlet_noise = True
+    yield
+    ConfigMCTS.enable_dirichlet_noise = False
+
+
+@pytest.mark.parametrize("name", ["c4_s25_noise", "nograv_5x5_s25_noise"])
+def test_play_game_with_root_noise_matches_reference(golden, game_cfg, monkeypatch, noise_on, name):
+    """self_play.play_game with ConfigMCTS.enable_dirichlet_noise: the game
+    runs on the device with its np.random stream (MT19937(seed) past the
+    model construction's draws) -- the reference's noisy play_game, bitwise."""
+    z = golden("mcts_" + name)
+    game_cfg(z)
+    off = 0
+    for g, seed in enumerate(z["seed"][:2]):
+        monkeypatch.setattr(self_play.time, "time", lambda s=seed: float(s))
+        states, policies, rewards, _ = self_play.play_game(0, Board.get_all_possible_moves(), int(z["sims"]),
+                                                           "test-run", {}, model=SyntheticEvaluator())
+        T = int(z["game_len"][g])
+        np.testing.assert_array_equal(states, z["state"][off:off + T])
+        np.testing.assert_array_equal(policies.view(np.uint64), z["policy"][off:off + T].view(np.uint64))
+        np.testing.assert_array_equal(rewards, z["reward"][off:off + T])
+        off += T
+        monkeypatch.undo()
+
+
+@pytest.mark.parametrize("name", ["c4_s25_noise", "c5_9x9_s50_noise", "nograv_5x5_s25_noise"])
+def test_mcts_with_root_noise_matches_reference(golden, game_cfg, noise_on, name):
+    """The single-tree MCTS API with ConfigMCTS.enable_dirichlet_noise: each
+    search draws its root-noise vectors from numpy's global stream
+    (mcts.root_noise_rows, az_tree_search_noise), then play() its one
+    random_sample -- the reference's stream order, so a seeded game is the
+    reference's noisy game bit for bit (root edge statistics every ply)."""
+    z = golden("mcts_" + name)
+    game_cfg(z)
+    S = int(z["sims"])
+    all_moves = Board.get_all_possible_moves()
+    off = 0
+    for g, seed in enumerate(z["seed"][:2]):
+        np.random.seed(int(seed))
+        np.random.rand(1, int(z["height"]), int(z["width"]), 4)  # play_game's model construction
+        m = MCTS(Board(), all_moves, False, {}, model=SyntheticEvaluator())
+        T = int(z["game_len"][g])
+        for ply in range(T):
+            m.search(S)
+            gi = off + ply
+            k = int(z["n_edges"][gi])
+            edges = m.current_root.edges
+            assert [e.visit_count for e in edges] == z["edge_n"][gi, :k].tolist(), (g, ply)
+            np.testing.assert_array_equal(np.array([e.total_action_value for e in edges]), z["edge_w"][gi, :k])
+            _, _, policy, move = m.play(m.board.fullmove_number >= 8, return_details=True)
+            np.testing.assert_array_equal(policy.view(np.uint64), z["policy"][gi].view(np.uint64))
+            assert all_moves.index(move) == z["moves"][gi]
+        assert m.board.is_game_over()
+        off += T
+
+
 def test_batched_play_matches_reference(golden, game_cfg):
     z = golden("mcts_c4_s25")
     game_cfg(z)
