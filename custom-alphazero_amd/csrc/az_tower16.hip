@@ -62,6 +62,7 @@
 
 #include "az_nn.h"
 #include "az_tree.h"
+#include "az_kloop_asm.h"
 
 namespace az {
 
@@ -497,6 +498,101 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   __builtin_amdgcn_s_setprio(0);
 }
 
+// k_loop with the groups of 4 k-steps in hand-scheduled assembly
+// (az_kloop_asm.h, gen_kloop_asm.py): the same k-steps, reads and MFMAs in
+// the same order per accumulator as k_loop's LAG ring, so the same sums
+// bit for bit.  accm / accr: the accumulators of the taps / the residual
+// steps (may be the same array)
+template <int MBW, int R, int C0, typename Mid = NoMid>
+__device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
+                                           const uint4* __restrict__ wres, t_f4 (&accm)[MBW][2],
+                                           t_f4 (&accr)[MBW][2], const int (&yx_)[MBW], int H, int W,
+                                           int zrow, int nq, int lane, int skw, int res_shift = 0,
+                                           Mid mid = Mid{}) {
+  static_assert(R == 0 || R == 4, "residual steps: none or the 1x1 projection's 4");
+  static_assert(C0 == 0 || (R == 0 && C0 == 2), "skipped chunks: the stem only, an even count");
+  const int gq = lane >> 4;
+  int r[MBW], yx[MBW];
+#pragma unroll
+  for (int mb = 0; mb < MBW; ++mb) {
+    yx[mb] = yx_[mb];
+    asm volatile("" : "+v"(yx[mb]));
+    r[mb] = pix_row(yx[mb], H * W, W);
+  }
+  // the weight streams' buffer descriptors as SGPR quads
+  auto quad = [](const void* p) {
+    const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+    return az_rsrc{(int)(unsigned)a, (int)(unsigned)(a >> 32) & 0xffff, 0x7fffffff, 0x00020000};
+  };
+  const az_rsrc rs_m = quad(wmain), rs_r = quad(R ? wres : wmain);
+  const int voff = ((nq * 2) * 2 * 64 + lane) * 16;
+  // LDS byte addresses (ds_read's operand): act's base + the row's offset
+  const int lbase = (int)(size_t)((__attribute__((address_space(3))) const char*)(const char*)act) + gq * 16;
+  auto own = [&](int(&a)[MBW]) {
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) a[mb] = (pix_ok(yx[mb]) ? r[mb] + res_shift : zrow + (r[mb] & 7)) * kPitch + lbase;
+  };
+  auto tap_addr = [&](int t, int(&a)[MBW]) {
+    const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) {
+      const int py = (yx[mb] >> 8) & 255, px = yx[mb] & 255;
+      const bool ok = py + dy >= 0 && py + dy < H && px + dx >= 0 && px + dx < W;
+      const int sr = r[mb] + dy * W + dx;
+      a[mb] = (ok ? sr : zrow + (sr & 7)) * kPitch + lbase;
+    }
+  };
+  az_u4 aq[MBW][2], bq[2][4];
+  int cur[MBW], nxt[MBW];
+  // prologue (asm too: a compiler load here would leave the compiler waiting
+  // for it, vmcnt(0) lgkmcnt(0), before every group of the loop)
+  if (R) own(cur);
+  else tap_addr(0, cur);
+  KPro<MBW, C0>::run(aq, bq, cur, voff, R ? rs_r : rs_m, R ? 36 * 16384 : C0 * 16384);
+  const bool young = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= 256;
+  auto prio = [&](bool hi) {
+    if (hi) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  };
+  prio(young);
+  if constexpr (R) {
+    tap_addr(0, nxt);
+    KGroup<MBW, 0, 0>::run(accr, aq, bq, cur, nxt, voff, rs_r, rs_m, 36 * 16384, 0);
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) cur[mb] = nxt[mb];
+    mid();
+  }
+  // 9 taps, each in three bodies by the wave's skip mask (slot plan: never 3);
+  // the last tap's prefetch re-reads its own first k-step (harmless, drained)
+#pragma unroll 1
+  for (int t = 0; t < 9; ++t) {
+    if (t == 6) prio(!young);
+    if (t < 8) tap_addr(t + 1, nxt);
+    else {
+#pragma unroll
+      for (int mb = 0; mb < MBW; ++mb) nxt[mb] = cur[mb];
+    }
+    const int m = (skw >> (2 * t)) & 3;
+    const int sc = 4 * t * 16384, sn = t < 8 ? (4 * (t + 1) + C0) * 16384 : sc + C0 * 16384;
+    if (m == 0) KGroup<MBW, C0, 0>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    else if (m == 1) KGroup<MBW, C0, (MBW > 1 ? 1 : 0)>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    else KGroup<MBW, C0, (MBW > 1 ? 2 : 0)>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) cur[mb] = nxt[mb];
+  }
+  KDrain<MBW>::run(accm, aq, bq);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// the tower's K loop: the assembly groups; the compiled loop (k_loop) stays
+// selectable for A/B runs of the two (EXTRA=-DAZ_KLOOP_CC: a diagnostic
+// build, its build flags say so)
+#ifdef AZ_KLOOP_CC
+#define AZ_KLOOP k_loop
+#else
+#define AZ_KLOOP k_loop_asm
+#endif
+
 // LDS-DMA of n_u4 16-byte words from global src into LDS dst (both
 // 16-byte aligned), the workgroup's waves in turn: no VGPRs, completes in the
 // background (the first vmcnt wait of a K loop covers it)
@@ -624,8 +720,8 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};
     __builtin_amdgcn_s_waitcnt(0);  // this wave's blob DMA pieces have landed ...
     __syncthreads();                // ... every wave's, and the input rows
-    if (first_chunk == 2) k_loop<MBW, 0, 2>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, skw);
-    else k_loop<MBW, 0>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, skw);
+    if (first_chunk == 2) AZ_KLOOP<MBW, 0, 2>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, skw);
+    else AZ_KLOOP<MBW, 0, 0>(bufH, T.stem_k, nullptr, acc, acc, yx, H, W, zH, nq, lane, skw);
     if (!dbuf) __syncthreads();  // in place: every wave is done reading the input before X overwrites it
   } else {
   // conv3x3 4 -> F + folded BN + ReLU on the MFMA: k = tap*4 + plane (36 of
@@ -742,8 +838,8 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       }
     // conv1, input X (in place: + the projection residual into accr)
     T16_WSTAMP(d, 0);
-    if constexpr (DB) k_loop<MBW, 0>(bufX, T.k1[d], nullptr, acc, acc, yx, H, W, zX, nq, lane, skw);
-    else k_loop<MBW, 4>(bufX, T.k1[d], T.k2[d], acc, accr_, yx, H, W, zX, nq, lane, skw);
+    if constexpr (DB) AZ_KLOOP<MBW, 0, 0>(bufX, T.k1[d], nullptr, acc, acc, yx, H, W, zX, nq, lane, skw);
+    else AZ_KLOOP<MBW, 4, 0>(bufX, T.k1[d], T.k2[d], acc, accr_, yx, H, W, zX, nq, lane, skw);
     T16_WSTAMP(d, 1);
     if (d < 4) T16_STAMP(2 + 4 * d);
     if (d < 4) T16_STAMP4(24 + 4 * d);
@@ -788,10 +884,11 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       // block streams the value dense's wv1 into X's tile behind the heads'
       // partials while the taps run (every wave a share).  The same sums in
       // the same order as the in-place form: bitwise the same outputs
+      const bool wv1x = T.wv1_xtile && d + 1 == depth;  // read before the K loop's asm ("memory")
       auto mid = [&]() {
         rescale();
         __syncthreads();
-        if (T.wv1_xtile && d + 1 == depth)
+        if (wv1x)
           dma_to_lds<NT>(reinterpret_cast<uint4*>(reinterpret_cast<float*>(bufX) + TR * 48), T.blob + T.off_wv1,
                          HW * J / 4, wave, lane);
       };
@@ -799,11 +896,12 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = t_f4{0.f, 0.f, 0.f, 0.f};  // conv1's sums are stored
-      k_loop<MBW, 4>(bufH, T.k2[d], T.k2[d], acc, acc, yx, H, W, zH, nq, lane, skw, -(TR + kZeroRows), mid);
+      AZ_KLOOP<MBW, 4, 0>(bufH, T.k2[d], T.k2[d], acc, acc, yx, H, W, zH, nq, lane, skw, -(TR + kZeroRows),
+                            mid);
     } else {
       rescale();
       // conv2 on H, on top of the residual
-      k_loop<MBW, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, skw);
+      AZ_KLOOP<MBW, 0, 0>(bufH, T.k2[d], nullptr, accr, accr, yx, H, W, zH, nq, lane, skw);
     }
     T16_WSTAMP(d, 3);
     if (d < 4) T16_STAMP(4 + 4 * d);

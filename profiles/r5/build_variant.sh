@@ -8,7 +8,7 @@ name=$1
 R=$(cd "$(dirname "$0")/../.." && pwd)
 W=/tmp/azvar_$name
 rm -rf $W && mkdir -p $W/csrc $W/include
-cp $R/custom-alphazero_amd/csrc/*.hip $R/custom-alphazero_amd/csrc/*.h $R/custom-alphazero_amd/csrc/Makefile $W/csrc/
+cp $R/custom-alphazero_amd/csrc/*.hip $R/custom-alphazero_amd/csrc/*.h $R/custom-alphazero_amd/csrc/*.py $R/custom-alphazero_amd/csrc/Makefile $W/csrc/
 cp $R/include/*.h $W/include/
 # the Makefile includes ../../include: mirror the layout
 mkdir -p $W/x && mv $W/csrc $W/x/csrc && mv $W/include $W/include_tmp && mkdir -p $W/include && mv $W/include_tmp/* $W/include/ && rmdir $W/include_tmp
