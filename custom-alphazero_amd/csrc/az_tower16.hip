@@ -498,6 +498,9 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   __builtin_amdgcn_s_setprio(0);
 }
 
+#ifndef AZ_KLOOP_PF
+#define AZ_KLOOP_PF 1
+#endif
 // k_loop with the groups of 4 k-steps in hand-scheduled assembly
 // (az_kloop_asm.h, gen_kloop_asm.py): the same k-steps, reads and MFMAs in
 // the same order per accumulator as k_loop's LAG ring, so the same sums
@@ -542,13 +545,17 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
       a[mb] = (ok ? sr : zrow + (sr & 7)) * kPitch + lbase;
     }
   };
-  az_u4 aq[MBW][2], bq[2][4];
+  // weight prefetch depth: PF k-steps ahead in NB buffers (2 ahead needs 4,
+  // so a 4-k-step group keeps each buffer's k-step fixed; the stem's
+  // 2-k-step groups prefetch 1 ahead)
+  constexpr int PF = C0 == 0 ? AZ_KLOOP_PF : 1, NB = PF == 1 ? 2 : 4;
+  az_u4 aq[MBW][2], bq[NB][4];
   int cur[MBW], nxt[MBW];
   // prologue (asm too: a compiler load here would leave the compiler waiting
   // for it, vmcnt(0) lgkmcnt(0), before every group of the loop)
   if (R) own(cur);
   else tap_addr(0, cur);
-  KPro<MBW, C0>::run(aq, bq, cur, voff, R ? rs_r : rs_m, R ? 36 * 16384 : C0 * 16384);
+  KPro<MBW, C0, PF>::run(aq, bq, cur, voff, R ? rs_r : rs_m, R ? 36 * 16384 : C0 * 16384);
   const bool young = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= 256;
   auto prio = [&](bool hi) {
     if (hi) __builtin_amdgcn_s_setprio(1);
@@ -557,7 +564,7 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
   prio(young);
   if constexpr (R) {
     tap_addr(0, nxt);
-    KGroup<MBW, 0, 0>::run(accr, aq, bq, cur, nxt, voff, rs_r, rs_m, 36 * 16384, 0);
+    KGroup<MBW, 0, 0, PF>::run(accr, aq, bq, cur, nxt, voff, rs_r, rs_m, 36 * 16384, 0);
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) cur[mb] = nxt[mb];
     mid();
@@ -574,13 +581,13 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
     }
     const int m = (skw >> (2 * t)) & 3;
     const int sc = 4 * t * 16384, sn = t < 8 ? (4 * (t + 1) + C0) * 16384 : sc + C0 * 16384;
-    if (m == 0) KGroup<MBW, C0, 0>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
-    else if (m == 1) KGroup<MBW, C0, (MBW > 1 ? 1 : 0)>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
-    else KGroup<MBW, C0, (MBW > 1 ? 2 : 0)>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    if (m == 0) KGroup<MBW, C0, 0, PF>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    else if (m == 1) KGroup<MBW, C0, (MBW > 1 ? 1 : 0), PF>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    else KGroup<MBW, C0, (MBW > 1 ? 2 : 0), PF>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) cur[mb] = nxt[mb];
   }
-  KDrain<MBW>::run(accm, aq, bq);
+  KDrain<MBW, NB>::run(accm, aq, bq);
   __builtin_amdgcn_s_setprio(0);
 }
 

@@ -39,7 +39,7 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "az_kloop_asm.h")
 KSTEP = 16384  # bytes of one k-step's packed B fragments (az_tower16.hip load_bk)
 
 
-def group_asm(MBW, C0, SKC, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
+def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     """Assembly text of one group (chunks C0..3) and its operand names.
     Operands (names used in the text):
       %[aK_T]   ring slot K (block), term T (0: t0, 1: t1)   "+v" az_u4
@@ -75,19 +75,24 @@ def group_asm(MBW, C0, SKC, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     last_mfma_slot = None  # ring slot the most recent MFMA group read
     for ci, c in enumerate(chunks):
         last_chunk = c == 3
-        prefetch = (not last_chunk) or HASNEXT
-        P = 4 if prefetch else 0
-        bs = c & 1  # this k-step's B buffer
+        prefetch = c + PF < 4 or HASNEXT
+        P = 4 * PF if prefetch else 0  # weight loads issued after this k-step's
+        NB = 2 if PF == 1 else 4
+        bs = c % NB  # this k-step's B buffer
         emit(f"; k-step chunk {c}")
         if prefetch:
-            bn = (c + 1) & 1
-            if not last_chunk:
-                emit(f"s_add_u32 %[tmp], %[sc], {(c + 1 - 0) * KSTEP}")
-                for q in range(4):
-                    emit(f"buffer_load_dwordx4 %[b{bn}_{q}], %[voff], %[rc], %[tmp] offen offset:{q * 1024}")
+            k = c + PF  # the k-step this one prefetches: of this group, or of the next
+            bn = k % NB
+            if k < 4:
+                emit(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
+                src = "%[rc], %[tmp]"
+            elif k == 4 + C0:
+                src = "%[rn], %[sn]"
             else:
-                for q in range(4):
-                    emit(f"buffer_load_dwordx4 %[b{bn}_{q}], %[voff], %[rn], %[sn] offen offset:{q * 1024}")
+                emit(f"s_add_u32 %[tmp], %[sn], {(k - 4 - C0) * KSTEP}")
+                src = "%[rn], %[tmp]"
+            for q in range(4):
+                emit(f"buffer_load_dwordx4 %[b{bn}_{q}], %[voff], {src} offen offset:{q * 1024}")
         b_waited = False
         for mb in range(MBW):
             if not skipped(mb):
@@ -148,12 +153,12 @@ def group_asm(MBW, C0, SKC, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     return "\\n\\t".join(lines)
 
 
-def operand_list(MBW, residual=False):
+def operand_list(MBW, NB=2):
     outs = []
     for k in range(MBW):
         for t in range(2):
             outs.append(f'[a{k}_{t}] "+v"(aq[{k}][{t}])')
-    for j in range(2):
+    for j in range(NB):
         for q in range(4):
             outs.append(f'[b{j}_{q}] "+v"(bq[{j}][{q}])')
     outs.append('[tmp] "=&s"(tmp)')
@@ -178,52 +183,64 @@ def main():
                "// register operands must be vector types (HIP's uint4 is a struct)\n"
                "typedef unsigned az_u4 __attribute__((ext_vector_type(4)));\n"
                "typedef float az_f4 __attribute__((ext_vector_type(4)));\n")
-    out.append("template <int MBW, int C0, int SKC>\nstruct KGroup;\n"
-               "template <int MBW, int C0>\nstruct KPro;\n"
-               "template <int MBW>\nstruct KDrain;\n")
-    # the prologue: the first k-step's B fragments and the A reads a group's
-    # predecessor leaves in flight (blocks 0..MBW-2 of chunk C0; one block: its own)
+    out.append("template <int MBW, int C0, int SKC, int PF>\nstruct KGroup;\n"
+               "template <int MBW, int C0, int PF>\nstruct KPro;\n"
+               "template <int MBW, int NB>\nstruct KDrain;\n")
+    # the prologue: the first PF k-steps' B fragments and the A reads a
+    # group's predecessor leaves in flight (blocks 0..MBW-2 of chunk C0; one
+    # block: its own)
     for MBW in (1, 2, 3, 4):
-        for C0 in (0, 2):
-            text = [f"buffer_load_dwordx4 %[b0_{q}], %[voff], %[rc], %[sc] offen offset:{q * 1024}" for q in range(4)]
+        for C0, PF in ((0, 1), (0, 2), (2, 1)):
+            NB = 2 if PF == 1 else 4
+            text = []
+            for k in range(PF):
+                if k:
+                    text.append(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
+                for q in range(4):
+                    text.append(f"buffer_load_dwordx4 %[b{(C0 + k) % NB}_{q}], %[voff], %[rc], "
+                                f"{'%[tmp]' if k else '%[sc]'} offen offset:{q * 1024}")
             for blk in range(max(MBW - 1, 1)):
                 text.append(f"ds_read_b128 %[a{blk}_0], %[d{blk}] offset:{64 * C0}")
                 text.append(f"ds_read_b128 %[a{blk}_1], %[d{blk}] offset:{64 * C0 + 256}")
             outs = [f'[a{k}_{t}] "+v"(aq[{k}][{t}])' for k in range(MBW) for t in range(2)]
-            outs += [f'[b0_{q}] "+v"(bq[0][{q}])' for q in range(4)]
+            outs += [f'[b{j}_{q}] "+v"(bq[{j}][{q}])' for j in range(NB) for q in range(4)]
+            outs.append('[tmp] "=&s"(tmp)')
             ins = [f'[d{k}] "v"(ad[{k}])' for k in range(MBW)] + ['[voff] "v"(voff)', '[rc] "s"(rc)', '[sc] "s"(sc)']
             body = "\\n\\t".join(text)
-            out.append(f"template <>\nstruct KPro<{MBW}, {C0}> {{\n"
-                       f"  __device__ __forceinline__ static void run(az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[2][4],\n"
+            out.append(f"template <>\nstruct KPro<{MBW}, {C0}, {PF}> {{\n"
+                       f"  __device__ __forceinline__ static void run(az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                        f"      const int (&ad)[{MBW}], int voff, az_rsrc rc, int sc) {{\n"
+                       f"    int tmp;\n"
                        f"    asm volatile(\"{body}\"\n"
                        f"        : {', '.join(outs)}\n"
                        f"        : {', '.join(ins)}\n"
                        f"        : \"memory\");\n"
                        f"  }}\n}};\n")
         # the drain: the last group's prefetches land before the registers are reused
-        outs = [f'"+v"(aq[{k}][{t}])' for k in range(MBW) for t in range(2)]
-        outs += [f'"+v"(bq[{j}][{q}])' for j in range(2) for q in range(4)]
-        outs += [f'"+v"(acc[{k}][{n}])' for k in range(MBW) for n in range(2)]
-        out.append(f"template <>\nstruct KDrain<{MBW}> {{\n"
-                   f"  __device__ __forceinline__ static void run(az_f4 (&acc)[{MBW}][2], az_u4 (&aq)[{MBW}][2],\n"
-                   f"      az_u4 (&bq)[2][4]) {{\n"
-                   f"    asm volatile(\"s_waitcnt vmcnt(0) lgkmcnt(0)\"\n"
-                   f"        : {', '.join(outs)}\n"
-                   f"        :\n"
-                   f"        : \"memory\");\n"
-                   f"  }}\n}};\n")
+        for NB in (2, 4):
+            outs = [f'"+v"(aq[{k}][{t}])' for k in range(MBW) for t in range(2)]
+            outs += [f'"+v"(bq[{j}][{q}])' for j in range(NB) for q in range(4)]
+            outs += [f'"+v"(acc[{k}][{n}])' for k in range(MBW) for n in range(2)]
+            out.append(f"template <>\nstruct KDrain<{MBW}, {NB}> {{\n"
+                       f"  __device__ __forceinline__ static void run(az_f4 (&acc)[{MBW}][2], az_u4 (&aq)[{MBW}][2],\n"
+                       f"      az_u4 (&bq)[{NB}][4]) {{\n"
+                       f"    asm volatile(\"s_waitcnt vmcnt(0) lgkmcnt(0)\"\n"
+                       f"        : {', '.join(outs)}\n"
+                       f"        :\n"
+                       f"        : \"memory\");\n"
+                       f"  }}\n}};\n")
     count = 0
     for MBW in (1, 2, 3, 4):
-        for C0 in (0, 2):
+        for C0, PF in ((0, 1), (0, 2), (2, 1)):
+            NB = 2 if PF == 1 else 4
             for SKC in (0, 1, 2):
                 if MBW == 1 and SKC:
                     continue
                 count += 1
-                text = group_asm(MBW, C0, SKC)
-                outs, ins = operand_list(MBW)
-                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}> {{\n"
-                           f"  __device__ __forceinline__ static void run(az_f4 (&acc)[{MBW}][2], az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[2][4],\n"
+                text = group_asm(MBW, C0, SKC, PF)
+                outs, ins = operand_list(MBW, NB)
+                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}, {PF}> {{\n"
+                           f"  __device__ __forceinline__ static void run(az_f4 (&acc)[{MBW}][2], az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                            f"      const int (&ad)[{MBW}], const int (&an)[{MBW}], int voff, az_rsrc rc, az_rsrc rn,\n"
                            f"      int sc, int sn) {{\n"
                            f"    int tmp;\n"

@@ -8,4 +8,4 @@ mkdir -p $out
 timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -x -v -k "forward or network or tower" \
   --timeout 200 --timeout-method thread > $out/tower_tests.log 2>&1 || { tail -30 $out/tower_tests.log; exit 1; }
 tail -3 $out/tower_tests.log
-bash profiles/r5/ab_bench.sh 2 "" base kloop_cc nwm4 2>&1 | tee $out/ab.txt
+bash profiles/r5/ab_bench.sh 2 "" base kloop_cc kloop_pf2 nwm4 2>&1 | tee $out/ab.txt
