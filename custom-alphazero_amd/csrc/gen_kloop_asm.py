@@ -189,7 +189,7 @@ def main():
     # the prologue: the first PF k-steps' B fragments and the A reads a
     # group's predecessor leaves in flight (blocks 0..MBW-2 of chunk C0; one
     # block: its own)
-    for MBW in (1, 2, 3, 4):
+    for MBW in (1, 2, 3, 4, 6):
         for C0, PF in ((0, 1), (0, 2), (2, 1)):
             NB = 2 if PF == 1 else 4
             text = []
@@ -230,7 +230,7 @@ def main():
                        f"        : \"memory\");\n"
                        f"  }}\n}};\n")
     count = 0
-    for MBW in (1, 2, 3, 4):
+    for MBW in (1, 2, 3, 4, 6):
         for C0, PF in ((0, 1), (0, 2), (2, 1)):
             NB = 2 if PF == 1 else 4
             for SKC in (0, 1, 2):
