@@ -498,8 +498,8 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   __builtin_amdgcn_s_setprio(0);
 }
 
-#ifndef AZ_KLOOP_PF
-#define AZ_KLOOP_PF 1
+#ifndef AZ_KLOOP_PF  // 2: +1% games/s over 1 at configs[1] (profiles/r5/ab_kloop.txt)
+#define AZ_KLOOP_PF 2
 #endif
 // k_loop with the groups of 4 k-steps in hand-scheduled assembly
 // (az_kloop_asm.h, gen_kloop_asm.py): the same k-steps, reads and MFMAs in
@@ -548,7 +548,8 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
   // weight prefetch depth: PF k-steps ahead in NB buffers (2 ahead needs 4,
   // so a 4-k-step group keeps each buffer's k-step fixed; the stem's
   // 2-k-step groups prefetch 1 ahead)
-  constexpr int PF = C0 == 0 ? AZ_KLOOP_PF : 1, NB = PF == 1 ? 2 : 4;
+  // (the 192-row tile's 6-block waves: 1 -- 2 spills 69 VGPRs there)
+  constexpr int PF = C0 == 0 && MBW < 6 ? AZ_KLOOP_PF : 1, NB = PF == 1 ? 2 : 4;
   az_u4 aq[MBW][2], bq[NB][4];
   int cur[MBW], nxt[MBW];
   // prologue (asm too: a compiler load here would leave the compiler waiting
@@ -1186,6 +1187,10 @@ namespace az {
 
 int tower16_tile_rows(int HW) {
   if (HW > 128) return 0;
+  // boards of 65-96 pixels (9x9): 192-row tiles of two boards (in place: two
+  // such tiles exceed the LDS), which halve the weight stream per board --
+  // round 5, configs[2]: 73.1 -> 81.3 games/s (profiles/r5/ab_9x9.txt)
+  if (HW > 64 && HW <= 96) return 192;
   // 128-row tiles unless 96 rows hold the same boards (more rows per tile, same work per board)
   const int b128 = std::min(128 / HW, kTowerMaxBoards), b96 = std::min(96 / HW, kTowerMaxBoards);
   if (b96 >= 1 && b96 * HW * 128 >= b128 * HW * 96) return 96;  // 96-row tiles are at least as full
@@ -1215,7 +1220,7 @@ bool tower16_wv1_xtile_fits(int HW, int tr, int hidden) {
   return tr && (HW * hidden) % 4 == 0 && (size_t)tr * 48 * 4 + (size_t)HW * hidden * 4 <= (size_t)tr * kPitch;
 }
 
-// The slot plan (128- and 96-row tiles, 8 waves: M half h = blocks
+// The slot plan (192-, 128- and 96-row tiles, 8 waves: M half h = blocks
 // (tr / 32) h ..).
 // A 3x3 'same' conv tap (dy, dx) reads zeros for every pixel on the board edge
 // it points past; a block whose 16 slots all hold such pixels (or are empty)
@@ -1340,7 +1345,7 @@ bool slot_plan_try(int H, int W, int tr, const std::vector<PlanBorder>& borders,
 void tower16_slot_plan(int H, int W, int tr, std::vector<int>& slot_pix, int skip[2]) {
   slot_pix.clear();
   skip[0] = skip[1] = 0;
-  if ((tr != 128 && tr != 96) || H < 3 || W < 3 || !tower16_boards_per_tile(H * W, tr)) return;
+  if ((tr != 192 && tr != 128 && tr != 96) || H < 3 || W < 3 || !tower16_boards_per_tile(H * W, tr)) return;
   const int half = tr / 32;
   // layouts in order: T, B | L, R; then top | bottom (e.g. one 9x9 board in a
   // 96-row tile: too few edge pixels for four blocks)
@@ -1420,7 +1425,10 @@ void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, c
                     const int* count, int n_max, int H, int W, int A, float* probs, float* values,
                     unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
-  if (tile_rows == 96)
+  if (tile_rows == 192)  // in place only (two 192-row tiles exceed the LDS)
+    launch_db<12, 2, false, false>(net, staged, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr, 0,
+                                   err, s);
+  else if (tile_rows == 96)
     launch_mbw<6, 2, false>(net, staged, dbuf, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr, 0,
                             err, s);
   else

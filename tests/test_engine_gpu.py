@@ -363,7 +363,7 @@ def random_boards(rng, k, H, W):
 def test_forward_matches_keras_restatement(shape, conv_algo):
     """Every conv algorithm (the one-launch fp16x2 tower, fp32 direct, the
     per-layer fp16x2 kernels) within NET_TOL of the float64 Keras restatement;
-    9x9 runs the tower's 96-row tiles, 5x5 five boards per tile."""
+    9x9 runs the tower's 192-row in-place tiles, 5x5 five boards per tile."""
     H, W, grav = shape
     eng, w = make_net_engine(H, W, 4, grav, slots=300, conv_algo=conv_algo)
     rng = np.random.RandomState(5)

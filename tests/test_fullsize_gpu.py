@@ -151,7 +151,7 @@ def test_c4_forward_at_bench_batches_matches_keras(c4_games, B):
 
 def test_c5_9x9_forward_at_bench_batch_matches_keras():
     """configs[2]'s launch size (3443 boards: one lane's live batch in
-    bench.py, one 9x9 board per 96-row tile) on random-playout positions,
+    bench.py, two 9x9 boards per 192-row tile) on random-playout positions,
     within NET_TOL of the float64 Keras restatement."""
     rng = np.random.RandomState(9)
     forward_vs_keras(9, 9, 5, oracle.full_state(playout_boards(rng, 3443, 9, 9)), seed=13)

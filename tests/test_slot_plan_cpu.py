@@ -31,4 +31,4 @@ def test_slot_plan_invariants(tmp_path):
     c4 = next(r for r in rows if (r["H"], r["W"]) == (6, 7))
     assert c4["plan"] and c4["skipped_block_taps"] == 12 and c4["conflicts"] <= 2, c4
     c5 = next(r for r in rows if (r["H"], r["W"]) == (9, 9))
-    assert c5["plan"] and c5["skipped_block_taps"] == 6, c5
+    assert c5["plan"] and c5["tile_rows"] == 192 and c5["skipped_block_taps"] == 12, c5  # two boards: all four edges
