@@ -81,15 +81,17 @@ def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
         bs = c % NB  # this k-step's B buffer
         emit(f"; k-step chunk {c}")
         if prefetch:
-            k = c + PF  # the k-step this one prefetches: of this group, or of the next
-            bn = k % NB
+            # the k-step this one prefetches: chunk k of this group, or (k >= 4)
+            # the next group's (k - 4)-th, chunk C0 + k - 4 (sn: its first)
+            k = c + PF
+            bn = (k if k < 4 else C0 + k - 4) % NB
             if k < 4:
                 emit(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
                 src = "%[rc], %[tmp]"
-            elif k == 4 + C0:
+            elif k == 4:
                 src = "%[rn], %[sn]"
             else:
-                emit(f"s_add_u32 %[tmp], %[sn], {(k - 4 - C0) * KSTEP}")
+                emit(f"s_add_u32 %[tmp], %[sn], {(k - 4) * KSTEP}")
                 src = "%[rn], %[tmp]"
             for q in range(4):
                 emit(f"buffer_load_dwordx4 %[b{bn}_{q}], %[voff], {src} offen offset:{q * 1024}")
@@ -153,6 +155,24 @@ def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     return "\\n\\t".join(lines)
 
 
+def prologue_asm(MBW, C0, PF):
+    """The prologue: the first PF k-steps' B fragments (rc, from soffset sc)
+    and the A reads a group's predecessor leaves in flight (blocks 0..MBW-2
+    of chunk C0; one block: its own)."""
+    NB = 2 if PF == 1 else 4
+    text = []
+    for k in range(PF):
+        if k:
+            text.append(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
+        for q in range(4):
+            text.append(f"buffer_load_dwordx4 %[b{(C0 + k) % NB}_{q}], %[voff], %[rc], "
+                        f"{'%[tmp]' if k else '%[sc]'} offen offset:{q * 1024}")
+    for blk in range(max(MBW - 1, 1)):
+        text.append(f"ds_read_b128 %[a{blk}_0], %[d{blk}] offset:{64 * C0}")
+        text.append(f"ds_read_b128 %[a{blk}_1], %[d{blk}] offset:{64 * C0 + 256}")
+    return "\\n\\t".join(text)
+
+
 def operand_list(MBW, NB=2):
     outs = []
     for k in range(MBW):
@@ -192,21 +212,11 @@ def main():
     for MBW in (1, 2, 3, 4, 6):
         for C0, PF in ((0, 1), (0, 2), (2, 1)):
             NB = 2 if PF == 1 else 4
-            text = []
-            for k in range(PF):
-                if k:
-                    text.append(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
-                for q in range(4):
-                    text.append(f"buffer_load_dwordx4 %[b{(C0 + k) % NB}_{q}], %[voff], %[rc], "
-                                f"{'%[tmp]' if k else '%[sc]'} offen offset:{q * 1024}")
-            for blk in range(max(MBW - 1, 1)):
-                text.append(f"ds_read_b128 %[a{blk}_0], %[d{blk}] offset:{64 * C0}")
-                text.append(f"ds_read_b128 %[a{blk}_1], %[d{blk}] offset:{64 * C0 + 256}")
+            body = prologue_asm(MBW, C0, PF)
             outs = [f'[a{k}_{t}] "+v"(aq[{k}][{t}])' for k in range(MBW) for t in range(2)]
             outs += [f'[b{j}_{q}] "+v"(bq[{j}][{q}])' for j in range(NB) for q in range(4)]
             outs.append('[tmp] "=&s"(tmp)')
             ins = [f'[d{k}] "v"(ad[{k}])' for k in range(MBW)] + ['[voff] "v"(voff)', '[rc] "s"(rc)', '[sc] "s"(sc)']
-            body = "\\n\\t".join(text)
             out.append(f"template <>\nstruct KPro<{MBW}, {C0}, {PF}> {{\n"
                        f"  __device__ __forceinline__ static void run(az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                        f"      const int (&ad)[{MBW}], int voff, az_rsrc rc, int sc) {{\n"

@@ -170,6 +170,7 @@ def test_tree_api_edges_match_reference(golden, name):
         eng = synth_engine(z, 1)
         eng.tree_reset([0], np.zeros((1, H, W), np.int8))
         rng = np.random.RandomState(int(seed))
+        rng.rand(1, H, W, 4)  # play_game's model construction (model.py:167-169)
         T = int(z["game_len"][g])
         for ply in range(T):
             if noisy:
