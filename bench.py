@@ -464,7 +464,7 @@ def chess_main(args):
     avg_ms = st1["conv_ms"] / max(launches, 1)
     roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, avg_ms, st1["conv_busy_ms"],
                          local_evals, launches, direct_flop, issued,
-                         os.path.join(REPO, "profiles", "r4", "pmc_chess.json"),
+                         os.path.join(REPO, "profiles", "r5", "pmc_chess.json"),
                          ("tower16_rows" if tower else "f16x2") if args.conv_algo != 1 else "direct", chess=True,
                          tower=tower)
     if rank == 0:
@@ -804,8 +804,8 @@ def main():
     per_forward = 1 if args.conv_algo == 0 else 2 * args.depth
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     boards_per_launch = local_evals / max(conv_launches / per_forward, 1)
-    pmc = os.path.join(REPO, "profiles", "r4", "pmc_tower.json")
-    # the PMC entry of this board shape (profiles/r4/collect_pmc.sh: 6x7 "tower16", 9x9 "tower16_9x9")
+    pmc = os.path.join(REPO, "profiles", "r5", "pmc_tower.json")
+    # the PMC entry of this board shape (profiles/r5/collect_pmc.sh: 6x7 "tower16", 9x9 "tower16_9x9")
     pmc_key = {0: "tower16", 1: "direct", 2: "f16x2"}[args.conv_algo]
     if (args.height, args.width) != (6, 7):
         pmc_key += f"_{args.height}x{args.width}"
