@@ -16,7 +16,7 @@
 //
 // Workgroup = 8 waves (two per SIMD): wave w takes M half w & 1 (MBW 16-row
 // blocks) and N quarter w >> 1 (32 output channels) -- in general M part
-// w % NWM, N quarter w / NWM (the chess 64-row tiles: NWM = 4, 16 waves).  The two waves loading
+// w % NWM, N quarter w / NWM (variants/nwm4.py: NWM = 4, 16 waves).  The two waves loading
 // one N quarter's weight fragments are then w and w ^ 1: a workgroup's waves
 // go to the SIMDs in the order 0, 2, 1, 3, so they sit on different SIMDs
 // and are both the older (waves 0-3) or both the younger (4-7) wave of their
@@ -1442,12 +1442,11 @@ void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged, bool db
   if (n_max <= 0 || tile_rows != 128) return;
   // a launch of fewer than 512 boards (chess self-play: 128 per lane) in
   // 2-board tiles would hold under a quarter of the 256 CUs: one board per
-  // 64-row tile then (MI355X has 256 CUs; the same sums, bitwise), in 16
-  // waves -- one 16-row block x 32 channels each, four waves per SIMD at 124
-  // VGPRs -- so the tile's latency (the chess step's bound: half the CUs
-  // idle) is hidden by four waves instead of two
+  // 64-row tile then (MI355X has 256 CUs; the same sums, bitwise), 8 waves of
+  // 2 blocks.  (16 waves of one block, four per SIMD: 1.16 M against 1.55 M
+  // expansions/s, profiles/r5/ab_chess.txt)
   if (n_max < 512)
-    launch_mbw<4, 4, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
+    launch_mbw<4, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
                            0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s);
   else
     launch_mbw<8, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,

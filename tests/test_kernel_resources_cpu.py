@@ -4,7 +4,7 @@ edge of that budget -- a change that makes the compiler spill inside the
 loops halves the kernel's speed (round 3: 140 spilled VGPRs, 2911 games/s
 against 5270).  hipcc's resource remarks for az_tower16.hip must show the
 double-buffered kernels every config runs (128-row Connect-4, 96-row 9x9,
-the chess input-row forms in 128-row tiles and 64-row tiles of 16 waves)
+the chess input-row forms in 128- and 64-row tiles)
 at no spilled VGPR, the in-place fallbacks at <= 8, and the 192-row in-place
 tile 9x9 runs (two accumulator sets of 6 blocks) at <= 24, outside its K
 loops.
@@ -47,7 +47,7 @@ def test_tower_kernel_register_budget(tmp_path):
     rows = [v for k, v in spills.items() if "tower16_kernelILi8ELi2ELb1ELb1E" in k]
     inplace = [v for k, v in spills.items() if "tower16_kernel" in k and "Lb0EEEv" in k and "ILi12E" not in k]
     t192 = [v for k, v in spills.items() if "tower16_kernelILi12ELi2ELb0ELb0E" in k]
-    rows64 = [v for k, v in spills.items() if "tower16_kernelILi4ELi4ELb1ELb1E" in k]
+    rows64 = [v for k, v in spills.items() if "tower16_kernelILi4ELi2ELb1ELb1E" in k]
     assert t128 and t96 and rows and rows64 and t192 and len(inplace) == 4, spills
     assert t128[0] == 0 and t96[0] == 0 and rows[0] == 0 and rows64[0] == 0, spills  # the forms every config runs
     assert max(inplace) <= 8, spills  # the in-place fallback (LDS too small for two tiles)
