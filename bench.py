@@ -85,6 +85,9 @@ def parse():
                          "8*S*A + H*W*A: ~5x the high-water mark measured at configs[1] and configs[3]), "
                          "'proof' (S*H*W*A + A, no game can overflow, capped at 40%% of free HBM) or a number; "
                          "an overflow is a device error, never an overrun")
+    ap.add_argument("--rng-skip", type=int, default=None,
+                    help="MT19937 words each game's stream discards after its seed (default: the reference "
+                         "play_game's model-construction draws, 2*H*W*4; 0: round 4's streams)")
     ap.add_argument("--compact", type=int, default=1,
                     help="1: reclaim the subtrees a game has left after every move (az_config.compact)")
     ap.add_argument("--no-cache-window", action="store_true",
@@ -657,7 +660,7 @@ def main():
     eng = az.Engine(args.height, args.width, args.n, True, args.sims, slots=args.slots,
                     evaluator=az.EVAL_NETWORK, depth=args.depth, device=dev_index,
                     cache_log2=args.cache_log2, lanes=args.lanes, conv_algo=args.conv_algo,
-                    compact=bool(args.compact), arena_edges=arena_edges_arg(args))
+                    compact=bool(args.compact), arena_edges=arena_edges_arg(args), rng_skip=args.rng_skip)
     eng.set_weights(named)
     tree_steps = 3
     total_moves = MAX_PREROLL + 2 * args.steps + tree_steps + args.warmup
