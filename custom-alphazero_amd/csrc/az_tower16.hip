@@ -498,6 +498,9 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   __builtin_amdgcn_s_setprio(0);
 }
 
+#ifndef AZ_KLOOP_TERM  // 1: term-major k-steps (gen_kloop_asm.term_group_asm)
+#define AZ_KLOOP_TERM 0
+#endif
 #ifndef AZ_KLOOP_PF  // 2: +1% games/s over 1 at configs[1] (profiles/r5/ab_kloop.txt)
 #define AZ_KLOOP_PF 2
 #endif
@@ -556,7 +559,7 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
   // for it, vmcnt(0) lgkmcnt(0), before every group of the loop)
   if (R) own(cur);
   else tap_addr(0, cur);
-  KPro<MBW, C0, PF>::run(aq, bq, cur, voff, R ? rs_r : rs_m, R ? 36 * 16384 : C0 * 16384);
+  KPro<MBW, C0, PF, AZ_KLOOP_TERM>::run(aq, bq, cur, voff, R ? rs_r : rs_m, R ? 36 * 16384 : C0 * 16384);
   const bool young = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= 256;
   auto prio = [&](bool hi) {
     if (hi) __builtin_amdgcn_s_setprio(1);
@@ -565,7 +568,7 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
   prio(young);
   if constexpr (R) {
     tap_addr(0, nxt);
-    KGroup<MBW, 0, 0, PF>::run(accr, aq, bq, cur, nxt, voff, rs_r, rs_m, 36 * 16384, 0);
+    KGroup<MBW, 0, 0, PF, AZ_KLOOP_TERM>::run(accr, aq, bq, cur, nxt, voff, rs_r, rs_m, 36 * 16384, 0);
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) cur[mb] = nxt[mb];
     mid();
@@ -582,9 +585,10 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
     }
     const int m = (skw >> (2 * t)) & 3;
     const int sc = 4 * t * 16384, sn = t < 8 ? (4 * (t + 1) + C0) * 16384 : sc + C0 * 16384;
-    if (m == 0) KGroup<MBW, C0, 0, PF>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
-    else if (m == 1) KGroup<MBW, C0, (MBW > 1 ? 1 : 0), PF>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
-    else KGroup<MBW, C0, (MBW > 1 ? 2 : 0), PF>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    constexpr int O = AZ_KLOOP_TERM;
+    if (m == 0) KGroup<MBW, C0, 0, PF, O>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    else if (m == 1) KGroup<MBW, C0, (MBW > 1 ? 1 : 0), PF, O>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
+    else KGroup<MBW, C0, (MBW > 1 ? 2 : 0), PF, O>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) cur[mb] = nxt[mb];
   }

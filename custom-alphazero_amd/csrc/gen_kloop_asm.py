@@ -155,6 +155,116 @@ def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     return "\\n\\t".join(lines)
 
 
+def term_group_asm(MBW, C0, SKC, PF=1):
+    """The same group in term-major order: per k-step all blocks' t1*B0
+    products (phase 0), then all blocks' t0*b1 (phase 1), then t0*B0 (phase
+    2), so an accumulator's three dependent MFMAs sit 2*MBW instructions
+    apart instead of 2 (each accumulator still sums t1*B0, t0*b1, t0*B0 in
+    that order: bitwise the block-major sums).  Reads by term: block mb's
+    next t1 fragment right after its phase-1 pair (t1 is dead after phase
+    0), its next t0 fragment after block mb+1's phase-2 pair (lagged: one
+    pair between the last reader and the load), the last block's in the
+    next k-step after block 0's phase-0 pair.  Weight fragments load in the
+    order 0, 2, 1, 3 (phase 0 needs fragments 0 and 2)."""
+    lines = []
+    emit = lines.append
+    chunks = list(range(C0, 4))
+    skipped = lambda mb: (SKC >> mb) & 1  # noqa: E731
+    NB = 2 if PF == 1 else 4
+    # reads in flight at group entry (the predecessor's or the prologue's),
+    # in issue order: every block's t1 of chunk C0, then t0 of blocks < MBW-1
+    issued = [(mb, C0, 1) for mb in range(MBW)] + [(mb, C0, 0) for mb in range(MBW - 1)]
+
+    def wait_a(blk, ch, term):
+        for i in range(len(issued) - 1, -1, -1):
+            if issued[i] == (blk, ch, term):
+                emit(f"s_waitcnt lgkmcnt({min(len(issued) - 1 - i, 15)})")
+                return
+        raise AssertionError(f"read of {(blk, ch, term)} not issued")
+
+    def read(blk, ch, term, addr):
+        emit(f"ds_read_b128 %[a{blk}_{term}], {addr} offset:{64 * ch + 256 * term}")
+        issued.append((blk, ch, term))
+
+    for c in chunks:
+        last_chunk = c == 3
+        bs = c % NB
+        P = 4 * PF
+        emit(f"; k-step chunk {c}")
+        k = c + PF
+        bn = (k if k < 4 else C0 + k - 4) % NB
+        if k < 4:
+            emit(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
+            src = "%[rc], %[tmp]"
+        elif k == 4:
+            src = "%[rn], %[sn]"
+        else:
+            emit(f"s_add_u32 %[tmp], %[sn], {(k - 4) * KSTEP}")
+            src = "%[rn], %[tmp]"
+        for q in (0, 2, 1, 3):
+            emit(f"buffer_load_dwordx4 %[b{bn}_{q}], %[voff], {src} offen offset:{q * 1024}")
+        live = [mb for mb in range(MBW) if not skipped(mb)]
+        # phase 0: t1 * B0
+        emit(f"s_waitcnt vmcnt({P + 2})")  # fragments 0 and 2 of this k-step
+        for i, mb in enumerate(live):
+            wait_a(mb, c, 1)
+            emit(f"v_mfma_f32_16x16x32_f16 %[c{mb}_0], %[b{bs}_0], %[a{mb}_1], %[c{mb}_0]")
+            emit(f"v_mfma_f32_16x16x32_f16 %[c{mb}_1], %[b{bs}_2], %[a{mb}_1], %[c{mb}_1]")
+            if i == 0 and not skipped(MBW - 1) and MBW > 1:
+                read(MBW - 1, c, 0, f"%[d{MBW - 1}]")  # the last block's t0, lagged from the k-step before
+        if MBW == 1:
+            read(0, c, 0, "%[d0]")
+        if not live and MBW > 1 and not skipped(MBW - 1):
+            read(MBW - 1, c, 0, f"%[d{MBW - 1}]")
+        # phase 1: t0 * b1; then the block's next t1
+        emit(f"s_waitcnt vmcnt({P})")
+        for mb in range(MBW):
+            if not skipped(mb):
+                wait_a(mb, c, 0)
+                emit(f"v_mfma_f32_16x16x32_f16 %[c{mb}_0], %[b{bs}_1], %[a{mb}_0], %[c{mb}_0]")
+                emit(f"v_mfma_f32_16x16x32_f16 %[c{mb}_1], %[b{bs}_3], %[a{mb}_0], %[c{mb}_1]")
+            if not last_chunk:
+                if not skipped(mb):
+                    read(mb, c + 1, 1, f"%[d{mb}]")
+            else:
+                read(mb, C0, 1, f"%[n{mb}]")
+        # phase 2: t0 * B0; then the previous block's next t0
+        last_mfma = None
+        for mb in range(MBW):
+            if not skipped(mb):
+                emit(f"v_mfma_f32_16x16x32_f16 %[c{mb}_0], %[b{bs}_0], %[a{mb}_0], %[c{mb}_0]")
+                emit(f"v_mfma_f32_16x16x32_f16 %[c{mb}_1], %[b{bs}_2], %[a{mb}_0], %[c{mb}_1]")
+                last_mfma = mb
+            if mb >= 1:
+                blk = mb - 1
+                if last_chunk or not skipped(blk):
+                    if last_mfma == blk:
+                        emit("s_nop 4")  # no pair between the slot's last reader and this load
+                    read(blk, C0 if last_chunk else c + 1, 0, f"%[n{blk}]" if last_chunk else f"%[d{blk}]")
+    emit("s_nop 7")
+    emit("s_nop 7")
+    return "\\n\\t".join(lines)
+
+
+def term_prologue_asm(MBW, C0, PF):
+    """The term-major group's entry state: the first PF k-steps' weights
+    (fragments 0, 2, 1, 3), every block's t1 of chunk C0, then the t0 of
+    blocks 0..MBW-2."""
+    NB = 2 if PF == 1 else 4
+    text = []
+    for k in range(PF):
+        if k:
+            text.append(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
+        for q in (0, 2, 1, 3):
+            text.append(f"buffer_load_dwordx4 %[b{(C0 + k) % NB}_{q}], %[voff], %[rc], "
+                        f"{'%[tmp]' if k else '%[sc]'} offen offset:{q * 1024}")
+    for blk in range(MBW):
+        text.append(f"ds_read_b128 %[a{blk}_1], %[d{blk}] offset:{64 * C0 + 256}")
+    for blk in range(MBW - 1):
+        text.append(f"ds_read_b128 %[a{blk}_0], %[d{blk}] offset:{64 * C0}")
+    return "\\n\\t".join(text)
+
+
 def prologue_asm(MBW, C0, PF):
     """The prologue: the first PF k-steps' B fragments (rc, from soffset sc)
     and the A reads a group's predecessor leaves in flight (blocks 0..MBW-2
@@ -203,21 +313,22 @@ def main():
                "// register operands must be vector types (HIP's uint4 is a struct)\n"
                "typedef unsigned az_u4 __attribute__((ext_vector_type(4)));\n"
                "typedef float az_f4 __attribute__((ext_vector_type(4)));\n")
-    out.append("template <int MBW, int C0, int SKC, int PF>\nstruct KGroup;\n"
-               "template <int MBW, int C0, int PF>\nstruct KPro;\n"
+    out.append("// ORD 0: block-major k-steps (group_asm), 1: term-major (term_group_asm)\n"
+               "template <int MBW, int C0, int SKC, int PF, int ORD>\nstruct KGroup;\n"
+               "template <int MBW, int C0, int PF, int ORD>\nstruct KPro;\n"
                "template <int MBW, int NB>\nstruct KDrain;\n")
     # the prologue: the first PF k-steps' B fragments and the A reads a
     # group's predecessor leaves in flight (blocks 0..MBW-2 of chunk C0; one
     # block: its own)
     for MBW in (1, 2, 3, 4, 6):
-        for C0, PF in ((0, 1), (0, 2), (2, 1)):
+        for C0, PF, ORD in [(c, p, o) for c, p in ((0, 1), (0, 2), (2, 1)) for o in (0, 1)]:
             NB = 2 if PF == 1 else 4
-            body = prologue_asm(MBW, C0, PF)
+            body = (term_prologue_asm if ORD else prologue_asm)(MBW, C0, PF)
             outs = [f'[a{k}_{t}] "+v"(aq[{k}][{t}])' for k in range(MBW) for t in range(2)]
             outs += [f'[b{j}_{q}] "+v"(bq[{j}][{q}])' for j in range(NB) for q in range(4)]
             outs.append('[tmp] "=&s"(tmp)')
             ins = [f'[d{k}] "v"(ad[{k}])' for k in range(MBW)] + ['[voff] "v"(voff)', '[rc] "s"(rc)', '[sc] "s"(sc)']
-            out.append(f"template <>\nstruct KPro<{MBW}, {C0}, {PF}> {{\n"
+            out.append(f"template <>\nstruct KPro<{MBW}, {C0}, {PF}, {ORD}> {{\n"
                        f"  __device__ __forceinline__ static void run(az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                        f"      const int (&ad)[{MBW}], int voff, az_rsrc rc, int sc) {{\n"
                        f"    int tmp;\n"
@@ -241,15 +352,15 @@ def main():
                        f"  }}\n}};\n")
     count = 0
     for MBW in (1, 2, 3, 4, 6):
-        for C0, PF in ((0, 1), (0, 2), (2, 1)):
+        for C0, PF, ORD in [(c, p, o) for c, p in ((0, 1), (0, 2), (2, 1)) for o in (0, 1)]:
             NB = 2 if PF == 1 else 4
             for SKC in (0, 1, 2):
                 if MBW == 1 and SKC:
                     continue
                 count += 1
-                text = group_asm(MBW, C0, SKC, PF)
+                text = (term_group_asm if ORD else group_asm)(MBW, C0, SKC, PF)
                 outs, ins = operand_list(MBW, NB)
-                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}, {PF}> {{\n"
+                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}, {PF}, {ORD}> {{\n"
                            f"  __device__ __forceinline__ static void run(az_f4 (&acc)[{MBW}][2], az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                            f"      const int (&ad)[{MBW}], const int (&an)[{MBW}], int voff, az_rsrc rc, az_rsrc rn,\n"
                            f"      int sc, int sn) {{\n"

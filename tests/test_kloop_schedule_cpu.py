@@ -37,6 +37,7 @@ class Machine:
         self.vm = deque()  # pending (reg, label)
         self.lgkm = deque()
         self.acc = {}  # (block, n) -> Counter of (kstep, q, t)
+        self.seq = {}  # (block, n) -> the (kstep, q, t) sequence in issue order
         self.log = []
 
     def land(self, q, keep):
@@ -94,6 +95,7 @@ class Machine:
                 assert al[0] == "A" and al[1] == ctx["d"] and al[2] == blk and al[3] == chunk, (line, al, ctx["d"], chunk)
                 assert not (ctx["skip"] >> blk) & 1, (line, "skipped block computed")
                 self.acc.setdefault((ctx["acc"], blk, n), Counter())[(kstep, bl[3], al[4], n)] += 1
+                self.seq.setdefault((ctx["acc"], blk, n), []).append((kstep, bl[3], al[4]))
             elif line.startswith("s_nop") or line.startswith(";") or not line:
                 pass
             else:
@@ -105,22 +107,27 @@ class Machine:
         assert not any(p[0] == dst for p in self.vm) and not any(p[0] == dst for p in self.lgkm), dst
 
 
-def run_loop(MBW, C0, PF, R, skw):
+ORDER = {0: [(0, 1), (1, 0), (0, 0)], 1: [(2, 1), (3, 0), (2, 0)]}  # per N block: t1*B0, t0*b1, t0*B0
+
+
+def run_loop(MBW, C0, PF, R, skw, ORD=0):
     m = Machine(MBW)
+    group = gen.term_group_asm if ORD else gen.group_asm
+    prologue = gen.term_prologue_asm if ORD else gen.prologue_asm
     # prologue: A from the phase's first source, B from its first k-step
     first_src = ("own",) if R else ("tap", 0)
     first_k = ("R", 0) if R else ("M", C0)
-    m.run(gen.prologue_asm(MBW, C0, PF), {"sc": first_k, "d": first_src, "skip": 0, "acc": "-",
+    m.run(prologue(MBW, C0, PF), {"sc": first_k, "d": first_src, "skip": 0, "acc": "-",
                                           "rc": first_k[0]})
     if R:
-        m.run(gen.group_asm(MBW, 0, 0, PF), {"sc": ("R", 0), "sn": ("M", 0), "d": ("own",), "n": ("tap", 0),
+        m.run(group(MBW, 0, 0, PF), {"sc": ("R", 0), "sn": ("M", 0), "d": ("own",), "n": ("tap", 0),
                                              "skip": 0, "acc": "res", "rc": "R", "rn": "M"})
     for t in range(9):
         mask = (skw >> (2 * t)) & 3
         skc = mask if MBW > 1 else 0
         nxt = ("tap", t + 1) if t < 8 else ("tap", 8)
         sn = ("M", 4 * (t + 1) + C0) if t < 8 else ("M", 4 * t + C0)
-        m.run(gen.group_asm(MBW, C0, skc, PF), {"sc": ("M", 4 * t), "sn": sn, "d": ("tap", t), "n": nxt,
+        m.run(group(MBW, C0, skc, PF), {"sc": ("M", 4 * t), "sn": sn, "d": ("tap", t), "n": nxt,
                                                  "skip": skc, "acc": "main", "rc": "M", "rn": "M"})
     m.land(m.vm, 0)
     m.land(m.lgkm, 0)
@@ -138,11 +145,17 @@ def run_loop(MBW, C0, PF, R, skw):
                         if nn == n:
                             want[(("M", 4 * t + c), q, tt, n)] += k
             assert got == want, (MBW, C0, PF, R, blk, n)
+            # the sum order each accumulator must keep (bitwise the compiled loop's)
+            seq = m.seq.get(("main", blk, n), [])
+            assert [x[1:] for x in seq] == ORDER[n] * (len(seq) // 3), (MBW, C0, PF, R, ORD, blk, n)
+            assert [x[0] for x in seq] == sorted(x[0] for x in seq), (MBW, C0, PF, R, ORD, blk, n)
             if R:
                 got = m.acc.get(("res", blk, n), Counter())
                 want = Counter({(("R", c), q, tt, n): k for c in range(4) for (q, tt, nn), k in NEEDED.items()
                                 if nn == n})
                 assert got == want, (MBW, C0, PF, R, blk, n, "residual")
+                seq = m.seq[("res", blk, n)]
+                assert [x[1:] for x in seq] == ORDER[n] * 4 and [x[0] for x in seq] == sorted(x[0] for x in seq)
 
 
 # the kernels' forms: (blocks per wave, first chunk, prefetch depth, residual steps)
@@ -155,7 +168,8 @@ SKIPS = [0, sum(1 << (2 * t) for t in (0, 1, 2)) | sum(2 << (2 * t) for t in (6,
 
 @pytest.mark.parametrize("MBW,C0,PF,R", FORMS)
 @pytest.mark.parametrize("skw", SKIPS)
-def test_kloop_schedule_is_exact(MBW, C0, PF, R, skw):
+@pytest.mark.parametrize("ORD", [0, 1])
+def test_kloop_schedule_is_exact(MBW, C0, PF, R, skw, ORD):
     if C0 and R:
         pytest.skip("the stem has no residual steps")
-    run_loop(MBW, C0, PF, R, skw if MBW > 1 else 0)
+    run_loop(MBW, C0, PF, R, skw if MBW > 1 else 0, ORD)
