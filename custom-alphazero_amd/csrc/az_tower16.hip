@@ -498,8 +498,8 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
   __builtin_amdgcn_s_setprio(0);
 }
 
-#ifndef AZ_KLOOP_TERM  // 1: term-major k-steps (gen_kloop_asm.term_group_asm)
-#define AZ_KLOOP_TERM 0
+#ifndef AZ_KLOOP_TERM  // 1: term-major k-steps (gen_kloop_asm.term_group_asm); 0: block-major
+#define AZ_KLOOP_TERM 1  // (within 1% of each other and of the compiled loop: profiles/r5/ab_term.txt)
 #endif
 #ifndef AZ_KLOOP_PF  // 2: +1% games/s over 1 at configs[1] (profiles/r5/ab_kloop.txt)
 #define AZ_KLOOP_PF 2
