@@ -44,6 +44,14 @@ import time
 
 import numpy as np
 
+# HIP hardware queues per process, read once at HIP's initialisation (before
+# torch or libaz touch the GPU): HIP's default 4 leaves a third lane's stream
+# sharing a queue; with 8 the engine's auto lane count runs configs[1] on 3
+# lanes, +4.9% games/s (profiles/r5/ab_queues_lanes.txt, ab_lanes_q8.txt)
+BENCH_HW_QUEUES = 8
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < BENCH_HW_QUEUES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(BENCH_HW_QUEUES)
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "custom-alphazero_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -575,7 +583,7 @@ def arena_edges_arg(args):
     return int(args.arena_edges)
 
 
-def tree_arena(args, st):
+def tree_arena(args, st, lanes):
     """The tree memory the engine chose and what the window used of it."""
     A, HW = args.width, args.height * args.width
     safe = args.sims * HW * A + A
@@ -588,7 +596,6 @@ def tree_arena(args, st):
     # capped at 2^31 - 1 edges, its indices' range, below arena_edges x slots)
     per_slot = pool // (2 * args.slots)
     proof = per_slot >= safe
-    lanes = args.lanes or (2 if args.slots >= 512 else 1)  # az_config.lanes = 0: auto
     half = pool // (2 * lanes)
     return {
         "compact": True, "sizing": args.arena_edges, "pool_edges_total": pool, "bytes_total": 32 * pool,
@@ -869,6 +876,8 @@ def main():
                 "global_batch": args.slots * world,
                 "parallelism": f"games sharded over {world} GPU(s)",
             },
+            "lanes": eng.lanes,
+            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "untimed_moves": pre,
             "untimed_rule": (f"max(--warmup, {MIN_PREROLL}) moves and until the transposition cache has "
                              f"turned over its live generations + {CACHE_TURNOVER_GENS} (stationary hit rate)"),
@@ -896,7 +905,7 @@ def main():
                 "semantics": "reference plays_inferences (mcts.py:122-143): board -> network output, shared "
                              "by all games on the GPU, emptied when weights change; bit-identical results",
             } if args.cache_log2 else None),
-            "tree_arena": tree_arena(args, st1),
+            "tree_arena": tree_arena(args, st1, eng.lanes),
             "cache_off": off,
             "roofline_tree": roofline_tree,
             "roofline": roof,

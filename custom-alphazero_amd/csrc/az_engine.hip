@@ -892,8 +892,16 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   if (c.depth == 0 || (c.conv_algo != AZ_CONV_DIRECT && !e->net.use_tower && c.board_width > 16))
     e->net.algo = AZ_CONV_DIRECT;
   e->net.err = e->t.stats + az::kStatErrors;
-  // lanes: 0 = auto (two streams once each lane still holds a few hundred games)
-  int nl = c.lanes > 0 ? c.lanes : (g.slots >= 512 ? 2 : 1);
+  // lanes: 0 = auto (two streams once each lane still holds a few hundred
+  // games; three for 1536-4096 slots when HIP gives the process a hardware
+  // queue per stream -- with 4 a third lane shares one and loses 27%:
+  // profiles/r5/ab_queues_lanes.txt; larger launches keep two)
+  int nl = c.lanes;
+  if (nl <= 0) {
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    const int queues = q && *q ? atoi(q) : 4;
+    nl = g.slots < 512 ? 1 : (queues >= 8 && g.slots >= 1536 && g.slots <= 4096) ? 3 : 2;
+  }
   nl = std::min(nl, std::min(g.slots, 8));
   if ((rc = make_lane(e, &e->whole, 0, g.slots, false))) return cleanup(rc);
   e->whole.stream = e->stream;
@@ -942,6 +950,8 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   *out = e;
   return 0;
 }
+
+int az_engine_lanes(const az_engine* eng) { return eng ? (int)eng->lanes.size() : 0; }
 
 int az_engine_destroy(az_engine* eng) {
   if (!eng) return 0;

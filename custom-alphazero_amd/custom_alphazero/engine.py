@@ -93,6 +93,7 @@ def _as_numpy(t):
 
 EXPORTED = (
     "az_abi_version", "az_last_error", "az_build_id", "az_build_flags", "az_engine_create", "az_engine_destroy",
+    "az_engine_lanes",
     "az_engine_set_weights", "az_encode", "az_forward", "az_selfplay_begin", "az_selfplay_step",
     "az_selfplay_run", "az_selfplay_results", "az_selfplay_drain", "az_tree_reset", "az_tree_release", "az_tree_search", "az_tree_search_noise", "az_tree_play",
     "az_tree_info", "az_tree_export", "az_stats_get", "az_timer_enable", "az_pow_table",
@@ -134,6 +135,7 @@ def load_library():
         "az_build_flags": (ctypes.c_char_p, []),
         "az_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(Config), ctypes.POINTER(P)]),
         "az_engine_destroy": (ctypes.c_int, [P]),
+        "az_engine_lanes": (ctypes.c_int, [P]),
         "az_engine_set_weights": (ctypes.c_int, [P, ctypes.POINTER(Tensor), ctypes.c_int]),
         "az_encode": (ctypes.c_int, [P, P, ctypes.c_int, P, P]),
         "az_forward": (ctypes.c_int, [P, P, ctypes.c_int, P, P]),
@@ -270,6 +272,11 @@ class Engine:
         self._n_games = 0
         self._host_fn = None     # the EVAL_FN object (kept alive while the engine may call it)
         self._host_error = None  # an exception the host evaluator raised inside a search
+
+    @property
+    def lanes(self):
+        """The slot groups (streams) the engine runs (az_engine_lanes)."""
+        return int(self._L.az_engine_lanes(self._h))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -165,6 +165,12 @@ const char* az_build_flags(void);
  * (self_play.py:46-57, utils.py:42-48). */
 int az_engine_create(int device, const az_config* cfg, az_engine** out);
 int az_engine_destroy(az_engine* eng);
+/* The number of slot groups (streams) the engine runs: az_config.lanes, or
+ * for lanes = 0 the engine's choice -- 1 below 512 slots; 3 for 1536-4096
+ * slots when the process has at least 8 HIP hardware queues
+ * (GPU_MAX_HW_QUEUES: a queue per lane stream; configs[1] +4.9% games/s over
+ * 2); else 2. */
+int az_engine_lanes(const az_engine* eng);
 
 /* Replaces PolicyValueModel.load_with_meta / set_weights
  * (model/tensorflow/model.py:190-201): the engine copies and folds them. */

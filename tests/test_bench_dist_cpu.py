@@ -190,11 +190,11 @@ def test_tree_arena_rule_states_the_pool_it_holds():
                               arena_edges="proof")
     safe = 100 * 42 * 7 + 7
     st = dict(arena_edges=safe, arena_pool_edges=2 * 4096 * safe, arena_pool_high=10, max_retained=5)
-    r = bench.tree_arena(args, st)
+    r = bench.tree_arena(args, st, 2)
     assert r["overflow_proof"] and r["pool_edges_per_half_per_slot"] == safe and "no game can overflow" in r["rule"]
     capped = dict(st, arena_pool_edges=2 * 2 * ((1 << 31) - 1))  # two lanes, each half at the index cap
     args.slots, args.sims = 65536, 400
-    r = bench.tree_arena(args, capped)
+    r = bench.tree_arena(args, capped, 2)
     assert not r["overflow_proof"] and r["pool_edges_per_half_per_slot"] == 2 * ((1 << 31) - 1) // 65536
     assert "share the pool" in r["rule"]
 
@@ -212,7 +212,7 @@ def test_bounded_arena_is_sized_from_the_measured_high_water_mark():
     assert bench.arena_edges_arg(argparse.Namespace(**dict(vars(args), arena_edges="proof"))) == 0
     assert bench.arena_edges_arg(argparse.Namespace(**dict(vars(args), arena_edges="1234"))) == 1234
     st = dict(arena_edges=5894, arena_pool_edges=2 * 4096 * 5894, arena_pool_high=2_090_000, max_retained=2485)
-    r = bench.tree_arena(args, st)
+    r = bench.tree_arena(args, st, 2)
     assert not r["overflow_proof"] and r["sizing"] == "bounded"
     assert r["lane_half_edges"] == 2048 * 5894 and r["high_water_fraction"] == round(2_090_000 / (2048 * 5894), 4)
     assert "measured high-water mark" in r["rule"]
