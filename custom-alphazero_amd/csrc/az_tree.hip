@@ -172,6 +172,11 @@ __device__ unsigned long long g_sel_stamps[16384][12];
 extern "C" int az_diag_sel_stamps(unsigned long long* out, int n_slots) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_stamps), (size_t)std::min(n_slots, 16384) * 96) == hipSuccess ? 0 : -1;
 }
+// the last select launch's dedup tail: entry and end stamps, duplicates resolved
+__device__ unsigned long long g_sel_tail[3];
+extern "C" int az_diag_sel_tail(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_tail), sizeof(g_sel_tail)) == hipSuccess ? 0 : -1;
+}
 #else
 #define AZ_SEL_STAMP(s, k) ((void)0)
 #define AZ_SEL_VALUE(s, k, v) ((void)0)
@@ -579,6 +584,12 @@ __device__ __forceinline__ void dedup_tail(const TreeDev& t, const CacheDev& c) 
   if (!last) return;  // block-uniform
   __threadfence();
   const int n = __hip_atomic_load(t.dup_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef AZ_SEL_STAMPS
+  if (threadIdx.x == 0) {
+    g_sel_tail[0] = wall_clock64();
+    g_sel_tail[2] = (unsigned long long)n;
+  }
+#endif
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int q = t.dup_q[i];
     const uint32_t slot = (uint32_t)t.eval_src[q] & 0x7fffffffu;
@@ -594,6 +605,9 @@ __device__ __forceinline__ void dedup_tail(const TreeDev& t, const CacheDev& c) 
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+#ifdef AZ_SEL_STAMPS
+    g_sel_tail[1] = wall_clock64();
+#endif
     atomicAdd(t.stats + kStatNNEvals, (unsigned long long)*t.nn_count);
     *t.sel_done = 0;  // the lane's next select launch counts from zero
   }

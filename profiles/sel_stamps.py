@@ -38,12 +38,17 @@ for _ in range(40):
 buf = np.zeros((16384, 12), np.uint64)
 phases = ["dispatch", "game_id", "prologue", "descent", "stats", "queue", "probe", "tail"]
 acc = {p: [] for p in phases}
+tails = []  # the dedup tail of each move's last select launch: (us from the launch's last slot end, us long, dups)
+tail = np.zeros(3, np.uint64)
+has_tail = hasattr(lib, "az_diag_sel_tail")
 span, depth_all, per_level = [], [], []
 lv_load, lv_reduce, lv_play = [], [], []
 for mv in range(6):
     eng.selfplay_step(1)
     eng.selfplay_drain()
     assert lib.az_diag_sel_stamps(buf.ctypes.data, 16384) == 0
+    if has_tail:
+        assert lib.az_diag_sel_tail(tail.ctypes.data) == 0
     rows = buf[(buf[:, 0] != 0) & (buf[:, 6] != 0)].astype(np.int64)
     rows = rows[np.argsort(rows[:, 0])]
     # launches: the two lanes' last selects run at different times
@@ -69,6 +74,9 @@ for mv in range(6):
         lv_load.append(part[d > 0, 8] / 100.0 / d[d > 0])
         lv_reduce.append(part[d > 0, 9] / 100.0 / d[d > 0])
         lv_play.append(part[d > 0, 10] / 100.0 / d[d > 0])
+    if has_tail and len(rows):
+        last_end = rows[:, 6].max()
+        tails.append(((int(tail[0]) - int(last_end)) / 100.0, (int(tail[1]) - int(tail[0])) / 100.0, int(tail[2])))
 
 print(f"{'synthetic evaluator' if synth else 'network evaluator'}: {len(span)} select launches, "
       f"launch span (first entry -> last end) mean {np.mean(span):.1f} us, max {np.max(span):.1f} us")
@@ -81,3 +89,7 @@ lv = np.concatenate(per_level)
 print(f"  depth mean {d.mean():.2f} max {d.max()}; descent per level mean {lv.mean():.2f} us p50 {np.median(lv):.2f}")
 print(f"  per level (s_waitcnt 0 at each stamp): edge+table loads {np.concatenate(lv_load).mean():.2f} us, "
       f"UCB + first-max + broadcast {np.concatenate(lv_reduce).mean():.2f} us, play {np.concatenate(lv_play).mean():.2f} us")
+if tails:
+    t = np.array(tails, np.float64)
+    print(f"dedup tail (last select launch of each move): starts {t[:, 0].mean():.1f} us after the last slot's end, "
+          f"runs {t[:, 1].mean():.1f} us (max {t[:, 1].max():.1f}), {t[:, 2].mean():.0f} duplicates")
