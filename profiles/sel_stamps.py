@@ -41,6 +41,8 @@ acc = {p: [] for p in phases}
 tails = []  # the dedup tail of each move's last select launch: (us from the launch's last slot end, us long, dups)
 tail = np.zeros(3, np.uint64)
 has_tail = hasattr(lib, "az_diag_sel_tail")
+if has_tail:
+    lib.az_diag_sel_tail.argtypes = [ctypes.c_void_p]
 span, depth_all, per_level = [], [], []
 lv_load, lv_reduce, lv_play = [], [], []
 for mv in range(6):
