@@ -574,7 +574,10 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
     mid();
   }
   // 9 taps, each in three bodies by the wave's skip mask (slot plan: never 3);
-  // the last tap's prefetch re-reads its own first k-step (harmless, drained)
+  // the last tap's prefetch re-reads its own first k-steps (drained; a peeled
+  // last tap without them -- the generator's HASNEXT = 0 groups -- made the
+  // allocator spill 400-550 VGPRs in the 128-row kernels)
+  constexpr int O = AZ_KLOOP_TERM;
 #pragma unroll 1
   for (int t = 0; t < 9; ++t) {
     if (t == 6) prio(!young);
@@ -585,7 +588,6 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
     }
     const int m = (skw >> (2 * t)) & 3;
     const int sc = 4 * t * 16384, sn = t < 8 ? (4 * (t + 1) + C0) * 16384 : sc + C0 * 16384;
-    constexpr int O = AZ_KLOOP_TERM;
     if (m == 0) KGroup<MBW, C0, 0, PF, O>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
     else if (m == 1) KGroup<MBW, C0, (MBW > 1 ? 1 : 0), PF, O>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);
     else KGroup<MBW, C0, (MBW > 1 ? 2 : 0), PF, O>::run(accm, aq, bq, cur, nxt, voff, rs_m, rs_m, sc, sn);

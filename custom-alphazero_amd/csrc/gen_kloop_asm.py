@@ -76,7 +76,7 @@ def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     for ci, c in enumerate(chunks):
         last_chunk = c == 3
         prefetch = c + PF < 4 or HASNEXT
-        P = 4 * PF if prefetch else 0  # weight loads issued after this k-step's
+        P = 4 * sum(1 for j in range(c + 1, c + PF + 1) if j <= 3 or HASNEXT)  # weight loads issued after this k-step's
         NB = 2 if PF == 1 else 4
         bs = c % NB  # this k-step's B buffer
         emit(f"; k-step chunk {c}")
@@ -155,7 +155,7 @@ def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     return "\\n\\t".join(lines)
 
 
-def term_group_asm(MBW, C0, SKC, PF=1):
+def term_group_asm(MBW, C0, SKC, PF=1, HASNEXT=1):
     """The same group in term-major order: per k-step all blocks' t1*B0
     products (phase 0), then all blocks' t0*b1 (phase 1), then t0*B0 (phase
     2), so an accumulator's three dependent MFMAs sit 2*MBW instructions
@@ -165,7 +165,9 @@ def term_group_asm(MBW, C0, SKC, PF=1):
     0), its next t0 fragment after block mb+1's phase-2 pair (lagged: one
     pair between the last reader and the load), the last block's in the
     next k-step after block 0's phase-0 pair.  Weight fragments load in the
-    order 0, 2, 1, 3 (phase 0 needs fragments 0 and 2)."""
+    order 0, 2, 1, 3 (phase 0 needs fragments 0 and 2).  HASNEXT = 0: the
+    loop's last group -- no prefetch or reads for a next one, so the drain
+    after it waits for nothing."""
     lines = []
     emit = lines.append
     chunks = list(range(C0, 4))
@@ -189,20 +191,25 @@ def term_group_asm(MBW, C0, SKC, PF=1):
     for c in chunks:
         last_chunk = c == 3
         bs = c % NB
-        P = 4 * PF
+        # weight loads issued after this k-step's: the next PF k-steps' (the next group's only with HASNEXT)
+        P = 4 * sum(1 for j in range(c + 1, c + PF + 1) if j <= 3 or HASNEXT)
         emit(f"; k-step chunk {c}")
         k = c + PF
         bn = (k if k < 4 else C0 + k - 4) % NB
+        src = None
         if k < 4:
             emit(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
             src = "%[rc], %[tmp]"
+        elif not HASNEXT:
+            pass
         elif k == 4:
             src = "%[rn], %[sn]"
         else:
             emit(f"s_add_u32 %[tmp], %[sn], {(k - 4) * KSTEP}")
             src = "%[rn], %[tmp]"
-        for q in (0, 2, 1, 3):
-            emit(f"buffer_load_dwordx4 %[b{bn}_{q}], %[voff], {src} offen offset:{q * 1024}")
+        if src:
+            for q in (0, 2, 1, 3):
+                emit(f"buffer_load_dwordx4 %[b{bn}_{q}], %[voff], {src} offen offset:{q * 1024}")
         live = [mb for mb in range(MBW) if not skipped(mb)]
         # phase 0: t1 * B0
         emit(f"s_waitcnt vmcnt({P + 2})")  # fragments 0 and 2 of this k-step
@@ -226,7 +233,7 @@ def term_group_asm(MBW, C0, SKC, PF=1):
             if not last_chunk:
                 if not skipped(mb):
                     read(mb, c + 1, 1, f"%[d{mb}]")
-            else:
+            elif HASNEXT:
                 read(mb, C0, 1, f"%[n{mb}]")
         # phase 2: t0 * B0; then the previous block's next t0
         last_mfma = None
@@ -237,7 +244,7 @@ def term_group_asm(MBW, C0, SKC, PF=1):
                 last_mfma = mb
             if mb >= 1:
                 blk = mb - 1
-                if last_chunk or not skipped(blk):
+                if (last_chunk and HASNEXT) or (not last_chunk and not skipped(blk)):
                     if last_mfma == blk:
                         emit("s_nop 4")  # no pair between the slot's last reader and this load
                     read(blk, C0 if last_chunk else c + 1, 0, f"%[n{blk}]" if last_chunk else f"%[d{blk}]")
@@ -314,7 +321,7 @@ def main():
                "typedef unsigned az_u4 __attribute__((ext_vector_type(4)));\n"
                "typedef float az_f4 __attribute__((ext_vector_type(4)));\n")
     out.append("// ORD 0: block-major k-steps (group_asm), 1: term-major (term_group_asm)\n"
-               "template <int MBW, int C0, int SKC, int PF, int ORD>\nstruct KGroup;\n"
+               "template <int MBW, int C0, int SKC, int PF, int ORD, int HN = 1>\nstruct KGroup;\n"
                "template <int MBW, int C0, int PF, int ORD>\nstruct KPro;\n"
                "template <int MBW, int NB>\nstruct KDrain;\n")
     # the prologue: the first PF k-steps' B fragments and the A reads a
@@ -354,13 +361,13 @@ def main():
     for MBW in (1, 2, 3, 4, 6):
         for C0, PF, ORD in [(c, p, o) for c, p in ((0, 1), (0, 2), (2, 1)) for o in (0, 1)]:
             NB = 2 if PF == 1 else 4
-            for SKC in (0, 1, 2):
+            for SKC, HN in [(k, h) for k in (0, 1, 2) for h in (1, 0)]:
                 if MBW == 1 and SKC:
                     continue
                 count += 1
-                text = (term_group_asm if ORD else group_asm)(MBW, C0, SKC, PF)
+                text = (term_group_asm if ORD else group_asm)(MBW, C0, SKC, PF, HN)
                 outs, ins = operand_list(MBW, NB)
-                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}, {PF}, {ORD}> {{\n"
+                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}, {PF}, {ORD}, {HN}> {{\n"
                            f"  __device__ __forceinline__ static void run(az_f4 (&acc)[{MBW}][2], az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                            f"      const int (&ad)[{MBW}], const int (&an)[{MBW}], int voff, az_rsrc rc, az_rsrc rn,\n"
                            f"      int sc, int sn) {{\n"

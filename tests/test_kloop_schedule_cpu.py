@@ -110,7 +110,7 @@ class Machine:
 ORDER = {0: [(0, 1), (1, 0), (0, 0)], 1: [(2, 1), (3, 0), (2, 0)]}  # per N block: t1*B0, t0*b1, t0*B0
 
 
-def run_loop(MBW, C0, PF, R, skw, ORD=0):
+def run_loop(MBW, C0, PF, R, skw, ORD=0, LAST_HN=1):
     m = Machine(MBW)
     group = gen.term_group_asm if ORD else gen.group_asm
     prologue = gen.term_prologue_asm if ORD else gen.prologue_asm
@@ -125,10 +125,15 @@ def run_loop(MBW, C0, PF, R, skw, ORD=0):
     for t in range(9):
         mask = (skw >> (2 * t)) & 3
         skc = mask if MBW > 1 else 0
+        # the last tap (HN = 1, as k_loop_asm runs it) prefetches its own first
+        # k-steps again, the drain waits for them; HN = 0: nothing in flight after it
         nxt = ("tap", t + 1) if t < 8 else ("tap", 8)
         sn = ("M", 4 * (t + 1) + C0) if t < 8 else ("M", 4 * t + C0)
-        m.run(group(MBW, C0, skc, PF), {"sc": ("M", 4 * t), "sn": sn, "d": ("tap", t), "n": nxt,
-                                                 "skip": skc, "acc": "main", "rc": "M", "rn": "M"})
+        hn = 1 if t < 8 else LAST_HN
+        m.run(group(MBW, C0, skc, PF, hn), {"sc": ("M", 4 * t), "sn": sn, "d": ("tap", t), "n": nxt,
+                                             "skip": skc, "acc": "main", "rc": "M", "rn": "M"})
+    if LAST_HN == 0:
+        assert not m.vm and not m.lgkm, (m.vm, m.lgkm)
     m.land(m.vm, 0)
     m.land(m.lgkm, 0)
     # every accumulator: each k-step's six products exactly once, skipped taps none
@@ -169,7 +174,8 @@ SKIPS = [0, sum(1 << (2 * t) for t in (0, 1, 2)) | sum(2 << (2 * t) for t in (6,
 @pytest.mark.parametrize("MBW,C0,PF,R", FORMS)
 @pytest.mark.parametrize("skw", SKIPS)
 @pytest.mark.parametrize("ORD", [0, 1])
-def test_kloop_schedule_is_exact(MBW, C0, PF, R, skw, ORD):
+@pytest.mark.parametrize("LAST_HN", [1, 0])
+def test_kloop_schedule_is_exact(MBW, C0, PF, R, skw, ORD, LAST_HN):
     if C0 and R:
         pytest.skip("the stem has no residual steps")
-    run_loop(MBW, C0, PF, R, skw if MBW > 1 else 0, ORD)
+    run_loop(MBW, C0, PF, R, skw if MBW > 1 else 0, ORD, LAST_HN)
