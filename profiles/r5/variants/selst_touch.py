@@ -1,0 +1,4 @@
+# Diagnostic build: select-phase stamps (profiles/sel_stamps.py) on the product's descent.
+s = open("az_tree.hip").read()
+s = "#define AZ_SEL_STAMPS 1\n" + s
+open("az_tree.hip", "w").write(s)
