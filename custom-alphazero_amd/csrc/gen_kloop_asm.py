@@ -39,7 +39,14 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "az_kloop_asm.h")
 KSTEP = 16384  # bytes of one k-step's packed B fragments (az_tower16.hip load_bk)
 
 
-def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
+def nbufs(PF):
+    """B buffers for a prefetch depth: k-step j of tap t lives in buffer
+    (4 (t mod 2) + j) mod NB -- so with 8 (PF 3-4) a group's buffers depend on
+    its tap's parity TP and the kernels dispatch on it."""
+    return 2 if PF == 1 else 4 if PF == 2 else 8
+
+
+def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1, TP=0):
     """Assembly text of one group (chunks C0..3) and its operand names.
     Operands (names used in the text):
       %[aK_T]   ring slot K (block), term T (0: t0, 1: t1)   "+v" az_u4
@@ -77,14 +84,14 @@ def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
         last_chunk = c == 3
         prefetch = c + PF < 4 or HASNEXT
         P = 4 * sum(1 for j in range(c + 1, c + PF + 1) if j <= 3 or HASNEXT)  # weight loads issued after this k-step's
-        NB = 2 if PF == 1 else 4
-        bs = c % NB  # this k-step's B buffer
+        NB = nbufs(PF)
+        bs = (4 * TP + c) % NB  # this k-step's B buffer
         emit(f"; k-step chunk {c}")
         if prefetch:
             # the k-step this one prefetches: chunk k of this group, or (k >= 4)
             # the next group's (k - 4)-th, chunk C0 + k - 4 (sn: its first)
             k = c + PF
-            bn = (k if k < 4 else C0 + k - 4) % NB
+            bn = (4 * TP + (k if k < 4 else C0 + k)) % NB
             if k < 4:
                 emit(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
                 src = "%[rc], %[tmp]"
@@ -155,7 +162,7 @@ def group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, LAGFIRST=0, LAST_NOP=1):
     return "\\n\\t".join(lines)
 
 
-def term_group_asm(MBW, C0, SKC, PF=1, HASNEXT=1):
+def term_group_asm(MBW, C0, SKC, PF=1, HASNEXT=1, TP=0):
     """The same group in term-major order: per k-step all blocks' t1*B0
     products (phase 0), then all blocks' t0*b1 (phase 1), then t0*B0 (phase
     2), so an accumulator's three dependent MFMAs sit 2*MBW instructions
@@ -172,7 +179,7 @@ def term_group_asm(MBW, C0, SKC, PF=1, HASNEXT=1):
     emit = lines.append
     chunks = list(range(C0, 4))
     skipped = lambda mb: (SKC >> mb) & 1  # noqa: E731
-    NB = 2 if PF == 1 else 4
+    NB = nbufs(PF)
     # reads in flight at group entry (the predecessor's or the prologue's),
     # in issue order: every block's t1 of chunk C0, then t0 of blocks < MBW-1
     issued = [(mb, C0, 1) for mb in range(MBW)] + [(mb, C0, 0) for mb in range(MBW - 1)]
@@ -190,12 +197,12 @@ def term_group_asm(MBW, C0, SKC, PF=1, HASNEXT=1):
 
     for c in chunks:
         last_chunk = c == 3
-        bs = c % NB
+        bs = (4 * TP + c) % NB
         # weight loads issued after this k-step's: the next PF k-steps' (the next group's only with HASNEXT)
         P = 4 * sum(1 for j in range(c + 1, c + PF + 1) if j <= 3 or HASNEXT)
         emit(f"; k-step chunk {c}")
         k = c + PF
-        bn = (k if k < 4 else C0 + k - 4) % NB
+        bn = (4 * TP + (k if k < 4 else C0 + k)) % NB
         src = None
         if k < 4:
             emit(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
@@ -253,17 +260,17 @@ def term_group_asm(MBW, C0, SKC, PF=1, HASNEXT=1):
     return "\\n\\t".join(lines)
 
 
-def term_prologue_asm(MBW, C0, PF):
+def term_prologue_asm(MBW, C0, PF, TP=0):
     """The term-major group's entry state: the first PF k-steps' weights
     (fragments 0, 2, 1, 3), every block's t1 of chunk C0, then the t0 of
     blocks 0..MBW-2."""
-    NB = 2 if PF == 1 else 4
+    NB = nbufs(PF)
     text = []
     for k in range(PF):
         if k:
             text.append(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
         for q in (0, 2, 1, 3):
-            text.append(f"buffer_load_dwordx4 %[b{(C0 + k) % NB}_{q}], %[voff], %[rc], "
+            text.append(f"buffer_load_dwordx4 %[b{(4 * TP + C0 + k) % NB}_{q}], %[voff], %[rc], "
                         f"{'%[tmp]' if k else '%[sc]'} offen offset:{q * 1024}")
     for blk in range(MBW):
         text.append(f"ds_read_b128 %[a{blk}_1], %[d{blk}] offset:{64 * C0 + 256}")
@@ -272,17 +279,17 @@ def term_prologue_asm(MBW, C0, PF):
     return "\\n\\t".join(text)
 
 
-def prologue_asm(MBW, C0, PF):
+def prologue_asm(MBW, C0, PF, TP=0):
     """The prologue: the first PF k-steps' B fragments (rc, from soffset sc)
     and the A reads a group's predecessor leaves in flight (blocks 0..MBW-2
     of chunk C0; one block: its own)."""
-    NB = 2 if PF == 1 else 4
+    NB = nbufs(PF)
     text = []
     for k in range(PF):
         if k:
             text.append(f"s_add_u32 %[tmp], %[sc], {k * KSTEP}")
         for q in range(4):
-            text.append(f"buffer_load_dwordx4 %[b{(C0 + k) % NB}_{q}], %[voff], %[rc], "
+            text.append(f"buffer_load_dwordx4 %[b{(4 * TP + C0 + k) % NB}_{q}], %[voff], %[rc], "
                         f"{'%[tmp]' if k else '%[sc]'} offen offset:{q * 1024}")
     for blk in range(max(MBW - 1, 1)):
         text.append(f"ds_read_b128 %[a{blk}_0], %[d{blk}] offset:{64 * C0}")
@@ -321,21 +328,29 @@ def main():
                "typedef unsigned az_u4 __attribute__((ext_vector_type(4)));\n"
                "typedef float az_f4 __attribute__((ext_vector_type(4)));\n")
     out.append("// ORD 0: block-major k-steps (group_asm), 1: term-major (term_group_asm)\n"
-               "template <int MBW, int C0, int SKC, int PF, int ORD, int HN = 1>\nstruct KGroup;\n"
-               "template <int MBW, int C0, int PF, int ORD>\nstruct KPro;\n"
+               "// TP: the tap's parity (selects the B buffers when PF >= 3: nbufs())\n"
+               "template <int MBW, int C0, int SKC, int PF, int ORD, int HN = 1, int TP = 0>\nstruct KGroup;\n"
+               "template <int MBW, int C0, int PF, int ORD, int TP = 0>\nstruct KPro;\n"
                "template <int MBW, int NB>\nstruct KDrain;\n")
     # the prologue: the first PF k-steps' B fragments and the A reads a
     # group's predecessor leaves in flight (blocks 0..MBW-2 of chunk C0; one
     # block: its own)
+    # forms: (C0, PF, ORD, TP); PF 3 (8 buffers) for the 1-2-block waves only
+    def forms(MBW):
+        f = [(c, p, o, 0) for c, p in ((0, 1), (0, 2), (2, 1)) for o in (0, 1)]
+        if MBW <= 2:
+            f += [(0, 3, 1, tp) for tp in (0, 1)]
+        return f
+
     for MBW in (1, 2, 3, 4, 6):
-        for C0, PF, ORD in [(c, p, o) for c, p in ((0, 1), (0, 2), (2, 1)) for o in (0, 1)]:
-            NB = 2 if PF == 1 else 4
-            body = (term_prologue_asm if ORD else prologue_asm)(MBW, C0, PF)
+        for C0, PF, ORD, TP in forms(MBW):
+            NB = nbufs(PF)
+            body = (term_prologue_asm if ORD else prologue_asm)(MBW, C0, PF, TP)
             outs = [f'[a{k}_{t}] "+v"(aq[{k}][{t}])' for k in range(MBW) for t in range(2)]
             outs += [f'[b{j}_{q}] "+v"(bq[{j}][{q}])' for j in range(NB) for q in range(4)]
             outs.append('[tmp] "=&s"(tmp)')
             ins = [f'[d{k}] "v"(ad[{k}])' for k in range(MBW)] + ['[voff] "v"(voff)', '[rc] "s"(rc)', '[sc] "s"(sc)']
-            out.append(f"template <>\nstruct KPro<{MBW}, {C0}, {PF}, {ORD}> {{\n"
+            out.append(f"template <>\nstruct KPro<{MBW}, {C0}, {PF}, {ORD}, {TP}> {{\n"
                        f"  __device__ __forceinline__ static void run(az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                        f"      const int (&ad)[{MBW}], int voff, az_rsrc rc, int sc) {{\n"
                        f"    int tmp;\n"
@@ -345,7 +360,7 @@ def main():
                        f"        : \"memory\");\n"
                        f"  }}\n}};\n")
         # the drain: the last group's prefetches land before the registers are reused
-        for NB in (2, 4):
+        for NB in ((2, 4, 8) if MBW <= 2 else (2, 4)):
             outs = [f'"+v"(aq[{k}][{t}])' for k in range(MBW) for t in range(2)]
             outs += [f'"+v"(bq[{j}][{q}])' for j in range(NB) for q in range(4)]
             outs += [f'"+v"(acc[{k}][{n}])' for k in range(MBW) for n in range(2)]
@@ -359,15 +374,15 @@ def main():
                        f"  }}\n}};\n")
     count = 0
     for MBW in (1, 2, 3, 4, 6):
-        for C0, PF, ORD in [(c, p, o) for c, p in ((0, 1), (0, 2), (2, 1)) for o in (0, 1)]:
-            NB = 2 if PF == 1 else 4
+        for C0, PF, ORD, TP in forms(MBW):
+            NB = nbufs(PF)
             for SKC, HN in [(k, h) for k in (0, 1, 2) for h in (1, 0)]:
                 if MBW == 1 and SKC:
                     continue
                 count += 1
-                text = (term_group_asm if ORD else group_asm)(MBW, C0, SKC, PF, HN)
+                text = (term_group_asm(MBW, C0, SKC, PF, HN, TP) if ORD else group_asm(MBW, C0, SKC, PF, HN, TP=TP))
                 outs, ins = operand_list(MBW, NB)
-                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}, {PF}, {ORD}, {HN}> {{\n"
+                out.append(f"template <>\nstruct KGroup<{MBW}, {C0}, {SKC}, {PF}, {ORD}, {HN}, {TP}> {{\n"
                            f"  __device__ __forceinline__ static void run(az_f4 (&acc)[{MBW}][2], az_u4 (&aq)[{MBW}][2], az_u4 (&bq)[{NB}][4],\n"
                            f"      const int (&ad)[{MBW}], const int (&an)[{MBW}], int voff, az_rsrc rc, az_rsrc rn,\n"
                            f"      int sc, int sn) {{\n"

@@ -113,14 +113,17 @@ ORDER = {0: [(0, 1), (1, 0), (0, 0)], 1: [(2, 1), (3, 0), (2, 0)]}  # per N bloc
 def run_loop(MBW, C0, PF, R, skw, ORD=0, LAST_HN=1):
     m = Machine(MBW)
     group = gen.term_group_asm if ORD else gen.group_asm
+
+    def grp(MBW, C0, skc, PF, hn, tp):  # tp: the tap's parity (the residual steps precede tap 0: 1)
+        return group(MBW, C0, skc, PF, hn, TP=tp)
     prologue = gen.term_prologue_asm if ORD else gen.prologue_asm
     # prologue: A from the phase's first source, B from its first k-step
     first_src = ("own",) if R else ("tap", 0)
     first_k = ("R", 0) if R else ("M", C0)
-    m.run(prologue(MBW, C0, PF), {"sc": first_k, "d": first_src, "skip": 0, "acc": "-",
+    m.run(prologue(MBW, C0, PF, 1 if R else 0), {"sc": first_k, "d": first_src, "skip": 0, "acc": "-",
                                           "rc": first_k[0]})
     if R:
-        m.run(group(MBW, 0, 0, PF), {"sc": ("R", 0), "sn": ("M", 0), "d": ("own",), "n": ("tap", 0),
+        m.run(grp(MBW, 0, 0, PF, 1, 1), {"sc": ("R", 0), "sn": ("M", 0), "d": ("own",), "n": ("tap", 0),
                                              "skip": 0, "acc": "res", "rc": "R", "rn": "M"})
     for t in range(9):
         mask = (skw >> (2 * t)) & 3
@@ -130,7 +133,7 @@ def run_loop(MBW, C0, PF, R, skw, ORD=0, LAST_HN=1):
         nxt = ("tap", t + 1) if t < 8 else ("tap", 8)
         sn = ("M", 4 * (t + 1) + C0) if t < 8 else ("M", 4 * t + C0)
         hn = 1 if t < 8 else LAST_HN
-        m.run(group(MBW, C0, skc, PF, hn), {"sc": ("M", 4 * t), "sn": sn, "d": ("tap", t), "n": nxt,
+        m.run(grp(MBW, C0, skc, PF, hn, t & 1), {"sc": ("M", 4 * t), "sn": sn, "d": ("tap", t), "n": nxt,
                                              "skip": skc, "acc": "main", "rc": "M", "rn": "M"})
     if LAST_HN == 0:
         assert not m.vm and not m.lgkm, (m.vm, m.lgkm)
@@ -165,7 +168,8 @@ def run_loop(MBW, C0, PF, R, skw, ORD=0, LAST_HN=1):
 
 # the kernels' forms: (blocks per wave, first chunk, prefetch depth, residual steps)
 FORMS = [(4, 0, 2, 0), (4, 0, 2, 4), (3, 0, 2, 0), (3, 0, 2, 4), (1, 0, 2, 0), (1, 0, 2, 4), (1, 2, 1, 0),
-         (4, 2, 1, 0), (6, 0, 1, 0), (6, 0, 1, 4), (2, 0, 2, 0), (2, 0, 2, 4), (4, 0, 1, 4), (1, 0, 1, 0)]
+         (4, 2, 1, 0), (6, 0, 1, 0), (6, 0, 1, 4), (2, 0, 2, 0), (2, 0, 2, 4), (4, 0, 1, 4), (1, 0, 1, 0),
+         (2, 0, 3, 0), (2, 0, 3, 4), (1, 0, 3, 0), (2, 2, 1, 0)]
 # skip words: none, a slot plan's (two border blocks, 3 taps each), every tap skipping one block
 SKIPS = [0, sum(1 << (2 * t) for t in (0, 1, 2)) | sum(2 << (2 * t) for t in (6, 7, 8)),
          sum((1 + (t & 1)) << (2 * t) for t in range(9))]
