@@ -505,10 +505,12 @@ __device__ __forceinline__ void k_loop(const uint4* __restrict__ act, const uint
 #define AZ_KLOOP_PF 2
 #endif
 // k_loop with the groups of 4 k-steps in hand-scheduled assembly
-// (az_kloop_asm.h, gen_kloop_asm.py): the same k-steps, reads and MFMAs in
-// the same order per accumulator as k_loop's LAG ring, so the same sums
-// bit for bit.  accm / accr: the accumulators of the taps / the residual
-// steps (may be the same array)
+// (az_kloop_asm.h, gen_kloop_asm.py; term-major by default): every
+// accumulator sums the same products in the same order as k_loop's, so
+// the same bits.  accm / accr: the accumulators of the taps / the residual
+// steps (may be the same array).  The schedule is checked symbolically by
+// tests/test_kloop_schedule_cpu.py and against the compiled ISA by
+// tests/test_kernel_resources_cpu.py
 template <int MBW, int R, int C0, typename Mid = NoMid>
 __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const uint4* __restrict__ wmain,
                                            const uint4* __restrict__ wres, t_f4 (&accm)[MBW][2],
