@@ -553,7 +553,9 @@ __device__ __forceinline__ void k_loop_asm(const uint4* __restrict__ act, const 
   // weight prefetch depth: PF k-steps ahead in NB buffers (2 ahead needs 4,
   // so a 4-k-step group keeps each buffer's k-step fixed; the stem's
   // 2-k-step groups prefetch 1 ahead)
-  // (the 192-row tile's 6-block waves: 1 -- 2 spills 69 VGPRs there)
+  // (the 192-row tile's 6-block waves: 1 -- 2 spills 69 VGPRs there.  3, in
+  // 8 buffers picked by the tap's parity -- gen_kloop_asm.nbufs -- spilled
+  // 627 VGPRs in chess's 2-block waves, one body per parity)
   constexpr int PF = C0 == 0 && MBW < 6 ? AZ_KLOOP_PF : 1, NB = PF == 1 ? 2 : 4;
   az_u4 aq[MBW][2], bq[NB][4];
   int cur[MBW], nxt[MBW];
@@ -699,7 +701,9 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     }
   }
   // this wave's tap skips (2 bits per tap over its blocks 0 and 1)
-  const int skw = planned ? T.skip[mh] : 0;
+  // (chess's 64-row tiles never run the plan: a compile-time 0 there, so
+  // each tap compiles to one body instead of three)
+  const int skw = (ROWS && 16 * MBT != 128) ? 0 : planned ? T.skip[mh] : 0;
   const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
   // double-buffered: one accumulator set (conv2 runs the block's 1x1
   // projection residual first, from X, which nothing overwrites before its

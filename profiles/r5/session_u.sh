@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-5 GPU session U (diagnostic): the tower without its weight loads
+# Round-5 GPU session U: (diagnostic) the tower without its weight loads
 # (variants/nob.py, wrong outputs) -- how much of the chess one-board tile
-# and of the Connect-4 tile the weight stream costs.
+# and of the Connect-4 tile the weight stream costs; then chess with one tap
+# body (product: compile-time skip word 0) vs three (variants/skwrt.py).
 set -o pipefail
 out=gpurun_out/r5u
 mkdir -p $out
@@ -12,3 +13,4 @@ for r in 1 2; do
     AZ_LIB_PATH=$lib timeout -k 10 120 python3 profiles/conv_bench.py 456 20 0 2>&1 | tail -1 | sed "s/^/$v c4 /" | tee -a $out/iso.txt || exit 1
   done
 done
+bash profiles/r5/ab_bench.sh 2 "--game chess" base skwrt 2>&1 | tee $out/ab_chess_skw.txt

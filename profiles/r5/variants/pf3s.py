@@ -1,5 +1,5 @@
-# (not buildable as a product form: weights 3 k-steps ahead need 8 B buffers
-# picked by the tap's parity, and the 6 asm bodies that dispatch makes in the
-# tap loop spilled 618 VGPRs in chess's 64-row kernel -- the generator keeps
-# the form, gen_kloop_asm.nbufs, checked by tests/test_kloop_schedule_cpu.py)
+# (not buildable: weights 3 k-steps ahead need 8 B buffers picked by the
+# tap's parity (gen_kloop_asm.nbufs, schedule-checked); with one body per
+# parity -- chess's 64-row tiles compile one skip body since round 5 -- the
+# 2-block kernel still spilled 627 VGPRs)
 raise SystemExit("pf3s: see the comment")
