@@ -1,13 +1,16 @@
 #!/bin/bash
 # in-bench A/B of libaz variants (AZ_LIB_PATH), alternating, games/s and the
 # tower roofline fields: bash profiles/r4/ab_bench.sh <rounds> "<bench args>" base v1 ...
+# (a variant "name:VAR=value" is the product library run with that environment setting)
 set -o pipefail
 rounds=$1; args=$2; shift 2
 mkdir -p gpurun_out
 for r in $(seq $rounds); do
   for v in "$@"; do
-    if [ "$v" = base ]; then lib=$PWD/custom-alphazero_amd/custom_alphazero/_lib/libaz.so; else lib=$PWD/profiles/ab_libs/$v/libaz.so; fi
-    AZ_LIB_PATH=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline $args > gpurun_out/abb_$v.json 2> gpurun_out/abb_$v.err || exit 1
+    envs=""
+    if [ "${v#*:}" != "$v" ]; then envs=${v#*:}; v=${v%%:*}; lib=$PWD/custom-alphazero_amd/custom_alphazero/_lib/libaz.so
+    elif [ "$v" = base ]; then lib=$PWD/custom-alphazero_amd/custom_alphazero/_lib/libaz.so; else lib=$PWD/profiles/ab_libs/$v/libaz.so; fi
+    env $envs AZ_LIB_PATH=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline $args > gpurun_out/abb_$v.json 2> gpurun_out/abb_$v.err || exit 1
     python3 -c "
 import json,sys
 d=json.loads(open('gpurun_out/abb_$v.json').read().strip().splitlines()[-1]); r=d['roofline']
