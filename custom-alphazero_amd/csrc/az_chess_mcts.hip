@@ -69,7 +69,8 @@ struct CTree {
   uint32_t* mt;            // [625][mt_stride] word-major MT19937 (a lane view offsets it)
   int32_t mt_stride;       // slots of the whole engine
   int32_t* eval_slot;      // [slots]
-  int32_t* eval_count;     // [1]
+  int32_t* eval_count;     // this simulation's queue length (one of the lane's two counters)
+  int32_t* next_count;     // the other: zeroed by this simulation's select launch for the next one
   unsigned long long* stats;
   const double* powtab;
   const int16_t* lut;
@@ -268,12 +269,43 @@ __global__ void tree_release_kernel(CTree t, int n, const int32_t* slots) {
   if (i < n) t.game_id[slots[i]] = -1;
 }
 
-// MCTS.select (mcts.py:111-120): one wave per slot
+// the leaf's is_game_over() (mcts.py:173-179): terminal leaves back up the
+// canonical get_result (1 checkmate, 0 draw); others are queued for evaluation.
+// One wave per slot: the wave generates the legal moves (legal_moves_wave,
+// one square per lane; a single lane per slot took 19 us per launch), lane 0
+// does the rest.
+// (Round 5: run by the select launch's wave right after its descent, on the
+// leaf in its registers -- one launch fewer on the lane's chain.)
+__device__ __forceinline__ void leaf_body(const CCfg& g, const CTree& t, int s, int lane, const Pos& q,
+                                          uint16_t* cand) {
+  bool check;
+  const int n = legal_moves_wave(q, cand, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check, lane);
+  if (lane != 0) return;
+  if (n < 0) {
+    flag(t, az::kErrIllegal);
+    return;
+  }
+  t.leaf_n[s] = n;
+  const int oc = outcome(q, n, check);
+  if (oc != AZ_CHESS_ONGOING) {
+    Edge* E = arena(g, t, s, t.half[s]);
+    backup(E, t.path + (size_t)s * g.max_depth, t.path_len[s], oc == AZ_CHESS_CHECKMATE ? 1.0 : 0.0);
+    atomicAdd(t.stats + az::kStatTerminal, 1ull);
+  } else {
+    const int qi = atomicAdd(t.eval_count, 1);
+    t.eval_slot[qi] = s;
+  }
+  atomicAdd(t.stats + az::kStatSims, 1ull);
+}
+
+// MCTS.select (mcts.py:111-120): one wave per slot, then the leaf's move
+// generation and queueing (leaf_body)
 __global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
+  __shared__ uint16_t cand[AZ_CHESS_MAX_MOVES];
   const int s = blockIdx.x, lane = threadIdx.x;
-  // the eval queue is filled by leaf_kernel, after this launch (a memset
-  // launch per simulation cost 5 us)
-  if (s == 0 && lane == 0) *t.eval_count = 0;
+  // the next simulation's queue counter (this one's was zeroed by the last
+  // simulation's launch; a memset launch per simulation cost 5 us)
+  if (s == 0 && lane == 0) *t.next_count = 0;
   if (t.game_id[s] < 0) return;
   const Edge* E = arena(g, t, s, t.half[s]);
   int32_t* path = t.path + (size_t)s * g.max_depth;
@@ -326,36 +358,7 @@ __global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
     store_pos(q, t.leaf[s]);
     t.path_len[s] = depth;
   }
-}
-
-// the leaf's is_game_over() (mcts.py:173-179): terminal leaves back up the
-// canonical get_result (1 checkmate, 0 draw); others are queued for evaluation.
-// One wave per slot: the wave generates the legal moves (legal_moves_wave,
-// one square per lane; a single lane per slot took 19 us per launch), lane 0
-// does the rest.
-__global__ __launch_bounds__(64) void leaf_kernel(CCfg g, CTree t) {
-  __shared__ uint16_t cand[AZ_CHESS_MAX_MOVES];
-  const int s = blockIdx.x, lane = threadIdx.x;
-  if (s >= g.slots || t.game_id[s] < 0) return;  // block-uniform
-  const Pos q = load_pos(t.leaf[s]);
-  bool check;
-  const int n = legal_moves_wave(q, cand, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check, lane);
-  if (lane != 0) return;
-  if (n < 0) {
-    flag(t, az::kErrIllegal);
-    return;
-  }
-  t.leaf_n[s] = n;
-  const int oc = outcome(q, n, check);
-  if (oc != AZ_CHESS_ONGOING) {
-    Edge* E = arena(g, t, s, t.half[s]);
-    backup(E, t.path + (size_t)s * g.max_depth, t.path_len[s], oc == AZ_CHESS_CHECKMATE ? 1.0 : 0.0);
-    atomicAdd(t.stats + az::kStatTerminal, 1ull);
-  } else {
-    const int qi = atomicAdd(t.eval_count, 1);
-    t.eval_slot[qi] = s;
-  }
-  atomicAdd(t.stats + az::kStatSims, 1ull);
+  leaf_body(g, t, s, lane, q, cand);
 }
 
 // Board.full_state of the queued leaves into the network input [q][64][128]:
@@ -704,6 +707,8 @@ struct CLane {
   float* probs = nullptr;
   float* values = nullptr;
   az::ConvTimer timer;
+  int32_t* counts = nullptr;  // [2] the eval queue counters, alternating by simulation
+  int par = 0;
 };
 
 struct az_chess_engine {
@@ -764,8 +769,10 @@ int check_errors(az_chess_engine* e) {
 int simulate(az_chess_engine* e, CLane& L) {
   hipStream_t s = L.stream;
   const int S = L.g.slots;
+  L.t.eval_count = L.counts + L.par;
+  L.t.next_count = L.counts + (L.par ^ 1);
+  L.par ^= 1;
   select_kernel<<<S, 64, 0, s>>>(L.g, L.t);
-  leaf_kernel<<<S, 64, 0, s>>>(L.g, L.t);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
     if (e->net.algo == AZ_CONV_F16X2)
       encode_queue_kernel<true><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
@@ -819,7 +826,10 @@ int make_lane(az_chess_engine* e, CLane* L, int first, int n) {
   t.mt += f;
   t.eval_slot += f;
   int rc;
-  if ((rc = e->alloc(&t.eval_count, 1))) return rc;
+  if ((rc = e->alloc(&t.eval_count, 2))) return rc;
+  AZC_HIP(hipMemset(t.eval_count, 0, 2 * sizeof(int32_t)));
+  L->counts = t.eval_count;
+  t.next_count = t.eval_count + 1;
   L->t = t;
   if (e->x) L->x = e->x + f * 64 * 128;
   for (int i = 0; i < 3; ++i) L->act[i] = e->act[i] ? e->act[i] + f * 64 * 128 : nullptr;
@@ -893,6 +903,7 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
       (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_count, 1)) ||
       (rc = e->alloc(&t.stats, az::kStatCount)))
     return cleanup(rc);
+  t.next_count = t.eval_count;  // (the lanes' views carry their own pair)
   {
     double* powtab = nullptr;
     if ((rc = e->alloc(&powtab, g.pow_len))) return cleanup(rc);

@@ -468,22 +468,24 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
 // Chess-size heads (A = 1880), used when the 1x1 head convs ran in the last
 // conv's epilogue (feat = [boards][HW] float4: policy ch 0, ch 1, value, 0).
 // policy_dense_kernel: Dense(2HW -> A) as a tiled GEMM over the live batch --
-// a workgroup owns 64 actions x 32 boards, stages the weight tile [2HW][64]
-// and the boards' flattened policy features [32][2HW] in LDS, and each thread
-// accumulates one action for 8 boards, s = bias + sum_i p[i] * w[i][a] in i
+// a workgroup owns 64 actions x 4NB boards, stages the weight tile [2HW][64]
+// and the boards' flattened policy features [4NB][2HW] in LDS, and each thread
+// accumulates one action for NB boards, s = bias + sum_i p[i] * w[i][a] in i
 // order, into `logits` (the probs buffer).  One wave per board could not hide
 // the 962 KB weight stream (60% of a chess step); here every weight is read
-// once per 32 boards.
-template <int K>
+// once per 4NB boards.  NB = 8 (32 boards) for large launches; a self-play
+// lane's 128 boards take NB = 2: 4x the workgroups (480), a quarter of the
+// FMA chain per thread -- the launch is latency-bound, on the lane's chain.
+template <int K, int NB>
 __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restrict__ feat,
                                                            const float* __restrict__ wpd,
                                                            const float* __restrict__ bpd,
                                                            const int* __restrict__ count, int n_static,
                                                            int HW, int A, float* __restrict__ logits) {
   __shared__ __attribute__((aligned(16))) float ws[K][64];
-  __shared__ __attribute__((aligned(16))) float ps[32][K];
+  __shared__ __attribute__((aligned(16))) float ps[4 * NB][K];
   const int n = count ? *count : n_static;
-  const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 32;
+  const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 4 * NB;
   if (b0 >= n) return;  // block-uniform
   const int t = threadIdx.x;
   // the tile's weight slab is contiguous (NetDev::pd_wt): 8 float4 loads per
@@ -502,7 +504,7 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
   }
   constexpr int HWK = K / 2;  // the launcher passes K = 2 * HW
 #pragma unroll
-  for (int k = 0; k < 32 * HWK / 256; ++k) {
+  for (int k = 0; k < 4 * NB * HWK / 256; ++k) {
     const int idx = t + 256 * k;
     const int b = idx / HWK, p = idx - b * HWK;
     const float4 f = feat[(size_t)min(b0 + b, n - 1) * HWK + p];  // clamped (rows past n unused)
@@ -510,18 +512,18 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
     ps[b][2 * p + 1] = f.y;
   }
   __syncthreads();
-  const int a = t & 63, bg = (t >> 6) * 8;
+  const int a = t & 63, bg = (t >> 6) * NB;
   if (a0 + a >= A) return;
   const float bias = bpd[a0 + a];
-  float acc[8];
+  float acc[NB];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = bias;
+  for (int j = 0; j < NB; ++j) acc[j] = bias;
   // the 8 boards' features as float4 over i (wave-uniform rows: LDS
   // broadcasts), 12 LDS reads per 32 FMAs instead of 36; same FMA order
   for (int i = 0; i < 2 * HW; i += 4) {
     const float w0 = ws[i][a], w1 = ws[i + 1][a], w2 = ws[i + 2][a], w3 = ws[i + 3][a];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < NB; ++j) {
       const float4 f = *reinterpret_cast<const float4*>(&ps[bg + j][i]);
       acc[j] = fmaf(f.x, w0, acc[j]);
       acc[j] = fmaf(f.y, w1, acc[j]);
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
     }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int j = 0; j < NB; ++j)
     if (b0 + bg + j < n) logits[(size_t)(b0 + bg + j) * A + a0 + a] = acc[j];
 }
 
@@ -565,6 +567,15 @@ __global__ __launch_bounds__(kTailThreads) void heads_tail_kernel(const float4* 
   __shared__ float red[kTailThreads / 64];
   const int n = count ? *count : n_static;
   const int t = threadIdx.x;
+  // chess (HW = 64, hidden <= 256): the thread's hidden unit's 64 value
+  // weights are loaded once, all in flight together, under the softmax (the
+  // loop below awaited them 16 at a time after it) -- the same sums
+  const bool pre = HW == 64 && hidden <= kTailThreads;
+  float wj[64];
+  if (pre && t < hidden) {
+#pragma unroll
+    for (int p = 0; p < 64; ++p) wj[p] = hw.wv1[p * hidden + t];
+  }
   for (int b = blockIdx.x; b < n; b += gridDim.x) {  // block-uniform
     __syncthreads();  // vflat of the previous board is no longer read
     for (int p = t; p < HW; p += kTailThreads) vflat[p] = feat[(size_t)b * HW + p].z;
@@ -592,11 +603,20 @@ __global__ __launch_bounds__(kTailThreads) void heads_tail_kernel(const float4* 
       if (a < A) row[a] = x[k] / z;
     }
     float part = 0.f;
-    for (int j = t; j < hidden; j += kTailThreads) {
-      float sv = hw.bv1[j];
+    if (pre) {
+      if (t < hidden) {
+        float sv = hw.bv1[t];
+#pragma unroll
+        for (int p = 0; p < 64; ++p) sv += vflat[p] * wj[p];
+        part += fmaxf(sv, 0.f) * hw.wv2[t];
+      }
+    } else {
+      for (int j = t; j < hidden; j += kTailThreads) {
+        float sv = hw.bv1[j];
 #pragma unroll 16
-      for (int p = 0; p < HW; ++p) sv += vflat[p] * hw.wv1[p * hidden + j];
-      part += fmaxf(sv, 0.f) * hw.wv2[j];
+        for (int p = 0; p < HW; ++p) sv += vflat[p] * hw.wv1[p * hidden + j];
+        part += fmaxf(sv, 0.f) * hw.wv2[j];
+      }
     }
     part = block_reduce(part, red, false);
     if (t == 0) values[b] = tanhf(part + hw.bv2[0]);
@@ -604,6 +624,16 @@ __global__ __launch_bounds__(kTailThreads) void heads_tail_kernel(const float4* 
 }
 
 // --------------------------------------------------------------- launchers
+static void launch_policy_dense(const float4* feat, const float* wt, const float* b, const int* count, int n_max,
+                                int HW, int A, float* logits, hipStream_t s) {
+  if (n_max <= 256)
+    policy_dense_kernel<128, 2><<<dim3((A + 63) / 64, (n_max + 7) / 8), 256, 0, s>>>(feat, wt, b, count, n_max, HW, A,
+                                                                                     logits);
+  else
+    policy_dense_kernel<128, 8><<<dim3((A + 63) / 64, (n_max + 31) / 32), 256, 0, s>>>(feat, wt, b, count, n_max, HW,
+                                                                                       A, logits);
+}
+
 void launch_encode(const Board* boards, const int* count, int n_max, int HW, float* x,
                    hipStream_t s) {
   const int total = n_max * HW;
@@ -673,8 +703,7 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
     HeadWeights hw{net.pc_w, net.pc_b, net.vc_w, net.vc_b, net.pd_w,
                    net.pd_b, net.v1_w, net.v1_b, net.v2_w, net.v2_b};
     const float4* feat = static_cast<const float4*>(act_a);
-    policy_dense_kernel<128><<<dim3((A + 63) / 64, (n_max + 31) / 32), 256, 0, s>>>(feat, net.pd_wt, net.pd_b, count,
-                                                                                 n_max, HW, A, probs);
+    launch_policy_dense(feat, net.pd_wt, net.pd_b, count, n_max, HW, A, probs, s);
     heads_tail_kernel<<<std::min(n_max, 2048), kTailThreads, 0, s>>>(feat, hw, count, n_max, HW, A, net.hidden, probs,
                                                                      values);
     return;
@@ -776,8 +805,7 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
   if (A > kMaxActions) {  // chess: 1880 actions
     if (f16 && HW == 64 && A <= kTailThreads * kTailPer && net.pd_wt) {
       const float4* feat = reinterpret_cast<const float4*>(act);
-      policy_dense_kernel<128><<<dim3((A + 63) / 64, (n_max + 31) / 32), 256, 0, s>>>(
-          feat, net.pd_wt, net.pd_b, count, n_max, HW, A, probs);
+      launch_policy_dense(feat, net.pd_wt, net.pd_b, count, n_max, HW, A, probs, s);
       heads_tail_kernel<<<std::min(n_max, 2048), kTailThreads, 0, s>>>(feat, hw, count, n_max, HW, A,
                                                                        net.hidden, probs, values);
     } else {
