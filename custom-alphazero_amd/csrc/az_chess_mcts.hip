@@ -71,6 +71,7 @@ struct CTree {
   int32_t* eval_slot;      // [slots]
   int32_t* eval_count;     // this simulation's queue length (one of the lane's two counters)
   int32_t* next_count;     // the other: zeroed by this simulation's select launch for the next one
+  int32_t* slot_q;         // [slots] the slot's queue entry in its last simulation, -1 none (the fused expand)
   unsigned long long* stats;
   const double* powtab;
   const int16_t* lut;
@@ -269,6 +270,95 @@ __global__ void tree_release_kernel(CTree t, int n, const int32_t* slots) {
   if (i < n) t.game_id[slots[i]] = -1;
 }
 
+// MCTS.evaluate_and_expand (mcts.py:145-161) + backup of queue entry b
+// (slot s) by one wave: the expand launch's, or -- fused -- the slot's wave
+// in the next simulation's select launch, before its descent
+struct ExpandSmem {
+  int act[AZ_CHESS_MAX_MOVES];
+  float sorted[AZ_CHESS_MAX_MOVES];
+  double prior[AZ_CHESS_MAX_MOVES];
+  int first_s;
+};
+
+__device__ void expand_body(const CCfg& g, const CTree& t, const float* __restrict__ probs,
+                            const float* __restrict__ values, int b, int s, int lane, ExpandSmem& sm) {
+  int* act = sm.act;
+  float* sorted = sm.sorted;
+  double* prior = sm.prior;
+  {
+    const int n = t.leaf_n[s];
+    const uint16_t* mv = t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES;
+    const float* pr = probs + (size_t)b * AZ_CHESS_ACTIONS;
+    __syncthreads();
+    for (int j = lane; j < n; j += 64) {
+      const int a = action_of(t.lut, mv[j]);
+      act[j] = a;
+      if (a < 0) flag(t, az::kErrIllegal);
+    }
+    __syncthreads();
+    // probabilities[legal_moves_mask]: the legal actions in action order
+    for (int j = lane; j < n; j += 64) {
+      const int a = act[j];
+      int r = 0;
+      for (int i = 0; i < n; ++i) r += act[i] < a;
+      sorted[r] = a >= 0 ? pr[a] : 0.f;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      // normalize_probabilities (mcts/utils.py:4-16)
+      const float sum = pairwise(sorted, n);
+      if (sum == 0.0f) {
+        for (int i = 0; i < n; ++i) prior[i] = 1.0 / (double)n;
+      } else {
+        for (int i = 0; i < n; ++i) prior[i] = (double)(float)(sorted[i] / sum);
+      }
+      const int first = t.top[s];
+      if (first + n > g.half_cap) {
+        flag(t, az::kErrArena);
+        sm.first_s = -1;
+      } else {
+        t.top[s] = first + n;
+        sm.first_s = first;
+      }
+    }
+    __syncthreads();
+    const int first = sm.first_s;
+    if (first < 0) return;
+    Edge* E = arena(g, t, s, t.half[s]);
+    // zip(probabilities, node.board.moves): positional, python-chess move order
+    for (int j = lane; j < n; j += 64) {
+      Edge e;
+      e.W = 0.0;
+      e.prior = prior[j];
+      e.N = 0;
+      e.child = az::kNoChild;
+      e.child_n = 0;
+      e.action = (int16_t)mv[j];
+      e.child_value = 0.f;
+      E[first + j] = e;
+    }
+    if (lane == 0) {
+      const int depth = t.path_len[s];
+      const int32_t* path = t.path + (size_t)s * g.max_depth;
+      const float value = values[b];
+      if (depth == 0) {
+        t.root_first[s] = first;
+        t.root_n[s] = n;
+        t.root_value[s] = value;
+      } else {
+        Edge& pe = E[path[depth - 1]];
+        pe.child = first;
+        pe.child_n = (int16_t)n;
+        pe.child_value = value;
+      }
+      backup(E, path, depth, -(double)value);
+      t.slot_exp[s] += 1;
+      atomicAdd(t.stats + az::kStatExpansions, 1ull);
+      atomicAdd(t.stats + az::kStatNNEvals, 1ull);
+    }
+  }
+}
+
 // the leaf's is_game_over() (mcts.py:173-179): terminal leaves back up the
 // canonical get_result (1 checkmate, 0 draw); others are queued for evaluation.
 // One wave per slot: the wave generates the legal moves (legal_moves_wave,
@@ -283,30 +373,48 @@ __device__ __forceinline__ void leaf_body(const CCfg& g, const CTree& t, int s, 
   if (lane != 0) return;
   if (n < 0) {
     flag(t, az::kErrIllegal);
+    t.slot_q[s] = -1;
     return;
   }
   t.leaf_n[s] = n;
+  int qi = -1;
   const int oc = outcome(q, n, check);
   if (oc != AZ_CHESS_ONGOING) {
     Edge* E = arena(g, t, s, t.half[s]);
     backup(E, t.path + (size_t)s * g.max_depth, t.path_len[s], oc == AZ_CHESS_CHECKMATE ? 1.0 : 0.0);
     atomicAdd(t.stats + az::kStatTerminal, 1ull);
   } else {
-    const int qi = atomicAdd(t.eval_count, 1);
+    qi = atomicAdd(t.eval_count, 1);
     t.eval_slot[qi] = s;
   }
+  t.slot_q[s] = qi;
   atomicAdd(t.stats + az::kStatSims, 1ull);
 }
 
 // MCTS.select (mcts.py:111-120): one wave per slot, then the leaf's move
-// generation and queueing (leaf_body)
-__global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t) {
+// generation and queueing (leaf_body).  FUSED: first the previous
+// simulation's expand of the slot's queued leaf (expand_body; its network
+// outputs are still in probs / values), so a search is select,
+// (network, select) x (sims - 1), network, expand: one tree launch per
+// simulation on the lane's chain instead of two
+template <bool FUSED>
+__global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t, const float* __restrict__ probs,
+                                                    const float* __restrict__ values) {
   __shared__ uint16_t cand[AZ_CHESS_MAX_MOVES];
+  __shared__ ExpandSmem esm;
   const int s = blockIdx.x, lane = threadIdx.x;
   // the next simulation's queue counter (this one's was zeroed by the last
   // simulation's launch; a memset launch per simulation cost 5 us)
   if (s == 0 && lane == 0) *t.next_count = 0;
   if (t.game_id[s] < 0) return;
+  if constexpr (FUSED) {
+    const int b = t.slot_q[s];  // wave-uniform
+    if (b >= 0) {
+      expand_body(g, t, probs, values, b, s, lane, esm);
+      // the wave's edge and path stores complete before its descent reads them
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+  }
   const Edge* E = arena(g, t, s, t.half[s]);
   int32_t* path = t.path + (size_t)s * g.max_depth;
   Pos q = load_pos(t.root[s]);
@@ -435,87 +543,13 @@ __global__ __launch_bounds__(256) void synth_kernel(CCfg g, CTree t, float* prob
   }
 }
 
-// MCTS.evaluate_and_expand (mcts.py:145-161) + backup, one wave per queued leaf
 __global__ __launch_bounds__(64) void expand_kernel(CCfg g, CTree t, const float* __restrict__ probs,
                                                     const float* __restrict__ values) {
-  __shared__ int act[AZ_CHESS_MAX_MOVES];
-  __shared__ float sorted[AZ_CHESS_MAX_MOVES];
-  __shared__ double prior[AZ_CHESS_MAX_MOVES];
-  __shared__ int first_s;
-  const int lane = threadIdx.x;
+  __shared__ ExpandSmem sm;
   const int n_q = *t.eval_count;
   for (int b = blockIdx.x; b < n_q; b += gridDim.x) {
-    const int s = t.eval_slot[b];
-    const int n = t.leaf_n[s];
-    const uint16_t* mv = t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES;
-    const float* pr = probs + (size_t)b * AZ_CHESS_ACTIONS;
-    __syncthreads();
-    for (int j = lane; j < n; j += 64) {
-      const int a = action_of(t.lut, mv[j]);
-      act[j] = a;
-      if (a < 0) flag(t, az::kErrIllegal);
-    }
-    __syncthreads();
-    // probabilities[legal_moves_mask]: the legal actions in action order
-    for (int j = lane; j < n; j += 64) {
-      const int a = act[j];
-      int r = 0;
-      for (int i = 0; i < n; ++i) r += act[i] < a;
-      sorted[r] = a >= 0 ? pr[a] : 0.f;
-    }
-    __syncthreads();
-    if (lane == 0) {
-      // normalize_probabilities (mcts/utils.py:4-16)
-      const float sum = pairwise(sorted, n);
-      if (sum == 0.0f) {
-        for (int i = 0; i < n; ++i) prior[i] = 1.0 / (double)n;
-      } else {
-        for (int i = 0; i < n; ++i) prior[i] = (double)(float)(sorted[i] / sum);
-      }
-      const int first = t.top[s];
-      if (first + n > g.half_cap) {
-        flag(t, az::kErrArena);
-        first_s = -1;
-      } else {
-        t.top[s] = first + n;
-        first_s = first;
-      }
-    }
-    __syncthreads();
-    const int first = first_s;
-    if (first < 0) continue;
-    Edge* E = arena(g, t, s, t.half[s]);
-    // zip(probabilities, node.board.moves): positional, python-chess move order
-    for (int j = lane; j < n; j += 64) {
-      Edge e;
-      e.W = 0.0;
-      e.prior = prior[j];
-      e.N = 0;
-      e.child = az::kNoChild;
-      e.child_n = 0;
-      e.action = (int16_t)mv[j];
-      e.child_value = 0.f;
-      E[first + j] = e;
-    }
-    if (lane == 0) {
-      const int depth = t.path_len[s];
-      const int32_t* path = t.path + (size_t)s * g.max_depth;
-      const float value = values[b];
-      if (depth == 0) {
-        t.root_first[s] = first;
-        t.root_n[s] = n;
-        t.root_value[s] = value;
-      } else {
-        Edge& pe = E[path[depth - 1]];
-        pe.child = first;
-        pe.child_n = (int16_t)n;
-        pe.child_value = value;
-      }
-      backup(E, path, depth, -(double)value);
-      t.slot_exp[s] += 1;
-      atomicAdd(t.stats + az::kStatExpansions, 1ull);
-      atomicAdd(t.stats + az::kStatNNEvals, 1ull);
-    }
+    __syncthreads();  // the previous entry's shared arrays are no longer read
+    expand_body(g, t, probs, values, b, t.eval_slot[b], threadIdx.x, sm);
   }
 }
 
@@ -709,6 +743,7 @@ struct CLane {
   az::ConvTimer timer;
   int32_t* counts = nullptr;  // [2] the eval queue counters, alternating by simulation
   int par = 0;
+  bool pending_expand = false;  // the last simulation's expand not launched yet
 };
 
 struct az_chess_engine {
@@ -772,7 +807,8 @@ int simulate(az_chess_engine* e, CLane& L) {
   L.t.eval_count = L.counts + L.par;
   L.t.next_count = L.counts + (L.par ^ 1);
   L.par ^= 1;
-  select_kernel<<<S, 64, 0, s>>>(L.g, L.t);
+  if (L.pending_expand) select_kernel<true><<<S, 64, 0, s>>>(L.g, L.t, L.probs, L.values);
+  else select_kernel<false><<<S, 64, 0, s>>>(L.g, L.t, nullptr, nullptr);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
     if (e->net.algo == AZ_CONV_F16X2)
       encode_queue_kernel<true><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
@@ -788,7 +824,16 @@ int simulate(az_chess_engine* e, CLane& L) {
   } else {
     synth_kernel<<<(S + 255) / 256, 256, 0, s>>>(L.g, L.t, L.probs, L.values);
   }
-  expand_kernel<<<S, 64, 0, s>>>(L.g, L.t, L.probs, L.values);
+  L.pending_expand = true;  // in the next simulation's select launch, or flush_expand
+  AZC_HIP(hipGetLastError());
+  return 0;
+}
+
+// the last simulation's expand of a search (its own launch, by queue entry)
+int flush_expand(CLane& L) {
+  if (!L.pending_expand) return 0;
+  L.pending_expand = false;
+  expand_kernel<<<L.g.slots, 64, 0, L.stream>>>(L.g, L.t, L.probs, L.values);
   AZC_HIP(hipGetLastError());
   return 0;
 }
@@ -825,6 +870,7 @@ int make_lane(az_chess_engine* e, CLane* L, int first, int n) {
   t.root_value += f;
   t.mt += f;
   t.eval_slot += f;
+  t.slot_q += f;
   int rc;
   if ((rc = e->alloc(&t.eval_count, 2))) return rc;
   AZC_HIP(hipMemset(t.eval_count, 0, 2 * sizeof(int32_t)));
@@ -900,7 +946,7 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
       (rc = e->alloc(&t.leaf_moves, S * AZ_CHESS_MAX_MOVES)) || (rc = e->alloc(&t.leaf_n, S)) ||
       (rc = e->alloc(&t.slot_exp, S)) || (rc = e->alloc(&t.root_value, S)) ||
       (rc = e->alloc(&t.mt, S * (kMtN + 1))) ||
-      (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_count, 1)) ||
+      (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_count, 1)) || (rc = e->alloc(&t.slot_q, S)) ||
       (rc = e->alloc(&t.stats, az::kStatCount)))
     return cleanup(rc);
   t.next_count = t.eval_count;  // (the lanes' views carry their own pair)
@@ -1017,6 +1063,7 @@ int az_chess_selfplay_begin(az_chess_engine* e, int64_t first_game, int64_t n_ga
   if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
     return az::fail_abi(AZ_E_STATE, "network evaluator selected but az_chess_engine_set_weights was not called");
   AZC_HIP(hipSetDevice(e->device));
+  for (CLane* L : e->lanes) L->pending_expand = false;  // (a search an error interrupted)
   int rc;
   if ((rc = sync_lanes(e))) return rc;
   for (void* p : e->sample_bufs) (void)hipFree(p);
@@ -1107,6 +1154,8 @@ int az_chess_selfplay_step(az_chess_engine* e, int n_moves, az_stats* st) {
     for (int s = 0; s < e->g.sims; ++s)
       for (CLane* L : e->lanes)
         if ((rc = simulate(e, *L))) return rc;
+    for (CLane* L : e->lanes)
+      if ((rc = flush_expand(*L))) return rc;
     for (CLane* L : e->lanes) play_kernel<<<L->g.slots, 64, 0, L->stream>>>(L->g, L->t, e->smp, CPlayOut{});
     AZC_HIP(hipGetLastError());
   }
@@ -1185,6 +1234,7 @@ int az_chess_tree_reset(az_chess_engine* e, int n, const int32_t* slots, const a
   if (e->cfg.evaluator == AZ_EVAL_NETWORK && !e->net.ready)
     return az::fail_abi(AZ_E_STATE, "network evaluator selected but az_chess_engine_set_weights was not called");
   AZC_HIP(hipSetDevice(e->device));
+  for (CLane* L : e->lanes) L->pending_expand = false;  // (a search an error interrupted)
   int rc;
   if ((rc = sync_lanes(e)) || (rc = tree_slot_list(e, n, slots))) return rc;
   if (!n) return 0;
@@ -1221,6 +1271,8 @@ int az_chess_tree_search(az_chess_engine* e, int n_sims) {
   for (int s = 0; s < n_sims; ++s)
     for (CLane* L : e->lanes)
       if ((rc = simulate(e, *L))) return rc;
+  for (CLane* L : e->lanes)
+    if ((rc = flush_expand(*L))) return rc;
   if ((rc = sync_lanes(e))) return rc;
   return check_errors(e);
 }
