@@ -687,6 +687,60 @@ AZC_HD int onehot_index(const Pos& q, int s) {
   return (q.co[1] & sq_bb(s)) ? t : 13 - t;
 }
 
+// chess.Board() (the start position)
+AZC_HD Pos start_pos() {
+  Pos q;
+  q.p[0] = 0x00FF00000000FF00ull;  // pawns
+  q.p[1] = 0x4200000000000042ull;  // knights
+  q.p[2] = 0x2400000000000024ull;  // bishops
+  q.p[3] = 0x8100000000000081ull;  // rooks
+  q.p[4] = 0x0800000000000008ull;  // queens
+  q.p[5] = 0x1000000000000010ull;  // kings
+  q.co[1] = 0x000000000000FFFFull;
+  q.co[0] = 0xFFFF000000000000ull;
+  q.castling = 0x8100000000000081ull;
+  q.ep = -1;
+  q.turn = 1;
+  q.rep = 0;
+  q.half = 0;
+  q.full = 1;
+  return q;
+}
+
+// Board.full_state's per-board planes 112-117 (chess/board.py full_state):
+// castling rights (own / opponent, queen- / king-side) and the move counters
+AZC_HD void state_feats(const Pos& cur, float (&feat)[6]) {
+  const bb c = clean_castling(cur);
+  const bb back_t = cur.turn ? RANK_1 : RANK_8, back_o = cur.turn ? RANK_8 : RANK_1;
+  feat[0] = (c & FILE_A & back_t) != 0;
+  feat[1] = (c & FILE_H & back_t) != 0;
+  feat[2] = (c & FILE_A & back_o) != 0;
+  feat[3] = (c & FILE_H & back_o) != 0;
+  feat[4] = (float)cur.full;
+  feat[5] = (float)cur.half;
+}
+
+// planes k0..k0+3 (k0 >= 64) of network-input pixel pix of a board whose
+// history is [0 x 6, start, cur] -- or [0 x 7, start-position state] for a
+// root set by reset (`initial`) -- as encode_queue_kernel writes them: planes
+// 84-97 the start position's one-hot (repetition plane 0), 98-111 the
+// board's (its repetition count), 112-117 state_feats, the rest 0
+AZC_HD void full_state4(const Pos& st, const Pos& cur, bool initial, const float (&feat)[6], int pix, int k0,
+                        float (&v)[4]) {
+  const int sq = (7 - (pix >> 3)) * 8 + (pix & 7);
+  const int st_idx = onehot_index(st, sq), cur_idx = initial ? st_idx : onehot_index(cur, sq);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + i;
+    float val = 0.f;
+    if (k >= 112 && k < 118) val = feat[k - 112];
+    else if (k >= 98 && k < 112)
+      val = k - 98 == 13 ? (initial ? 0.f : (float)cur.rep) : (cur_idx == k - 98 ? 1.f : 0.f);
+    else if (k >= 84 && k < 98 && !initial) val = k - 84 == 13 ? 0.f : (st_idx == k - 84 ? 1.f : 0.f);
+    v[i] = val;
+  }
+}
+
 // move -> action index (position in get_all_possible_moves), via the table
 // [from][to][promo slot] built on the host (-1 = not an action)
 AZC_HD int promo_slot(int promo) { return promo ? promo - 1 : 0; }  // 0, 1 N, 2 B, 3 R, 4 Q

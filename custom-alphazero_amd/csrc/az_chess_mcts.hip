@@ -190,25 +190,6 @@ __device__ __forceinline__ void backup(Edge* E, const int32_t* path, int depth, 
   }
 }
 
-__device__ Pos start_pos() {
-  Pos q;
-  q.p[0] = 0x00FF00000000FF00ull;  // pawns
-  q.p[1] = 0x4200000000000042ull;  // knights
-  q.p[2] = 0x2400000000000024ull;  // bishops
-  q.p[3] = 0x8100000000000081ull;  // rooks
-  q.p[4] = 0x0800000000000008ull;  // queens
-  q.p[5] = 0x1000000000000010ull;  // kings
-  q.co[1] = 0x000000000000FFFFull;
-  q.co[0] = 0xFFFF000000000000ull;
-  q.castling = 0x8100000000000081ull;
-  q.ep = -1;
-  q.turn = 1;
-  q.rep = 0;
-  q.half = 0;
-  q.full = 1;
-  return q;
-}
-
 __device__ void slot_reset(const CCfg& g, const CTree& t, const CSamples& smp, int s, int64_t gid) {
   az_chess_pos a;
   store_pos(start_pos(), a);
@@ -490,34 +471,19 @@ __global__ __launch_bounds__(256) void encode_queue_kernel(CCfg g, CTree t, void
       sp[0] = start_pos();
       sp[1] = load_pos(t.leaf[s]);
       initial = t.path_len[s] == 0 && t.initial[s];
-      const Pos& cur = sp[1];
-      const bb c = clean_castling(cur);
-      const bb back_t = cur.turn ? RANK_1 : RANK_8, back_o = cur.turn ? RANK_8 : RANK_1;
-      feat[0] = (c & FILE_A & back_t) != 0;
-      feat[1] = (c & FILE_H & back_t) != 0;
-      feat[2] = (c & FILE_A & back_o) != 0;
-      feat[3] = (c & FILE_H & back_o) != 0;
-      feat[4] = (float)cur.full;
-      feat[5] = (float)cur.half;
+      float f[6];
+      state_feats(sp[1], f);
+      for (int i = 0; i < 6; ++i) feat[i] = f[i];
     }
     __syncthreads();
     const size_t row0 = (size_t)b * 64;
+    float f[6];
+    for (int i = 0; i < 6; ++i) f[i] = feat[i];
     for (int e2 = threadIdx.x; e2 < 64 * (32 - 8 * kStemFirstChunk); e2 += blockDim.x) {
       const int per = 32 - 8 * kStemFirstChunk;  // float4 per pixel written
-      const int pix = e2 / per, e = pix * 32 + 8 * kStemFirstChunk + e2 % per, k0 = (e & 31) * 4;
-      const int sq = (7 - (pix >> 3)) * 8 + (pix & 7);
-      const int st_idx = onehot_index(sp[0], sq), cur_idx = initial ? st_idx : onehot_index(sp[1], sq);
+      const int pix = e2 / per, e = pix * 32 + 8 * kStemFirstChunk + e2 % per;
       float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + i;
-        float val = 0.f;
-        if (k >= 112 && k < 118) val = feat[k - 112];
-        else if (k >= 98 && k < 112)
-          val = k - 98 == 13 ? (initial ? 0.f : (float)sp[1].rep) : (cur_idx == k - 98 ? 1.f : 0.f);
-        else if (k >= 84 && k < 98 && !initial) val = k - 84 == 13 ? 0.f : (st_idx == k - 84 ? 1.f : 0.f);
-        v[i] = val;
-      }
+      full_state4(sp[0], sp[1], initial != 0, f, pix, (e & 31) * 4, v);
       az::store_act4<SPLIT>(x, row0 + pix, e & 31, make_float4(v[0], v[1], v[2], v[3]));
     }
   }
@@ -810,17 +776,27 @@ int simulate(az_chess_engine* e, CLane& L) {
   if (L.pending_expand) select_kernel<true><<<S, 64, 0, s>>>(L.g, L.t, L.probs, L.values);
   else select_kernel<false><<<S, 64, 0, s>>>(L.g, L.t, nullptr, nullptr);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
-    if (e->net.algo == AZ_CONV_F16X2)
-      encode_queue_kernel<true><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
-    else
-      encode_queue_kernel<false><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
+    // the one-launch tower builds the leaves' input planes itself (no encode
+    // launch on the chain; az_nn.h TowerLeaves); the other forms read rows
+    const bool tower = e->net.algo == AZ_CONV_F16X2 && e->net.use_tower && e->net.tower;
+    az::TowerLeaves lv;
+    lv.eval_slot = L.t.eval_slot;
+    lv.leaf = L.t.leaf;
+    lv.path_len = L.t.path_len;
+    lv.initial = L.t.initial;
+    if (!tower) {
+      if (e->net.algo == AZ_CONV_F16X2)
+        encode_queue_kernel<true><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
+      else
+        encode_queue_kernel<false><<<std::min(S, 2048), 256, 0, s>>>(L.g, L.t, L.x);
+    }
     // history slots 0-5 (planes 0-83) are always empty in self-play (every
     // board's history is [0 x 6, start, board] or [0 x 7, start]): the stem
     // skips input chunks 0-1 (planes 0-63; they would add exact zeros) and
-    // encode_queue_kernel writes planes 64-127 only
+    // the planes 64-127 only are written
     az::launch_forward(e->net, L.x, L.t.eval_count, S, 8, 8, AZ_CHESS_ACTIONS, L.act[0], L.act[1],
                        L.act[2], L.probs, L.values, s, L.timer.enabled ? &L.timer : nullptr, nullptr,
-                       kStemFirstChunk);
+                       kStemFirstChunk, tower ? &lv : nullptr);
   } else {
     synth_kernel<<<(S + 255) / 256, 256, 0, s>>>(L.g, L.t, L.probs, L.values);
   }

@@ -77,9 +77,20 @@ void launch_tower16(const TowerNet* net, int tile_rows, int staged_floats, bool 
 // into feat [n * HW] for the dense heads' kernels (policy_dense_kernel,
 // heads_tail_kernel).  first_chunk: input channel chunks (32) below it are
 // known zero and skipped (chess self-play: planes 0-63)
+// chess self-play (round 5): the tower builds its boards' input planes in
+// LDS from the leaves the select launch queued -- queue entry b's slot
+// eval_slot[b], its position leaf[slot] (az_chess_pos), path_len / initial
+// for the history form -- instead of reading rows an encode launch wrote
+// (the same bits: az_chess.h full_state4 is encode_queue_kernel's code)
+struct TowerLeaves {
+  const int32_t* eval_slot = nullptr;
+  const void* leaf = nullptr;
+  const int32_t* path_len = nullptr;
+  const int32_t* initial = nullptr;
+};
 void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged_floats, bool dbuf, const void* rows,
                          int first_chunk, const int* count, int n_max, int H, int W, float4* feat,
-                         unsigned long long* err, hipStream_t s);
+                         unsigned long long* err, hipStream_t s, const TowerLeaves* leaves = nullptr);
 
 // Folded (BatchNorm-in) weights resident in HBM, packed for the kernels (not
 // Keras layouts).  AZ_CONV_F16X2 (default): conv16_kernel packs (fp16 term
@@ -217,7 +228,7 @@ int load_network(NetDev& net, const ::az_tensor* tensors, int n, int in_ch, int 
 void launch_forward(const NetDev& net, const void* x, const int* count, int n_max, int H, int W,
                     int A, void* act_a, void* act_b, void* act_c, float* probs, float* values,
                     hipStream_t s, ConvTimer* timer, const Board* boards = nullptr,
-                    int stem_first_chunk = 0);
+                    int stem_first_chunk = 0, const TowerLeaves* leaves = nullptr);
 // fp32 rows [n][c_src] -> the network's input layout for in_ch > 4: [n][F] zero-padded, as split16
 // rows (split = true) or fp32
 void launch_pad_rows(const float* src, int n, int c_src, void* dst, bool split, hipStream_t s);

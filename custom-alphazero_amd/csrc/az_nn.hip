@@ -477,11 +477,9 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ ac
 // lane's 128 boards take NB = 2: 4x the workgroups (480), a quarter of the
 // FMA chain per thread -- the launch is latency-bound, on the lane's chain.
 template <int K, int NB>
-__global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restrict__ feat,
-                                                           const float* __restrict__ wpd,
-                                                           const float* __restrict__ bpd,
-                                                           const int* __restrict__ count, int n_static,
-                                                           int HW, int A, float* __restrict__ logits) {
+__device__ __forceinline__ void policy_dense_body(const float4* __restrict__ feat, const float* __restrict__ wpd,
+                                                  const float* __restrict__ bpd, const int* __restrict__ count,
+                                                  int n_static, int HW, int A, float* __restrict__ logits) {
   __shared__ __attribute__((aligned(16))) float ws[K][64];
   __shared__ __attribute__((aligned(16))) float ps[4 * NB][K];
   const int n = count ? *count : n_static;
@@ -536,6 +534,15 @@ __global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restr
     if (b0 + bg + j < n) logits[(size_t)(b0 + bg + j) * A + a0 + a] = acc[j];
 }
 
+template <int K, int NB>
+__global__ __launch_bounds__(256) void policy_dense_kernel(const float4* __restrict__ feat,
+                                                           const float* __restrict__ wpd,
+                                                           const float* __restrict__ bpd,
+                                                           const int* __restrict__ count, int n_static,
+                                                           int HW, int A, float* __restrict__ logits) {
+  policy_dense_body<K, NB>(feat, wpd, bpd, count, n_static, HW, A, logits);
+}
+
 // softmax over the logits in place + the value head (Dense(hidden) ReLU ->
 // Dense(1) tanh), one board per 256-thread workgroup: a thread holds 8 of
 // the board's logits in registers (one read, one exp, one write per logit)
@@ -558,6 +565,70 @@ __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) 
   return r;
 }
 
+// one board's softmax (in place over its logits) and value head; every
+// thread of the 256 takes part (block reductions).  pre: chess's preloaded
+// value weights wj (heads_tail_kernel)
+__device__ __forceinline__ void tail_board(const float4* __restrict__ feat, const HeadWeights& hw, int HW, int A,
+                                           int hidden, float* __restrict__ probs, float* __restrict__ values,
+                                           int b, bool pre, const float (&wj)[64], float* vflat, float* red) {
+  const int t = threadIdx.x;
+  __syncthreads();  // vflat of the previous board is no longer read
+  for (int p = t; p < HW; p += kTailThreads) vflat[p] = feat[(size_t)b * HW + p].z;
+  float* row = probs + (size_t)b * A;
+  float x[kTailPer];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kTailPer; ++k) {
+    const int a = t + k * kTailThreads;
+    x[k] = a < A ? row[a] : -INFINITY;
+    m = fmaxf(m, x[k]);
+  }
+  m = block_reduce(m, red, true);
+  float z = 0.f;
+#pragma unroll
+  for (int k = 0; k < kTailPer; ++k) {
+    const int a = t + k * kTailThreads;
+    x[k] = a < A ? expf(x[k] - m) : 0.f;
+    z += x[k];
+  }
+  z = block_reduce(z, red, false);  // its barriers also publish vflat
+#pragma unroll
+  for (int k = 0; k < kTailPer; ++k) {
+    const int a = t + k * kTailThreads;
+    if (a < A) row[a] = x[k] / z;
+  }
+  float part = 0.f;
+  if (pre) {
+    if (t < hidden) {
+      float sv = hw.bv1[t];
+#pragma unroll
+      for (int p = 0; p < 64; ++p) sv += vflat[p] * wj[p];
+      part += fmaxf(sv, 0.f) * hw.wv2[t];
+    }
+  } else {
+    for (int j = t; j < hidden; j += kTailThreads) {
+      float sv = hw.bv1[j];
+#pragma unroll 16
+      for (int p = 0; p < HW; ++p) sv += vflat[p] * hw.wv1[p * hidden + j];
+      part += fmaxf(sv, 0.f) * hw.wv2[j];
+    }
+  }
+  part = block_reduce(part, red, false);
+  if (t == 0) values[b] = tanhf(part + hw.bv2[0]);
+}
+
+__device__ __forceinline__ bool tail_preload(const HeadWeights& hw, int HW, int hidden, float (&wj)[64]) {
+  // chess (HW = 64, hidden <= 256): the thread's hidden unit's 64 value
+  // weights are loaded once, all in flight together, under the softmax (the
+  // loop awaited them 16 at a time after it) -- the same sums
+  const bool pre = HW == 64 && hidden <= kTailThreads;
+  if (pre && (int)threadIdx.x < hidden) {
+#pragma unroll
+    for (int p = 0; p < 64; ++p) wj[p] = hw.wv1[p * hidden + threadIdx.x];
+  }
+  return pre;
+}
+
 __global__ __launch_bounds__(kTailThreads) void heads_tail_kernel(const float4* __restrict__ feat, HeadWeights hw,
                                                                   const int* __restrict__ count, int n_static,
                                                                   int HW, int A, int hidden,
@@ -566,61 +637,10 @@ __global__ __launch_bounds__(kTailThreads) void heads_tail_kernel(const float4* 
   __shared__ float vflat[kMaxCells];
   __shared__ float red[kTailThreads / 64];
   const int n = count ? *count : n_static;
-  const int t = threadIdx.x;
-  // chess (HW = 64, hidden <= 256): the thread's hidden unit's 64 value
-  // weights are loaded once, all in flight together, under the softmax (the
-  // loop below awaited them 16 at a time after it) -- the same sums
-  const bool pre = HW == 64 && hidden <= kTailThreads;
   float wj[64];
-  if (pre && t < hidden) {
-#pragma unroll
-    for (int p = 0; p < 64; ++p) wj[p] = hw.wv1[p * hidden + t];
-  }
-  for (int b = blockIdx.x; b < n; b += gridDim.x) {  // block-uniform
-    __syncthreads();  // vflat of the previous board is no longer read
-    for (int p = t; p < HW; p += kTailThreads) vflat[p] = feat[(size_t)b * HW + p].z;
-    float* row = probs + (size_t)b * A;
-    float x[kTailPer];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < kTailPer; ++k) {
-      const int a = t + k * kTailThreads;
-      x[k] = a < A ? row[a] : -INFINITY;
-      m = fmaxf(m, x[k]);
-    }
-    m = block_reduce(m, red, true);
-    float z = 0.f;
-#pragma unroll
-    for (int k = 0; k < kTailPer; ++k) {
-      const int a = t + k * kTailThreads;
-      x[k] = a < A ? expf(x[k] - m) : 0.f;
-      z += x[k];
-    }
-    z = block_reduce(z, red, false);  // its barriers also publish vflat
-#pragma unroll
-    for (int k = 0; k < kTailPer; ++k) {
-      const int a = t + k * kTailThreads;
-      if (a < A) row[a] = x[k] / z;
-    }
-    float part = 0.f;
-    if (pre) {
-      if (t < hidden) {
-        float sv = hw.bv1[t];
-#pragma unroll
-        for (int p = 0; p < 64; ++p) sv += vflat[p] * wj[p];
-        part += fmaxf(sv, 0.f) * hw.wv2[t];
-      }
-    } else {
-      for (int j = t; j < hidden; j += kTailThreads) {
-        float sv = hw.bv1[j];
-#pragma unroll 16
-        for (int p = 0; p < HW; ++p) sv += vflat[p] * hw.wv1[p * hidden + j];
-        part += fmaxf(sv, 0.f) * hw.wv2[j];
-      }
-    }
-    part = block_reduce(part, red, false);
-    if (t == 0) values[b] = tanhf(part + hw.bv2[0]);
-  }
+  const bool pre = tail_preload(hw, HW, hidden, wj);
+  for (int b = blockIdx.x; b < n; b += gridDim.x)  // block-uniform
+    tail_board(feat, hw, HW, A, hidden, probs, values, b, pre, wj, vflat, red);
 }
 
 // --------------------------------------------------------------- launchers
@@ -681,7 +701,8 @@ static void launch_direct(const float* in, const float* res_in, const float* w, 
 
 void launch_forward(const NetDev& net, const void* x, const int* count, int n_max, int H, int W,
                     int A, void* act_a, void* act_b, void* act_c, float* probs, float* values,
-                    hipStream_t s, ConvTimer* timer, const Board* boards, int stem_first_chunk) {
+                    hipStream_t s, ConvTimer* timer, const Board* boards, int stem_first_chunk,
+                    const TowerLeaves* leaves) {
   if (n_max <= 0) return;
   const int HW = H * W;
   constexpr int F = 128;
@@ -698,7 +719,7 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
     // (features into act_a), then the dense heads as below
     if (timer) timer->begin(s);
     launch_tower16_rows(net.tower, net.tower_rows, net.tower_staged, net.tower_dbuf, x, stem_first_chunk, count,
-                        n_max, H, W, static_cast<float4*>(act_a), net.err, s);
+                        n_max, H, W, static_cast<float4*>(act_a), net.err, s, leaves);
     if (timer) timer->end(s, 1);
     HeadWeights hw{net.pc_w, net.pc_b, net.vc_w, net.vc_b, net.pd_w,
                    net.pd_b, net.v1_w, net.v1_b, net.v2_w, net.v2_b};

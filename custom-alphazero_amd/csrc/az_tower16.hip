@@ -63,6 +63,7 @@
 #include "az_nn.h"
 #include "az_tree.h"
 #include "az_kloop_asm.h"
+#include "az_chess.h"
 
 namespace az {
 
@@ -642,7 +643,8 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
                                                                float* __restrict__ probs,
                                                                float* __restrict__ values,
                                                                float4* __restrict__ feat, int first_chunk,
-                                                               unsigned long long* __restrict__ err) {
+                                                               unsigned long long* __restrict__ err,
+                                                               TowerLeaves lv) {
   constexpr int MBW = MBT / NWM;  // M blocks per wave
   constexpr int TR = 16 * MBT;    // tile rows
   constexpr int NT = NWM * 256;
@@ -718,21 +720,39 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
     // input rows -> H's tile (512 B split16 per pixel: t0 copied, t1 from the
     // rows' x 2^12 scale to the tower's unscaled term), then the stem conv
     // (F -> F over the padded input channels) as a K loop into X
-    const uint4* src = rows + (size_t)b0 * HW * 32;
     char* dst = reinterpret_cast<char*>(bufH);
-#pragma unroll 4
-    for (int i = tid; i < live * 32; i += NT) {
-      uint4 v = gld(src + i);
-      if ((i & 31) >= 16) {
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const az_h2 h = __builtin_bit_cast(az_h2, w[k]);
-          w[k] = pk_f16((float)h[0] * 0x1p-12f, (float)h[1] * 0x1p-12f);
-        }
-        v = make_uint4(w[0], w[1], w[2], w[3]);
+    // the second term's x 2^12 scale (rows) -> the tower's unscaled term
+    auto t1_unscale = [](uint32_t w) {
+      const az_h2 h = __builtin_bit_cast(az_h2, w);
+      return pk_f16((float)h[0] * 0x1p-12f, (float)h[1] * 0x1p-12f);
+    };
+    if (lv.leaf) {
+      // planes 64-127 of each pixel from the board's queued leaf (chess
+      // self-play, first_chunk 2: planes 0-63 are never read), the float4s
+      // encode_queue_kernel would have stored, split and unscaled alike
+      const azc::Pos st = azc::start_pos();
+      for (int i = tid; i < live * 16; i += NT) {
+        const int rr = i >> 4, c4 = 16 + (i & 15), b = rr / HW, pix = rr - b * HW;
+        const int s = *gbl(lv.eval_slot + b0 + b);
+        const azc::Pos cur = azc::load_pos(static_cast<const az_chess_pos*>(lv.leaf)[s]);
+        const bool initial = *gbl(lv.path_len + s) == 0 && *gbl(lv.initial + s) != 0;
+        float f[6], v[4];
+        azc::state_feats(cur, f);
+        azc::full_state4(st, cur, initial, f, pix, 4 * c4, v);
+        uint2 t0, t1;
+        split16x4(make_float4(v[0], v[1], v[2], v[3]), t0, t1);
+        char* q = dst + rr * kPitch;
+        *reinterpret_cast<uint2*>(q + 8 * c4) = t0;
+        *reinterpret_cast<uint2*>(q + 256 + 8 * c4) = make_uint2(t1_unscale(t1.x), t1_unscale(t1.y));
       }
-      *reinterpret_cast<uint4*>(dst + (i >> 5) * kPitch + (i & 31) * 16) = v;
+    } else {
+      const uint4* src = rows + (size_t)b0 * HW * 32;
+#pragma unroll 4
+      for (int i = tid; i < live * 32; i += NT) {
+        uint4 v = gld(src + i);
+        if ((i & 31) >= 16) v = make_uint4(t1_unscale(v.x), t1_unscale(v.y), t1_unscale(v.z), t1_unscale(v.w));
+        *reinterpret_cast<uint4*>(dst + (i >> 5) * kPitch + (i & 31) * 16) = v;
+      }
     }
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb)
@@ -1408,7 +1428,7 @@ void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out) {
 template <int MBT, int NWM, bool ROWS, bool DB>
 static void launch_db(const TowerNet* net, int staged, const Board* boards, const float4* x, const uint4* rows,
                       const int* count, int n_max, int H, int W, int A, float* probs, float* values, float4* feat,
-                      int first_chunk, unsigned long long* err, hipStream_t s) {
+                      int first_chunk, unsigned long long* err, hipStream_t s, TowerLeaves lv = {}) {
   const int bpw = tower16_boards_per_tile(H * W, 16 * MBT);
   const int grid = (n_max + bpw - 1) / bpw;
   const size_t bytes = tower16_lds_bytes(H * W, 16 * MBT, staged, DB);
@@ -1419,18 +1439,19 @@ static void launch_db(const TowerNet* net, int staged, const Board* boards, cons
     attr = true;
   }
   tower16_kernel<MBT, NWM, ROWS, DB><<<grid, NWM * 256, bytes, s>>>(net, boards, x, rows, count, n_max, H, W, A,
-                                                                    bpw, probs, values, feat, first_chunk, err);
+                                                                    bpw, probs, values, feat, first_chunk, err, lv);
 }
 template <int MBT, int NWM, bool ROWS>
 static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* boards, const float4* x,
                        const uint4* rows, const int* count, int n_max, int H, int W, int A, float* probs,
-                       float* values, float4* feat, int first_chunk, unsigned long long* err, hipStream_t s) {
+                       float* values, float4* feat, int first_chunk, unsigned long long* err, hipStream_t s,
+                       TowerLeaves lv = {}) {
   if (dbuf)
     launch_db<MBT, NWM, ROWS, true>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat,
-                                    first_chunk, err, s);
+                                    first_chunk, err, s, lv);
   else
     launch_db<MBT, NWM, ROWS, false>(net, staged, boards, x, rows, count, n_max, H, W, A, probs, values, feat,
-                                     first_chunk, err, s);
+                                     first_chunk, err, s, lv);
 }
 
 void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, const Board* boards, const float4* x,
@@ -1450,8 +1471,10 @@ void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, c
 
 void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged, bool dbuf, const void* rows,
                          int first_chunk, const int* count, int n_max, int H, int W, float4* feat,
-                         unsigned long long* err, hipStream_t s) {
+                         unsigned long long* err, hipStream_t s, const TowerLeaves* leaves) {
   if (n_max <= 0 || tile_rows != 128) return;
+  // the leaves' planes are built for the self-play stem (planes 64-127)
+  const TowerLeaves lv = leaves && first_chunk == 2 ? *leaves : TowerLeaves{};
   // a launch of fewer than 512 boards (chess self-play: 128 per lane) in
   // 2-board tiles would hold under a quarter of the 256 CUs: one board per
   // 64-row tile then (MI355X has 256 CUs; the same sums, bitwise), 8 waves of
@@ -1459,10 +1482,10 @@ void launch_tower16_rows(const TowerNet* net, int tile_rows, int staged, bool db
   // expansions/s, profiles/r5/ab_chess.txt)
   if (n_max < 512)
     launch_mbw<4, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
-                           0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s);
+                           0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s, lv);
   else
     launch_mbw<8, 2, true>(net, staged, dbuf, nullptr, nullptr, static_cast<const uint4*>(rows), count, n_max, H, W,
-                           0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s);
+                           0, nullptr, nullptr, feat, first_chunk == 2 ? 2 : 0, err, s, lv);
 }
 
 }  // namespace az

@@ -98,40 +98,85 @@ def test_kloop_asm_invariants(tmp_path):
     groups_seen = 0
     for st in starts:
         en = next(i for i in range(st, len(lines)) if lines[i].startswith(".Lfunc_end"))
-        segs, seg, kind = [], [], "gap"
-        for l in lines[st:en]:
+        # basic blocks (labels .LBB*), each a list of ("asm", [code]) / ("gap", [code]) pieces, and
+        # their successors: the check follows control flow, not the text order the compiler chose
+        blocks, names, cur, kind, seg = [], {}, [], "gap", []
+        for l in lines[st + 1:en]:
+            m = re.match(r"^(\.LBB\S+):", l)
+            if m:
+                cur.append((kind, seg))
+                blocks.append(cur)
+                names[m.group(1)] = len(blocks)
+                cur, kind, seg = [], "gap", []
+                continue
             if ";;#ASMSTART" in l or ";;#ASMEND" in l:
-                segs.append((kind, seg))
+                cur.append((kind, seg))
                 seg, kind = [], ("asm" if ";;#ASMSTART" in l else "gap")
                 continue
             code = l.split(";")[0].strip()
             if code and not code.startswith("."):
                 seg.append(code)
-        segs.append((kind, seg))
-        body = "\n".join("\n".join(x) for _, x in segs)
+        cur.append((kind, seg))
+        blocks.append(cur)
+        body = "\n".join("\n".join(x) for b in blocks for _, x in b)
         assert "scratch_" not in body or "Lb0EEEv" in lines[st], lines[st]  # spill-free product forms
-        inflight = None  # registers the last group's loads may still write
-        for kind, seg in segs:
-            if kind == "asm":
-                loads = [x for x in seg if x.startswith(("ds_read", "buffer_load"))]
-                if any(x.startswith("v_mfma") for x in seg):
-                    groups_seen += 1
-                    inflight = set()
-                    for x in loads:
-                        inflight |= _regs(x.split(",")[0])
-                elif any(x.startswith("s_waitcnt vmcnt(0) lgkmcnt(0)") for x in seg):
-                    inflight = None  # the drain
-                elif loads:  # the prologue: its loads are in flight into the first group
-                    inflight = set()
-                    for x in loads:
-                        inflight |= _regs(x.split(",")[0])
-                continue
-            if inflight is None:
-                continue
-            for x in seg:
-                # a vmcnt wait would drain the weight prefetch (lgkmcnt: the rare
-                # rescale path's own LDS reads, over-waiting the ring reads only)
-                assert not (x.startswith("s_waitcnt") and "vmcnt" in x), (lines[st][:80], x)
-                assert not x.startswith("scratch_"), (lines[st][:80], x)  # a spill inside the K loop
-                assert not (_regs(x) & inflight), (lines[st][:80], x)
+
+        def succ(k):
+            codes = [x for kd, sg in blocks[k] if kd == "gap" for x in sg]
+            last = codes[-1] if codes else ""
+            op = last.split()[0] if last else ""
+            if op == "s_endpgm":
+                return []
+            if op == "s_branch":
+                return [names[last.split()[1]]]
+            out = [k + 1] if k + 1 < len(blocks) else []
+            if op.startswith("s_cbranch"):
+                out.append(names[last.split()[1]])
+            return out
+
+        def run(k, inflight, check):
+            """the block's exit state from its entry state: registers the
+            last group's loads may still write (None: drained / none)"""
+            for kd, sg in blocks[k]:
+                if kd == "asm":
+                    loads = [x for x in sg if x.startswith(("ds_read", "buffer_load"))]
+                    if any(x.startswith("v_mfma") for x in sg):
+                        inflight = set()
+                        for x in loads:
+                            inflight |= _regs(x.split(",")[0])
+                    elif any(x.startswith("s_waitcnt vmcnt(0) lgkmcnt(0)") for x in sg):
+                        inflight = None  # the drain
+                    elif loads:  # the prologue: its loads are in flight into the first group
+                        inflight = set()
+                        for x in loads:
+                            inflight |= _regs(x.split(",")[0])
+                    continue
+                if inflight is None:
+                    continue
+                for x in sg:
+                    if check:
+                        # a vmcnt wait would drain the weight prefetch (lgkmcnt: the rare
+                        # rescale path's own LDS reads, over-waiting the ring reads only)
+                        assert not (x.startswith("s_waitcnt") and "vmcnt" in x), (lines[st][:80], x)
+                        assert not x.startswith("scratch_"), (lines[st][:80], x)  # a spill inside the K loop
+                        assert not (_regs(x) & inflight), (lines[st][:80], x)
+            return inflight
+
+        entry = [None] * len(blocks)  # None: not reached, or reached drained
+        reached = [False] * len(blocks)
+        reached[0] = True
+        work = [0]
+        while work:  # forward dataflow to a fixpoint (states only grow)
+            k = work.pop()
+            out = run(k, entry[k], False)
+            for n in succ(k):
+                new = entry[n] if out is None else (set(out) | (entry[n] or set()))
+                if not reached[n] or new != entry[n]:
+                    reached[n] = True
+                    entry[n] = new
+                    work.append(n)
+        for k in range(len(blocks)):
+            if reached[k]:
+                run(k, entry[k], True)
+        groups_seen += sum(1 for b in blocks for kd, sg in b if kd == "asm" and any(x.startswith("v_mfma") for x in sg))
     assert groups_seen > 0
