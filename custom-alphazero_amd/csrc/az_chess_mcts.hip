@@ -181,12 +181,16 @@ __device__ T pairwise(const T* a, int n) {
   return pw_136(a, n2) + pw_136(a + n2, n - n2);
 }
 
-__device__ __forceinline__ void backup(Edge* E, const int32_t* path, int depth, double v) {
-  for (int d = depth - 1; d >= 0; --d) {
+// MCTS.backup (mcts.py:163-168): from the leaf's parent edge up, N + 1 and
+// W + v with v negated per level -- by the slot's wave, one path level per
+// lane (the levels are distinct edges): level d gets W + v * (-1)^(depth-1-d),
+// the addend the serial walk gives it, so the same bits without the serial
+// walk's chain of dependent loads (two memory round trips per level)
+__device__ __forceinline__ void backup_wave(Edge* E, const int32_t* path, int depth, double v, int lane) {
+  for (int d = lane; d < depth; d += 64) {
     Edge& e = E[path[d]];
     e.N += 1;
-    e.W += v;
-    v = -v;
+    e.W += ((depth - 1 - d) & 1) ? -v : v;
   }
 }
 
@@ -257,7 +261,7 @@ __global__ void tree_release_kernel(CTree t, int n, const int32_t* slots) {
 struct ExpandSmem {
   int act[AZ_CHESS_MAX_MOVES];
   float sorted[AZ_CHESS_MAX_MOVES];
-  double prior[AZ_CHESS_MAX_MOVES];
+  float sum;
   int first_s;
 };
 
@@ -265,7 +269,6 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
                             const float* __restrict__ values, int b, int s, int lane, ExpandSmem& sm) {
   int* act = sm.act;
   float* sorted = sm.sorted;
-  double* prior = sm.prior;
   {
     const int n = t.leaf_n[s];
     const uint16_t* mv = t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES;
@@ -286,13 +289,9 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
     }
     __syncthreads();
     if (lane == 0) {
-      // normalize_probabilities (mcts/utils.py:4-16)
-      const float sum = pairwise(sorted, n);
-      if (sum == 0.0f) {
-        for (int i = 0; i < n; ++i) prior[i] = 1.0 / (double)n;
-      } else {
-        for (int i = 0; i < n; ++i) prior[i] = (double)(float)(sorted[i] / sum);
-      }
+      // normalize_probabilities (mcts/utils.py:4-16): the sum in numpy's
+      // pairwise order here, the quotients per lane below
+      sm.sum = pairwise(sorted, n);
       const int first = t.top[s];
       if (first + n > g.half_cap) {
         flag(t, az::kErrArena);
@@ -304,13 +303,14 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
     }
     __syncthreads();
     const int first = sm.first_s;
+    const float sum = sm.sum;
     if (first < 0) return;
     Edge* E = arena(g, t, s, t.half[s]);
     // zip(probabilities, node.board.moves): positional, python-chess move order
     for (int j = lane; j < n; j += 64) {
       Edge e;
       e.W = 0.0;
-      e.prior = prior[j];
+      e.prior = sum == 0.0f ? 1.0 / (double)n : (double)(float)(sorted[j] / sum);
       e.N = 0;
       e.child = az::kNoChild;
       e.child_n = 0;
@@ -318,10 +318,10 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
       e.child_value = 0.f;
       E[first + j] = e;
     }
+    const int depth = t.path_len[s];
+    const int32_t* path = t.path + (size_t)s * g.max_depth;
+    const float value = values[b];
     if (lane == 0) {
-      const int depth = t.path_len[s];
-      const int32_t* path = t.path + (size_t)s * g.max_depth;
-      const float value = values[b];
       if (depth == 0) {
         t.root_first[s] = first;
         t.root_n[s] = n;
@@ -332,7 +332,9 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
         pe.child_n = (int16_t)n;
         pe.child_value = value;
       }
-      backup(E, path, depth, -(double)value);
+    }
+    backup_wave(E, path, depth, -(double)value, lane);
+    if (lane == 0) {
       t.slot_exp[s] += 1;
       atomicAdd(t.stats + az::kStatExpansions, 1ull);
       atomicAdd(t.stats + az::kStatNNEvals, 1ull);
@@ -351,18 +353,21 @@ __device__ __forceinline__ void leaf_body(const CCfg& g, const CTree& t, int s, 
                                           uint16_t* cand) {
   bool check;
   const int n = legal_moves_wave(q, cand, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check, lane);
-  if (lane != 0) return;
-  if (n < 0) {
-    flag(t, az::kErrIllegal);
-    t.slot_q[s] = -1;
+  if (n < 0) {  // wave-uniform
+    if (lane == 0) {
+      flag(t, az::kErrIllegal);
+      t.slot_q[s] = -1;
+    }
     return;
   }
+  const int oc = outcome(q, n, check);  // wave-uniform
+  if (oc != AZ_CHESS_ONGOING)
+    backup_wave(arena(g, t, s, t.half[s]), t.path + (size_t)s * g.max_depth, t.path_len[s],
+                oc == AZ_CHESS_CHECKMATE ? 1.0 : 0.0, lane);
+  if (lane != 0) return;
   t.leaf_n[s] = n;
   int qi = -1;
-  const int oc = outcome(q, n, check);
   if (oc != AZ_CHESS_ONGOING) {
-    Edge* E = arena(g, t, s, t.half[s]);
-    backup(E, t.path + (size_t)s * g.max_depth, t.path_len[s], oc == AZ_CHESS_CHECKMATE ? 1.0 : 0.0);
     atomicAdd(t.stats + az::kStatTerminal, 1ull);
   } else {
     qi = atomicAdd(t.eval_count, 1);
