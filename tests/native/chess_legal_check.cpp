@@ -6,7 +6,10 @@
 // At every interior node: legal_moves twice (the count pass and the expand
 // pass of the round-1 device perft, which once disagreed run to run) must give
 // the same list, equal to the oracle's, and the leaf counts must be the
-// published perft numbers.
+// published perft numbers.  At every 61st node (and the roots) the network
+// input planes the chess tower builds from a queued leaf (az_chess.h
+// state_feats / full_state4, planes 64-127, both history forms) must equal
+// the oracle's Board.full_state (orc_chess_full_state), planes 0-63 zero.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,9 +21,45 @@ extern "C" {
 int orc_chess_from_fen(const char* fen, az_chess_pos* out);
 int orc_chess_legal(const az_chess_pos* p, uint16_t* out);
 void orc_chess_push(az_chess_pos* p, uint16_t m);
+void orc_chess_full_state(const az_chess_pos* hist, const uint8_t* valid, const az_chess_pos* cur, double* out);
 }
 
-static long long g_nodes = 0, g_fail = 0;
+static long long g_nodes = 0, g_fail = 0, g_planes = 0;
+
+// full_state4 against the oracle for position cp as a played board (history
+// [0 x 6, start, cp]) and as a reset root ([0 x 7, start-position state])
+static void planes_check(const az_chess_pos& cp) {
+  az_chess_pos start;
+  orc_chess_from_fen("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", &start);
+  std::vector<double> ref(64 * 118);
+  const azc::Pos st = azc::start_pos(), cur = azc::load_pos(cp);
+  float f[6];
+  azc::state_feats(cur, f);
+  for (int initial = 0; initial < 2; ++initial) {
+    az_chess_pos hist[8];
+    uint8_t valid[8] = {0, 0, 0, 0, 0, 0, 0, 1};
+    for (auto& h : hist) h = start;
+    if (!initial) {
+      hist[7] = cp;
+      valid[6] = 1;
+    }
+    orc_chess_full_state(hist, valid, &cp, ref.data());
+    long bad = 0;
+    for (int pix = 0; pix < 64; ++pix) {
+      for (int k = 0; k < 64; ++k) bad += ref[pix * 118 + k] != 0.0;
+      for (int k0 = 64; k0 < 128; k0 += 4) {
+        float v[4];
+        azc::full_state4(st, cur, initial != 0, f, pix, k0, v);
+        for (int i = 0; i < 4; ++i) {
+          const int k = k0 + i;
+          bad += (double)v[i] != (k < 118 ? ref[pix * 118 + k] : 0.0);
+        }
+      }
+    }
+    ++g_planes;
+    if (bad && g_fail++ < 5) fprintf(stderr, "planes mismatch (%ld, initial %d)\n", bad, initial);
+  }
+}
 
 static unsigned long long walk(const azc::Pos& q, int depth) {
   // move buffers sized exactly AZ_CHESS_MAX_MOVES: ASan sees any write past them
@@ -31,6 +70,7 @@ static unsigned long long walk(const azc::Pos& q, int depth) {
   az_chess_pos cp;
   azc::store_pos(q, cp);
   const int no = orc_chess_legal(&cp, o.data());
+  if (g_nodes % 61 == 0) planes_check(cp);
   ++g_nodes;
   if (na != nb || ca != cb || na != no || memcmp(a.data(), b.data(), na * 2) || memcmp(a.data(), o.data(), na * 2)) {
     if (g_fail++ < 5) fprintf(stderr, "mismatch: %d/%d vs oracle %d\n", na, nb, no);
@@ -78,6 +118,6 @@ int main() {
     printf("perft(%d) %llu (expected %llu) %s\n", d, got, c.counts[d - 1], c.fen);
     bad += got != c.counts[d - 1];
   }
-  printf("nodes generated %lld, mismatches %lld\n", g_nodes, g_fail);
+  printf("nodes generated %lld, input planes checked %lld, mismatches %lld\n", g_nodes, g_planes, g_fail);
   return bad || g_fail ? 1 : 0;
 }

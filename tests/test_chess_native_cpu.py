@@ -2,7 +2,8 @@
 AddressSanitizer + UBSan and walked over the perft trees of the standard
 positions against the oracle (tests/native/chess_legal_check.cpp): no memory
 or undefined-behaviour error, two generations per position identical, lists
-equal to the oracle's, published perft counts.  No GPU."""
+equal to the oracle's, published perft counts; the chess tower's input planes (full_state4) equal
+the oracle's full_state at sampled nodes.  No GPU."""
 import os
 import subprocess
 
@@ -24,6 +25,8 @@ def test_device_rules_clean_under_asan_ubsan(built):
     r = subprocess.run([built], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+    planes = int(r.stdout.split("input planes checked ")[1].split(",")[0])
+    assert planes > 1000, r.stdout  # az_chess.h full_state4 (the tower's chess input) vs the oracle
     assert r.stdout.count("(expected") == 6
     for line in r.stdout.splitlines():
         if line.startswith("perft("):
