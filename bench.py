@@ -15,10 +15,11 @@ replaced by new ones (game g seeded MT19937(g)).
 Steady state, whatever --warmup says: all slots start at ply 0 together
 and the shared transposition cache (the reference's plays_inferences)
 starts empty, so the first moves are not representative.  Untimed moves
-run until at least --warmup moves have passed AND the cache has turned over
-three eviction generations (az_tree.h: its hit rate is then stationary) --
-every one of them real work.  The line states the cache's capacity,
-generation, live fill, age in moves and the window's hit rate.
+run until at least --warmup moves have passed AND the cache is full and has
+taken 1.5x its capacity in inserts (least-recently-used eviction, az_tree.h:
+its content and hit rate are then stationary, profiles/r6/cache_curve*) --
+every one of them real work.  The line states the cache's capacity, fill,
+generation, age in moves and the window's hit rate.
 value = games drained in the K timed steps, summed over ranks / max-over-
 ranks wall time.
 
@@ -60,8 +61,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 de
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16/fp16 MFMA (no 2:1 sparsity)
 MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
-MAX_PREROLL = 800
-CACHE_TURNOVER_GENS = 2         # cache generations past the live ones before the window (hit rate stationary)
+MAX_PREROLL = 4000
+CACHE_TURNOVER = 1.5            # cache inserts / capacity before the window (full table turned over: stationary)
+CACHE_FULL = 0.98               # ... and the table this full
 
 
 def parse():
@@ -86,8 +88,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=0, help="slot groups on separate HIP streams (0 = auto)")
     ap.add_argument("--conv-algo", type=int, default=0, help="0 fp16x2 direct (default), 1 fp32 direct")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
-    ap.add_argument("--cache-log2", type=int, default=25,
-                    help="transposition cache (the reference's plays_inferences) entries = 2^N; 0 = off")
+    ap.add_argument("--cache-log2", type=int, default=26,
+                    help="transposition cache (the reference's plays_inferences) entries = 2^N (2^26: 4.6 GB "
+                         "of the 288 GB at configs[1]); 0 = off")
     ap.add_argument("--arena-edges", default="bounded",
                     help="tree edges per slot, the average of a lane's pooled halves: 'bounded' (default, "
                          "8*S*A + H*W*A: ~5x the high-water mark measured at configs[1] and configs[3]), "
@@ -680,7 +683,8 @@ def main():
         st, _ = step_and_drain(eng)
         pre += 1
         gen_ok = (not args.cache_log2 or not st["cache_gen_size"]
-                  or st["cache_generation"] >= st["cache_live_gens"] + CACHE_TURNOVER_GENS)
+                  or (st["cache_inserts"] >= CACHE_TURNOVER * st["cache_capacity"]
+                      and st["cache_entries"] >= CACHE_FULL * st["cache_capacity"]))
         done = pre >= max(args.warmup, MIN_PREROLL) and gen_ok
         if world > 1:  # every rank runs the same number of untimed moves
             (done,) = _reduce([0.0 if done else 1.0], SUM, world, args, dev)
@@ -843,10 +847,6 @@ def main():
     cap = st1["cache_capacity"]
     gen_size = st1["cache_gen_size"]
     gen = st1["cache_generation"]
-    live_gens = st1["cache_live_gens"]
-    # inserts of the live generations (refreshed older entries come on top)
-    live = (st1["cache_inserts"] - max(gen - live_gens + 1, 0) * gen_size) if gen_size else \
-        st1["cache_inserts"]
     game_name = "Connect-4 6x7" if (args.height, args.width, args.n) == (6, 7, 4) else \
         f"Connect-{args.n} {args.height}x{args.width}"
     cfg_ref = {(6, 7, 4, 100): "BASELINE.json configs[1]", (9, 9, 5, 200): "BASELINE.json configs[2]",
@@ -879,8 +879,9 @@ def main():
             "lanes": eng.lanes,
             "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "untimed_moves": pre,
-            "untimed_rule": (f"max(--warmup, {MIN_PREROLL}) moves and until the transposition cache has "
-                             f"turned over its live generations + {CACHE_TURNOVER_GENS} (stationary hit rate)"),
+            "untimed_rule": (f"max(--warmup, {MIN_PREROLL}) moves and until the transposition cache is "
+                             f"{CACHE_FULL:.0%} full and has taken {CACHE_TURNOVER}x its capacity in inserts "
+                             f"(LRU content turned over: stationary hit rate, profiles/r6/cache_curve*)"),
             "games_timed": int(drained_all),
             "games_timed_basis": "games whose samples reached the host in the window (az_selfplay_drain "
                                  "after every step -- the previous move's games while the next move runs "
@@ -893,13 +894,15 @@ def main():
             "transposition_cache": ({
                 "capacity": cap,
                 "hit_rate": round(hits_all / max(exp_all, 1), 4),
-                "eviction": ({"inserts_per_generation": gen_size, "live_generations": live_gens,
-                              "rule": f"lookups use the last {live_gens} generations and a hit moves the "
-                                      f"entry into the current one; inserts reuse entries "
-                                      f"{live_gens + 1}+ generations old (az_tree.h)"} if gen_size else None),
+                "eviction": ({"inserts_per_generation": gen_size,
+                              "rule": "least recently used: every entry is looked up, a hit moves it into the "
+                                      "current generation, an insert into a full 16-slot bucket evicts its "
+                                      "oldest entry 2+ generations old (az_tree.h)"} if gen_size else None),
                 "generation_at_window_end": gen,
-                "inserted_in_live_generations": int(live),
-                "fill_lower_bound": round(live / cap, 4) if cap else None,
+                "entries": st1["cache_entries"],
+                "fill": round(st1["cache_entries"] / cap, 4) if cap else None,
+                "inserts_over_capacity_at_window_end": round(st1["cache_inserts"] / cap, 3) if cap else None,
+                "bytes": cap * (32 + 4 + 4 * (A + 1)) if cap else None,
                 "age_moves_at_window_start": pre,
                 "inserts_in_window": d["cache_inserts"],
                 "semantics": "reference plays_inferences (mcts.py:122-143): board -> network output, shared "

@@ -270,7 +270,7 @@ int cache_clear(az_engine* e) {
   int rc;
   if ((rc = sync_all(e))) return rc;
   AZ_HIP(hipMemsetAsync(e->cache.state, 0, ((size_t)e->cache.mask + 1) * sizeof(uint32_t), e->stream));
-  AZ_HIP(hipMemsetAsync(e->cache.ctl, 0, 2 * sizeof(unsigned long long), e->stream));
+  AZ_HIP(hipMemsetAsync(e->cache.ctl, 0, 4 * sizeof(unsigned long long), e->stream));
   AZ_HIP(hipStreamSynchronize(e->stream));
   return 0;
 }
@@ -841,17 +841,17 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
     const size_t cap = (size_t)1 << c.cache_log2;
     az::CacheDev& cd = e->cache;
     if ((rc = e->alloc(&cd.keys, cap)) || (rc = e->alloc(&cd.state, cap)) ||
-        (rc = e->alloc(&cd.pay, cap * (A + 1))) || (rc = e->alloc(&cd.ctl, 2)))
+        (rc = e->alloc(&cd.pay, cap * (A + 1))) || (rc = e->alloc(&cd.ctl, 4)))
       return cleanup(rc);
     cd.mask = (uint32_t)(cap - 1);
     cd.enabled = 1;
-    // eviction by generations of cap/kCacheGenDiv inserts, when a generation outlasts
-    // three moves of every slot's inserts (the lane-drift bound, az_tree.h);
-    // otherwise the table only fills (entries are never overwritten)
+    // LRU eviction by generations of cap/kCacheGenDiv inserts, when a generation
+    // outlasts three moves of every slot's inserts (the lane-drift bound,
+    // az_tree.h); otherwise the table only fills (entries are never overwritten)
     const unsigned long long gen = cap / az::kCacheGenDiv;
     cd.gen_size = gen > 3ull * (unsigned long long)g.slots * (unsigned long long)g.sims ? gen : 0;
     if (hipMemset(cd.state, 0, cap * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(cd.ctl, 0, 2 * sizeof(unsigned long long)) != hipSuccess)
+        hipMemset(cd.ctl, 0, 4 * sizeof(unsigned long long)) != hipSuccess)
       return cleanup(fail(AZ_E_HIP, "cache memset failed"));
   }
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
@@ -1103,12 +1103,12 @@ int az_stats_get(az_engine* e, az_stats* st) {
   st->cache_hits = (int64_t)h[az::kStatCacheHits];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
   if (e->cache.ctl) {
-    unsigned long long ctl[2];
+    unsigned long long ctl[3];
     AZ_HIP(hipMemcpy(ctl, e->cache.ctl, sizeof(ctl), hipMemcpyDeviceToHost));
     st->cache_generation = (int64_t)ctl[0];
     st->cache_inserts = (int64_t)ctl[1];
     st->cache_gen_size = (int64_t)e->cache.gen_size;
-    st->cache_live_gens = (int64_t)az::kCacheLiveGens;
+    st->cache_entries = (int64_t)ctl[2];
     st->cache_capacity = (int64_t)e->cache.mask + 1;
   }
   st->games_drained = e->drained;

@@ -120,33 +120,32 @@ struct TreeDev {
 // acquire loads one after another, and games/s fell the longer a run went.)
 // The evaluator is deterministic per board, so hits never change a search.
 //
-// Eviction by generations (the reference's dict grows without bound until
-// the next model; a fixed table would fill up and stop taking inserts).  Each `gen_size` inserts start a new generation;
-// lookups use entries of the current and previous generation only (a hit on
-// the previous generation moves the entry into the current one, so boards
-// the games keep reaching stay live), and an insert may overwrite an entry
-// at least kCacheReuseAge generations old.  A
-// reader checks liveness in select and reads the payload in expand, one
-// simulation later; an overwrite in between needs kCacheReuseAge -
-// (kCacheLiveGens - 1) = 2 generation turns inside that window, i.e. 2 * gen_size inserts.  The engine
-// bounds the drift between lanes to two moves (move events, az_engine.hip)
-// and enables eviction only when 2 * gen_size > lanes' inserts in three moves
-// (slots * sims * 3), so a payload is never overwritten while a reader holds
-// its index.
+// Eviction: least recently used, by generations (the reference's dict grows
+// without bound until the next model; a fixed table keeps what it can).
+// Every Ready entry is live -- a lookup accepts any of them, so the whole
+// table serves as plays_inferences.  Each `gen_size` inserts start a new
+// generation; a hit on an entry of an older generation moves it into the
+// current one (one CAS per entry per generation), so an entry's generation
+// is when it was last used.  An insert takes the bucket's first empty slot,
+// else its least recently used entry at least kCacheEvictAge generations old
+// (dropped when every entry is younger: a bucket of boards all in use).
+//
+// Overwrite safety: select finds an entry and expand reads its payload one
+// launch later.  Every hit leaves select stamped with the reader's generation
+// G (an older entry's refresh CAS must win; when it loses, the slot may be
+// being overwritten and the board counts as a miss).  The engine enables
+// eviction only when gen_size exceeds three moves of every slot's inserts
+// (slots * sims * 3: the lane drift is bounded to two moves by move events,
+// az_engine.hip), so at most one generation turn falls inside a reader's
+// window, an insert sees the entry at most 1 generation old, and
+// kCacheEvictAge = 2 keeps it.
 //
 // State word: [31:16] 16-bit fingerprint (hash bits 48-63, so most probes
 // need no key read), [15:2] generation mod 2^14, [1:0] status.
 enum : uint32_t { kCacheEmpty = 0, kCacheClaimed = 1, kCacheReady = 2 };
 constexpr uint32_t kCacheGenMask = 0x3fff;
-#ifndef AZ_CACHE_GEN_DIV  // A/B builds (profiles/ab_libs.sh)
-#define AZ_CACHE_GEN_DIV 16
-#endif
-#ifndef AZ_CACHE_LIVE
-#define AZ_CACHE_LIVE 6
-#endif
-constexpr uint32_t kCacheGenDiv = AZ_CACHE_GEN_DIV;       // a generation = capacity / kCacheGenDiv inserts
-constexpr uint32_t kCacheLiveGens = AZ_CACHE_LIVE;        // ages 0 .. kCacheLiveGens - 1 are looked up
-constexpr uint32_t kCacheReuseAge = kCacheLiveGens + 1;  // older entries may be overwritten
+constexpr uint32_t kCacheGenDiv = 16;   // a generation = capacity / kCacheGenDiv inserts
+constexpr uint32_t kCacheEvictAge = 2;  // an insert may overwrite entries this many generations old
 AZ_HD uint32_t cache_fp(uint64_t h) { return (uint32_t)(h >> 48); }
 AZ_HD uint32_t cache_age(uint32_t st, uint32_t gen) { return (gen - (st >> 2)) & kCacheGenMask; }
 AZ_HD uint32_t cache_word(uint32_t fp, uint32_t gen, uint32_t status) {
@@ -158,7 +157,8 @@ struct CacheDev {
   float* pay = nullptr;        // [cap][A+1]: probs then value
   uint32_t mask = 0;           // cap - 1
   int enabled = 0;
-  unsigned long long* ctl = nullptr;  // device [0] generation, [1] inserts since the last clear
+  unsigned long long* ctl = nullptr;  // device [0] generation, [1] inserts since the last clear,
+                                      // [2] of them into empty slots (= entries held)
   unsigned long long gen_size = 0;    // inserts per generation; 0 = no eviction
 };
 constexpr int kCacheBucket = 16;  // slots per bucket (cache_log2 >= 4)

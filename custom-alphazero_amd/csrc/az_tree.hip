@@ -215,8 +215,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   // concurrently by another lane's insert kernel: the acquire load pairs with
   // its release exchange, so a Ready entry's key and payload are complete
   // (a Claimed one reads as absent: the leaf is evaluated here, same result).
-  // Only live generations count (az_tree.h); older entries are skipped, not
-  // treated as the end of the probe chain.
+  // Every Ready entry is live (LRU eviction, az_tree.h).
   const uint64_t h = board_hash(b);
   {
     // the board's bucket: kCacheBucket state words (one 64-B segment) read
@@ -239,7 +238,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
       if (stop) continue;
       if (st == kCacheEmpty) {  // inserts fill a bucket in slot order: nothing past this
         stop = true;
-      } else if ((st & 3u) == kCacheReady && (st >> 16) == fp && cache_age(st, gen) < kCacheLiveGens) {
+      } else if ((st & 3u) == kCacheReady && (st >> 16) == fp) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (same_board(c.keys[base + k], b)) {
           hit = k;
@@ -248,13 +247,23 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
         }
       }
     }
-    if (hit >= 0) {
+    bool use = hit >= 0;
+    if (use && cache_age(hst, gen) != 0) {
+      // a hit on an older generation moves the entry into the current one
+      // (its last use: inserts evict the least recently used), at most one CAS
+      // per entry per generation.  The CAS must win -- or find the entry
+      // already moved by another reader and still this board -- else an insert
+      // may be overwriting the slot and the board counts as a miss (az_tree.h)
+      const uint32_t want = cache_word(fp, gen, kCacheReady);
+      const uint32_t prev = atomicCAS(c.state + base + hit, hst, want);
+      if (prev != hst) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        use = prev == want && same_board(c.keys[base + hit], b);
+      }
+    }
+    if (use) {
       const uint32_t idx = base + hit;
       t.eval_src[q] = (int32_t)idx;
-      // a hit on an older live generation moves the entry into the current
-      // one, so boards the games keep reaching stay live (the reference's
-      // dict never forgets them); at most one CAS per entry per generation
-      if (cache_age(hst, gen) != 0) atomicCAS(c.state + idx, hst, cache_word(fp, gen, kCacheReady));
       AZ_SEL_STAMP(s, 5);
       AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
       wave_stat(t, kStatCacheHits);
@@ -626,8 +635,9 @@ __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, Tre
 
 // ------------------------------------------------------------ cache insert
 // plays_inferences[repr(board)] = probabilities, value (mcts.py:142): one
-// writer per distinct board (dedup), racing only for empty slots or slots
-// whose entry is kCacheReuseAge generations old (az_tree.h).
+// writer per distinct board (dedup), racing only for the bucket's first empty
+// slot or its least recently used entry kCacheEvictAge+ generations old
+// (az_tree.h); a lost race moves on to the next candidate.
 __device__ void cache_insert_row(const GameCfg& g, const TreeDev& t, const CacheDev& c,
                                  const float* __restrict__ probs, const float* __restrict__ values, int u) {
   if (u >= *t.nn_count) return;
@@ -641,14 +651,34 @@ __device__ void cache_insert_row(const GameCfg& g, const TreeDev& t, const Cache
   for (int k = 0; k < kCacheBucket; ++k)
     w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int slot = -1;
+  bool was_empty = false;
+  uint32_t tried = 0;  // slots whose CAS lost (claimed or refreshed meanwhile)
+  for (int attempt = 0; attempt < kCacheBucket && slot < 0; ++attempt) {
+    // candidate: the first empty slot, else the oldest evictable entry (the
+    // first of equal ages); scanned with constant indices (w stays in VGPRs)
+    int pick = -1;
+    uint32_t pst = 0, page = 0;
+    bool pempty = false;
 #pragma unroll
-  for (int k = 0; k < kCacheBucket; ++k) {  // the first reusable slot this insert wins
-    const uint32_t st = w[k];
-    if (slot >= 0) continue;
-    const bool reusable = st == kCacheEmpty || (c.gen_size && cache_age(st, gen) >= kCacheReuseAge);
-    if (reusable && atomicCAS(c.state + base + k, st, cache_word(fp, gen, kCacheClaimed)) == st) slot = k;
+    for (int k = 0; k < kCacheBucket; ++k) {
+      const uint32_t st = w[k];
+      if (pempty || ((tried >> k) & 1u)) continue;
+      if (st == kCacheEmpty) {
+        pick = k, pst = st, pempty = true;
+      } else if (c.gen_size) {
+        const uint32_t age = cache_age(st, gen);
+        if (age >= kCacheEvictAge && age > page) pick = k, pst = st, page = age;
+      }
+    }
+    if (pick < 0) return;  // every entry of the bucket is in use: evaluated again when met
+    if (atomicCAS(c.state + base + pick, pst, cache_word(fp, gen, kCacheClaimed)) == pst) {
+      slot = pick;
+      was_empty = pempty;
+    } else {
+      tried |= 1u << pick;
+    }
   }
-  if (slot < 0) return;  // every slot of the bucket is live: the board is evaluated again when met
+  if (slot < 0) return;
   const uint32_t idx = base + slot;
   c.keys[idx] = b;
   float* dst = c.pay + (size_t)idx * (g.A + 1);
@@ -657,6 +687,7 @@ __device__ void cache_insert_row(const GameCfg& g, const TreeDev& t, const Cache
   __threadfence();
   atomicExch(c.state + idx, cache_word(fp, gen, kCacheReady));
   wave_stat(t, kStatCacheInserts);
+  if (was_empty) wave_claim64(c.ctl + 2);
   // every gen_size-th insert since the clear opens a new generation
   const unsigned long long n = wave_claim64(c.ctl + 1) + 1;
   if (c.gen_size && n % c.gen_size == 0) atomicAdd(c.ctl, 1ull);
@@ -677,9 +708,9 @@ __global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, const Board*
 // (mcts/utils.py:4-16), then backup(-value) (mcts.py:175, 163-168).
 // With INSERT the same launch also publishes this simulation's evaluated
 // boards to the cache (blocks from exp_blocks on, one nn row per thread):
-// the leaves expanded here read only entries live at select time, which an
-// insert never reuses (kCacheLiveGens < kCacheReuseAge, az_tree.h), so the
-// two halves are independent and share one launch instead of two.
+// the entries the leaves expanded here read were stamped with the current
+// generation by select, which an insert never evicts (kCacheEvictAge,
+// az_tree.h), so the two halves are independent and share one launch.
 template <int MAXA, bool INSERT>
 __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
                                                      const float* __restrict__ probs,

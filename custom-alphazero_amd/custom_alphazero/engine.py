@@ -68,7 +68,7 @@ class Stats(ctypes.Structure):
         ("path_edges", ctypes.c_int64), ("cache_inserts", ctypes.c_int64),
         ("cache_generation", ctypes.c_int64), ("cache_gen_size", ctypes.c_int64),
         ("cache_capacity", ctypes.c_int64), ("games_drained", ctypes.c_int64),
-        ("max_retained", ctypes.c_int64), ("cache_live_gens", ctypes.c_int64),
+        ("max_retained", ctypes.c_int64), ("cache_entries", ctypes.c_int64),
         ("arena_edges", ctypes.c_int64), ("issued_flop_per_board", ctypes.c_double),
         ("arena_pool_edges", ctypes.c_int64), ("arena_pool_high", ctypes.c_int64),
     ]

@@ -133,14 +133,16 @@ typedef struct az_stats {
     double tree_ms;           /* their summed device time */
     int64_t path_edges;       /* edges on the selected paths (sum of select depths) */
     int64_t cache_inserts;    /* transposition-cache inserts since the last clear */
-    int64_t cache_generation; /* eviction generations since the last clear (az_tree.h) */
+    int64_t cache_generation; /* eviction generations since the last clear (az_tree.h: a generation is
+                                 cache_gen_size inserts, an entry's stamp is its last use) */
     int64_t cache_gen_size;   /* inserts per generation (0 = no eviction: the table only fills) */
     int64_t cache_capacity;   /* cache entries (2^cache_log2; 0 = no cache) */
     int64_t games_drained;    /* finished games az_selfplay_drain has returned this batch */
     int64_t max_retained;     /* compact: most edges a compaction kept (the arena high-water mark
                                  before the next search) since engine creation */
-    int64_t cache_live_gens;  /* generations a lookup accepts (ages 0 .. n-1; a hit moves the entry
-                                 into the current one); entries n+ generations old may be overwritten */
+    int64_t cache_entries;    /* entries the cache holds (every one is looked up: a hit moves it into
+                                 the current generation, an insert into a full bucket evicts its least
+                                 recently used entry 2+ generations old; ABI 10, was cache_live_gens) */
     int64_t arena_edges;      /* tree edges per slot this engine allocated (compact: per half, the
                                  average over a lane's pool) */
     double issued_flop_per_board; /* MFMA FLOP the network forward issues per board (the one-launch

@@ -229,15 +229,18 @@ def test_selfplay_synthetic_many_games_vs_oracle(cache_log2, lanes, compact):
 
 @pytest.mark.parametrize("lanes", [1, 2, 3])
 def test_cache_eviction_generations_are_transparent(lanes):
-    """A cache small enough to turn over many eviction generations (az_tree.h:
-    entries older than the live generations are overwritten while other lanes
-    read the table, hits move entries into the current generation) leaves
-    every game bitwise equal to the oracle."""
-    eng = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC, cache_log2=18, lanes=lanes)
-    games = selfplay_games(eng, 3000, 384, base_seed=9)
+    """A cache small enough to fill and turn over many times (az_tree.h: every
+    entry is looked up, a hit moves it into the current generation, an insert
+    into a full bucket evicts its least recently used entry 2+ generations old
+    while other lanes read the table) leaves every game bitwise equal to the
+    oracle."""
+    eng = az.Engine(6, 7, 4, True, 50, slots=32, evaluator=az.EVAL_SYNTHETIC, cache_log2=17, lanes=lanes)
+    games = selfplay_games(eng, 3000, 512, base_seed=9)
     st = eng.stats()
-    assert st["cache_gen_size"] == 2 ** 18 // 16  # kCacheGenDiv
-    assert st["cache_generation"] >= st["cache_live_gens"] + 2, st["cache_generation"]
+    assert st["cache_gen_size"] == 2 ** 17 // 16  # kCacheGenDiv
+    assert st["cache_generation"] >= 24, st["cache_generation"]  # > 1.5 turnovers of the table
+    assert st["cache_entries"] >= 0.99 * 2 ** 17, st["cache_entries"]  # full: inserts evicted entries
+    assert st["cache_entries"] <= 2 ** 17
     assert st["cache_hits"] > 0 and st["errors"] == 0
     for g, got in enumerate(games):
         ref = oracle.play_game(6, 7, 4, True, 50, 9 + 3000 + g)
@@ -245,8 +248,9 @@ def test_cache_eviction_generations_are_transparent(lanes):
         np.testing.assert_array_equal(got["moves"], ref["moves"])
         np.testing.assert_array_equal(got["policy"].view(np.uint64), ref["policy"].view(np.uint64))
         assert got["expansions"] == ref["expansions"]
-    # too small for the lane-drift bound: eviction stays off (the table only fills)
-    small = az.Engine(6, 7, 4, True, 50, slots=96, evaluator=az.EVAL_SYNTHETIC, cache_log2=14, lanes=lanes)
+    # too small for the lane-drift bound (gen_size <= 3 * slots * sims): eviction
+    # stays off and the table only fills
+    small = az.Engine(6, 7, 4, True, 50, slots=32, evaluator=az.EVAL_SYNTHETIC, cache_log2=16, lanes=lanes)
     assert small.stats()["cache_gen_size"] == 0
 
 
