@@ -221,6 +221,55 @@ AZ_HD int play_bb(const GameCfg& g, const BoardMasks& mk, Board& b, int a) {
   return status;
 }
 
+// play_bb for one gravity shape known at compile time whose cells fit one
+// 64-bit word (Connect-4's 6x7: 42 cells) -- the select descent plays a move
+// per tree level on every lane of the game's group, and play_bb's runtime
+// n / W loops of 128-bit variable shifts cost ~1.7 us a level.
+// Here every shift is a constant: a run of N through stride S is
+// x & x>>S & x>>2S & ..., masked to the cells a run may start from (no
+// wrap past the board edge; vertical runs past the last row read zeros).
+// Same status and board as play() for every board the search reaches
+// (tests/native/play_bb_check.cpp).
+template <int H, int W>
+constexpr uint64_t c64_col0() {
+  uint64_t m = 0;
+  for (int y = 0; y < H; ++y) m |= 1ull << (y * W);
+  return m;
+}
+template <int H, int W, int lo, int hi>  // cells with lo <= x <= hi
+constexpr uint64_t c64_cols() {
+  uint64_t m = 0;
+  for (int x = lo; x <= hi; ++x) m |= c64_col0<H, W>() << x;
+  return m;
+}
+template <int S, int N>
+AZ_HD uint64_t c64_run(uint64_t x) {  // bit p: cells p, p + S, ..., p + (N - 1) S all set
+  uint64_t m = x;
+#pragma unroll
+  for (int i = 1; i < N; ++i) m &= x >> (i * S);
+  return m;
+}
+template <int H, int W, int N>
+AZ_HD int play_c64(Board& b, int a) {
+  static_assert(H * W <= 64 && N >= 2 && N <= H && N <= W, "one-word gravity shapes");
+  constexpr uint64_t col0 = c64_col0<H, W>();
+  constexpr uint64_t left = c64_cols<H, W, 0, W - N>();      // a run to the right fits
+  constexpr uint64_t right = c64_cols<H, W, N - 1, W - 1>();  // a run to the left fits
+  constexpr uint64_t top = (1ull << W) - 1;
+  const uint64_t own = b.own[0], opp = b.opp[0];
+  const uint64_t occ = own | opp;
+  const int k = __builtin_popcountll(~occ & (col0 << a));  // the column's empty cells: its top rows
+  if (k == 0) return -1;
+  const uint64_t stone = 1ull << ((k - 1) * W + a);
+  const uint64_t mine = own | stone;
+  const uint64_t win = (c64_run<1, N>(mine) & left) | c64_run<W, N>(mine) | (c64_run<W + 1, N>(mine) & left) |
+                       (c64_run<W - 1, N>(mine) & right);
+  const int status = win ? kWin : ((~(occ | stone) & top) == 0 ? kDraw : kOngoing);
+  b.own[0] = opp;
+  b.opp[0] = mine;  // (the high words stay 0: every cell is in word 0)
+  return status;
+}
+
 // ---------------------------------------------------------------- numerics
 // numpy float32 add.reduce = identity 0 + pairwise_sum (8 accumulators from
 // n >= 8, 128-element blocks).  normalize_probabilities (mcts/utils.py:4-16)

@@ -35,6 +35,18 @@ int fail(int code, const std::string& msg) {
 // float_pow -> pow(n, 0.5), which is NOT sqrt for 1,638 n <= 2e6.
 double (*volatile g_pow)(double, double) = pow;
 
+// HIP hardware queues of this process (GPU_MAX_HW_QUEUES, HIP's default 4),
+// read once when the library loads -- HIP reads the variable at its own
+// initialisation, so a value set later would not describe the queues HIP
+// made; the lane rule (az_engine_lanes) uses this snapshot.  The Python
+// package sets 8 at import before anything initialises HIP.
+int read_hw_queues() {
+  const char* q = getenv("GPU_MAX_HW_QUEUES");
+  const int v = q && *q ? atoi(q) : 0;
+  return v > 0 ? v : 4;
+}
+const int g_hw_queues_at_load = read_hw_queues();
+
 }  // namespace
 
 namespace az {
@@ -898,8 +910,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   // profiles/r5/ab_queues_lanes.txt; larger launches keep two)
   int nl = c.lanes;
   if (nl <= 0) {
-    const char* q = getenv("GPU_MAX_HW_QUEUES");
-    const int queues = q && *q ? atoi(q) : 4;
+    const int queues = g_hw_queues_at_load;
     nl = g.slots < 512 ? 1 : (queues >= 8 && g.slots >= 1536 && g.slots <= 4096) ? 3 : 2;
   }
   nl = std::min(nl, std::min(g.slots, 8));

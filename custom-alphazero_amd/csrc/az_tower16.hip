@@ -687,6 +687,9 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // (the plan is for the TowerNet's tile height: a smaller tile of the same
   // boards -- chess's 64-row tiles -- runs in natural order, the same bits)
   const bool planned = 16 * MBT == T.tile_rows;
+  // wv1 staged behind X's dead tile only in the tile height it was sized for
+  // (tower16_wv1_xtile_fits); a smaller tile reads it from L2
+  const bool wv1_xt = T.wv1_xtile && 16 * MBT == T.tile_rows;
   const int* plan = planned ? T.slot_pix : nullptr;
   T16_STAMP(56);
 #pragma unroll
@@ -924,7 +927,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       // block streams the value dense's wv1 into X's tile behind the heads'
       // partials while the taps run (every wave a share).  The same sums in
       // the same order as the in-place form: bitwise the same outputs
-      const bool wv1x = T.wv1_xtile && d + 1 == depth;  // read before the K loop's asm ("memory")
+      const bool wv1x = wv1_xt && d + 1 == depth;  // read before the K loop's asm ("memory")
       auto mid = [&]() {
         rescale();
         __syncthreads();
@@ -1038,7 +1041,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   T16_STAMP4(54);
   T16_STAMP(42);
   T16_STAMP4(43);
-  if (T.wv1_xtile) __builtin_amdgcn_s_waitcnt(0);  // this wave's wv1 DMA pieces have landed ...
+  if (wv1_xt) __builtin_amdgcn_s_waitcnt(0);  // this wave's wv1 DMA pieces have landed ...
   __syncthreads();  // ... the partials are complete; no activation row is read any more
   T16_STAMP(18);
   if constexpr (ROWS) {
@@ -1159,7 +1162,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
       else policy_part(base, gbl(T.blob + T.off_wpd));
       if (base == 0) {
         if (T.wv1_lds) value_part(blob + T.off_wv1);
-        else if (T.wv1_xtile) value_part(reinterpret_cast<const float*>(bufX) + TR * 48);
+        else if (wv1_xt) value_part(reinterpret_cast<const float*>(bufX) + TR * 48);
         else value_part(gbl(T.blob + T.off_wv1));
       }
       if (base == 0) T16_STAMP(45);

@@ -416,7 +416,9 @@ __device__ __forceinline__ void select_body(const GameCfg& g, const TreeDev& t, 
 // Lane j loads edge j (contiguous, one 32-byte record per lane), the group
 // sums N and takes the first-maximum UCB by shuffles -- the same float64
 // expressions as the serial loop, so the chosen edge is identical.
-template <int L, bool NOISE>
+// SHAPE 1: Connect-4 (6x7, n = 4, gravity) with the compile-time one-word
+// play (play_c64); 0: any shape through play_bb's runtime masks.
+template <int L, bool NOISE, int SHAPE>
 __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDev& t, const CacheDev& c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -557,7 +559,8 @@ __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDe
     AZ_SEL_PHASE(ph_reduce);
     if (j == 0) path[depth] = first + best;
     ++depth;
-    status = play_bb(g, mk, b, action);
+    if constexpr (SHAPE == 1) status = play_c64<6, 7, 4>(b, action);
+    else status = play_bb(g, mk, b, action);
     AZ_SEL_PHASE(ph_play);
     if (status < 0) {
       if (j == 0) flag_error(t, kErrIllegal);
@@ -627,9 +630,9 @@ __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t
   select_body<NOISE>(g, t, c);
   dedup_tail(t, c);
 }
-template <int L, bool NOISE>
+template <int L, bool NOISE, int SHAPE = 0>
 __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
-  select_group_body<L, NOISE>(g, t, c);
+  select_group_body<L, NOISE, SHAPE>(g, t, c);
   dedup_tail(t, c);
 }
 
@@ -1064,6 +1067,12 @@ static inline int game_blocks(int n) { return (n + kGameBlock - 1) / kGameBlock;
 void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStream_t s) {
   const int lanes = g.A <= 8 ? 8 : g.A <= 16 ? 16 : g.A <= 32 ? 32 : g.A <= 64 ? 64 : 1;
   const int blocks = (int)(((int64_t)g.slots * lanes + kGameBlock - 1) / kGameBlock);
+  const bool c4 = g.H == 6 && g.W == 7 && g.n == 4 && g.gravity && lanes == 8;
+  if (c4) {  // Connect-4: the compile-time one-word play (play_c64)
+    if (g.noise) select_group_kernel<8, true, 1><<<blocks, kGameBlock, 0, s>>>(g, t, c);
+    else select_group_kernel<8, false, 1><<<blocks, kGameBlock, 0, s>>>(g, t, c);
+    return;
+  }
   if (g.noise) {  // the root-noise instantiations (the default path carries none of their code)
     switch (lanes) {
       case 8: select_group_kernel<8, true><<<blocks, kGameBlock, 0, s>>>(g, t, c); break;

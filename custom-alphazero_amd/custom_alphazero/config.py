@@ -22,7 +22,7 @@ class ConfigSelfPlay:
     games_per_call = 4096        # games per play() call (reference: cpu_count()-1)
     concurrent_games = 4096      # device slots (trees in flight)
     base_seed = None             # None -> time-based like self_play.py:45
-    cache_log2 = 22              # device plays_inferences entries (2^k); 0 = no cache
+    cache_log2 = 26              # device plays_inferences entries (2^k, LRU; 2^26 = 4.6 GB for C4); 0 = no cache
     lanes = 0                    # slot groups on separate HIP streams (0 = auto)
     chess_concurrent_games = 256 # chess device slots (BASELINE configs[4]: 2048 games / 8 GPUs)
     chess_max_plies = 512        # chess games stop (as draws) here; the reference has no cap

@@ -441,6 +441,14 @@ class Engine:
                                     _ptr(moves), _ptr(status), _ptr(policy)))
         return moves, status, policy
 
+    def tree_info(self, slot):
+        """The slot's tree header alone (az_tree_info: no edge copy)."""
+        info = np.zeros(5, np.int64)
+        rv = np.zeros(1, np.float32)
+        _check(self._L.az_tree_info(self._h, int(slot), _ptr(info), _ptr(rv)))
+        return dict(arena_top=int(info[0]), root_first=int(info[1]), root_n=int(info[2]), ply=int(info[3]),
+                    active=bool(info[4]), root_value=float(rv[0]))
+
     def tree_export(self, slot):
         info = np.zeros(5, np.int64)
         rv = np.zeros(1, np.float32)

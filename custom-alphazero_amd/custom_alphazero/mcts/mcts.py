@@ -165,7 +165,7 @@ class MCTS:
         # selections, or n - 1 when the first one expands the root (:111-120);
         # nothing else in a search draws, so drawing them up front takes the
         # same words in the same order
-        expanded = self._engine.tree_export(0)["root_n"] > 0
+        expanded = self._engine.tree_info(0)["root_n"] > 0
         rows = n if expanded else max(n - 1, 0)
         noise = root_noise_rows(np.random, len(self.board.moves), rows, len(self.all_possible_moves))
         self._engine.tree_search(n, noise=noise[None])

@@ -398,7 +398,12 @@ def _length_words(lens):
 
 
 def _decode_strings(raw, shape, key="string tensor"):
-    """-> (value, the entry crc32c TF computes while reading it)."""
+    """-> (value, the entry crc32c TF computes while reading it).
+
+    Also reads the LEGACY layout this package's round-3/4 writer produced
+    (the masked crc32c over the lengths' varint bytes, the entry crc32c over
+    the raw bytes), so a model saved by those builds still loads: its entry
+    checksum is then crc32c(raw), which the caller compares as before."""
     n = int(np.prod(shape)) if shape else 1
     pos, lens = 0, []
     for _ in range(n):
@@ -406,8 +411,13 @@ def _decode_strings(raw, shape, key="string tensor"):
         lens.append(ln)
     words = _length_words(lens)
     stored = bytes(raw[pos:pos + 4])
+    legacy = False
     if len(stored) != 4 or struct.unpack("<I", stored)[0] != mask(crc32c(words)):
-        raise ValueError(f"{key}: string lengths checksum mismatch")
+        if len(stored) == 4 and struct.unpack("<I", stored)[0] == mask(crc32c(bytes(raw[:pos]))):
+            legacy = True  # the round-3/4 writer: checksum of the varint bytes
+        else:
+            raise ValueError(f"{key}: string lengths checksum mismatch (neither TensorFlow's layout, the "
+                             f"lengths as uint32 words, nor this package's legacy varint-byte layout)")
     pos += 4
     out = []
     for ln in lens:
@@ -415,7 +425,7 @@ def _decode_strings(raw, shape, key="string tensor"):
         pos += ln
     if pos != len(raw):
         raise ValueError(f"{key}: string tensor size mismatch")
-    crc = crc32c(words + stored + b"".join(out))
+    crc = crc32c(bytes(raw)) if legacy else crc32c(words + stored + b"".join(out))
     return (out[0] if not shape else out), crc
 
 

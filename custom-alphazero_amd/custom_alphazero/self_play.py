@@ -25,7 +25,7 @@ from custom_alphazero.config import (ConfigConnectN, ConfigGeneral, ConfigMCTS, 
 from custom_alphazero.connect_n.board import Board
 from custom_alphazero.connect_n.move import Move
 from custom_alphazero.mcts.mcts import MCTS, SyntheticEvaluator
-from custom_alphazero.utils import best_saved_model
+from custom_alphazero.utils import best_saved_model, input_dim
 
 get_all_possible_moves = Board.get_all_possible_moves
 
@@ -45,11 +45,12 @@ def play_game(process_id: int, all_possible_moves: List[Move], mcts_iterations: 
     np.random.seed(seed)
     if model is None:
         model = best_saved_model(run_id)  # its constructor draws np.random.rand(1, *input_dim)
-    elif ConfigGeneral.game != "chess":
+    else:
         # a caller's model: take the draws the reference's model construction
-        # makes at this point (model/tensorflow/model.py:167-169)
-        c = ConfigConnectN
-        np.random.rand(1, c.board_height, c.board_width, 4)
+        # makes at this point (model/tensorflow/model.py:167-169), whatever the
+        # game, so the stream after them -- chess's game seed below included --
+        # does not depend on whether a model was passed
+        np.random.rand(1, *input_dim())
     if ConfigMCTS.enable_dirichlet_noise and ConfigGeneral.game != "chess":
         # root noise draws from the game's own stream: the game runs on the
         # batched engine as game 0 of a one-game batch seeded like this

@@ -170,7 +170,9 @@ int az_engine_destroy(az_engine* eng);
 /* The number of slot groups (streams) the engine runs: az_config.lanes, or
  * for lanes = 0 the engine's choice -- 1 below 512 slots; 3 for 1536-4096
  * slots when the process has at least 8 HIP hardware queues
- * (GPU_MAX_HW_QUEUES: a queue per lane stream; configs[1] +4.9% games/s over
+ * (GPU_MAX_HW_QUEUES as the environment held it when libaz loaded -- HIP reads
+ * it once at its initialisation; the Python package sets 8 at import: a queue
+ * per lane stream; configs[1] +4.9% games/s over
  * 2); else 2. */
 int az_engine_lanes(const az_engine* eng);
 

@@ -13,7 +13,7 @@ int main() {
                       {1, 8, 4, 1}, {6, 7, 5, 1}, {2, 64, 4, 1}, {11, 11, 5, 0}, {4, 5, 6, 1}, {8, 16, 4, 0},
                       {16, 8, 9, 1}, {7, 6, 4, 0}};
   std::mt19937_64 rng(12345);
-  long checked = 0, bad = 0;
+  long checked = 0, checked_c64 = 0, bad = 0;
   for (const Cfg& cf : cfgs) {
     az::GameCfg g{};
     g.H = cf.H; g.W = cf.W; g.HW = cf.H * cf.W; g.n = cf.n; g.gravity = cf.gravity;
@@ -30,6 +30,15 @@ int main() {
             if (++bad < 10) printf("mismatch H=%d W=%d n=%d grav=%d ply=%d a=%d: %d vs %d\n", g.H, g.W, g.n,
                                    g.gravity, ply, a, s1, s2);
           }
+          // the compile-time one-word form the select descent uses for Connect-4
+          if (cf.H == 6 && cf.W == 7 && cf.n == 4 && cf.gravity) {
+            az::Board b3 = b;
+            const int s3 = az::play_c64<6, 7, 4>(b3, a);
+            ++checked_c64;
+            if (s1 != s3 || (s1 >= 0 && memcmp(&b1, &b3, sizeof(b1)) != 0)) {
+              if (++bad < 10) printf("play_c64 mismatch ply=%d a=%d: %d vs %d\n", ply, a, s1, s3);
+            }
+          }
         }
         int legal[az::kMaxActions], nl = 0;
         for (int a = 0; a < g.A; ++a) {
@@ -42,6 +51,6 @@ int main() {
       }
     }
   }
-  printf("play_bb: %ld actions checked, %ld mismatches\n", checked, bad);
+  printf("play_bb: %ld actions checked (%ld also by play_c64<6,7,4>), %ld mismatches\n", checked, checked_c64, bad);
   return bad ? 1 : 0;
 }

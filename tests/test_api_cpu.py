@@ -1,5 +1,8 @@
 """Host-side drop-in API (connect_n Board/Move, normalize_probabilities)
 against the reference's own outputs (golden vectors)."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -7,6 +10,8 @@ from custom_alphazero.config import ConfigConnectN
 from custom_alphazero.connect_n.board import Board
 from custom_alphazero.connect_n.move import Move
 from custom_alphazero.mcts.utils import normalize_probabilities
+
+PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "custom-alphazero_amd")
 
 
 @pytest.fixture
@@ -140,3 +145,20 @@ def test_root_noise_rows_are_numpys_dirichlet_draws():
         np.testing.assert_array_equal(rows[r, :5], rs.dirichlet(np.ones(5) * 0.03))
     assert not rows[:, 5:].any()
     assert root_noise_rows(np.random.RandomState(3), 5, 0, 7).shape == (1, 7)
+
+
+@pytest.mark.parametrize("env,want", [({}, "8"), ({"GPU_MAX_HW_QUEUES": "4"}, "8"),
+                                      ({"GPU_MAX_HW_QUEUES": "12"}, "12"),
+                                      ({"GPU_MAX_HW_QUEUES": "4", "AZ_KEEP_HW_QUEUES": "1"}, "4")])
+def test_package_import_sets_the_benched_hw_queues(env, want):
+    """Importing the package before HIP initialises gives the process the 8
+    hardware queues bench.py runs with (the engine's auto rule then picks 3
+    lanes at 1536-4096 slots, as in the bench line), unless the caller set
+    more or asked to keep its value."""
+    import subprocess
+    e = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "AZ_KEEP_HW_QUEUES")}
+    e.update(env)
+    code = ("import os, sys; sys.path.insert(0, %r); import custom_alphazero; "
+            "print(os.environ['GPU_MAX_HW_QUEUES'])" % PKG)
+    out = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == want

@@ -293,3 +293,14 @@ def test_load_with_meta_accepts_reference_hash(tmp_path, game_cfg, golden):
     meta = json.loads((tmp_path / ConfigPath.model_meta).read_text())
     assert meta["hash"] == int(case["hash"]) and meta["content_hash"] == m.content_hash
     m.load_with_meta(str(tmp_path))
+
+
+def test_play_engine_runs_the_benched_lanes():
+    """The drop-in play()'s engine at configs[1]'s 4096 slots runs the lane
+    count bench.py reports: the package import gave the process the 8 HIP
+    hardware queues bench.py asks for, so the auto rule picks 3 lanes
+    (VERDICT r5 item 6)."""
+    import os
+    assert int(os.environ["GPU_MAX_HW_QUEUES"]) >= 8
+    eng = self_play._batched_engine(SyntheticEvaluator(), 4096, sims=4)
+    assert eng.lanes == 3

@@ -21,3 +21,4 @@ def test_play_bb_matches_play(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 mismatches" in out.stdout
+    assert "(0 also" not in out.stdout  # the one-word Connect-4 form (play_c64) was checked too

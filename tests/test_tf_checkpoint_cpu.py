@@ -87,6 +87,33 @@ def test_checkpoint_string_entry_carries_the_tensorflow_crc(tmp_path):
     assert T.read_checkpoint(prefix)[T.OBJECT_GRAPH_KEY] == g
 
 
+def test_legacy_string_layout_still_loads(tmp_path):
+    """A checkpoint written by this package's round-3/4 writer: the
+    string tensor's masked crc32c covers the lengths' VARINT bytes and its
+    entry crc32c is crc32c of the raw bytes.  Hand-assembled here (a 200-byte
+    object graph: the varint and uint32 forms differ) and read back whole."""
+    g = bytes(range(200))
+    lens = bytes([0xC8, 0x01])
+    raw = lens + struct.pack("<I", _mask_hand(_crc32c_bitwise(lens))) + g
+    assert T._decode_strings(raw, ()) == (g, _crc32c_bitwise(raw))
+    prefix = str(tmp_path / "model")
+    v = np.arange(3, dtype=np.float32)
+    with open(prefix + T.DATA_SUFFIX, "wb") as f:
+        f.write(raw + v.tobytes())
+    entries = [(T.OBJECT_GRAPH_KEY.encode(), T._entry_proto(T.DT_STRING, (), 0, len(raw), _crc32c_bitwise(raw))),
+               (b"v", T._entry_proto(T.NP_DT[v.dtype], v.shape, len(raw), v.nbytes, _crc32c_bitwise(v.tobytes())))]
+    header = T._pb_varint(1, 1) + T._pb_bytes(3, T._pb_varint(1, 1))
+    T.write_table(prefix + ".index", [(b"", header)] + sorted(entries))
+    out = T.read_checkpoint(prefix)
+    assert out[T.OBJECT_GRAPH_KEY] == g
+    np.testing.assert_array_equal(out["v"], v)
+    # a corrupted legacy entry still fails, naming both layouts
+    bad = bytearray(raw)
+    bad[2] ^= 1
+    with pytest.raises(ValueError, match="legacy"):
+        T._decode_strings(bytes(bad), ())
+
+
 def test_snappy_literals_and_overlapping_copies():
     # "abcd" literal, then a 1-byte-offset copy of 8 from offset 4 (overlaps
     # its own output), then a 2-byte-offset copy of 3 from offset 12
