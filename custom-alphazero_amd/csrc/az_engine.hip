@@ -674,6 +674,37 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
         tn.slot_pix = reinterpret_cast<const int*>(q);
       }
     }
+    // dual launches (tower16_dual_kernel): boards of 33-48 cells (Connect-4)
+    // in 128-row tiles of three may also run 96-row tiles of two, with a
+    // slot plan of their own, when a launch holds at most two boards per CU
+    // that the lanes' towers leave each other (2 * CUs / lanes: Connect-4 at
+    // configs[1], ~120 live boards per lane launch with the LRU cache, gains
+    // 4.4%; at 373 or 1113 boards the 96-row tiles lose 20%, profiles/r6/)
+    tn.alt_rows = 0;
+    tn.alt_slot_pix = nullptr;
+    tn.alt_skip[0] = tn.alt_skip[1] = 0;
+    tn.alt_max_boards = -1;
+    if (!rows_tower && tn.tile_rows == 128 && tn.dbuf && tower16_boards_per_tile(HW, 128) == 3 &&
+        tower16_boards_per_tile(HW, 96) == 2 && tower16_heads_fit(HW, 96, A, net.hidden, true)) {
+      int dev = 0, cus = 0;
+      AZ_HIP(hipGetDevice(&dev));
+      AZ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      tn.alt_rows = 96;
+      tn.alt_max_boards = 2 * std::max(1, cus / std::max(1, net.lanes));
+      std::vector<int> pix;
+      int skip[2] = {0, 0};
+      if (!net.tower_natural_order && net.board_h * net.board_w == HW)
+        tower16_slot_plan(net.board_h, net.board_w, 96, pix, skip);
+      tn.alt_skip[0] = skip[0];
+      tn.alt_skip[1] = skip[1];
+      if (!pix.empty()) {
+        void* q = nullptr;
+        AZ_HIP(hipMalloc(&q, pix.size() * sizeof(int)));
+        owned.push_back(q);
+        AZ_HIP(hipMemcpy(q, pix.data(), pix.size() * sizeof(int), hipMemcpyHostToDevice));
+        tn.alt_slot_pix = reinterpret_cast<const int*>(q);
+      }
+    }
     tn.depth = net.depth;
     tn.hidden = net.hidden;
     if (!net.tower) {
@@ -691,6 +722,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     net.tower_staged = tn.staged_floats;
     net.tower_dbuf = tn.dbuf != 0;
     net.tower_rows = tn.tile_rows;
+    net.tower_alt_rows = tn.alt_rows;
     // (chess: as self-play runs it, the stem's known-zero input chunks 0-1 skipped)
     net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip, rows_tower, 2);
   }
@@ -934,6 +966,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
           return cleanup(fail(AZ_E_HIP, "hipEventCreate failed"));
     }
   }
+  e->net.lanes = (int)e->lanes.size();  // (the tower's dual-launch threshold, load_network)
   if (g.halves > 1)  // pooled arenas, one pool per lane (whose indices stay below 2^31)
     for (Lane* L : e->lanes)
       if ((rc = alloc_pool(e, L, std::min<int64_t>((int64_t)g.arena_cap * L->n, (1ll << 31) - 1))))

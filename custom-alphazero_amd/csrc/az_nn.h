@@ -41,6 +41,13 @@ struct TowerNet {
   // skips (2 bits per tap over the wave's blocks 0 and 1)
   const int* slot_pix;
   int skip[2];
+  // dual launches (tower16_dual_kernel): an alternative, shorter tile height
+  // for launches of at most alt_max_boards live boards, with its own slot
+  // plan (0 / null: one tile height)
+  int alt_rows;
+  const int* alt_slot_pix;
+  int alt_skip[2];
+  int alt_max_boards;
 };
 // the slot plan of 128-row tiles: border blocks (16 slots whose pixels all
 // sit on one board edge) skip the three taps that read past that edge; empty
@@ -68,9 +75,10 @@ constexpr size_t kTowerLdsMax = 160 * 1024;
 void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out);
 // boards (self-play: the eval queue's boards) or x ([n][HW][4] one-hot planes,
 // az_forward) -> probs [n][A], values [n]; count (device, may be null -> n_max)
-void launch_tower16(const TowerNet* net, int tile_rows, int staged_floats, bool dbuf, const Board* boards, const float4* x, const int* count,
-                    int n_max, int H, int W, int A, float* probs, float* values, unsigned long long* err,
-                    hipStream_t s);
+// alt_rows: the TowerNet's alternative tile height (a dual launch), 0 = none
+void launch_tower16(const TowerNet* net, int tile_rows, int alt_rows, int staged_floats, bool dbuf, const Board* boards,
+                    const float4* x, const int* count, int n_max, int H, int W, int A, float* probs, float* values,
+                    unsigned long long* err, hipStream_t s);
 // the input-row form (chess): rows [n][HW] of 512 B split16 (t0 of F
 // channels, t1 x 2^12; az_nn's store_act4) -> the stem, the residual tower
 // and the heads' 1x1 convs; per pixel float4 (relu(p0), relu(p1), relu(v), 0)
@@ -105,6 +113,8 @@ struct NetDev {
   int tower_staged = 0;       // its blob floats staged in LDS
   bool tower_dbuf = false;    // its activations double-buffered (TowerNet::dbuf)
   int tower_rows = 0;         // its tile rows (TowerNet::tile_rows)
+  int tower_alt_rows = 0;     // the dual launch's alternative tile rows (TowerNet::alt_rows; 0 none)
+  int lanes = 1;              // the engine's lanes (streams whose towers share the CUs): the dual threshold
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   int board_h = 0, board_w = 0;  // Connect-N board (the tower's slot plan)
   double issued_flop_per_board = 0;  // MFMA FLOP a forward issues per board (tower; az_stats)

@@ -634,17 +634,12 @@ __device__ __forceinline__ void dma_to_lds(uint4* dst, const float* src, int n_u
 // convs (per pixel float4 features into feat) -- the dense heads (1880
 // logits) run in their own kernels
 template <int MBT, int NWM, bool ROWS, bool DB>
-__global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet* __restrict__ net,
-                                                               const Board* __restrict__ boards,
-                                                               const float4* __restrict__ x,
-                                                               const uint4* __restrict__ rows,
-                                                               const int* __restrict__ count, int n_static,
-                                                               int H, int W, int A, int bpw,
-                                                               float* __restrict__ probs,
-                                                               float* __restrict__ values,
-                                                               float4* __restrict__ feat, int first_chunk,
-                                                               unsigned long long* __restrict__ err,
-                                                               TowerLeaves lv) {
+__device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, const Board* __restrict__ boards,
+                                             const float4* __restrict__ x, const uint4* __restrict__ rows,
+                                             int n, int H, int W, int A, int bpw, float* __restrict__ probs,
+                                             float* __restrict__ values, float4* __restrict__ feat,
+                                             int first_chunk, unsigned long long* __restrict__ err,
+                                             TowerLeaves lv) {
   constexpr int MBW = MBT / NWM;  // M blocks per wave
   constexpr int TR = 16 * MBT;    // tile rows
   constexpr int NT = NWM * 256;
@@ -664,7 +659,6 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   float* blob = reinterpret_cast<float*>(&sm + 1);  // the staged small weights (TowerNet::blob prefix)
 
   const int HW = H * W;
-  const int n = count ? *count : n_static;
   const int b0 = blockIdx.x * bpw;
   if (b0 >= n) return;  // block-uniform
   const int nbrd = min(bpw, n - b0);
@@ -686,11 +680,13 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   int yx[MBW];
   // (the plan is for the TowerNet's tile height: a smaller tile of the same
   // boards -- chess's 64-row tiles -- runs in natural order, the same bits)
-  const bool planned = 16 * MBT == T.tile_rows;
+  // (the alternative tile height of a dual launch has a plan of its own)
+  const bool alt = 16 * MBT != T.tile_rows && 16 * MBT == T.alt_rows;
+  const bool planned = 16 * MBT == T.tile_rows || alt;
   // wv1 staged behind X's dead tile only in the tile height it was sized for
-  // (tower16_wv1_xtile_fits); a smaller tile reads it from L2
+  // (tower16_wv1_xtile_fits); another tile height reads it from L2
   const bool wv1_xt = T.wv1_xtile && 16 * MBT == T.tile_rows;
-  const int* plan = planned ? T.slot_pix : nullptr;
+  const int* plan = !planned ? nullptr : alt ? T.alt_slot_pix : T.slot_pix;
   T16_STAMP(56);
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb) {
@@ -708,7 +704,7 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   // this wave's tap skips (2 bits per tap over its blocks 0 and 1)
   // (chess's 64-row tiles never run the plan: a compile-time 0 there, so
   // each tap compiles to one body instead of three)
-  const int skw = (ROWS && 16 * MBT != 128) ? 0 : planned ? T.skip[mh] : 0;
+  const int skw = (ROWS && 16 * MBT != 128) ? 0 : !planned ? 0 : alt ? T.alt_skip[mh] : T.skip[mh];
   const int cq0 = 8 * nq + gq;  // channel quad of a lane's N block 0 (block 1: + 4)
   // double-buffered: one accumulator set (conv2 runs the block's 1x1
   // projection residual first, from X, which nothing overwrites before its
@@ -1207,6 +1203,51 @@ __global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet*
   T16_RSTAMP(23);
 }
 
+template <int MBT, int NWM, bool ROWS, bool DB>
+__global__ __launch_bounds__(NWM * 256, NWM) void tower16_kernel(const TowerNet* __restrict__ net,
+                                                               const Board* __restrict__ boards,
+                                                               const float4* __restrict__ x,
+                                                               const uint4* __restrict__ rows,
+                                                               const int* __restrict__ count, int n_static,
+                                                               int H, int W, int A, int bpw,
+                                                               float* __restrict__ probs,
+                                                               float* __restrict__ values,
+                                                               float4* __restrict__ feat, int first_chunk,
+                                                               unsigned long long* __restrict__ err,
+                                                               TowerLeaves lv) {
+  tower16_tile<MBT, NWM, ROWS, DB>(net, boards, x, rows, count ? *count : n_static, H, W, A, bpw, probs, values,
+                                   feat, first_chunk, err, lv);
+}
+
+// One launch, two tile heights, chosen on the device by the live board count
+// (the host enqueues the launch before the select that fills the queue has
+// run): a launch of at most T.alt_max_boards boards runs the alternative,
+// shorter tiles (Connect-4: 96 rows of two boards instead of 128 rows of
+// three -- 3 M blocks per wave instead of 4, so a tile's latency drops by a
+// quarter), a larger one the primary tiles (fewer weight passes; the
+// shorter tiles' 1.5x tiles would outnumber the CUs).  With the LRU
+// transposition cache a Connect-4 lane evaluates ~120 boards per simulation
+// and the step is bound by each lane's chain of launches: +4.4% games/s
+// (profiles/r6/ab_t96.txt); at 373 / 1113 boards the shorter tiles lose 20%
+// (ab_t96off.txt, ab_t96s400.txt).  Grid: the alternative's tiles; the
+// primary's blocks past its tiles leave at once.  Every board's outputs are
+// the same bits in either tile (batch invariance, the slot plans' bitwise
+// order).
+template <int MBT, int MBT2, bool DB>
+__global__ __launch_bounds__(512, 2) void tower16_dual_kernel(const TowerNet* __restrict__ net,
+                                                              const Board* __restrict__ boards,
+                                                              const float4* __restrict__ x,
+                                                              const int* __restrict__ count, int n_static,
+                                                              int H, int W, int A, int bpw, int bpw2,
+                                                              float* __restrict__ probs, float* __restrict__ values,
+                                                              unsigned long long* __restrict__ err) {
+  const int n = count ? *count : n_static;
+  if (n <= net->alt_max_boards)  // uniform over the launch
+    tower16_tile<MBT2, 2, false, DB>(net, boards, x, nullptr, n, H, W, A, bpw2, probs, values, nullptr, 0, err, {});
+  else
+    tower16_tile<MBT, 2, false, DB>(net, boards, x, nullptr, n, H, W, A, bpw, probs, values, nullptr, 0, err, {});
+}
+
 }  // namespace
 
 #ifdef AZ_T16_STAMPS
@@ -1457,10 +1498,24 @@ static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* 
                                      first_chunk, err, s, lv);
 }
 
-void launch_tower16(const TowerNet* net, int tile_rows, int staged, bool dbuf, const Board* boards, const float4* x,
-                    const int* count, int n_max, int H, int W, int A, float* probs, float* values,
+void launch_tower16(const TowerNet* net, int tile_rows, int alt_rows, int staged, bool dbuf, const Board* boards,
+                    const float4* x, const int* count, int n_max, int H, int W, int A, float* probs, float* values,
                     unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
+  if (tile_rows == 128 && alt_rows == 96 && dbuf) {  // Connect-4: 96- or 128-row tiles by the live count
+    const int bpw = tower16_boards_per_tile(H * W, 128), bpw2 = tower16_boards_per_tile(H * W, 96);
+    const int grid = (n_max + bpw2 - 1) / bpw2;
+    const size_t bytes = tower16_lds_bytes(H * W, 128, staged, true);  // the larger layout
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_dual_kernel<8, 6, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTowerLdsMax);
+      attr = true;
+    }
+    tower16_dual_kernel<8, 6, true><<<grid, 512, bytes, s>>>(net, boards, x, count, n_max, H, W, A, bpw, bpw2, probs,
+                                                             values, err);
+    return;
+  }
   if (tile_rows == 192)  // in place only (two 192-row tiles exceed the LDS)
     launch_db<12, 2, false, false>(net, staged, boards, x, nullptr, count, n_max, H, W, A, probs, values, nullptr, 0,
                                    err, s);

@@ -17,9 +17,15 @@ int main() {
   bool first = true;
   printf("[");
   for (int H = 3; H <= 11; ++H)
-    for (int W = 3; W <= 11; ++W) {
-      const int HW = H * W, tr = az::tower16_tile_rows(HW);
-      if (!tr) continue;
+    for (int W = 3; W <= 11; ++W)
+      for (int alt = 0; alt < 2; ++alt) {
+      // alt: the dual launch's 96-row tiles of two boards beside 128-row tiles
+      // of three (round 6, Connect-4's shape class)
+      const int HW = H * W, tr0 = az::tower16_tile_rows(HW);
+      const bool dual = tr0 == 128 && az::tower16_boards_per_tile(HW, 128) == 3 &&
+                        az::tower16_boards_per_tile(HW, 96) == 2;
+      if (!tr0 || (alt && !dual)) continue;
+      const int tr = alt ? 96 : tr0;
       const int nb = az::tower16_boards_per_tile(HW, tr), half = tr / 32;
       std::vector<int> pix;
       int skip[2];
@@ -63,9 +69,9 @@ int main() {
             for (int r = 0; r < 8; ++r) conflicts += cnt[r] > 1 ? cnt[r] - 1 : 0;
           }
       }
-      printf("%s{\"H\": %d, \"W\": %d, \"tile_rows\": %d, \"boards\": %d, \"plan\": %d, \"dup\": %d, "
+      printf("%s{\"H\": %d, \"W\": %d, \"tile_rows\": %d, \"alt\": %d, \"boards\": %d, \"plan\": %d, \"dup\": %d, "
              "\"missing\": %d, \"bad\": %d, \"pads\": %d, \"skipped_block_taps\": %d, \"conflicts\": %d}",
-             first ? "" : ",\n", H, W, tr, nb, (int)!pix.empty(), dup, missing, bad_skip, pads, skipped, conflicts);
+             first ? "" : ",\n", H, W, tr, alt, nb, (int)!pix.empty(), dup, missing, bad_skip, pads, skipped, conflicts);
       first = false;
     }
   printf("]\n");

@@ -477,6 +477,22 @@ def test_forward_is_batch_invariant(conv_algo):
         np.testing.assert_array_equal(v, v_all[lo:hi])
 
 
+def test_tower_dual_launch_tiles_are_bitwise_equal():
+    """Connect-4's dual tower launch (round 6, tower16_dual_kernel) runs
+    96-row tiles of two boards when a launch holds at most 2 * CUs / lanes
+    boards and 128-row tiles of three above: a board's outputs are the same
+    bits either way (and within NET_TOL of the float64 restatement)."""
+    eng, w = make_net_engine(slots=1024, conv_algo=az.CONV_F16X2, lanes=1)  # one lane: 96-row up to 512
+    rng = np.random.RandomState(5)
+    x = oracle.full_state(random_boards(rng, 900, 6, 7))
+    p_big, v_big = eng.forward(x)            # 900 boards: 128-row tiles
+    p_small, v_small = eng.forward(x[:301])  # 301 boards: 96-row tiles (one half-full)
+    np.testing.assert_array_equal(p_small, p_big[:301])
+    np.testing.assert_array_equal(v_small, v_big[:301])
+    rp, rv = keras_ref.forward(w, x[:301], depth=4)
+    assert np.abs(p_small - rp).max() < NET_TOL and np.abs(v_small - rv).max() < NET_TOL
+
+
 @pytest.mark.parametrize("cache_log2,lanes", [(0, 1), (18, 1), (18, 2)])
 def test_selfplay_network_replays_on_oracle(cache_log2, lanes):
     """Device self-play with the real network: the oracle, fed the engine's

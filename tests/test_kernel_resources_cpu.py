@@ -48,6 +48,9 @@ def test_tower_kernel_register_budget(tmp_path):
     inplace = [v for k, v in spills.items() if "tower16_kernel" in k and "Lb0EEEv" in k and "ILi12E" not in k]
     t192 = [v for k, v in spills.items() if "tower16_kernelILi12ELi2ELb0ELb0E" in k]
     rows64 = [v for k, v in spills.items() if "tower16_kernelILi4ELi2ELb1ELb1E" in k]
+    # round 6: Connect-4's dual launch (128- or 96-row tiles by the live count)
+    dual = [v for k, v in spills.items() if "tower16_dual_kernelILi8ELi6ELb1E" in k]
+    assert dual and dual[0] == 0, spills
     assert t128 and t96 and rows and rows64 and t192 and len(inplace) == 4, spills
     assert t128[0] == 0 and t96[0] == 0 and rows[0] == 0 and rows64[0] == 0, spills  # the forms every config runs
     assert max(inplace) <= 8, spills  # the in-place fallback (LDS too small for two tiles)
@@ -93,8 +96,9 @@ def test_kloop_asm_invariants(tmp_path):
          os.path.join(CSRC, "az_tower16.hip"), "-o", str(s_file)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = s_file.read_text().split("\n")
-    starts = [i for i, l in enumerate(lines) if re.match(r"^_ZN2az12_GLOBAL__N_114tower16_kernel\S*:", l)]
-    assert len(starts) == 9
+    starts = [i for i, l in enumerate(lines)
+              if re.match(r"^_ZN2az12_GLOBAL__N_1(14tower16_kernel|19tower16_dual_kernel)\S*:", l)]
+    assert len(starts) == 10  # 9 tower16_kernel forms + Connect-4's dual launch (round 6)
     groups_seen = 0
     for st in starts:
         en = next(i for i in range(st, len(lines)) if lines[i].startswith(".Lfunc_end"))
