@@ -103,6 +103,8 @@ def parse():
                     help="1: reclaim the subtrees a game has left after every move (az_config.compact)")
     ap.add_argument("--no-cache-window", action="store_true",
                     help="skip the second timed window with the cache bypassed")
+    ap.add_argument("--max-plies", type=int, default=512,
+                    help="chess: games stop (as draws) after this many plies (the engine's cap; the reference has none)")
     ap.add_argument("--share-devices", action="store_true",
                     help="rehearsal: allow more ranks than visible GPUs (ranks share devices; "
                          "the line reports shared_devices)")
@@ -439,30 +441,58 @@ def chess_main(args):
     dev_index, dev = _init_dist(args, world, local_rank)
     named, _flat = _device_weights(spec, host_w, rank, world, args, dev)
     eng = az.ChessEngine(mcts_iterations=args.sims, slots=args.slots, evaluator=az.EVAL_NETWORK,
-                         max_plies=512, depth=args.depth, device=dev_index, conv_algo=args.conv_algo,
+                         max_plies=args.max_plies, depth=args.depth, device=dev_index, conv_algo=args.conv_algo,
                          lanes=args.lanes)
     eng.set_weights(named)
     budget = args.slots * 2
     eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)
     eng.selfplay_step(args.warmup)
+    eng.selfplay_drain()  # (games the untimed moves finished: not the window's)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     eng.timer(True)
     st0 = eng.stats()
     t0 = time.perf_counter()
-    eng.selfplay_step(args.steps)
+    # as the Connect-N window: enqueue move m, then copy to the host the games
+    # move m-1 finished (az_chess_selfplay_drain never waits for the running move)
+    parts = []
+    for _ in range(args.steps):
+        eng.selfplay_step(1, sync=False)
+        parts.append(eng.selfplay_drain())
     torch.cuda.synchronize()
+    parts.append(eng.selfplay_drain())
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st1 = check_device(eng, "the timed window")
     eng.timer(False)
+    window = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    drained = len(window["lengths"])
+    # ---- N>1: the window's chess games to rank 0 (replay-buffer gather; a
+    # chess game outlasts a short window, so often none -- the path runs anyway)
+    gather = None
+    if world > 1:
+        from custom_alphazero import distributed as D
+        t_g = time.perf_counter()
+        gstats = {}
+        gg = D.gather_games(window, device=None if args.dist_backend == "gloo" else dev, stats=gstats)
+        gt = time.perf_counter() - t_g
+        if rank == 0:
+            gather = {"games": int(len(gg["lengths"])), "samples": int(len(gg["moves"])),
+                      "policy_entries": int(len(gg["policy_actions"])), "bytes": gstats["wire_bytes"],
+                      "bytes_note": "what rank 0 received from the other ranks (its own games stay put)",
+                      "seconds": round(gt, 4),
+                      "how": f"compact chess records (80-byte positions, u16 moves, sparse root policies: "
+                             f"distributed.pack_chess) + per-game counts; a gather of the sizes, then each rank "
+                             f"sends its blob to rank 0 only (point-to-point over {args.dist_backend}) after "
+                             f"the timed window"}
     d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
                                       "terminal_visits", "evaluations")}
     local_evals = d["evaluations"]
-    g, e, s, p, ev = _reduce([d["games_done"], d["expansions"], d["simulations"], d["plies"],
-                              d["evaluations"]], dist.ReduceOp.SUM if world > 1 else None, world, args, dev)
+    g, e, s, p, ev, dr = _reduce([d["games_done"], d["expansions"], d["simulations"], d["plies"],
+                                  d["evaluations"], drained], dist.ReduceOp.SUM if world > 1 else None, world,
+                                 args, dev)
     (elapsed,) = _reduce([elapsed], dist.ReduceOp.MAX if world > 1 else None, world, args, dev)
     F, HW = 128, 64
     direct_flop = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
@@ -506,6 +536,10 @@ def chess_main(args):
             "simulations_per_s": round(s / elapsed, 1),
             "network_evaluations_per_s": round(ev / elapsed, 1),
             "games_timed": int(g),
+            "games_drained": int(dr),
+            "games_drained_basis": "games whose records reached the host in the window (az_chess_selfplay_drain "
+                                   "after every asynchronous step, and once more after the final synchronize)",
+            "replay_buffer_gather": gather,
             "lanes": args.lanes or "auto",
             "roofline": roof,
             "cpu_baseline": base,

@@ -90,6 +90,8 @@ struct CSamples {
   int32_t* result = nullptr;
   int32_t* term = nullptr;
   int32_t* expansions = nullptr;
+  int64_t* done_ids = nullptr;                 // [G] game ids in the order they finished
+  unsigned long long* done_count = nullptr;    // [1] (az_chess_selfplay_drain)
 };
 
 // MCTS.play through the tree API (az_chess_tree_play); all null/-1 in self-play
@@ -679,6 +681,11 @@ __global__ __launch_bounds__(64) void play_kernel(CCfg g, CTree t, CSamples smp,
       smp.result[gi] = done_code == AZ_CHESS_CHECKMATE ? 1 : 0;
       smp.term[gi] = done_code;
       smp.expansions[gi] = t.slot_exp[s];
+      // the drain's finish-order list (its records are complete: stored above)
+      if (smp.done_ids) {
+        __threadfence();
+        smp.done_ids[atomicAdd(smp.done_count, 1ull)] = smp.first_game + gi;
+      }
     }
     atomicAdd(t.stats + az::kStatGamesDone, 1ull);
     const unsigned long long next = atomicAdd(t.stats + az::kStatNextGame, 1ull);
@@ -715,6 +722,7 @@ struct CLane {
   int32_t* counts = nullptr;  // [2] the eval queue counters, alternating by simulation
   int par = 0;
   bool pending_expand = false;  // the last simulation's expand not launched yet
+  hipEvent_t move_done[4] = {nullptr, nullptr, nullptr, nullptr};  // move m's end on this lane (m % 4)
 };
 
 struct az_chess_engine {
@@ -734,6 +742,15 @@ struct az_chess_engine {
   float* values = nullptr;
   std::vector<void*> owned, sample_bufs;
   int64_t sp_n = 0;
+  // asynchronous steps + drain (ABI 10), as the Connect-N engine: per move m
+  // the last lane to finish it stores the games-finished count into pinned
+  // snap_host[m % 4] (az::launch_move_end); the drain copies the games of the
+  // newest move whose snapshot is complete on pack_stream
+  int64_t moves_issued = 0, batch_first_move = 0, drained = 0;
+  int32_t* move_arrive = nullptr;           // device [4]
+  unsigned long long* snap_dev = nullptr;   // pinned [4] (device view)
+  unsigned long long* snap_host = nullptr;  // its host view
+  hipStream_t pack_stream = nullptr;
   // tree API staging (allocated on first use)
   double* tree_u = nullptr;
   int32_t *tree_move = nullptr, *tree_status = nullptr, *tree_pol_n = nullptr, *tree_slots = nullptr;
@@ -983,7 +1000,18 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
     e->lanes.push_back(L);
     const int lo = (int)((int64_t)g.slots * l / nl), hi = (int)((int64_t)g.slots * (l + 1) / nl);
     if ((rc = make_lane(e, L, lo, hi - lo))) return cleanup(rc);
+    for (hipEvent_t& ev : L->move_done)
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+        return cleanup(az::fail_abi(AZ_E_HIP, "hipEventCreate failed"));
   }
+  // the drain's move snapshots (pinned, coherent) and its own stream
+  if ((rc = e->alloc(&e->move_arrive, 4))) return cleanup(rc);
+  if (hipMemset(e->move_arrive, 0, 4 * sizeof(int32_t)) != hipSuccess ||
+      hipHostMalloc(&e->snap_host, 4 * sizeof(unsigned long long), hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&e->snap_dev, e->snap_host, 0) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->pack_stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(az::fail_abi(AZ_E_HIP, "drain snapshot allocation failed"));
+  for (int i = 0; i < 4; ++i) e->snap_host[i] = 0;
   *out = e;
   return 0;
 }
@@ -997,8 +1025,15 @@ int az_chess_engine_destroy(az_chess_engine* e) {
       (void)hipStreamSynchronize(L->stream);
       (void)hipStreamDestroy(L->stream);
     }
+    for (hipEvent_t ev : L->move_done)
+      if (ev) (void)hipEventDestroy(ev);
     delete L;
   }
+  if (e->pack_stream) {
+    (void)hipStreamSynchronize(e->pack_stream);
+    (void)hipStreamDestroy(e->pack_stream);
+  }
+  if (e->snap_host) (void)hipHostFree(e->snap_host);
   for (void* p : e->sample_bufs) (void)hipFree(p);
   for (void* p : e->owned) (void)hipFree(p);
   if (e->timer_ref) (void)hipEventDestroy(e->timer_ref);
@@ -1068,8 +1103,12 @@ int az_chess_selfplay_begin(az_chess_engine* e, int64_t first_game, int64_t n_ga
       (rc = get((void**)&smp.pol_a, G * P * M * sizeof(int16_t))) ||
       (rc = get((void**)&smp.pol_p, G * P * M * sizeof(double))) ||
       (rc = get((void**)&smp.length, G * sizeof(int32_t))) || (rc = get((void**)&smp.result, G * sizeof(int32_t))) ||
-      (rc = get((void**)&smp.term, G * sizeof(int32_t))) || (rc = get((void**)&smp.expansions, G * sizeof(int32_t))))
+      (rc = get((void**)&smp.term, G * sizeof(int32_t))) || (rc = get((void**)&smp.expansions, G * sizeof(int32_t))) ||
+      (rc = get((void**)&smp.done_ids, G * sizeof(int64_t))) ||
+      (rc = get((void**)&smp.done_count, sizeof(unsigned long long))))
     return rc;
+  e->drained = 0;
+  e->batch_first_move = e->moves_issued;
   unsigned long long st[az::kStatCount] = {0};
   const int64_t first_wave = std::min<int64_t>(n_games, e->g.slots);
   st[az::kStatNextGame] = (unsigned long long)(first_game + first_wave);
@@ -1128,21 +1167,97 @@ int az_chess_stats(az_chess_engine* e, az_stats* st) {
 
 int az_chess_selfplay_step(az_chess_engine* e, int n_moves, az_stats* st) {
   if (!e || n_moves < 0) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  if (!e->smp.done_count) return az::fail_abi(AZ_E_STATE, "az_chess_selfplay_begin was not called");
   AZC_HIP(hipSetDevice(e->device));
   int rc;
+  const bool multi = e->lanes.size() > 1;
   for (int mv = 0; mv < n_moves; ++mv) {
+    const int64_t m = e->moves_issued++;
     // lanes interleaved per simulation so every stream always has work queued
     for (int s = 0; s < e->g.sims; ++s)
       for (CLane* L : e->lanes)
         if ((rc = simulate(e, *L))) return rc;
     for (CLane* L : e->lanes)
       if ((rc = flush_expand(*L))) return rc;
-    for (CLane* L : e->lanes) play_kernel<<<L->g.slots, 64, 0, L->stream>>>(L->g, L->t, e->smp, CPlayOut{});
+    for (CLane* L : e->lanes) {
+      // a lane plays move m once every other lane has finished move m - 1, so
+      // move m - 1's games-finished snapshot holds no game of move m (the
+      // drain's contract, as the Connect-N engine's)
+      if (multi && m > e->batch_first_move)
+        for (CLane* O : e->lanes)
+          if (O != L) AZC_HIP(hipStreamWaitEvent(L->stream, O->move_done[(m - 1) % 4], 0));
+      play_kernel<<<L->g.slots, 64, 0, L->stream>>>(L->g, L->t, e->smp, CPlayOut{});
+      az::launch_move_end(e->move_arrive + m % 4, (int)e->lanes.size(), e->smp.done_count, e->snap_dev + m % 4,
+                          L->stream);
+      AZC_HIP(hipEventRecord(L->move_done[m % 4], L->stream));
+    }
     AZC_HIP(hipGetLastError());
   }
+  if (!st) return 0;  // asynchronous (ABI 10): the moves run on while the caller drains earlier ones
   if ((rc = sync_lanes(e))) return rc;
   if ((rc = check_errors(e))) return rc;
-  if (st) return az_chess_stats(e, st);
+  return az_chess_stats(e, st);
+}
+
+int az_chess_selfplay_drain(az_chess_engine* e, int64_t max_games, int64_t* n_out, int64_t* game_ids,
+                            int32_t* lengths, int32_t* results, int32_t* terminations, int32_t* expansions,
+                            az_chess_pos* positions, uint16_t* moves, int32_t* policy_n, int16_t* policy_actions,
+                            double* policy_probs) {
+  if (!e || !n_out || max_games < 0) return az::fail_abi(AZ_E_INVALID, "bad arguments");
+  *n_out = 0;
+  if (!e->smp.done_count) return 0;  // no self-play batch begun
+  AZC_HIP(hipSetDevice(e->device));
+  // the newest move whose count snapshot is complete; if the last issued move
+  // is still running, wait for the one before it (never for the running one)
+  const int64_t last = e->moves_issued - 1;
+  int64_t k = -1;
+  bool last_done = last >= e->batch_first_move;
+  if (last_done)
+    for (CLane* L : e->lanes) last_done = last_done && hipEventQuery(L->move_done[last % 4]) == hipSuccess;
+  if (last_done) {
+    k = last;
+  } else if (last - 1 >= e->batch_first_move) {
+    k = last - 1;
+    for (CLane* L : e->lanes) AZC_HIP(hipEventSynchronize(L->move_done[k % 4]));
+  }
+  if (k < 0) return 0;
+  const unsigned long long done = __atomic_load_n(e->snap_host + k % 4, __ATOMIC_ACQUIRE);
+  const int64_t n = std::min<int64_t>((int64_t)done - e->drained, max_games);
+  if (n <= 0) return 0;
+  // the finished games' ids, then each game's records (complete once its id
+  // is listed: the play kernel stores them first); pack_stream holds nothing else
+  std::vector<int64_t> ids((size_t)n);
+  AZC_HIP(hipMemcpyAsync(ids.data(), e->smp.done_ids + e->drained, (size_t)n * sizeof(int64_t),
+                         hipMemcpyDeviceToHost, e->pack_stream));
+  AZC_HIP(hipStreamSynchronize(e->pack_stream));
+  const CSamples& s = e->smp;
+  const size_t P = (size_t)s.plies, M = AZ_CHESS_MAX_MOVES;
+  hipStream_t q = e->pack_stream;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t gi = ids[(size_t)i] - s.first_game;
+    if (gi < 0 || gi >= s.n_games) return az::fail_abi(AZ_E_STATE, "drained game id outside the batch");
+    if (game_ids) game_ids[i] = ids[(size_t)i];
+    if (lengths) AZC_HIP(hipMemcpyAsync(lengths + i, s.length + gi, sizeof(int32_t), hipMemcpyDeviceToHost, q));
+    if (results) AZC_HIP(hipMemcpyAsync(results + i, s.result + gi, sizeof(int32_t), hipMemcpyDeviceToHost, q));
+    if (terminations)
+      AZC_HIP(hipMemcpyAsync(terminations + i, s.term + gi, sizeof(int32_t), hipMemcpyDeviceToHost, q));
+    if (expansions)
+      AZC_HIP(hipMemcpyAsync(expansions + i, s.expansions + gi, sizeof(int32_t), hipMemcpyDeviceToHost, q));
+    if (positions)
+      AZC_HIP(hipMemcpyAsync(positions + i * P, s.pos + gi * P, P * sizeof(az_chess_pos), hipMemcpyDeviceToHost, q));
+    if (moves) AZC_HIP(hipMemcpyAsync(moves + i * P, s.moves + gi * P, P * sizeof(uint16_t), hipMemcpyDeviceToHost, q));
+    if (policy_n)
+      AZC_HIP(hipMemcpyAsync(policy_n + i * P, s.pol_n + gi * P, P * sizeof(int32_t), hipMemcpyDeviceToHost, q));
+    if (policy_actions)
+      AZC_HIP(hipMemcpyAsync(policy_actions + i * P * M, s.pol_a + gi * P * M, P * M * sizeof(int16_t),
+                             hipMemcpyDeviceToHost, q));
+    if (policy_probs)
+      AZC_HIP(hipMemcpyAsync(policy_probs + i * P * M, s.pol_p + gi * P * M, P * M * sizeof(double),
+                             hipMemcpyDeviceToHost, q));
+  }
+  AZC_HIP(hipStreamSynchronize(q));
+  e->drained += n;
+  *n_out = n;
   return 0;
 }
 

@@ -11,9 +11,11 @@ remain, both over torch.distributed ("nccl" = RCCL over xGMI on MI355X,
     best model from disk (utils.py:64-78);
   * gather_games: each rank's finished games to rank 0 only, in global game
     order (a gather of the sizes, then point-to-point sends to rank 0),
-    shipped compact (canonical int8 boards, float64 policies, int16 moves, one
-    result per game) and expanded to full_state only on rank 0 -- the
-    analogue of joblib's result return (self_play.py:112-118).
+    shipped compact -- Connect-N: canonical int8 boards, float64 policies,
+    int16 moves, one result per game; chess (BASELINE configs[4]): the 80-byte
+    positions, u16 moves and the sparse root policies (pack_chess) -- and
+    expanded to full_state only on rank 0: the analogue of joblib's result
+    return (self_play.py:112-118).
 Because a game's trajectory depends only on its seed (base_seed + game id)
 and the per-board evaluator, the gathered samples are identical for any
 number of ranks (tests/test_distributed_cpu.py).
@@ -67,7 +69,7 @@ def broadcast_weights(named: Sequence[Tuple[str, "object"]], device=None, src: i
 
 
 def _pack(results: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
-    """Per-rank engine results -> compact flat arrays."""
+    """Per-rank Connect-N engine results -> compact flat arrays."""
     lengths = results["lengths"].astype(np.int64)
     n = len(lengths)
     boards = np.concatenate([results["boards"][g, :lengths[g]] for g in range(n)]) \
@@ -81,23 +83,77 @@ def _pack(results: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
                 expansions=results["expansions"].astype(np.int64))
 
 
+POS_BYTES = 80  # sizeof(az_chess_pos), include/az_chess.h
+
+
+def pack_chess(results: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    """Per-rank chess engine results (ChessEngine.selfplay_results or
+    selfplay_drain: dense [game][max_plies] rows) -> the compact chess record:
+    per game its id, length, result, termination and expansions; per sample
+    (ply) the canonical root position's 80 bytes (az_chess_pos), the move
+    played and the root's edge count; per root edge its action index and
+    visit probability (the sparse MCTS.play policy, mcts.py:182-222) -- only
+    the plies each game played and the edges each root had."""
+    lengths = np.asarray(results["lengths"], np.int64)
+    n = len(lengths)
+    ids = np.asarray(results["game_ids"], np.int64) if "game_ids" in results else np.full(n, -1, np.int64)
+    pos = np.ascontiguousarray(results["positions"])
+    rows = [(g, int(lengths[g])) for g in range(n)]
+    positions = np.concatenate([pos[g, :T].view(np.uint8).reshape(T, POS_BYTES) for g, T in rows]) \
+        if n else np.zeros((0, POS_BYTES), np.uint8)
+    moves = np.concatenate([results["moves"][g, :T] for g, T in rows]).astype(np.uint16) \
+        if n else np.zeros(0, np.uint16)
+    pn = np.concatenate([results["policy_n"][g, :T] for g, T in rows]).astype(np.int64) \
+        if n else np.zeros(0, np.int64)
+    M = results["policy_actions"].shape[-1] if n else 1
+    if n:
+        pa = np.concatenate([results["policy_actions"][g, :T] for g, T in rows])
+        pp = np.concatenate([results["policy_probs"][g, :T] for g, T in rows])
+        keep = np.arange(M)[None, :] < pn[:, None]
+        actions, probs = pa[keep].astype(np.int16), pp[keep].astype(np.float64)
+    else:
+        actions, probs = np.zeros(0, np.int16), np.zeros(0, np.float64)
+    return dict(game_ids=ids, lengths=lengths, results=np.asarray(results["results"]).astype(np.int8),
+                terminations=np.asarray(results["terminations"]).astype(np.int8),
+                expansions=np.asarray(results["expansions"]).astype(np.int64), positions=positions,
+                moves=moves, policy_n=pn.astype(np.int16), policy_actions=actions, policy_probs=probs)
+
+
+# wire layouts: (field, dtype, leading axis: "games" | "samples" | "entries", trailing shape)
+_WIRE = {
+    "connect_n": [("lengths", np.int64, "games", ()), ("results", np.int8, "games", ()),
+                  ("expansions", np.int64, "games", ()), ("boards", np.int8, "samples", None),
+                  ("policies", np.float64, "samples", None), ("moves", np.int16, "samples", ())],
+    "chess": [("game_ids", np.int64, "games", ()), ("lengths", np.int64, "games", ()),
+              ("results", np.int8, "games", ()), ("terminations", np.int8, "games", ()),
+              ("expansions", np.int64, "games", ()), ("positions", np.uint8, "samples", (POS_BYTES,)),
+              ("moves", np.uint16, "samples", ()), ("policy_n", np.int16, "samples", ()),
+              ("policy_actions", np.int16, "entries", ()), ("policy_probs", np.float64, "entries", ())],
+}
+
+
 def gather_games(results: Dict[str, np.ndarray], device=None, dst: int = 0, stats=None):
     """Gather every rank's compact games to `dst` only: the per-rank sizes by
-    one `gather` of three int64s, then each other rank `send`s its byte blob
-    (exact length, no padding) and `dst` `recv`s them in rank order -- under
-    nccl both are RCCL point-to-point transfers between the ranks' GPUs over
-    xGMI; no rank but `dst` receives or holds another rank's games.  Returns
+    one `gather` of four int64s (bytes, games, samples, policy entries), then
+    each other rank `send`s its byte blob (exact length, no padding) and `dst`
+    `recv`s them in rank order -- under nccl both are RCCL point-to-point
+    transfers between the ranks' GPUs over xGMI; no rank but `dst` receives or
+    holds another rank's games.  Connect-N records (engine results: boards,
+    policies, moves) or chess records (ChessEngine results: positions,
+    sparse policies; pack_chess) -- every rank passes the same kind.  Returns
     the concatenated dict on `dst`, None elsewhere; `stats` (a dict) gets
     `wire_bytes`, the bytes `dst` received from the other ranks."""
     import torch
     import torch.distributed as dist
 
-    packed = _pack(results)
-    order = ("lengths", "results", "expansions", "boards", "policies", "moves")
-    blob = b"".join(np.ascontiguousarray(packed[k]).tobytes() for k in order)
+    kind = "chess" if "positions" in results else "connect_n"
+    packed = pack_chess(results) if kind == "chess" else _pack(results)
+    spec = _WIRE[kind]
+    blob = b"".join(np.ascontiguousarray(packed[k]).tobytes() for k, _, _, _ in spec)
+    n_entries = len(packed["policy_actions"]) if kind == "chess" else 0
     world, rank = dist.get_world_size(), dist.get_rank()
     device = collective_device(device)
-    sizes = torch.tensor([len(blob), len(packed["lengths"]), len(packed["moves"])], dtype=torch.int64,
+    sizes = torch.tensor([len(blob), len(packed["lengths"]), len(packed["moves"]), n_entries], dtype=torch.int64,
                          device=device)
     all_sizes = [torch.zeros_like(sizes) for _ in range(world)] if rank == dst else None
     dist.gather(sizes, gather_list=all_sizes, dst=dst)
@@ -117,18 +173,15 @@ def gather_games(results: Dict[str, np.ndarray], device=None, dst: int = 0, stat
         q.wait()
     if stats is not None:
         stats["wire_bytes"] = int(sum(all_sizes[r][0] for r in range(world) if r != dst))
-    board_shape = packed["boards"].shape[1:]
-    A = packed["policies"].shape[1]
+    trailing = {"boards": packed["boards"].shape[1:], "policies": packed["policies"].shape[1:]} \
+        if kind == "connect_n" else {}
     parts: List[Dict[str, np.ndarray]] = []
     for r in range(world):
         raw = blob if r == dst else (bufs[r].cpu().numpy().tobytes() if bufs[r] is not None else b"")
-        n_games, n_samples = all_sizes[r][1], all_sizes[r][2]
-        spec = [("lengths", np.int64, (n_games,)), ("results", np.int8, (n_games,)),
-                ("expansions", np.int64, (n_games,)),
-                ("boards", np.int8, (n_samples,) + tuple(board_shape)),
-                ("policies", np.float64, (n_samples, A)), ("moves", np.int16, (n_samples,))]
+        count = {"games": all_sizes[r][1], "samples": all_sizes[r][2], "entries": all_sizes[r][3]}
         off, part = 0, {}
-        for k, dt, shape in spec:
+        for k, dt, axis, tail in spec:
+            shape = (count[axis],) + tuple(trailing[k] if tail is None else tail)
             nbytes = int(np.prod(shape)) * np.dtype(dt).itemsize
             part[k] = np.frombuffer(raw[off:off + nbytes], dtype=dt).reshape(shape)
             off += nbytes
@@ -166,8 +219,12 @@ def selfplay_sharded(runner: Callable[[int, int, int], Dict[str, np.ndarray]], n
 
 
 def engine_runner(engine):
-    """Adapter: a custom_alphazero.engine.Engine as a selfplay_sharded runner."""
+    """Adapter: a custom_alphazero.engine.Engine (or ChessEngine) as a
+    selfplay_sharded runner (chess results carry their game ids)."""
     def run(first, count, base_seed):
         engine.selfplay_run(first, count, base_seed)
-        return engine.selfplay_results()
+        res = engine.selfplay_results()
+        if "positions" in res:
+            res["game_ids"] = first + np.arange(count, dtype=np.int64)
+        return res
     return run

@@ -102,7 +102,8 @@ EXPORTED = (
     "az_chess_all_moves", "az_chess_legal", "az_chess_encode", "az_chess_play", "az_chess_perft",
     "az_chess_engine_create", "az_chess_engine_destroy", "az_chess_engine_set_weights",
     "az_chess_forward", "az_chess_selfplay_begin", "az_chess_selfplay_step", "az_chess_selfplay_run",
-    "az_chess_selfplay_results", "az_chess_stats", "az_chess_timer_enable", "az_chess_tree_reset",
+    "az_chess_selfplay_results", "az_chess_selfplay_drain", "az_chess_stats", "az_chess_timer_enable",
+    "az_chess_tree_reset",
     "az_chess_tree_release", "az_chess_tree_search", "az_chess_tree_play", "az_chess_tree_info",
     "az_chess_tree_export",
 )
@@ -171,6 +172,7 @@ def load_library():
         "az_chess_selfplay_step": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(Stats)]),
         "az_chess_selfplay_run": (ctypes.c_int, [P, I64, I64, ctypes.c_uint32, ctypes.POINTER(Stats)]),
         "az_chess_selfplay_results": (ctypes.c_int, [P] + [P] * 9),
+        "az_chess_selfplay_drain": (ctypes.c_int, [P, I64, P] + [P] * 10),
         "az_chess_stats": (ctypes.c_int, [P, ctypes.POINTER(Stats)]),
         "az_chess_timer_enable": (ctypes.c_int, [P, ctypes.c_int]),
         "az_chess_tree_reset": (ctypes.c_int, [P, ctypes.c_int, P, P]),
@@ -539,10 +541,44 @@ class ChessEngine:
                                                int(base_seed) & 0xFFFFFFFF))
         self._n_games = int(n_games)
 
-    def selfplay_step(self, n_moves=1):
+    def selfplay_step(self, n_moves=1, sync=True):
+        """Enqueue n_moves moves for every slot; sync=False returns at once (no
+        stats) and selfplay_drain returns the games of the newest move whose
+        snapshot is complete (az_chess_selfplay_step with st = NULL, ABI 10)."""
+        if not sync:
+            _check(self._L.az_chess_selfplay_step(self._h, int(n_moves), None))
+            return None
         st = Stats()
         _check(self._L.az_chess_selfplay_step(self._h, int(n_moves), ctypes.byref(st)))
         return st.as_dict()
+
+    def selfplay_drain(self, max_games=None, chunk=64):
+        """Games finished since the previous drain (az_chess_selfplay_drain):
+        the arrays of selfplay_results with a leading axis over the drained
+        games in finish order, plus `game_ids`.  Chunked: a chess game's dense
+        rows are ~1.3 MB (max_plies x 256 policy entries)."""
+        from custom_alphazero.chess.kernels import POS_DTYPE
+        left = int(max_games if max_games is not None else max(self._n_games, 1))
+        P, M = self.max_plies, self.MAX_MOVES
+        keys = ("game_ids", "lengths", "results", "terminations", "expansions", "positions", "moves",
+                "policy_n", "policy_actions", "policy_probs")
+        parts = []
+        while left > 0:
+            G = min(chunk, left)
+            n = ctypes.c_int64(0)
+            out = dict(game_ids=np.zeros(G, np.int64), lengths=np.zeros(G, np.int32),
+                       results=np.zeros(G, np.int32), terminations=np.zeros(G, np.int32),
+                       expansions=np.zeros(G, np.int32), positions=np.zeros((G, P), POS_DTYPE),
+                       moves=np.zeros((G, P), np.uint16), policy_n=np.zeros((G, P), np.int32),
+                       policy_actions=np.zeros((G, P, M), np.int16),
+                       policy_probs=np.zeros((G, P, M), np.float64))
+            _check(self._L.az_chess_selfplay_drain(self._h, G, ctypes.byref(n), *(_ptr(out[k]) for k in keys)))
+            k = int(n.value)
+            parts.append({key: v[:k].copy() for key, v in out.items()})
+            left -= k
+            if k < G:
+                break
+        return {key: np.concatenate([p[key] for p in parts]) for key in keys}
 
     def selfplay_run(self, first_game, n_games, base_seed):
         st = Stats()

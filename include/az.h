@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define AZ_ABI_VERSION 9
+#define AZ_ABI_VERSION 10
 
 #define AZ_OK 0
 #define AZ_E_INVALID -1  /* bad argument / config */

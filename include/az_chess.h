@@ -137,6 +137,9 @@ int az_chess_forward(az_chess_engine* eng, const float* x, int n, float* probs, 
  * seeded with MT19937(base_seed + g); slots refilled as games end. */
 int az_chess_selfplay_begin(az_chess_engine* eng, int64_t first_game, int64_t n_games,
                             uint32_t base_seed);
+/* With st = NULL the moves are only enqueued (ABI 10): the call returns at once
+ * and device errors surface at the next synchronizing call; with st it waits
+ * for them and fills the stats. */
 int az_chess_selfplay_step(az_chess_engine* eng, int n_moves, az_stats* st);
 int az_chess_selfplay_run(az_chess_engine* eng, int64_t first_game, int64_t n_games,
                           uint32_t base_seed, az_stats* st);
@@ -150,6 +153,21 @@ int az_chess_selfplay_results(az_chess_engine* eng, int32_t* lengths, int32_t* r
                               int32_t* terminations, int32_t* expansions, az_chess_pos* positions,
                               uint16_t* moves, int32_t* policy_n, int16_t* policy_actions,
                               double* policy_probs);
+/* The games that finished since the previous drain (ABI 10; at most
+ * max_games, in the order they finished) while self-play runs on: the
+ * reference's result return (self_play.py:112-118), one step at a time, as
+ * az_selfplay_drain does for Connect-N.  *n_out = games copied; per game i:
+ * game_ids[i], lengths/results/terminations/expansions[i], and its rows as
+ * az_chess_selfplay_results: positions [i][P], moves [i][P], policy_n
+ * [i][P], policy_actions [i][P][AZ_CHESS_MAX_MOVES], policy_probs
+ * [i][P][AZ_CHESS_MAX_MOVES] (P = max_plies; rows past the game's length are
+ * zero).  "Finished" = by the end of the newest move whose games-finished
+ * snapshot is complete: the drain never waits for a running move.  Any
+ * output but n_out may be NULL. */
+int az_chess_selfplay_drain(az_chess_engine* eng, int64_t max_games, int64_t* n_out, int64_t* game_ids,
+                            int32_t* lengths, int32_t* results, int32_t* terminations, int32_t* expansions,
+                            az_chess_pos* positions, uint16_t* moves, int32_t* policy_n,
+                            int16_t* policy_actions, double* policy_probs);
 int az_chess_stats(az_chess_engine* eng, az_stats* st);
 
 /* MCTS tree API on chess boards (mcts/mcts.py:86-222 with a chess Board):

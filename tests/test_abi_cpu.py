@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     for name in header_functions():
         assert hasattr(lib, name), name
     L = az.load_library()
-    assert L.az_abi_version() == 9
+    assert L.az_abi_version() == 10
 
 
 def test_product_library_is_not_a_diagnostic_build():

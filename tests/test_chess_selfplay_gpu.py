@@ -228,3 +228,40 @@ def test_chess_play_api_matches_oracle():
         assert np.array_equal(rewards[off:off + T], exp)
         off += T
     assert off == len(states) == len(policies) == len(rewards)
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_chess_drain_returns_every_game_once(lanes):
+    """az_chess_selfplay_drain (ABI 10): asynchronous steps, a drain after
+    each -- the games of the newest move whose snapshot is complete, never
+    waiting for the running one -- then the rest after a synchronize: every
+    game once, each record equal to az_chess_selfplay_results' rows."""
+    import torch
+    from custom_alphazero import engine as az
+    eng = az.ChessEngine(mcts_iterations=10, slots=6, evaluator=az.EVAL_SYNTHETIC, max_plies=9, lanes=lanes)
+    n_games = 20
+    eng.selfplay_begin(300, n_games, 4)
+    parts = []
+    for _ in range(60):  # more moves than the batch needs (9-ply cap, 6 slots); idle slots skip
+        eng.selfplay_step(1, sync=False)
+        parts.append(eng.selfplay_drain())
+    torch.cuda.synchronize()
+    st = eng.stats()  # synchronizes the lanes
+    assert st["active_slots"] == 0 and st["errors"] == 0
+    parts.append(eng.selfplay_drain())
+    assert len(eng.selfplay_drain()["lengths"]) == 0
+    got = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    assert sorted(got["game_ids"].tolist()) == list(range(300, 300 + n_games))
+    ref = eng.selfplay_results()
+    gi = got["game_ids"] - 300
+    for k in ("lengths", "results", "terminations", "expansions", "moves", "policy_n", "policy_actions"):
+        np.testing.assert_array_equal(got[k], ref[k][gi], err_msg=k)
+    np.testing.assert_array_equal(got["positions"].view(np.uint8), ref["positions"][gi].view(np.uint8))
+    np.testing.assert_array_equal(got["policy_probs"].view(np.uint64), ref["policy_probs"][gi].view(np.uint64))
+    # and the games are the oracle's
+    for i in range(3):
+        r = C.play_game(10, 4 + 300 + i, 9)
+        g = int(np.nonzero(got["game_ids"] == 300 + i)[0][0])
+        assert got["lengths"][g] == r["T"]
+        np.testing.assert_array_equal(got["moves"][g, :r["T"]], r["moves"])
+    eng.close()

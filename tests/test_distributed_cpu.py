@@ -100,3 +100,78 @@ def test_shard_blocks_cover_all_games():
             assert [f for f, _ in blocks] == sorted(f for f, _ in blocks)
             for (f0, c0), (f1, _) in zip(blocks, blocks[1:]):
                 assert f0 + c0 == f1
+
+
+# ---------------------------------------------------------------- chess
+# BASELINE configs[4] (chess over 8 GPUs): the chess record through the same
+# gather (distributed.pack_chess: 80-byte positions, u16 moves, sparse root
+# policies), each rank's games from the chess oracle (oracle/chess_oracle.c,
+# the C restatement the GPU chess engine is bitwise against).
+CH_SIMS, CH_PLIES, CH_SEED = 8, 6, 70
+
+
+def chess_oracle_runner(first, count, base_seed):
+    import chess_oracle as C
+    from custom_alphazero.chess.kernels import POS_DTYPE
+    P, M = CH_PLIES, 256
+    out = dict(game_ids=first + np.arange(count, dtype=np.int64), lengths=np.zeros(count, np.int32),
+               results=np.zeros(count, np.int32), terminations=np.zeros(count, np.int32),
+               expansions=np.zeros(count, np.int32), positions=np.zeros((count, P), POS_DTYPE),
+               moves=np.zeros((count, P), np.uint16), policy_n=np.zeros((count, P), np.int32),
+               policy_actions=np.zeros((count, P, M), np.int16), policy_probs=np.zeros((count, P, M)))
+    for i in range(count):
+        r = C.play_game(CH_SIMS, base_seed + first + i, CH_PLIES)
+        T = r["T"]
+        out["lengths"][i], out["results"][i], out["terminations"][i] = T, r["result"], r["termination"]
+        out["expansions"][i] = r["expansions"]
+        for k in ("positions", "moves", "policy_n", "policy_actions", "policy_probs"):
+            out[k][i, :T] = r[k]
+    return out
+
+
+def _chess_worker(rank, world, port, outdir, n_games):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (os.path.join(repo, "custom-alphazero_amd"), os.path.join(repo, "oracle"), here):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from custom_alphazero import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, count = D.shard(n_games, world, rank)
+    stats = {}
+    g = D.gather_games(chess_oracle_runner(first, count, CH_SEED), stats=stats)
+    if rank == 0:
+        np.savez(os.path.join(outdir, f"chess{world}.npz"), wire=stats["wire_bytes"], **g)
+    else:
+        assert g is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_games", [(1, 5), (2, 5), (3, 2)])
+def test_chess_records_gather_gloo(tmp_path, world, n_games):
+    """the chess replay buffer reaches rank 0 -- every
+    rank's compact chess games, in global game order, byte for byte the
+    records one rank playing every game packs; rank 0 receives exactly the
+    other ranks' bytes."""
+    from custom_alphazero import distributed as D
+    mp.start_processes(_chess_worker, args=(world, _free_port(), str(tmp_path), n_games), nprocs=world,
+                       start_method="spawn")
+    got = np.load(tmp_path / f"chess{world}.npz")
+    ref = D.pack_chess(chess_oracle_runner(0, n_games, CH_SEED))
+    for k, v in ref.items():
+        assert got[k].dtype == v.dtype, k
+        np.testing.assert_array_equal(got[k], v, err_msg=k)
+    assert got["policy_probs"].view(np.uint64).tolist() == ref["policy_probs"].view(np.uint64).tolist()
+    # the sparse policy: one entry per root edge of every sample, summing to 1
+    assert len(ref["policy_actions"]) == int(ref["policy_n"].astype(np.int64).sum())
+    off = 0
+    for n in ref["policy_n"]:
+        assert abs(ref["policy_probs"][off:off + n].sum() - 1.0) < 1e-12
+        off += n
+    c0 = D.shard(n_games, world, 0)[1]
+    mine = D.pack_chess(chess_oracle_runner(0, c0, CH_SEED))
+    total = sum(v.nbytes for v in ref.values())
+    assert int(got["wire"]) == total - sum(v.nbytes for v in mine.values())

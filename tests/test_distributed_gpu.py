@@ -135,3 +135,74 @@ def test_bench_two_ranks_gathers_every_rank(outer_launcher):
     gather = line["replay_buffer_gather"]
     assert gather is not None and gather["games"] == line["games_timed"] > 0
     assert gather["samples"] >= 7 * gather["games"]
+
+
+# ---------------------------------------------------------------- chess
+# BASELINE configs[4] (2048 chess games over 8 GPUs): each rank's ChessEngine
+# plays its shard, the compact chess records reach rank 0
+CH_SIMS, CH_PLIES, CH_GAMES, CH_SEED = 12, 10, 10, 31
+
+
+def _chess_worker(rank, world, port, outdir):
+    _paths()
+    import torch.distributed as dist
+    from custom_alphazero import distributed as D
+    from custom_alphazero import engine as az
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = az.ChessEngine(mcts_iterations=CH_SIMS, slots=4, evaluator=az.EVAL_SYNTHETIC, max_plies=CH_PLIES)
+    g = D.selfplay_sharded(D.engine_runner(eng), CH_GAMES, CH_SEED, device="cpu")
+    eng.close()
+    if rank == 0:
+        np.savez(os.path.join(outdir, f"chess{world}.npz"), **g)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_chess_selfplay_gathers_one_engines_records(tmp_path):
+    """Two ranks on cuda:0 over gloo, a ChessEngine each (synthetic
+    evaluator) on its shard: rank 0's gathered chess records are byte for
+    byte those one engine playing every game id packs (distributed.pack_chess),
+    and the games are the chess oracle's."""
+    world = 2
+    mp.start_processes(_chess_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    got = dict(np.load(tmp_path / f"chess{world}.npz"))
+    _paths()
+    from custom_alphazero import distributed as D
+    from custom_alphazero import engine as az
+    eng = az.ChessEngine(mcts_iterations=CH_SIMS, slots=4, evaluator=az.EVAL_SYNTHETIC, max_plies=CH_PLIES)
+    ref = D.pack_chess(D.engine_runner(eng)(0, CH_GAMES, CH_SEED))
+    eng.close()
+    assert len(got["lengths"]) == CH_GAMES
+    for k, v in ref.items():
+        assert got[k].dtype == v.dtype, k
+        np.testing.assert_array_equal(got[k].view(np.uint8), v.view(np.uint8), err_msg=k)
+    import chess_oracle as C
+    off = 0
+    for g in range(CH_GAMES):
+        r = C.play_game(CH_SIMS, CH_SEED + g, CH_PLIES)
+        T = r["T"]
+        assert got["lengths"][g] == T and got["results"][g] == r["result"]
+        np.testing.assert_array_equal(got["moves"][off:off + T], r["moves"])
+        off += T
+
+
+@pytest.mark.timeout(300)
+def test_bench_chess_two_ranks_gathers_every_rank():
+    """bench.py --game chess --gpus 2 (gloo, two ranks on the box's one GPU):
+    games capped at 3 plies finish inside the window, are drained on each
+    rank and gathered to rank 0 (replay_buffer_gather counts every rank's)."""
+    args = [sys.executable, os.path.join(REPO, "bench.py"), "--game", "chess", "--gpus", "2", "--dist-backend",
+            "gloo", "--slots", "8", "--sims", "16", "--steps", "6", "--warmup", "1", "--max-plies", "3",
+            "--no-cpu-baseline", "--share-devices"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=280, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    gather = line["replay_buffer_gather"]
+    assert gather is not None and gather["games"] == line["games_drained"] > 0
+    assert gather["samples"] <= 3 * gather["games"] and gather["policy_entries"] >= gather["samples"]

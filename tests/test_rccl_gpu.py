@@ -78,6 +78,11 @@ def _worker(rank, port, outdir):
     g = D.selfplay_sharded(D.engine_runner(eng), N_GAMES, BASE_SEED)  # gather: RCCL gather (+ point-to-point for other ranks) on cuda:0
     eng.close()
     np.savez(os.path.join(outdir, "rccl.npz"), **g)
+    # the chess record (configs[4]) through the same RCCL gather from device memory
+    ceng = az.ChessEngine(mcts_iterations=8, slots=4, evaluator=az.EVAL_SYNTHETIC, max_plies=8)
+    cg = D.selfplay_sharded(D.engine_runner(ceng), 6, 5)
+    ceng.close()
+    np.savez(os.path.join(outdir, "rccl_chess.npz"), **cg)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -99,3 +104,10 @@ def test_rccl_weight_broadcast_and_game_gather_on_device(tmp_path):
     for k in ("lengths", "results", "expansions", "boards", "moves"):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     np.testing.assert_array_equal(got["policies"].view(np.uint64), ref["policies"].view(np.uint64))
+    cgot = dict(np.load(tmp_path / "rccl_chess.npz"))
+    ceng = az.ChessEngine(mcts_iterations=8, slots=4, evaluator=az.EVAL_SYNTHETIC, max_plies=8)
+    cref = D.pack_chess(D.engine_runner(ceng)(0, 6, 5))
+    ceng.close()
+    assert len(cgot["lengths"]) == 6
+    for k, v in cref.items():
+        np.testing.assert_array_equal(cgot[k].view(np.uint8), v.view(np.uint8), err_msg=k)
