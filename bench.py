@@ -88,9 +88,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=0, help="slot groups on separate HIP streams (0 = auto)")
     ap.add_argument("--conv-algo", type=int, default=0, help="0 fp16x2 direct (default), 1 fp32 direct")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
-    ap.add_argument("--cache-log2", type=int, default=26,
-                    help="transposition cache (the reference's plays_inferences) entries = 2^N (2^26: 4.6 GB "
-                         "of the 288 GB at configs[1]); 0 = off")
+    ap.add_argument("--cache-log2", type=int, default=None,
+                    help="transposition cache (the reference's plays_inferences) entries = 2^N (default 26: "
+                         "4.6 GB of the 288 GB at configs[1]; chess 20: 1.2 GB); 0 = off")
     ap.add_argument("--arena-edges", default="bounded",
                     help="tree edges per slot, the average of a lane's pooled halves: 'bounded' (default, "
                          "8*S*A + H*W*A: ~5x the high-water mark measured at configs[1] and configs[3]), "
@@ -110,7 +110,8 @@ def parse():
                          "the line reports shared_devices)")
     args = ap.parse_args()
     chess = args.game == "chess"
-    for k, c4, ch in (("steps", 30, 3), ("warmup", 5, 2), ("slots", 4096, 256), ("sims", 100, 800)):
+    for k, c4, ch in (("steps", 30, 3), ("warmup", 5, 2), ("slots", 4096, 256), ("sims", 100, 800),
+                      ("cache_log2", 26, 20)):
         if getattr(args, k) is None:
             setattr(args, k, ch if chess else c4)
     return args
@@ -442,7 +443,7 @@ def chess_main(args):
     named, _flat = _device_weights(spec, host_w, rank, world, args, dev)
     eng = az.ChessEngine(mcts_iterations=args.sims, slots=args.slots, evaluator=az.EVAL_NETWORK,
                          max_plies=args.max_plies, depth=args.depth, device=dev_index, conv_algo=args.conv_algo,
-                         lanes=args.lanes)
+                         lanes=args.lanes, cache_log2=args.cache_log2)
     eng.set_weights(named)
     budget = args.slots * 2
     eng.selfplay_begin(first_game=rank * budget, n_games=budget, base_seed=0)
@@ -488,11 +489,11 @@ def chess_main(args):
                              f"sends its blob to rank 0 only (point-to-point over {args.dist_backend}) after "
                              f"the timed window"}
     d = {k: st1[k] - st0[k] for k in ("games_done", "expansions", "simulations", "plies",
-                                      "terminal_visits", "evaluations")}
+                                      "terminal_visits", "evaluations", "cache_hits")}
     local_evals = d["evaluations"]
-    g, e, s, p, ev, dr = _reduce([d["games_done"], d["expansions"], d["simulations"], d["plies"],
-                                  d["evaluations"], drained], dist.ReduceOp.SUM if world > 1 else None, world,
-                                 args, dev)
+    g, e, s, p, ev, dr, hits = _reduce([d["games_done"], d["expansions"], d["simulations"], d["plies"],
+                                        d["evaluations"], drained, d["cache_hits"]],
+                                       dist.ReduceOp.SUM if world > 1 else None, world, args, dev)
     (elapsed,) = _reduce([elapsed], dist.ReduceOp.MAX if world > 1 else None, world, args, dev)
     F, HW = 128, 64
     direct_flop = HW * 2 * F * F * 19 * args.depth     # direct 3x3 + 1x1 residual, tower only
@@ -537,6 +538,14 @@ def chess_main(args):
             "network_evaluations_per_s": round(ev / elapsed, 1),
             "games_timed": int(g),
             "games_drained": int(dr),
+            "transposition_cache": ({
+                "capacity": st1["cache_capacity"], "hit_rate": round(hits / max(e, 1), 4),
+                "entries": st1["cache_entries"], "inserts": st1["cache_inserts"],
+                "dedup_share": round(1 - (ev + hits) / max(e, 1), 4),
+                "semantics": "reference plays_inferences (mcts.py:122-143) on chess boards: key = leaf position + "
+                             "history form, payload = masked priors + value; identical leaves of one simulation "
+                             "share a network row; bit-identical results (LRU eviction, az_tree.h scheme)",
+            } if args.cache_log2 else None),
             "games_drained_basis": "games whose records reached the host in the window (az_chess_selfplay_drain "
                                    "after every asynchronous step, and once more after the final synchronize)",
             "replay_buffer_gather": gather,

@@ -71,10 +71,47 @@ struct CTree {
   int32_t* eval_slot;      // [slots]
   int32_t* eval_count;     // this simulation's queue length (one of the lane's two counters)
   int32_t* next_count;     // the other: zeroed by this simulation's select launch for the next one
-  int32_t* slot_q;         // [slots] the slot's queue entry in its last simulation, -1 none (the fused expand)
+  int32_t* slot_q;         // [slots] the slot's leaf in its last simulation (the fused expand): its
+                           // network row (>= 0), kQHit (served by the transposition cache: the
+                           // payload copied to leaf_pay), -1 none; kQDup0 - k while a duplicate waits
+                           // for the launch's last block (tag slot k of the dedup table)
   unsigned long long* stats;
   const double* powtab;
   const int16_t* lut;
+  // transposition cache (round 6; null when off) = the reference's
+  // plays_inferences for chess boards (mcts.py:122-143): key = the leaf
+  // position + its history form (the network input is a function of both),
+  // payload = the masked, action-ordered network priors (normalize's input)
+  // and the value.  Per-simulation dedup of identical leaves (step table,
+  // epoch-tagged) gives duplicates the owner's network row.
+  float* leaf_pay;         // [slots][kPayFloats] a hit's payload, copied in the select launch
+  uint64_t* step_tag;      // [step_mask + 1] (epoch << 32) | fingerprint
+  int32_t* step_row;       // [step_mask + 1] the owner's network row
+  uint32_t step_mask;
+  uint32_t epoch;
+  int32_t* dup_q;          // [slots] duplicate slots of this simulation
+  int32_t* dup_count;      // this simulation's (the lane's counts block, alternating)
+  int32_t* next_dup;       // the next simulation's (zeroed by this select launch)
+  uint32_t* sel_done;      // [1] select blocks finished (the last resolves the duplicates)
+};
+
+constexpr int kQHit = -2, kQDup0 = -3;
+// transposition cache entry: key (position + history form), state word, payload
+struct ChessKey {
+  az_chess_pos pos;  // 80 B
+  int32_t initial;   // the root's [0 x 7, start] history form (see encode_queue_kernel)
+  int32_t pad[3];
+};
+static_assert(sizeof(ChessKey) == 96, "ChessKey is 6 uint4");
+constexpr int kPayFloats = AZ_CHESS_MAX_MOVES + 4;  // priors in action order [n], then value at [256]
+struct ChessCache {
+  ChessKey* keys = nullptr;      // [cap]
+  uint32_t* state = nullptr;     // [cap] az_tree.h cache_word (fingerprint, generation, status)
+  float* pay = nullptr;          // [cap][kPayFloats]
+  uint32_t mask = 0;
+  int enabled = 0;
+  unsigned long long* ctl = nullptr;  // [0] generation, [1] inserts since the clear, [2] into empty slots
+  unsigned long long gen_size = 0;
 };
 
 struct CSamples {
@@ -257,6 +294,157 @@ __global__ void tree_release_kernel(CTree t, int n, const int32_t* slots) {
   if (i < n) t.game_id[slots[i]] = -1;
 }
 
+// ------------------------------------------------- transposition cache
+// (az_tree.h's scheme: 16-slot buckets, LRU eviction by generations, a hit
+// refreshes its entry into the current generation.)  The select wave that
+// hits copies the payload into its slot's leaf_pay right away, so a reader
+// holds an entry only for the few microseconds between its probe (which
+// leaves the entry stamped with the current generation) and the copy: an
+// insert evicts entries kCacheEvictAge+ generations old, and two generation
+// turns (2 * cap / 16 inserts) cannot fall inside that window.
+__device__ __forceinline__ uint64_t key_hash(const Pos& q, int initial) {
+  return az::splitmix64(pos_hash(q, initial) ^ ((uint64_t)(uint32_t)q.turn << 8) ^ ((uint64_t)(uint32_t)q.rep << 16));
+}
+__device__ __forceinline__ uint32_t key_bucket(const ChessCache& c, uint64_t h) {
+  return (uint32_t)h & c.mask & ~(uint32_t)(az::kCacheBucket - 1);
+}
+__device__ __forceinline__ bool same_key(const ChessKey* a, const az_chess_pos& pos, int initial) {
+  const uint4* x = reinterpret_cast<const uint4*>(a);
+  const uint4* y = reinterpret_cast<const uint4*>(&pos);
+  uint4 v[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[i] = x[i];  // issued together: one round trip
+  bool eq = v[5].x == (uint32_t)initial;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint4 w = y[i];
+    eq = eq && v[i].x == w.x && v[i].y == w.y && v[i].z == w.z && v[i].w == w.w;
+  }
+  return eq;
+}
+
+// The wave's leaf (slot s, n legal moves) against the cache: true = a hit,
+// its n priors and value copied to leaf_pay[s].  Lane 0 probes; every lane
+// copies.
+__device__ bool cache_probe_wave(const CTree& t, const ChessCache& c, int s, int lane, const az_chess_pos& key,
+                                 int initial, uint64_t h, int n) {
+  int idx = -1;
+  if (lane == 0) {
+    const uint32_t gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t fp = az::cache_fp(h), base = key_bucket(c, h);
+    uint32_t w[az::kCacheBucket];
+#pragma unroll
+    for (int k = 0; k < az::kCacheBucket; ++k)
+      w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int hit = -1;
+    uint32_t hst = 0;
+    bool stop = false;
+#pragma unroll
+    for (int k = 0; k < az::kCacheBucket; ++k) {
+      const uint32_t st = w[k];
+      if (stop) continue;
+      if (st == az::kCacheEmpty) {  // buckets fill in slot order
+        stop = true;
+      } else if ((st & 3u) == az::kCacheReady && (st >> 16) == fp) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (same_key(c.keys + base + k, key, initial)) {
+          hit = k;
+          hst = st;
+          stop = true;
+        }
+      }
+    }
+    if (hit >= 0 && az::cache_age(hst, gen) != 0) {
+      // into the current generation (the LRU stamp); the CAS must win, or find
+      // the entry moved there by another reader and still this key
+      const uint32_t want = az::cache_word(fp, gen, az::kCacheReady);
+      const uint32_t prev = atomicCAS(c.state + base + hit, hst, want);
+      if (prev != hst) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (!(prev == want && same_key(c.keys + base + hit, key, initial))) hit = -1;
+      }
+    }
+    idx = hit >= 0 ? (int)(base + hit) : -1;
+  }
+  idx = __shfl(idx, 0);
+  if (idx < 0) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (every lane reads the payload)
+  const float* src = c.pay + (size_t)idx * kPayFloats;
+  float* dst = t.leaf_pay + (size_t)s * kPayFloats;
+  for (int j = lane; j < n; j += 64) dst[j] = src[j];
+  if (lane == 0) dst[AZ_CHESS_MAX_MOVES] = src[AZ_CHESS_MAX_MOVES];
+  return true;
+}
+
+// plays_inferences[repr(board)] = (priors, value) (mcts.py:142) by the wave of
+// the leaf's network row owner: the bucket's first empty slot, else its least
+// recently used entry kCacheEvictAge+ generations old (az_tree.h); dropped
+// when every entry is in use
+__device__ void cache_insert_wave(const CTree& t, const ChessCache& c, int s, int lane, const float* sorted, int n,
+                                  float value) {
+  const az_chess_pos& key = t.leaf[s];
+  const int initial = t.path_len[s] == 0 && t.initial[s];
+  const Pos q = load_pos(key);
+  const uint64_t h = key_hash(q, initial);
+  int idx = -1;
+  if (lane == 0) {
+    const uint32_t gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t fp = az::cache_fp(h), base = key_bucket(c, h);
+    uint32_t w[az::kCacheBucket];
+#pragma unroll
+    for (int k = 0; k < az::kCacheBucket; ++k)
+      w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t tried = 0;
+    bool empty = false;
+    for (int attempt = 0; attempt < az::kCacheBucket && idx < 0; ++attempt) {
+      int pick = -1;
+      uint32_t pst = 0, page = 0;
+      bool pempty = false;
+#pragma unroll
+      for (int k = 0; k < az::kCacheBucket; ++k) {
+        const uint32_t st = w[k];
+        if (pempty || ((tried >> k) & 1u)) continue;
+        if (st == az::kCacheEmpty) {
+          pick = k, pst = st, pempty = true;
+        } else if (c.gen_size) {
+          const uint32_t age = az::cache_age(st, gen);
+          if (age >= az::kCacheEvictAge && age > page) pick = k, pst = st, page = age;
+        }
+      }
+      if (pick < 0) break;
+      if (atomicCAS(c.state + base + pick, pst, az::cache_word(fp, gen, az::kCacheClaimed)) == pst) {
+        idx = (int)(base + pick);
+        empty = pempty;
+      } else {
+        tried |= 1u << pick;
+      }
+    }
+    if (idx >= 0) {
+      if (empty) atomicAdd(c.ctl + 2, 1ull);
+      const unsigned long long m = atomicAdd(c.ctl + 1, 1ull) + 1;
+      if (c.gen_size && m % c.gen_size == 0) atomicAdd(c.ctl, 1ull);
+      atomicAdd(t.stats + az::kStatCacheInserts, 1ull);
+    }
+  }
+  idx = __shfl(idx, 0);
+  if (idx < 0) return;
+  float* dst = c.pay + (size_t)idx * kPayFloats;
+  for (int j = lane; j < n; j += 64) dst[j] = sorted[j];
+  if (lane == 0) dst[AZ_CHESS_MAX_MOVES] = value;
+  if (lane < 6) {
+    uint4 v;
+    if (lane < 5) v = reinterpret_cast<const uint4*>(&key)[lane];
+    else v = make_uint4((uint32_t)initial, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(c.keys + idx)[lane] = v;
+  }
+  __threadfence();  // every lane's key and payload stores, device-wide, before the publish
+  if (lane == 0)
+    atomicExch(c.state + idx, az::cache_word(az::cache_fp(h),
+                                             (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT),
+                                             az::kCacheReady));
+}
+
 // MCTS.evaluate_and_expand (mcts.py:145-161) + backup of queue entry b
 // (slot s) by one wave: the expand launch's, or -- fused -- the slot's wave
 // in the next simulation's select launch, before its descent
@@ -267,29 +455,40 @@ struct ExpandSmem {
   int first_s;
 };
 
-__device__ void expand_body(const CCfg& g, const CTree& t, const float* __restrict__ probs,
+// b: the slot's network row, or kQHit (its cached priors and value in leaf_pay)
+__device__ void expand_body(const CCfg& g, const CTree& t, const ChessCache& c, const float* __restrict__ probs,
                             const float* __restrict__ values, int b, int s, int lane, ExpandSmem& sm) {
   int* act = sm.act;
   float* sorted = sm.sorted;
   {
     const int n = t.leaf_n[s];
     const uint16_t* mv = t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES;
-    const float* pr = probs + (size_t)b * AZ_CHESS_ACTIONS;
+    const bool hit = b == kQHit;
     __syncthreads();
-    for (int j = lane; j < n; j += 64) {
-      const int a = action_of(t.lut, mv[j]);
-      act[j] = a;
-      if (a < 0) flag(t, az::kErrIllegal);
+    if (hit) {  // plays_inferences[repr(board)] (mcts.py:123-128): the masked priors as stored
+      const float* lp = t.leaf_pay + (size_t)s * kPayFloats;
+      for (int j = lane; j < n; j += 64) sorted[j] = lp[j];
+    } else {
+      const float* pr = probs + (size_t)b * AZ_CHESS_ACTIONS;
+      for (int j = lane; j < n; j += 64) {
+        const int a = action_of(t.lut, mv[j]);
+        act[j] = a;
+        if (a < 0) flag(t, az::kErrIllegal);
+      }
+      __syncthreads();
+      // probabilities[legal_moves_mask]: the legal actions in action order
+      for (int j = lane; j < n; j += 64) {
+        const int a = act[j];
+        int r = 0;
+        for (int i = 0; i < n; ++i) r += act[i] < a;
+        sorted[r] = a >= 0 ? pr[a] : 0.f;
+      }
     }
     __syncthreads();
-    // probabilities[legal_moves_mask]: the legal actions in action order
-    for (int j = lane; j < n; j += 64) {
-      const int a = act[j];
-      int r = 0;
-      for (int i = 0; i < n; ++i) r += act[i] < a;
-      sorted[r] = a >= 0 ? pr[a] : 0.f;
-    }
-    __syncthreads();
+    const float value = hit ? t.leaf_pay[(size_t)s * kPayFloats + AZ_CHESS_MAX_MOVES] : values[b];
+    // the network row's owner publishes it (duplicates of this simulation share the row)
+    const bool owner = !hit && t.eval_slot[b] == s;
+    if (owner && c.enabled) cache_insert_wave(t, c, s, lane, sorted, n, value);
     if (lane == 0) {
       // normalize_probabilities (mcts/utils.py:4-16): the sum in numpy's
       // pairwise order here, the quotients per lane below
@@ -322,7 +521,6 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
     }
     const int depth = t.path_len[s];
     const int32_t* path = t.path + (size_t)s * g.max_depth;
-    const float value = values[b];
     if (lane == 0) {
       if (depth == 0) {
         t.root_first[s] = first;
@@ -339,7 +537,8 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
     if (lane == 0) {
       t.slot_exp[s] += 1;
       atomicAdd(t.stats + az::kStatExpansions, 1ull);
-      atomicAdd(t.stats + az::kStatNNEvals, 1ull);
+      if (hit) atomicAdd(t.stats + az::kStatCacheHits, 1ull);
+      else if (owner) atomicAdd(t.stats + az::kStatNNEvals, 1ull);
     }
   }
 }
@@ -351,8 +550,13 @@ __device__ void expand_body(const CCfg& g, const CTree& t, const float* __restri
 // does the rest.
 // (Round 5: run by the select launch's wave right after its descent, on the
 // leaf in its registers -- one launch fewer on the lane's chain.)
-__device__ __forceinline__ void leaf_body(const CCfg& g, const CTree& t, int s, int lane, const Pos& q,
-                                          uint16_t* cand) {
+// With the transposition cache on, an ongoing leaf is first looked up
+// (cache_probe_wave: a hit copies its payload, slot_q = kQHit); a miss takes a
+// network row unless an identical leaf of this simulation already did
+// (per-simulation dedup: the step table's epoch-tagged fingerprint; a tag
+// match is a candidate the launch's last block confirms by the full key).
+__device__ __forceinline__ void leaf_body(const CCfg& g, const CTree& t, const ChessCache& c, int s, int lane,
+                                          const Pos& q, uint16_t* cand) {
   bool check;
   const int n = legal_moves_wave(q, cand, t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES, &check, lane);
   if (n < 0) {  // wave-uniform
@@ -366,17 +570,98 @@ __device__ __forceinline__ void leaf_body(const CCfg& g, const CTree& t, int s, 
   if (oc != AZ_CHESS_ONGOING)
     backup_wave(arena(g, t, s, t.half[s]), t.path + (size_t)s * g.max_depth, t.path_len[s],
                 oc == AZ_CHESS_CHECKMATE ? 1.0 : 0.0, lane);
+  uint64_t h = 0;
+  bool hit = false;
+  if (oc == AZ_CHESS_ONGOING && c.enabled) {  // wave-uniform
+    const int initial = t.path_len[s] == 0 && t.initial[s];
+    h = key_hash(q, initial);
+    az_chess_pos key;
+    store_pos(q, key);
+    hit = cache_probe_wave(t, c, s, lane, key, initial, h, n);
+  }
   if (lane != 0) return;
   t.leaf_n[s] = n;
   int qi = -1;
   if (oc != AZ_CHESS_ONGOING) {
     atomicAdd(t.stats + az::kStatTerminal, 1ull);
-  } else {
+  } else if (hit) {
+    qi = kQHit;
+  } else if (!c.enabled) {
     qi = atomicAdd(t.eval_count, 1);
     t.eval_slot[qi] = s;
+  } else {
+    const uint64_t tag = ((uint64_t)t.epoch << 32) | (uint32_t)(h >> 32);
+    uint32_t sl = (uint32_t)h & t.step_mask;
+    for (uint32_t p = 0; p <= t.step_mask; ++p) {
+      const uint64_t cur = __hip_atomic_load(t.step_tag + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(cur >> 32) != t.epoch) {  // empty in this epoch: try to own it
+        const uint64_t prev = atomicCAS((unsigned long long*)(t.step_tag + sl), cur, tag);
+        if (prev == cur) {
+          qi = atomicAdd(t.eval_count, 1);
+          t.eval_slot[qi] = s;
+          t.step_row[sl] = qi;
+          break;
+        }
+        if (prev != tag) continue;  // another tag took the slot: re-read it
+      } else if (cur != tag) {
+        sl = (sl + 1) & t.step_mask;
+        continue;
+      }
+      qi = kQDup0 - (int)sl;  // a candidate duplicate: the last block confirms it
+      t.dup_q[atomicAdd(t.dup_count, 1)] = s;
+      break;
+    }
   }
   t.slot_q[s] = qi;
   atomicAdd(t.stats + az::kStatSims, 1ull);
+}
+
+// The select launch's last block: its duplicate candidates get the owner's
+// network row when the full keys (position + history form) agree, else a row
+// of their own (a fingerprint collision).  Every block counts itself done
+// after a device-scope fence; the block whose count completes the grid sees
+// every block's queue stores.
+__device__ void dup_tail(const CTree& t, const ChessCache& c, int lane) {
+  if (!c.enabled) return;  // uniform
+  __shared__ int last;
+  // the wave's queue stores drained, one release, the count; the block that
+  // completes it acquires (MI355X_MICROARCH.md, valid forms)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd(t.sel_done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;  // block-uniform
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nd = __hip_atomic_load(t.dup_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = lane; i < nd; i += 64) {
+    const int s2 = t.dup_q[i];
+    const int sl = kQDup0 - t.slot_q[s2];
+    const int row = t.step_row[sl];
+    const int o = t.eval_slot[row];
+    const int i2 = t.path_len[s2] == 0 && t.initial[s2], io = t.path_len[o] == 0 && t.initial[o];
+    const uint4* a = reinterpret_cast<const uint4*>(t.leaf + s2);
+    const uint4* b = reinterpret_cast<const uint4*>(t.leaf + o);
+    bool same = i2 == io;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint4 x = a[k], y = b[k];
+      same = same && x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
+    }
+    if (same) {
+      t.slot_q[s2] = row;
+    } else {
+      const int r2 = atomicAdd(t.eval_count, 1);
+      t.eval_slot[r2] = s2;
+      t.slot_q[s2] = r2;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) *t.sel_done = 0;  // the lane's next select launch counts from zero
 }
 
 // MCTS.select (mcts.py:111-120): one wave per slot, then the leaf's move
@@ -386,19 +671,15 @@ __device__ __forceinline__ void leaf_body(const CCfg& g, const CTree& t, int s, 
 // (network, select) x (sims - 1), network, expand: one tree launch per
 // simulation on the lane's chain instead of two
 template <bool FUSED>
-__global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t, const float* __restrict__ probs,
-                                                    const float* __restrict__ values) {
-  __shared__ uint16_t cand[AZ_CHESS_MAX_MOVES];
-  __shared__ ExpandSmem esm;
+__device__ __forceinline__ void select_slot(const CCfg& g, const CTree& t, const ChessCache& c,
+                                            const float* __restrict__ probs, const float* __restrict__ values,
+                                            uint16_t* cand, ExpandSmem& esm) {
   const int s = blockIdx.x, lane = threadIdx.x;
-  // the next simulation's queue counter (this one's was zeroed by the last
-  // simulation's launch; a memset launch per simulation cost 5 us)
-  if (s == 0 && lane == 0) *t.next_count = 0;
   if (t.game_id[s] < 0) return;
   if constexpr (FUSED) {
     const int b = t.slot_q[s];  // wave-uniform
-    if (b >= 0) {
-      expand_body(g, t, probs, values, b, s, lane, esm);
+    if (b >= 0 || b == kQHit) {
+      expand_body(g, t, c, probs, values, b, s, lane, esm);
       // the wave's edge and path stores complete before its descent reads them
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
@@ -454,7 +735,21 @@ __global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t, const float
     store_pos(q, t.leaf[s]);
     t.path_len[s] = depth;
   }
-  leaf_body(g, t, s, lane, q, cand);
+  leaf_body(g, t, c, s, lane, q, cand);
+}
+template <bool FUSED>
+__global__ __launch_bounds__(64) void select_kernel(CCfg g, CTree t, ChessCache c, const float* __restrict__ probs,
+                                                    const float* __restrict__ values) {
+  __shared__ uint16_t cand[AZ_CHESS_MAX_MOVES];
+  __shared__ ExpandSmem esm;
+  // the next simulation's queue counters (this one's were zeroed by the last
+  // simulation's launch; a memset launch per simulation cost 5 us)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *t.next_count = 0;
+    if (t.next_dup) *t.next_dup = 0;
+  }
+  select_slot<FUSED>(g, t, c, probs, values, cand, esm);
+  dup_tail(t, c, threadIdx.x);
 }
 
 // Board.full_state of the queued leaves into the network input [q][64][128]:
@@ -516,14 +811,15 @@ __global__ __launch_bounds__(256) void synth_kernel(CCfg g, CTree t, float* prob
   }
 }
 
-__global__ __launch_bounds__(64) void expand_kernel(CCfg g, CTree t, const float* __restrict__ probs,
+// a search's last expand (its own launch): one wave per slot whose last
+// simulation queued its leaf (a network row or a cache hit)
+__global__ __launch_bounds__(64) void expand_kernel(CCfg g, CTree t, ChessCache c, const float* __restrict__ probs,
                                                     const float* __restrict__ values) {
   __shared__ ExpandSmem sm;
-  const int n_q = *t.eval_count;
-  for (int b = blockIdx.x; b < n_q; b += gridDim.x) {
-    __syncthreads();  // the previous entry's shared arrays are no longer read
-    expand_body(g, t, probs, values, b, t.eval_slot[b], threadIdx.x, sm);
-  }
+  const int s = blockIdx.x;
+  if (t.game_id[s] < 0) return;
+  const int b = t.slot_q[s];
+  if (b >= 0 || b == kQHit) expand_body(g, t, c, probs, values, b, s, threadIdx.x, sm);
 }
 
 // MCTS.play (mcts.py:182-222) for every active slot + the self-play loop's
@@ -723,6 +1019,7 @@ struct CLane {
   int par = 0;
   bool pending_expand = false;  // the last simulation's expand not launched yet
   hipEvent_t move_done[4] = {nullptr, nullptr, nullptr, nullptr};  // move m's end on this lane (m % 4)
+  ChessCache cache{};  // the engine's (flush_expand has no engine pointer)
 };
 
 struct az_chess_engine {
@@ -733,6 +1030,7 @@ struct az_chess_engine {
   CTree t{};
   std::vector<CLane*> lanes;
   CSamples smp{};
+  ChessCache cache{};  // the transposition cache (az_chess_config.cache_log2; enabled = 0 when off)
   az::NetDev net{};
   az::ConvTimer timer;
   hipEvent_t timer_ref = nullptr;
@@ -792,11 +1090,16 @@ int check_errors(az_chess_engine* e) {
 int simulate(az_chess_engine* e, CLane& L) {
   hipStream_t s = L.stream;
   const int S = L.g.slots;
-  L.t.eval_count = L.counts + L.par;
-  L.t.next_count = L.counts + (L.par ^ 1);
+  // the queue and duplicate counters: one pair per simulation parity (the
+  // select launch zeroes the other pair, the next simulation's)
+  L.t.eval_count = L.counts + 2 * L.par;
+  L.t.dup_count = L.counts + 2 * L.par + 1;
+  L.t.next_count = L.counts + 2 * (L.par ^ 1);
+  L.t.next_dup = L.counts + 2 * (L.par ^ 1) + 1;
   L.par ^= 1;
-  if (L.pending_expand) select_kernel<true><<<S, 64, 0, s>>>(L.g, L.t, L.probs, L.values);
-  else select_kernel<false><<<S, 64, 0, s>>>(L.g, L.t, nullptr, nullptr);
+  L.t.epoch += 1;  // a fresh dedup table (tags of older epochs read as empty)
+  if (L.pending_expand) select_kernel<true><<<S, 64, 0, s>>>(L.g, L.t, e->cache, L.probs, L.values);
+  else select_kernel<false><<<S, 64, 0, s>>>(L.g, L.t, e->cache, nullptr, nullptr);
   if (L.g.evaluator == AZ_EVAL_NETWORK) {
     // the one-launch tower builds the leaves' input planes itself (no encode
     // launch on the chain; az_nn.h TowerLeaves); the other forms read rows
@@ -831,7 +1134,7 @@ int simulate(az_chess_engine* e, CLane& L) {
 int flush_expand(CLane& L) {
   if (!L.pending_expand) return 0;
   L.pending_expand = false;
-  expand_kernel<<<L.g.slots, 64, 0, L.stream>>>(L.g, L.t, L.probs, L.values);
+  expand_kernel<<<L.g.slots, 64, 0, L.stream>>>(L.g, L.t, L.cache, L.probs, L.values);
   AZC_HIP(hipGetLastError());
   return 0;
 }
@@ -869,11 +1172,25 @@ int make_lane(az_chess_engine* e, CLane* L, int first, int n) {
   t.mt += f;
   t.eval_slot += f;
   t.slot_q += f;
+  if (t.leaf_pay) t.leaf_pay += f * kPayFloats;
   int rc;
-  if ((rc = e->alloc(&t.eval_count, 2))) return rc;
-  AZC_HIP(hipMemset(t.eval_count, 0, 2 * sizeof(int32_t)));
+  if ((rc = e->alloc(&t.eval_count, 4))) return rc;
+  AZC_HIP(hipMemset(t.eval_count, 0, 4 * sizeof(int32_t)));
   L->counts = t.eval_count;
-  t.next_count = t.eval_count + 1;
+  t.dup_count = t.eval_count + 1;
+  t.next_count = t.eval_count + 2;
+  t.next_dup = t.eval_count + 3;
+  // the lane's per-simulation dedup table (load factor <= 25%) and duplicates list
+  size_t cap = 256;
+  while (cap < 4 * (size_t)n) cap <<= 1;
+  if ((rc = e->alloc(&t.step_tag, cap)) || (rc = e->alloc(&t.step_row, cap)) || (rc = e->alloc(&t.dup_q, n)) ||
+      (rc = e->alloc(&t.sel_done, 1)))
+    return rc;
+  AZC_HIP(hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)));
+  AZC_HIP(hipMemset(t.sel_done, 0, sizeof(uint32_t)));
+  t.step_mask = (uint32_t)(cap - 1);
+  t.epoch = 0;
+  L->cache = e->cache;
   L->t = t;
   if (e->x) L->x = e->x + f * 64 * 128;
   for (int i = 0; i < 3; ++i) L->act[i] = e->act[i] ? e->act[i] + f * 64 * 128 : nullptr;
@@ -976,6 +1293,26 @@ int az_chess_engine_create(int device, const az_chess_config* cfg, az_chess_engi
       if ((rc = e->alloc(&e->act[i], S * 64 * 128))) return cleanup(rc);
   }
   t.mt_stride = g.slots;
+  // the transposition cache (mcts.py:122-143 on chess boards)
+  if (c.cache_log2 < 0 || c.cache_log2 > 28 || (c.cache_log2 > 0 && c.cache_log2 < 4))
+    return cleanup(az::fail_abi(AZ_E_INVALID, "cache_log2 must be 0 (no cache) or 4..28"));
+  t.leaf_pay = nullptr;
+  if (c.cache_log2 > 0) {
+    const size_t cap = (size_t)1 << c.cache_log2;
+    ChessCache& cc = e->cache;
+    if ((rc = e->alloc(&cc.keys, cap)) || (rc = e->alloc(&cc.state, cap)) ||
+        (rc = e->alloc(&cc.pay, cap * kPayFloats)) || (rc = e->alloc(&cc.ctl, 4)) ||
+        (rc = e->alloc(&t.leaf_pay, S * kPayFloats)))
+      return cleanup(rc);
+    cc.mask = (uint32_t)(cap - 1);
+    cc.enabled = 1;
+    // LRU by generations of cap/16 inserts (a reader holds an entry only
+    // between its probe and its payload copy, inside one select launch)
+    cc.gen_size = cap / az::kCacheGenDiv;
+    if (hipMemset(cc.state, 0, cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(cc.ctl, 0, 4 * sizeof(unsigned long long)) != hipSuccess)
+      return cleanup(az::fail_abi(AZ_E_HIP, "cache memset failed"));
+  }
   e->net.depth = c.depth;
   // depth 0: the fp16x2 chain runs the heads' 1x1 convs inside the last
   // block's conv2, so a tower without blocks takes the fp32 MFMA path
@@ -1046,6 +1383,12 @@ int az_chess_engine_set_weights(az_chess_engine* e, const az_tensor* tensors, in
   if (!e || (!tensors && n)) return az::fail_abi(AZ_E_INVALID, "null argument");
   if (e->cfg.evaluator != AZ_EVAL_NETWORK) return az::fail_abi(AZ_E_STATE, "engine has no network evaluator");
   AZC_HIP(hipSetDevice(e->device));
+  int rc;
+  if ((rc = sync_lanes(e))) return rc;
+  if (e->cache.state) {  // a new model empties plays_inferences (self_play.py:145-146)
+    AZC_HIP(hipMemset(e->cache.state, 0, ((size_t)e->cache.mask + 1) * sizeof(uint32_t)));
+    AZC_HIP(hipMemset(e->cache.ctl, 0, 4 * sizeof(unsigned long long)));
+  }
   return az::load_network(e->net, tensors, n, AZ_CHESS_PLANES, 64, AZ_CHESS_ACTIONS, e->cfg.bn_epsilon,
                           e->owned);
 }
@@ -1137,6 +1480,16 @@ int az_chess_stats(az_chess_engine* e, az_stats* st) {
   st->plies = (int64_t)h[az::kStatPlies];
   st->errors = (int64_t)h[az::kStatErrors];
   st->evaluations = (int64_t)h[az::kStatNNEvals];
+  st->cache_hits = (int64_t)h[az::kStatCacheHits];
+  if (e->cache.ctl) {
+    unsigned long long ctl[3];
+    AZC_HIP(hipMemcpy(ctl, e->cache.ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+    st->cache_generation = (int64_t)ctl[0];
+    st->cache_inserts = (int64_t)ctl[1];
+    st->cache_entries = (int64_t)ctl[2];
+    st->cache_gen_size = (int64_t)e->cache.gen_size;
+    st->cache_capacity = (int64_t)e->cache.mask + 1;
+  }
   st->issued_flop_per_board = e->net.use_tower && e->net.tower ? e->net.issued_flop_per_board : 0.0;
   st->active_slots = std::count_if(gid.begin(), gid.end(), [](int64_t v) { return v >= 0; });
   // conv-busy time = union of the timed conv intervals over all lanes

@@ -589,12 +589,20 @@ __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDe
 __device__ __forceinline__ void dedup_tail(const TreeDev& t, const CacheDev& c) {
   if (!c.enabled) return;  // uniform
   __shared__ int last;
-  __threadfence();  // this thread's eval_src / nn_board / step_row / dup_q stores, device-wide
+  // every wave's eval_src / nn_board / step_row / dup_q stores drained, then
+  // ONE release per block before its count (not a full fence per wave); the
+  // block completing the count acquires (MI355X_MICROARCH.md, valid forms)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(t.sel_done, 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd(t.sel_done, 1u) == gridDim.x - 1;
+  }
   __syncthreads();
   if (!last) return;  // block-uniform
-  __threadfence();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int n = __hip_atomic_load(t.dup_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef AZ_SEL_STAMPS
   if (threadIdx.x == 0) {

@@ -48,7 +48,8 @@ class ChessConfig(ctypes.Structure):
         ("evaluator", ctypes.c_int32), ("filters", ctypes.c_int32), ("depth", ctypes.c_int32),
         ("value_hidden", ctypes.c_int32), ("max_plies", ctypes.c_int32),
         ("bn_epsilon", ctypes.c_double), ("arena_edges", ctypes.c_int64),
-        ("conv_algo", ctypes.c_int32), ("lanes", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6),
+        ("conv_algo", ctypes.c_int32), ("lanes", ctypes.c_int32), ("cache_log2", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
     ]
 
 
@@ -501,7 +502,7 @@ class ChessEngine:
     def __init__(self, mcts_iterations=800, slots=256, evaluator=EVAL_NETWORK, max_plies=512,
                  index_move_greedy=8, exploration_constant=1.5, filters=128, depth=4,
                  value_hidden=256, bn_epsilon=1e-3, arena_edges=0, conv_algo=CONV_F16X2,
-                 device=0, lanes=0):
+                 device=0, lanes=0, cache_log2=0):
         L = load_library()
         self.slots, self.mcts_iterations = slots, mcts_iterations
         self.max_plies = max_plies if max_plies > 0 else 512
@@ -509,7 +510,7 @@ class ChessEngine:
                           exploration_constant=exploration_constant, slots=slots,
                           evaluator=evaluator, filters=filters, depth=depth,
                           value_hidden=value_hidden, max_plies=max_plies, bn_epsilon=bn_epsilon,
-                          arena_edges=arena_edges, conv_algo=conv_algo, lanes=lanes)
+                          arena_edges=arena_edges, conv_algo=conv_algo, lanes=lanes, cache_log2=cache_log2)
         handle = ctypes.c_void_p()
         _check(L.az_chess_engine_create(int(device), ctypes.byref(cfg), ctypes.byref(handle)))
         self._h, self._L, self._n_games = handle, L, 0

@@ -141,7 +141,7 @@ def _chess_engine(model, n_slots, sims):
     check_mcts_config("chess")
     synthetic = isinstance(model, SyntheticEvaluator)
     key = (sims, n_slots, synthetic, ConfigMCTS.index_move_greedy, ConfigMCTS.exploration_constant,
-           ConfigModel.depth, ConfigSelfPlay.chess_max_plies)
+           ConfigModel.depth, ConfigSelfPlay.chess_max_plies, ConfigSelfPlay.chess_cache_log2)
     eng = _CHESS_ENGINES.get(key)
     if eng is None:
         eng = az.ChessEngine(sims, slots=n_slots,
@@ -150,7 +150,8 @@ def _chess_engine(model, n_slots, sims):
                              index_move_greedy=ConfigMCTS.index_move_greedy,
                              exploration_constant=ConfigMCTS.exploration_constant,
                              filters=ConfigModel.filters, depth=ConfigModel.depth,
-                             value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon)
+                             value_hidden=ConfigModel.value_hidden, bn_epsilon=ConfigModel.bn_epsilon,
+                             cache_log2=ConfigSelfPlay.chess_cache_log2)
         eng.weights_key = None
         _CHESS_ENGINES.clear()
         _CHESS_ENGINES[key] = eng

@@ -113,7 +113,13 @@ typedef struct az_chess_config {
                                      stem over the 118 planes zero-padded to 128 */
     int32_t lanes;                /* slot groups searched on separate HIP streams (0 = auto: 2 from
                                      128 slots, else 1); results do not depend on it */
-    int32_t reserved[6];
+    int32_t cache_log2;           /* ABI 10: transposition cache entries = 2^cache_log2, the
+                                     reference's plays_inferences on chess boards (mcts.py:122-143):
+                                     key = the leaf position + its history form, ~1.1 KB per entry
+                                     (the masked priors, up to 256, and the value); identical leaves
+                                     of one simulation share a network row.  0 = off, else 4..28;
+                                     results are identical either way */
+    int32_t reserved[5];
 } az_chess_config;
 /* Scope: no Dirichlet root noise (ConfigMCTS.enable_dirichlet_noise,
  * mcts.py:70-85) in the chess engine.  The reference's chess MCTS cannot run

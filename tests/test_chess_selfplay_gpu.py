@@ -34,20 +34,28 @@ def _compare(r, g, ref, tag):
                               ref["policy_probs"][t, :n].view(np.uint64)), (tag, g, t)
 
 
-@pytest.mark.parametrize("sims,plies,slots,games,greedy,lanes", [
-    (24, 40, 3, 5, 8, 1),      # slot refill, the reference's greedy threshold (never reached)
-    (24, 40, 3, 5, 8, 3),      # same games on three streams: results do not depend on lanes
-    (16, 30, 4, 4, 1, 2),      # greedy from the first move (one-hot policy, one draw consumed)
-    (8, 400, 4, 6, 8, 2),      # long games: checkmate / stalemate / 75-move / cap terminations
-    (2, 60, 2, 2, 8, 1),       # S=2: the root expansion plus one visit
+@pytest.mark.parametrize("sims,plies,slots,games,greedy,lanes,cache", [
+    (24, 40, 3, 5, 8, 1, 0),      # slot refill, the reference's greedy threshold (never reached)
+    (24, 40, 3, 5, 8, 3, 0),      # same games on three streams: results do not depend on lanes
+    (16, 30, 4, 4, 1, 2, 0),      # greedy from the first move (one-hot policy, one draw consumed)
+    (8, 400, 4, 6, 8, 2, 0),      # long games: checkmate / stalemate / 75-move / cap terminations
+    (2, 60, 2, 2, 8, 1, 0),       # S=2: the root expansion plus one visit
+    # round 6: the transposition cache + per-simulation dedup (identical games
+    # at the start: every slot's leaves coincide), and a table small enough
+    # to fill and evict (LRU) while other lanes read it
+    (24, 40, 3, 5, 8, 1, 16), (24, 40, 6, 8, 8, 3, 16), (8, 400, 4, 6, 8, 2, 16), (32, 60, 8, 8, 8, 2, 6),
 ])
-def test_chess_selfplay_synthetic_matches_oracle(sims, plies, slots, games, greedy, lanes):
+def test_chess_selfplay_synthetic_matches_oracle(sims, plies, slots, games, greedy, lanes, cache):
     from custom_alphazero import engine as az
     eng = _engine(mcts_iterations=sims, slots=slots, evaluator=az.EVAL_SYNTHETIC, max_plies=plies,
-                  index_move_greedy=greedy, lanes=lanes)
+                  index_move_greedy=greedy, lanes=lanes, cache_log2=cache)
     st = eng.selfplay_run(0, games, 1000)
     r = eng.selfplay_results()
     assert st["errors"] == 0 and st["games_done"] == games
+    if cache == 16:  # the cache served leaves (and dedup shared rows): fewer network rows than expansions
+        assert st["cache_hits"] > 0 and st["evaluations"] + st["cache_hits"] < st["expansions"]
+    if cache == 6:  # 64 entries: filled, then evicted many times over
+        assert st["cache_generation"] >= 2 * 16 and st["cache_entries"] == 2 ** 6
     for g in range(games):
         ref = C.play_game(sims, 1000 + g, plies, greedy_ply=greedy)
         _compare(r, g, ref, "synthetic")
@@ -168,10 +176,18 @@ def test_chess_activation_range_is_rescaled_not_failed():
     lay.close()
 
 
-def test_chess_selfplay_network_replays_on_oracle(chess_net):
-    eng, _ = chess_net
-    eng.selfplay_run(0, 3, 77)
+@pytest.mark.parametrize("cache", [0, 18])
+def test_chess_selfplay_network_replays_on_oracle(chess_net, cache):
+    eng, w = chess_net
+    if cache:  # the same network on an engine with the transposition cache
+        from custom_alphazero import engine as az
+        eng = _engine(mcts_iterations=16, slots=64, evaluator=az.EVAL_NETWORK, max_plies=12, lanes=2,
+                      cache_log2=cache)
+        eng.set_weights(w.items())
+    st = eng.selfplay_run(0, 3, 77)
     r = eng.selfplay_results()
+    if cache:  # the three games search identically until their first draw: dedup shares rows
+        assert st["evaluations"] + st["cache_hits"] < st["expansions"]
 
     def cb(pos, initial):
         x = C.full_state(*C.reference_history(pos, bool(initial)), pos)[None].astype(np.float32)
@@ -181,6 +197,8 @@ def test_chess_selfplay_network_replays_on_oracle(chess_net):
     for g in range(3):
         ref = C.play_game(16, 77 + g, 12, callback=cb)
         _compare(r, g, ref, "network")
+    if cache:
+        eng.close()
 
 
 def test_chess_engine_errors():
