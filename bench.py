@@ -90,7 +90,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo for rehearsals")
     ap.add_argument("--cache-log2", type=int, default=None,
                     help="transposition cache (the reference's plays_inferences) entries = 2^N (default 26: "
-                         "4.6 GB of the 288 GB at configs[1]; chess 20: 1.2 GB); 0 = off")
+                         "4.6 GB of the 288 GB at configs[1]; chess 0: its cache measured 3-5%% slower in the opening, "
+                         "profiles/r6/ab_chess_r5.txt); 0 = off")
     ap.add_argument("--arena-edges", default="bounded",
                     help="tree edges per slot, the average of a lane's pooled halves: 'bounded' (default, "
                          "8*S*A + H*W*A: ~5x the high-water mark measured at configs[1] and configs[3]), "
@@ -111,7 +112,7 @@ def parse():
     args = ap.parse_args()
     chess = args.game == "chess"
     for k, c4, ch in (("steps", 30, 3), ("warmup", 5, 2), ("slots", 4096, 256), ("sims", 100, 800),
-                      ("cache_log2", 26, 20)):
+                      ("cache_log2", 26, 0)):
         if getattr(args, k) is None:
             setattr(args, k, ch if chess else c4)
     return args
@@ -455,12 +456,18 @@ def chess_main(args):
     eng.timer(True)
     st0 = eng.stats()
     t0 = time.perf_counter()
-    # as the Connect-N window: enqueue move m, then copy to the host the games
-    # move m-1 finished (az_chess_selfplay_drain never waits for the running move)
+    # the K moves in one synchronous call, then the drain of the games they
+    # finished (inside the timed region).  The Connect-N window's form --
+    # enqueue move m, drain move m - 1 -- measured 6% slower here: 1.569 vs
+    # 1.674 M expansions/s on one box (profiles/r6/ab_chess_win.txt; kept as
+    # AZ_CHESS_ASYNC_WINDOW=1, the drain API is the same)
     parts = []
-    for _ in range(args.steps):
-        eng.selfplay_step(1, sync=False)
-        parts.append(eng.selfplay_drain())
+    if os.environ.get("AZ_CHESS_ASYNC_WINDOW") == "1":
+        for _ in range(args.steps):
+            eng.selfplay_step(1, sync=False)
+            parts.append(eng.selfplay_drain())
+    else:
+        eng.selfplay_step(args.steps)
     torch.cuda.synchronize()
     parts.append(eng.selfplay_drain())
     if world > 1:

@@ -437,7 +437,11 @@ __device__ void cache_insert_wave(const CTree& t, const ChessCache& c, int s, in
     else v = make_uint4((uint32_t)initial, 0u, 0u, 0u);
     reinterpret_cast<uint4*>(c.keys + idx)[lane] = v;
   }
-  __threadfence();  // every lane's key and payload stores, device-wide, before the publish
+  // every lane's key and payload stores drained, then one agent release
+  // before the publish (MI355X_MICROARCH.md, valid producer forms)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0)
     atomicExch(c.state + idx, az::cache_word(az::cache_fp(h),
                                              (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED,

@@ -649,54 +649,71 @@ __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, Tre
 // writer per distinct board (dedup), racing only for the bucket's first empty
 // slot or its least recently used entry kCacheEvictAge+ generations old
 // (az_tree.h); a lost race moves on to the next candidate.
+// Called by every thread of an insert block (u: the thread's evaluator row;
+// past the rows, no entry).  The entries' keys and payloads are published
+// behind ONE release per block (every wave's stores drained, a barrier, lane
+// 0's agent release, a barrier, then each thread's state word) instead of a
+// full fence per wave (MI355X_MICROARCH.md, valid producer forms).
 __device__ void cache_insert_row(const GameCfg& g, const TreeDev& t, const CacheDev& c,
                                  const float* __restrict__ probs, const float* __restrict__ values, int u) {
-  if (u >= *t.nn_count) return;
-  const Board b = t.nn_board[u];
-  const uint64_t h = board_hash(b);
-  const uint32_t gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t fp = cache_fp(h);
-  const uint32_t base = cache_bucket(c, h);
-  uint32_t w[kCacheBucket];
-#pragma unroll
-  for (int k = 0; k < kCacheBucket; ++k)
-    w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int slot = -1;
+  const int rows = *t.nn_count;
+  if ((u - (int)threadIdx.x) >= rows) return;  // block-uniform: the whole block past the rows
+  int idx = -1;
+  uint32_t word = 0;
   bool was_empty = false;
-  uint32_t tried = 0;  // slots whose CAS lost (claimed or refreshed meanwhile)
-  for (int attempt = 0; attempt < kCacheBucket && slot < 0; ++attempt) {
-    // candidate: the first empty slot, else the oldest evictable entry (the
-    // first of equal ages); scanned with constant indices (w stays in VGPRs)
-    int pick = -1;
-    uint32_t pst = 0, page = 0;
-    bool pempty = false;
+  if (u < rows) {
+    const Board b = t.nn_board[u];
+    const uint64_t h = board_hash(b);
+    const uint32_t gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t fp = cache_fp(h);
+    const uint32_t base = cache_bucket(c, h);
+    uint32_t w[kCacheBucket];
 #pragma unroll
-    for (int k = 0; k < kCacheBucket; ++k) {
-      const uint32_t st = w[k];
-      if (pempty || ((tried >> k) & 1u)) continue;
-      if (st == kCacheEmpty) {
-        pick = k, pst = st, pempty = true;
-      } else if (c.gen_size) {
-        const uint32_t age = cache_age(st, gen);
-        if (age >= kCacheEvictAge && age > page) pick = k, pst = st, page = age;
+    for (int k = 0; k < kCacheBucket; ++k)
+      w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t tried = 0;  // slots whose CAS lost (claimed or refreshed meanwhile)
+    for (int attempt = 0; attempt < kCacheBucket && idx < 0; ++attempt) {
+      // candidate: the first empty slot, else the oldest evictable entry (the
+      // first of equal ages); scanned with constant indices (w stays in VGPRs)
+      int pick = -1;
+      uint32_t pst = 0, page = 0;
+      bool pempty = false;
+#pragma unroll
+      for (int k = 0; k < kCacheBucket; ++k) {
+        const uint32_t st = w[k];
+        if (pempty || ((tried >> k) & 1u)) continue;
+        if (st == kCacheEmpty) {
+          pick = k, pst = st, pempty = true;
+        } else if (c.gen_size) {
+          const uint32_t age = cache_age(st, gen);
+          if (age >= kCacheEvictAge && age > page) pick = k, pst = st, page = age;
+        }
+      }
+      if (pick < 0) break;  // every entry of the bucket is in use: evaluated again when met
+      if (atomicCAS(c.state + base + pick, pst, cache_word(fp, gen, kCacheClaimed)) == pst) {
+        idx = (int)(base + pick);
+        was_empty = pempty;
+      } else {
+        tried |= 1u << pick;
       }
     }
-    if (pick < 0) return;  // every entry of the bucket is in use: evaluated again when met
-    if (atomicCAS(c.state + base + pick, pst, cache_word(fp, gen, kCacheClaimed)) == pst) {
-      slot = pick;
-      was_empty = pempty;
-    } else {
-      tried |= 1u << pick;
+    if (idx >= 0) {
+      c.keys[idx] = b;
+      float* dst = c.pay + (size_t)idx * (g.A + 1);
+      for (int a = 0; a < g.A; ++a) dst[a] = probs[(size_t)u * g.A + a];
+      dst[g.A] = values[u];
+      word = cache_word(fp, gen, kCacheReady);
     }
   }
-  if (slot < 0) return;
-  const uint32_t idx = base + slot;
-  c.keys[idx] = b;
-  float* dst = c.pay + (size_t)idx * (g.A + 1);
-  for (int a = 0; a < g.A; ++a) dst[a] = probs[(size_t)u * g.A + a];
-  dst[g.A] = values[u];
-  __threadfence();
-  atomicExch(c.state + idx, cache_word(fp, gen, kCacheReady));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (idx < 0) return;
+  atomicExch(c.state + idx, word);
   wave_stat(t, kStatCacheInserts);
   if (was_empty) wave_claim64(c.ctl + 2);
   // every gen_size-th insert since the clear opens a new generation
@@ -722,7 +739,10 @@ __global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, const Board*
 // the entries the leaves expanded here read were stamped with the current
 // generation by select, which an insert never evicts (kCacheEvictAge,
 // az_tree.h), so the two halves are independent and share one launch.
-template <int MAXA, bool INSERT>
+// SHAPE 1 (Connect-4, 6x7, n = 4, gravity): the legal columns are the top
+// row's empty cells, in action order = moves order, and fewer than 8 of them,
+// so normalize's numpy sum is the plain left-to-right one -- no cell scans.
+template <int MAXA, bool INSERT, int SHAPE = 0>
 __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
                                                      const float* __restrict__ probs,
                                                      const float* __restrict__ values, int exp_blocks) {
@@ -746,12 +766,28 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     v = values[row];
   }
   float masked[MAXA];
-  int nl = 0;
-  for (int a = 0; a < g.A; ++a)
-    if (action_cell(g, b, a) >= 0) masked[nl++] = p[a];
   int moves[MAXA];
-  const int nm = moves_order(g, b, moves);
-  const float sum = pairwise_sum_f32(masked, nl);
+  int nl = 0, nm = 0;
+  float sum = 0.0f;
+  uint32_t legal = 0;
+  if constexpr (SHAPE == 1) {
+    static_assert(MAXA >= 7, "Connect-4 actions");
+    legal = (uint32_t)(~(b.own[0] | b.opp[0])) & 0x7fu;  // columns with room
+    float pa[7];
+#pragma unroll
+    for (int a = 0; a < 7; ++a) pa[a] = p[a];  // issued together
+#pragma unroll
+    for (int a = 0; a < 7; ++a)
+      if ((legal >> a) & 1u) sum += pa[a];  // numpy pairwise_sum below 8 elements: 0 + a0 + a1 + ...
+#pragma unroll
+    for (int a = 0; a < 7; ++a) masked[a] = pa[a];
+    nl = nm = __builtin_popcount(legal);
+  } else {
+    for (int a = 0; a < g.A; ++a)
+      if (action_cell(g, b, a) >= 0) masked[nl++] = p[a];
+    nm = moves_order(g, b, moves);
+    sum = pairwise_sum_f32(masked, nl);
+  }
   Edge* E = slot_edges(g, t, s);
   int first = t.arena_top[s];
   if (g.halves > 1) {
@@ -779,18 +815,36 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     flag_error(t, kErrArena);
     return;
   }
-  for (int k = 0; k < nm; ++k) {
-    Edge e;
-    e.W = 0.0;
-    // zip(probabilities, board.moves) pairs priors (action order) with moves
-    // (moves order) by position -- mcts.py:151; identical orders with gravity
-    e.prior = sum == 0.0f ? 1.0 / (double)nl : (double)(masked[k] / sum);
-    e.N = 0;
-    e.child = kNoChild;
-    e.child_n = 0;
-    e.action = (int16_t)(moves[k] | (sum == 0.0f ? kPrior64 : 0));
-    e.child_value = 0.f;
-    E[first + k] = e;
+  if constexpr (SHAPE == 1) {
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 7; ++a)
+      if ((legal >> a) & 1u) {
+        Edge e;
+        e.W = 0.0;
+        e.prior = sum == 0.0f ? 1.0 / (double)nl : (double)(masked[a] / sum);
+        e.N = 0;
+        e.child = kNoChild;
+        e.child_n = 0;
+        e.action = (int16_t)(a | (sum == 0.0f ? kPrior64 : 0));
+        e.child_value = 0.f;
+        E[first + k] = e;
+        ++k;
+      }
+  } else {
+    for (int k = 0; k < nm; ++k) {
+      Edge e;
+      e.W = 0.0;
+      // zip(probabilities, board.moves) pairs priors (action order) with moves
+      // (moves order) by position -- mcts.py:151; identical orders with gravity
+      e.prior = sum == 0.0f ? 1.0 / (double)nl : (double)(masked[k] / sum);
+      e.N = 0;
+      e.child = kNoChild;
+      e.child_n = 0;
+      e.action = (int16_t)(moves[k] | (sum == 0.0f ? kPrior64 : 0));
+      e.child_value = 0.f;
+      E[first + k] = e;
+    }
   }
   t.arena_top[s] = first + nm;
   const int depth = t.path_len[s];
@@ -1110,7 +1164,10 @@ void launch_expand(const GameCfg& g, const TreeDev& t, const CacheDev& c, const 
   const int eb = game_blocks(g.slots);
   const bool ins = c.enabled;
   const int grid = eb + (ins ? game_blocks(g.slots) : 0);
-  if (g.A <= 16) {
+  if (g.H == 6 && g.W == 7 && g.n == 4 && g.gravity) {  // Connect-4: the top-row form
+    if (ins) expand_kernel<16, true, 1><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
+    else expand_kernel<16, false, 1><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
+  } else if (g.A <= 16) {
     if (ins) expand_kernel<16, true><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
     else expand_kernel<16, false><<<grid, kGameBlock, 0, s>>>(g, t, c, probs, values, eb);
   } else {

@@ -26,7 +26,8 @@ class ConfigSelfPlay:
     lanes = 0                    # slot groups on separate HIP streams (0 = auto)
     chess_concurrent_games = 256 # chess device slots (BASELINE configs[4]: 2048 games / 8 GPUs)
     chess_max_plies = 512        # chess games stop (as draws) here; the reference has no cap
-    chess_cache_log2 = 20        # chess plays_inferences entries (2^k, ~1.1 KB each); 0 = no cache
+    chess_cache_log2 = 0         # chess plays_inferences entries (2^k, ~1.1 KB each; 0 = off: slower in
+                                 # the opening at 0.18 hits, profiles/r6/ab_chess_r5.txt)
 
 
 class ConfigChess:
