@@ -338,19 +338,25 @@ __device__ bool cache_probe_wave(const CTree& t, const ChessCache& c, int s, int
       w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int hit = -1;
     uint32_t hst = 0;
+    uint32_t cm = 0;  // fingerprint matches (buckets fill in slot order), then one acquire, then the keys
     bool stop = false;
 #pragma unroll
     for (int k = 0; k < az::kCacheBucket; ++k) {
       const uint32_t st = w[k];
       if (stop) continue;
-      if (st == az::kCacheEmpty) {  // buckets fill in slot order
-        stop = true;
-      } else if ((st & 3u) == az::kCacheReady && (st >> 16) == fp) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (st == az::kCacheEmpty) stop = true;
+      else if ((st & 3u) == az::kCacheReady && (st >> 16) == fp) cm |= 1u << k;
+    }
+    if (cm) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (; cm; cm &= cm - 1) {
+        const int k = __builtin_ctz(cm);
         if (same_key(c.keys + base + k, key, initial)) {
           hit = k;
-          hst = st;
-          stop = true;
+#pragma unroll
+          for (int kk = 0; kk < az::kCacheBucket; ++kk)
+            if (kk == k) hst = w[kk];
+          break;
         }
       }
     }

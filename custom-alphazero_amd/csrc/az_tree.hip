@@ -231,19 +231,29 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
       w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int hit = -1;
     uint32_t hst = 0;
+    // the fingerprint matches (inserts fill a bucket in slot order: nothing
+    // past an empty slot), then ONE acquire for the wave -- a fence per
+    // candidate position had the wave invalidating its CU's L1 (the tower
+    // tiles' weight fragments too) up to 16 times -- then the keys in order
+    uint32_t cm = 0;
     bool stop = false;
 #pragma unroll
     for (int k = 0; k < kCacheBucket; ++k) {
       const uint32_t st = w[k];
       if (stop) continue;
-      if (st == kCacheEmpty) {  // inserts fill a bucket in slot order: nothing past this
-        stop = true;
-      } else if ((st & 3u) == kCacheReady && (st >> 16) == fp) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (st == kCacheEmpty) stop = true;
+      else if ((st & 3u) == kCacheReady && (st >> 16) == fp) cm |= 1u << k;
+    }
+    if (cm) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (; cm; cm &= cm - 1) {
+        const int k = __builtin_ctz(cm);
         if (same_board(c.keys[base + k], b)) {
           hit = k;
-          hst = st;
-          stop = true;
+#pragma unroll
+          for (int kk = 0; kk < kCacheBucket; ++kk)
+            if (kk == k) hst = w[kk];  // (constant indices: w stays in VGPRs)
+          break;
         }
       }
     }
