@@ -63,7 +63,7 @@ int fail_abi(int code, const std::string& msg) { return fail(code, msg); }
 // the evaluator is deterministic per board).
 struct Lane {
   int first = 0, n = 0;
-  int32_t* counts = nullptr;  // [2][4] eval/miss/nn/dup counts by simulation parity
+  int32_t* counts = nullptr;  // [2][4][kCountStride] eval/miss/nn/dup counts by simulation parity
   hipStream_t stream = nullptr;
   az::GameCfg g{};
   az::TreeDev t{};
@@ -180,11 +180,12 @@ az::Board board_from_cells(const int8_t* cells, int HW) {
 
 // point a tree view's four counters at parity p of the [2][4] block at base
 void set_counts(az::TreeDev& t, int32_t* base, int p) {
-  t.eval_count = base + 4 * p;
-  t.miss_count = t.eval_count + 1;
-  t.nn_count = t.eval_count + 2;
-  t.dup_count = t.eval_count + 3;
-  t.next_counts = base + 4 * (p ^ 1);
+  constexpr int K = az::kCountStride;
+  t.eval_count = base + 4 * K * p;
+  t.miss_count = t.eval_count + K;
+  t.nn_count = t.eval_count + 2 * K;
+  t.dup_count = t.eval_count + 3 * K;
+  t.next_counts = base + 4 * K * (p ^ 1);
 }
 
 void cells_from_board(const az::Board& b, int HW, int8_t* cells) {
@@ -420,12 +421,12 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
     int rc;
     size_t cap = 1024;
     while (cap < 4 * (size_t)n) cap <<= 1;
-    if ((rc = e->alloc(&t.eval_count, 8)) || (rc = e->alloc(&t.step_tag, cap)) ||
+    if ((rc = e->alloc(&t.eval_count, az::kCountWords)) || (rc = e->alloc(&t.step_tag, cap)) ||
         (rc = e->alloc(&t.step_row, cap)) || (rc = e->alloc(&t.sel_done, 1)))
       return rc;
     AZ_HIP(hipMemset(t.sel_done, 0, sizeof(uint32_t)));
     AZ_HIP(hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)));
-    AZ_HIP(hipMemset(t.eval_count, 0, 8 * sizeof(int32_t)));
+    AZ_HIP(hipMemset(t.eval_count, 0, az::kCountWords * sizeof(int32_t)));
     set_counts(t, t.eval_count, 0);
     t.step_mask = (uint32_t)(cap - 1);
     t.epoch = 0;
@@ -852,7 +853,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_board, S)) ||
       (rc = e->alloc(&t.eval_src, S)) || (rc = e->alloc(&t.miss_q, S)) ||
       (rc = e->alloc(&t.nn_board, S)) ||
-      (rc = e->alloc(&t.eval_count, 8)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
+      (rc = e->alloc(&t.eval_count, az::kCountWords)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
       (rc = e->alloc(&t.sel_done, 1)) ||
       (rc = e->alloc(&t.last_move, S)) || (rc = e->alloc(&t.last_status, S)) ||
       (rc = e->alloc(&t.last_policy, S * A)))
@@ -899,7 +900,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       return cleanup(fail(AZ_E_HIP, "cache memset failed"));
   }
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(t.eval_count, 0, 8 * sizeof(int32_t)) != hipSuccess ||
+      hipMemset(t.eval_count, 0, az::kCountWords * sizeof(int32_t)) != hipSuccess ||
       hipMemset(t.sel_done, 0, sizeof(uint32_t)) != hipSuccess ||
       hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
     return cleanup(fail(AZ_E_HIP, "memset failed"));

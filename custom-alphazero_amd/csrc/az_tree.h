@@ -19,23 +19,31 @@ struct Edge {
 };
 static_assert(sizeof(Edge) == 32, "Edge must stay 32 bytes");
 
-// Counters/stat words (unsigned long long, device).
+// Counters/stat words (unsigned long long, device), each on a 128-byte line
+// of its own (kStatStride words apart): every wave of every lane adds to them
+// (wave-aggregated atomics), and counters sharing a line serialised in its
+// L2 channel (round 6).  An index below is the word offset of its counter.
+constexpr int kStatStride = 16;
 enum : int {
-  kStatExpansions = 0,   // evaluate_and_expand calls
-  kStatTerminal = 1,     // terminal leaf visits
-  kStatGamesDone = 2,
-  kStatErrors = 3,       // bit flags below
-  kStatSims = 4,         // per-slot simulations
-  kStatPlies = 5,
-  kStatNextGame = 6,     // next game id to hand to a free slot
-  kStatCacheHits = 7,    // expansions served by the transposition cache
-  kStatNNEvals = 8,      // boards the evaluator actually computed
-  kStatCacheInserts = 9,
-  kStatPathEdges = 10,   // edges on the selected paths (sum of select depths)
-  kStatMaxRetained = 11, // compaction: most edges kept (atomicMax)
-  kStatPoolHigh = 12,    // pooled arenas: most edges a lane's half held at a move's end (atomicMax)
-  kStatCount = 13        // (kStatCacheInserts counts since engine creation; CacheDev::ctl since a clear)
+  kStatExpansions = 0 * kStatStride,   // evaluate_and_expand calls
+  kStatTerminal = 1 * kStatStride,     // terminal leaf visits
+  kStatGamesDone = 2 * kStatStride,
+  kStatErrors = 3 * kStatStride,       // bit flags below
+  kStatSims = 4 * kStatStride,         // per-slot simulations
+  kStatPlies = 5 * kStatStride,
+  kStatNextGame = 6 * kStatStride,     // next game id to hand to a free slot
+  kStatCacheHits = 7 * kStatStride,    // expansions served by the transposition cache
+  kStatNNEvals = 8 * kStatStride,      // boards the evaluator actually computed
+  kStatCacheInserts = 9 * kStatStride,
+  kStatPathEdges = 10 * kStatStride,   // edges on the selected paths (sum of select depths)
+  kStatMaxRetained = 11 * kStatStride, // compaction: most edges kept (atomicMax)
+  kStatPoolHigh = 12 * kStatStride,    // pooled arenas: most edges a lane's half held at a move's end (atomicMax)
+  kStatCount = 13 * kStatStride        // words (kStatCacheInserts counts since engine creation; CacheDev::ctl since a clear)
 };
+// a lane's per-simulation queue counters (eval, miss, nn, dup), one block per
+// simulation parity, each counter on a 128-byte line of its own
+constexpr int kCountStride = 32;
+constexpr int kCountWords = 2 * 4 * kCountStride;
 enum : unsigned long long {
   kErrArena = 1, kErrPow = 2, kErrPath = 4, kErrIllegal = 8, kErrNoRoot = 16,
   kErrActRange = 32,  // a conv16 activation beyond the split16 range (|x| > 32752)
@@ -90,7 +98,7 @@ struct TreeDev {
   // eval/miss/nn/dup counts are one block of 4; two blocks alternate by
   // simulation (epoch parity): the select kernel zeroes the other block, the
   // next simulation's, so no memset launch sits between simulations
-  int32_t* next_counts;        // [4] the block the next simulation uses
+  int32_t* next_counts;        // [4 * kCountStride] the block the next simulation uses
   uint32_t* sel_done;          // [1] select blocks finished (the last one resolves the dedup, 0 after)
   uint64_t* step_tag;          // [step_cap] per-simulation dedup table: (epoch << 32) | fp32
   int32_t* step_row;           // [step_cap] evaluator row of the tag's owner

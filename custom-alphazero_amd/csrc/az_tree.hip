@@ -346,7 +346,7 @@ __device__ __forceinline__ bool argmax_before(double v, int i, double bv, int bi
 // Serial descent, one lane per game (used when the action space exceeds 64).
 template <bool NOISE>
 __device__ __forceinline__ void select_body(const GameCfg& g, const TreeDev& t, const CacheDev& c) {
-  if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
+  if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x * kCountStride] = 0;  // next simulation's counts
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= g.slots || t.game_id[s] < 0) return;
   const BoardMasks mk = board_masks(g);
@@ -430,7 +430,7 @@ __device__ __forceinline__ void select_body(const GameCfg& g, const TreeDev& t, 
 // play (play_c64); 0: any shape through play_bb's runtime masks.
 template <int L, bool NOISE, int SHAPE>
 __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDev& t, const CacheDev& c) {
-  if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x] = 0;  // next simulation's counts
+  if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x * kCountStride] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = gid / L, j = gid % L;
 #ifdef AZ_SEL_STAMPS
