@@ -890,11 +890,15 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       return cleanup(rc);
     cd.mask = (uint32_t)(cap - 1);
     cd.enabled = 1;
-    // LRU eviction by generations of cap/kCacheGenDiv inserts, when a generation
-    // outlasts three moves of every slot's inserts (the lane-drift bound,
-    // az_tree.h); otherwise the table only fills (entries are never overwritten)
-    const unsigned long long gen = cap / az::kCacheGenDiv;
-    cd.gen_size = gen > 3ull * (unsigned long long)g.slots * (unsigned long long)g.sims ? gen : 0;
+    // LRU eviction by generations of cap/kCacheGenDiv inserts -- or, for a
+    // larger batch, of more than three moves of every slot's inserts (the
+    // lane-drift bound, az_tree.h: configs[2]'s 8192 x S=200 and configs[3]'s
+    // 4096 x S=400 need it at 2^26 entries) while at most cap/4 (four
+    // generations per turnover keep the LRU order meaningful); otherwise the
+    // table only fills (entries are never overwritten)
+    const unsigned long long bound = 3ull * (unsigned long long)g.slots * (unsigned long long)g.sims + 1;
+    const unsigned long long gen = std::max<unsigned long long>(cap / az::kCacheGenDiv, bound);
+    cd.gen_size = gen <= cap / 4 ? gen : 0;
     if (hipMemset(cd.state, 0, cap * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(cd.ctl, 0, 4 * sizeof(unsigned long long)) != hipSuccess)
       return cleanup(fail(AZ_E_HIP, "cache memset failed"));

@@ -248,9 +248,12 @@ def test_cache_eviction_generations_are_transparent(lanes):
         np.testing.assert_array_equal(got["moves"], ref["moves"])
         np.testing.assert_array_equal(got["policy"].view(np.uint64), ref["policy"].view(np.uint64))
         assert got["expansions"] == ref["expansions"]
-    # too small for the lane-drift bound (gen_size <= 3 * slots * sims): eviction
-    # stays off and the table only fills
-    small = az.Engine(6, 7, 4, True, 50, slots=32, evaluator=az.EVAL_SYNTHETIC, cache_log2=16, lanes=lanes)
+    # a generation must outlast three moves of every slot's inserts (the
+    # lane-drift bound): cap/16 below it takes 3 * slots * sims + 1 inserts per
+    # generation while that is at most cap/4; smaller tables only fill
+    mid = az.Engine(6, 7, 4, True, 50, slots=32, evaluator=az.EVAL_SYNTHETIC, cache_log2=16, lanes=lanes)
+    assert mid.stats()["cache_gen_size"] == 3 * 32 * 50 + 1
+    small = az.Engine(6, 7, 4, True, 50, slots=32, evaluator=az.EVAL_SYNTHETIC, cache_log2=14, lanes=lanes)
     assert small.stats()["cache_gen_size"] == 0
 
 
