@@ -672,20 +672,6 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
   for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 2) sm.flag[tid] = 0;  // published by the barrier after the stem's MFMAs
 
-  // the tile's boards (b0 .. b0 + nbrd - 1: known before the slot plan says
-  // which slot takes which), issued first so the stem's board operands wait
-  // for one memory round trip instead of two (plan, then boards)
-  // (not the 192-row in-place tile: at the edge of its register budget)
-  constexpr int kPreBoards = 4;
-  constexpr bool kPre = !ROWS && MBT <= 8;
-  Board tbd[kPreBoards];
-  if constexpr (kPre) {
-    if (boards && bpw <= kPreBoards) {
-#pragma unroll
-      for (int k = 0; k < kPreBoards; ++k)
-        if (k < nbrd) tbd[k] = boards[b0 + k];
-    }
-  }
   const int mh = wave % NWM, nq = wave / NWM, r16 = lane & 15, gq = lane >> 4;
   // a lane's slots r0 + 16 mb and their pixel words: the slot plan's
   // (T.slot_pix, a full tile's boards; the boards past this tile's are
@@ -803,18 +789,7 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
       Board bd[SG];
       if (boards) {
 #pragma unroll
-        for (int i = 0; i < SG; ++i) {
-          const int bi = yx[g0 + i] >> 16;
-          if (kPre && bpw <= kPreBoards) {  // the prefetched board, picked by selects (no dynamic index)
-            Board sel = tbd[0];
-#pragma unroll
-            for (int k = 1; k < kPreBoards; ++k)
-              if (bi == k) sel = tbd[k];
-            bd[i] = sel;
-          } else {
-            bd[i] = gld(boards + b0 + bi);
-          }
-        }
+        for (int i = 0; i < SG; ++i) bd[i] = gld(boards + b0 + (yx[g0 + i] >> 16));
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
