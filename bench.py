@@ -291,7 +291,9 @@ def conv_kernel_name(conv_algo, chess=False, tower=False):
                 "operands as two fp16 terms, 3 products per k-step -- activations double-buffered in LDS, 1x1 "
                 "projection residuals, head 1x1 convs; the 1880-logit dense heads follow in their own kernels)")
     if conv_algo == 0 and not chess:
-        return ("tower16_kernel (the whole forward in one launch per lane-simulation: the stem and the "
+        return ("tower16_kernel / tower16_dual_kernel (Connect-4: 96-row tiles of two boards when the launch "
+                "holds few live boards, else 128-row tiles of three) (the whole forward in one launch per "
+                "lane-simulation: the stem and the "
                 "residual tower's 8 3x3 convs as implicit GEMMs on the 16x16x32 fp16 MFMA -- fp32-accurate, both operands "
                 "as two fp16 terms, 3 products per k-step -- with activations double-buffered in LDS, 1x1 projection "
                 "residuals, head 1x1 convs, dense heads, softmax, tanh)")
@@ -516,7 +518,7 @@ def chess_main(args):
     avg_ms = st1["conv_ms"] / max(launches, 1)
     roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, avg_ms, st1["conv_busy_ms"],
                          local_evals, launches, direct_flop, issued,
-                         os.path.join(REPO, "profiles", "r5", "pmc_chess.json"),
+                         os.path.join(REPO, "profiles", "r6", "pmc_chess.json"),
                          ("tower16_rows" if tower else "f16x2") if args.conv_algo != 1 else "direct", chess=True,
                          tower=tower)
     if rank == 0:
@@ -861,15 +863,19 @@ def main():
     HW, F = args.height * args.width, 128
     direct_flop = HW * 2 * F * F * 19 * args.depth
     issued = 3 * direct_flop if args.conv_algo != 1 else direct_flop
-    if args.conv_algo == 0 and st1.get("issued_flop_per_board", 0) > 0:
-        # the tower reports what it issues: its tiles' pad rows and stem in,
-        # the slot plan's skipped border taps (exact zeros) out
-        issued = st1["issued_flop_per_board"]
     per_forward = 1 if args.conv_algo == 0 else 2 * args.depth
     conv_avg_ms = conv_ms / max(conv_launches, 1)
     boards_per_launch = local_evals / max(conv_launches / per_forward, 1)
-    pmc = os.path.join(REPO, "profiles", "r5", "pmc_tower.json")
-    # the PMC entry of this board shape (profiles/r5/collect_pmc.sh: 6x7 "tower16", 9x9 "tower16_9x9")
+    if args.conv_algo == 0 and st1.get("issued_flop_per_board", 0) > 0:
+        # the tower reports what it issues: its tiles' pad rows and stem in,
+        # the slot plan's skipped border taps (exact zeros) out; the dual
+        # launch runs its smaller tiles at <= tower_small_max_boards live
+        # boards (judged here by the mean launch)
+        issued = st1["issued_flop_per_board"]
+        if 0 < boards_per_launch <= st1.get("tower_small_max_boards", -1):
+            issued = st1["issued_flop_per_board_small"]
+    pmc = os.path.join(REPO, "profiles", "r6", "pmc_tower.json")
+    # the PMC entry of this board shape (profiles/r6/collect_pmc.sh: 6x7 "tower16", 9x9 "tower16_9x9")
     pmc_key = {0: "tower16", 1: "direct", 2: "f16x2"}[args.conv_algo]
     if (args.height, args.width) != (6, 7):
         pmc_key += f"_{args.height}x{args.width}"

@@ -1501,6 +1501,7 @@ int az_chess_stats(az_chess_engine* e, az_stats* st) {
     st->cache_capacity = (int64_t)e->cache.mask + 1;
   }
   st->issued_flop_per_board = e->net.use_tower && e->net.tower ? e->net.issued_flop_per_board : 0.0;
+  st->tower_small_max_boards = -1;  // (chess: one tile height)
   st->active_slots = std::count_if(gid.begin(), gid.end(), [](int64_t v) { return v >= 0; });
   // conv-busy time = union of the timed conv intervals over all lanes
   std::vector<az::ConvTimer*> timers = {&e->timer};

@@ -726,6 +726,9 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     net.tower_alt_rows = tn.alt_rows;
     // (chess: as self-play runs it, the stem's known-zero input chunks 0-1 skipped)
     net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip, rows_tower, 2);
+    net.issued_flop_per_board_small =
+        tn.alt_rows ? tower16_issued_flop_per_board(HW, tn.alt_rows, net.depth, tn.alt_skip, rows_tower, 2) : 0.0;
+    net.tower_small_max_boards = tn.alt_rows ? tn.alt_max_boards : -1;
   }
   net.ready = true;
   return 0;
@@ -1168,6 +1171,8 @@ int az_stats_get(az_engine* e, az_stats* st) {
     st->arena_pool_high = (int64_t)h[az::kStatPoolHigh];
   }
   st->issued_flop_per_board = e->net.issued_flop_per_board;
+  st->issued_flop_per_board_small = e->net.issued_flop_per_board_small;
+  st->tower_small_max_boards = e->net.tower_small_max_boards;
   return 0;
 }
 

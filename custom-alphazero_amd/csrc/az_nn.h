@@ -117,6 +117,8 @@ struct NetDev {
   int lanes = 1;              // the engine's lanes (streams whose towers share the CUs): the dual threshold
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)
   int board_h = 0, board_w = 0;  // Connect-N board (the tower's slot plan)
+  double issued_flop_per_board_small = 0;  // the dual launch's alternative tiles (az_stats)
+  int tower_small_max_boards = -1;          // TowerNet::alt_max_boards (az_stats)
   double issued_flop_per_board = 0;  // MFMA FLOP a forward issues per board (tower; az_stats)
   float* stem_w = nullptr;  // in_ch == 4: [36][F] (k = tap*4 + c), VALU stem kernels
   float* stem_b = nullptr;  // [F]

@@ -72,6 +72,7 @@ class Stats(ctypes.Structure):
         ("max_retained", ctypes.c_int64), ("cache_entries", ctypes.c_int64),
         ("arena_edges", ctypes.c_int64), ("issued_flop_per_board", ctypes.c_double),
         ("arena_pool_edges", ctypes.c_int64), ("arena_pool_high", ctypes.c_int64),
+        ("issued_flop_per_board_small", ctypes.c_double), ("tower_small_max_boards", ctypes.c_int64),
     ]
 
     def as_dict(self):

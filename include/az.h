@@ -153,6 +153,10 @@ typedef struct az_stats {
                                      k-steps of 96 MFMAs (28.3 MFLOP) per board */
     int64_t arena_pool_edges; /* compact: edges of every lane's two pool halves (0 uncompacted) */
     int64_t arena_pool_high;  /* compact: most edges one lane's half held at a move's end */
+    double issued_flop_per_board_small; /* the dual tower launch's smaller tiles (Connect-4: 96 rows of
+                                           two boards), which a launch runs when it holds at most
+                                           tower_small_max_boards live boards; 0 = no dual launch */
+    int64_t tower_small_max_boards;     /* that threshold (2 x CUs / lanes; -1 = no dual launch) */
 } az_stats;
 
 int az_abi_version(void);
