@@ -685,6 +685,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     tn.alt_slot_pix = nullptr;
     tn.alt_skip[0] = tn.alt_skip[1] = 0;
     tn.alt_max_boards = -1;
+    tn.alt_staged_floats = tn.alt_wpd_lds = tn.alt_wv1_lds = 0;
     if (!rows_tower && tn.tile_rows == 128 && tn.dbuf && tower16_boards_per_tile(HW, 128) == 3 &&
         tower16_boards_per_tile(HW, 96) == 2 && tower16_heads_fit(HW, 96, A, net.hidden, true)) {
       int dev = 0, cus = 0;
@@ -692,6 +693,15 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
       AZ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
       tn.alt_rows = 96;
       tn.alt_max_boards = 2 * std::max(1, cus / std::max(1, net.lanes));
+      // the largest staging the 96-row layout holds (it has 64 rows fewer
+      // than the 128-row one: the whole blob, where 128 rows leave wv1 in L2)
+      for (int i = 0; i < 3; ++i)
+        if (tower16_lds_bytes(HW, 96, prefix[i], true) <= kTowerLdsMax) {
+          tn.alt_staged_floats = prefix[i];
+          tn.alt_wv1_lds = i == 0;
+          tn.alt_wpd_lds = i <= 1;
+          break;
+        }
       std::vector<int> pix;
       int skip[2] = {0, 0};
       if (!net.tower_natural_order && net.board_h * net.board_w == HW)
@@ -724,6 +734,7 @@ int load_network(NetDev& net, const az_tensor* tensors, int n, int in_ch, int HW
     net.tower_dbuf = tn.dbuf != 0;
     net.tower_rows = tn.tile_rows;
     net.tower_alt_rows = tn.alt_rows;
+    net.tower_alt_staged = tn.alt_staged_floats;
     // (chess: as self-play runs it, the stem's known-zero input chunks 0-1 skipped)
     net.issued_flop_per_board = tower16_issued_flop_per_board(HW, tn.tile_rows, net.depth, tn.skip, rows_tower, 2);
     net.issued_flop_per_board_small =

@@ -48,6 +48,9 @@ struct TowerNet {
   const int* alt_slot_pix;
   int alt_skip[2];
   int alt_max_boards;
+  // its LDS staging: the blob prefix (the 96-row layout holds the whole blob,
+  // value dense wv1 included, where the 128-row one leaves wv1 in L2)
+  int alt_staged_floats, alt_wpd_lds, alt_wv1_lds;
 };
 // the slot plan of 128-row tiles: border blocks (16 slots whose pixels all
 // sit on one board edge) skip the three taps that read past that edge; empty
@@ -76,7 +79,8 @@ void tower16_stem_pack(const double* w, int e, std::vector<uint16_t>& out);
 // boards (self-play: the eval queue's boards) or x ([n][HW][4] one-hot planes,
 // az_forward) -> probs [n][A], values [n]; count (device, may be null -> n_max)
 // alt_rows: the TowerNet's alternative tile height (a dual launch), 0 = none
-void launch_tower16(const TowerNet* net, int tile_rows, int alt_rows, int staged_floats, bool dbuf, const Board* boards,
+void launch_tower16(const TowerNet* net, int tile_rows, int alt_rows, int alt_staged_floats, int staged_floats,
+                    bool dbuf, const Board* boards,
                     const float4* x, const int* count, int n_max, int H, int W, int A, float* probs, float* values,
                     unsigned long long* err, hipStream_t s);
 // the input-row form (chess): rows [n][HW] of 512 B split16 (t0 of F
@@ -113,6 +117,7 @@ struct NetDev {
   int tower_staged = 0;       // its blob floats staged in LDS
   bool tower_dbuf = false;    // its activations double-buffered (TowerNet::dbuf)
   int tower_rows = 0;         // its tile rows (TowerNet::tile_rows)
+  int tower_alt_staged = 0;   // its staged blob floats (TowerNet::alt_staged_floats)
   int tower_alt_rows = 0;     // the dual launch's alternative tile rows (TowerNet::alt_rows; 0 none)
   int lanes = 1;              // the engine's lanes (streams whose towers share the CUs): the dual threshold
   int in_ch = 4;            // input planes: 4 (Connect-N) or 118 (chess, padded to F)

@@ -709,7 +709,7 @@ void launch_forward(const NetDev& net, const void* x, const int* count, int n_ma
   const bool f16 = net.algo == AZ_CONV_F16X2;
   if (f16 && net.use_tower && net.in_ch == 4 && net.tower) {  // the whole forward in one launch
     if (timer) timer->begin(s);
-    launch_tower16(net.tower, net.tower_rows, net.tower_alt_rows, net.tower_staged, net.tower_dbuf, boards,
+    launch_tower16(net.tower, net.tower_rows, net.tower_alt_rows, net.tower_alt_staged, net.tower_staged, net.tower_dbuf, boards,
                    boards ? nullptr : static_cast<const float4*>(x), count, n_max, H, W, A, probs, values, net.err, s);
     if (timer) timer->end(s, 1);
     return;

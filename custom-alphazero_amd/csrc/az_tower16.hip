@@ -667,8 +667,14 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
   const int zrow = TR;
   T16_RSTAMP(22);
   T16_STAMP(0);
+  // the alternative tile height of a dual launch: a slot plan and an LDS
+  // staging of its own
+  const bool alt = 16 * MBT != T.tile_rows && 16 * MBT == T.alt_rows;
   // small weights into LDS, in the background of the stem
-  dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob, T.staged_floats / 4, wave, lane);
+  dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob, (alt ? T.alt_staged_floats : T.staged_floats) / 4, wave,
+                 lane);
+  const bool wpd_lds = alt ? T.alt_wpd_lds : T.wpd_lds;
+  const bool wv1_lds = alt ? T.alt_wv1_lds : T.wv1_lds;
   for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 2) sm.flag[tid] = 0;  // published by the barrier after the stem's MFMAs
 
@@ -680,8 +686,6 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
   int yx[MBW];
   // (the plan is for the TowerNet's tile height: a smaller tile of the same
   // boards -- chess's 64-row tiles -- runs in natural order, the same bits)
-  // (the alternative tile height of a dual launch has a plan of its own)
-  const bool alt = 16 * MBT != T.tile_rows && 16 * MBT == T.alt_rows;
   const bool planned = 16 * MBT == T.tile_rows || alt;
   // wv1 staged behind X's dead tile only in the tile height it was sized for
   // (tower16_wv1_xtile_fits); another tile height reads it from L2
@@ -1154,10 +1158,10 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
       else value_part_n(wv1, IC<kTowerMaxBoards>{});
     };
     for (int base = 0;; base += OP) {  // block-uniform
-      if (T.wpd_lds) policy_part(base, blob + T.off_wpd);
+      if (wpd_lds) policy_part(base, blob + T.off_wpd);
       else policy_part(base, gbl(T.blob + T.off_wpd));
       if (base == 0) {
-        if (T.wv1_lds) value_part(blob + T.off_wv1);
+        if (wv1_lds) value_part(blob + T.off_wv1);
         else if (wv1_xt) value_part(reinterpret_cast<const float*>(bufX) + TR * 48);
         else value_part(gbl(T.blob + T.off_wv1));
       }
@@ -1498,14 +1502,16 @@ static void launch_mbw(const TowerNet* net, int staged, bool dbuf, const Board* 
                                      first_chunk, err, s, lv);
 }
 
-void launch_tower16(const TowerNet* net, int tile_rows, int alt_rows, int staged, bool dbuf, const Board* boards,
+void launch_tower16(const TowerNet* net, int tile_rows, int alt_rows, int alt_staged, int staged, bool dbuf,
+                    const Board* boards,
                     const float4* x, const int* count, int n_max, int H, int W, int A, float* probs, float* values,
                     unsigned long long* err, hipStream_t s) {
   if (n_max <= 0) return;
   if (tile_rows == 128 && alt_rows == 96 && dbuf) {  // Connect-4: 96- or 128-row tiles by the live count
     const int bpw = tower16_boards_per_tile(H * W, 128), bpw2 = tower16_boards_per_tile(H * W, 96);
     const int grid = (n_max + bpw2 - 1) / bpw2;
-    const size_t bytes = tower16_lds_bytes(H * W, 128, staged, true);  // the larger layout
+    const size_t bytes = std::max(tower16_lds_bytes(H * W, 128, staged, true),  // the larger of the two layouts
+                                  tower16_lds_bytes(H * W, 96, alt_staged, true));
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&tower16_dual_kernel<8, 6, true>),
