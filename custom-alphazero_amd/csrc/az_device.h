@@ -29,8 +29,6 @@ struct GameCfg {
   double noise_alpha;           // dirichlet_noise_value (config.py:53)
   double noise_ratio;           // dirichlet_noise_ratio (config.py:54)
   int rng_skip;                 // MT19937 words a game's stream discards after seeding (az_config.rng_skip)
-  int runahead;                 // self-play with the cache: simulations a select launch may complete on
-                                // cache hits and terminal leaves (az_tree.hip, run-ahead); 0 = one per launch
 };
 
 // Edge::action carries the action index in its low 14 bits; kPrior64 marks

@@ -146,10 +146,6 @@ struct az_engine {
 
 namespace {
 
-// self-play run-ahead (az_tree.hip): simulations one select launch may
-// complete on cache hits before the slot waits for the network
-constexpr int kRunAhead = 8;
-
 int check_device_errors(az_engine* e) {
   unsigned long long err = 0;
   AZ_HIP(hipMemcpy(&err, e->t.stats + az::kStatErrors, sizeof(err), hipMemcpyDeviceToHost));
@@ -222,19 +218,15 @@ int host_evaluate(az_engine* e, Lane& L, const az::Board* rows, const int32_t* n
 }
 
 // one simulation for every active slot of a lane (MCTS.search body,
-// mcts.py:171-180), enqueued on the lane's stream; run-ahead (self-play):
-// each slot's select may complete up to `runahead` simulations on cache hits
-// (az_tree.hip), the move's remaining launches leave at once
-int simulate(az_engine* e, Lane& L, int runahead = 0) {
+// mcts.py:171-180), enqueued on the lane's stream
+int simulate(az_engine* e, Lane& L) {
   hipStream_t s = L.stream;
-  az::GameCfg g = L.g;
-  g.runahead = runahead;
   L.t.epoch += 1;  // fresh per-simulation dedup table (tags of older epochs read as empty)
   // eval_count, miss_count, nn_count, dup_count: the epoch parity's block of
   // four (zeroed by the previous simulation's select kernel, or at creation)
   set_counts(L.t, L.counts, L.t.epoch & 1);
   if (L.tree_timer.enabled) L.tree_timer.begin(s);
-  az::launch_select(g, L.t, e->cache, s);
+  az::launch_select(L.g, L.t, e->cache, s);
   if (L.tree_timer.enabled) L.tree_timer.end(s, 1);
   const az::Board* rows = L.t.eval_board;
   const int32_t* n_rows = L.t.eval_count;
@@ -255,7 +247,7 @@ int simulate(az_engine* e, Lane& L, int runahead = 0) {
     az::launch_synth_eval(L.g, rows, n_rows, L.probs, L.values, s);
   }
   if (L.tree_timer.enabled) L.tree_timer.begin(s);
-  az::launch_expand(g, L.t, e->cache, L.probs, L.values, s);
+  az::launch_expand(L.g, L.t, e->cache, L.probs, L.values, s);
   if (L.tree_timer.enabled) L.tree_timer.end(s, 1);
   AZ_HIP(hipGetLastError());
   return 0;
@@ -415,8 +407,6 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
   t.path += f * g.max_depth;
   t.path_len += f;
   t.slot_expansions += f;
-  t.sim_done += f;
-  t.sim_tag += f;
   t.mt += f;  // word-major: stride stays the whole engine's slot count
   t.eval_slot += f;
   t.eval_board += f;
@@ -815,7 +805,6 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   g.noise_alpha = c.dirichlet_alpha;
   g.noise_ratio = c.dirichlet_ratio;
   g.rng_skip = c.rng_skip;
-  g.runahead = 0;  // self-play turns it on per call (az_selfplay_step)
   if (c.rng_skip < 0) {
     delete e;
     return fail(AZ_E_INVALID, "rng_skip must be >= 0");
@@ -875,7 +864,6 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       (rc = e->alloc(&t.ply, S)) || (rc = e->alloc(&t.game_id, S)) ||
       (rc = e->alloc(&t.path, S * g.max_depth)) || (rc = e->alloc(&t.path_len, S)) ||
       (rc = e->alloc(&t.slot_expansions, S)) || (rc = e->alloc(&t.mt, S * (az::kMtN + 1))) ||
-      (rc = e->alloc(&t.sim_done, S)) || (rc = e->alloc(&t.sim_tag, S)) ||
       (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_board, S)) ||
       (rc = e->alloc(&t.eval_src, S)) || (rc = e->alloc(&t.miss_q, S)) ||
       (rc = e->alloc(&t.nn_board, S)) ||
@@ -932,7 +920,6 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(t.eval_count, 0, az::kCountWords * sizeof(int32_t)) != hipSuccess ||
       hipMemset(t.sel_done, 0, sizeof(uint32_t)) != hipSuccess ||
-      hipMemset(t.sim_tag, 0, S * sizeof(uint32_t)) != hipSuccess ||
       hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
     return cleanup(fail(AZ_E_HIP, "memset failed"));
   // evaluator buffers (batch = slots)
@@ -1309,11 +1296,10 @@ int az_selfplay_step(az_engine* e, int n_moves, az_stats* st) {
   const bool multi = e->lanes.size() > 1;
   for (int mv = 0; mv < n_moves; ++mv) {
     const int64_t m = e->moves_issued++;
-    for (Lane* L : e->lanes) L->t.move_no = (uint32_t)(m + 1);
     // lanes interleaved per simulation so every stream always has work queued
     for (int s = 0; s < e->g.sims; ++s)
       for (Lane* L : e->lanes)
-        if ((rc = simulate(e, *L, e->cache.enabled ? kRunAhead : 0))) return rc;
+        if ((rc = simulate(e, *L))) return rc;
     for (Lane* L : e->lanes) {
       // a lane plays move m once every other lane has finished move m - 1, so
       // move m - 1's snapshot (taken by the last of them) holds no game of

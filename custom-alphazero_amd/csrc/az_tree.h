@@ -116,11 +116,6 @@ struct TreeDev {
   const double* noise_in;
   int32_t* noise_cur;          // [slots] rows consumed
   int32_t noise_rows;
-  // run-ahead (GameCfg::runahead): the slot's simulations completed in move
-  // sim_tag[s] (a tag other than move_no reads as none)
-  int32_t* sim_done;           // [slots]
-  uint32_t* sim_tag;           // [slots]
-  uint32_t move_no;            // the move the lane's launches belong to (1, 2, ...)
 };
 
 // Transposition cache = the reference's plays_inferences (mcts/mcts.py:122-143,

@@ -188,72 +188,104 @@ __device__ __forceinline__ bool same_board(const Board& a, const Board& b) {
          a.opp[1] == b.opp[1];
 }
 
-// repr(board) in plays_inferences (mcts.py:123): the cache entry holding
-// board b (hash h), or -1.  Entries may be published concurrently by another
-// lane's insert kernel: the acquire pairs with its release, so a Ready entry's
-// key and payload are complete (a Claimed one reads as absent: the leaf is
-// evaluated, same result).  Every Ready entry is live (LRU eviction, az_tree.h).
-__device__ __forceinline__ int cache_lookup(const CacheDev& c, const Board& b, uint64_t h) {
-  // the board's bucket: kCacheBucket state words (one 64-B segment) read
-  // at once with relaxed loads, scanned in registers; a candidate's key is
-  // read after an acquire fence (pairs with the insert's release)
-  const uint32_t gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t fp = cache_fp(h);
-  const uint32_t base = cache_bucket(c, h);
-  uint32_t w[kCacheBucket];
-#pragma unroll
-  for (int k = 0; k < kCacheBucket; ++k)
-    w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int hit = -1;
-  uint32_t hst = 0;
-  // the fingerprint matches (inserts fill a bucket in slot order: nothing
-  // past an empty slot), then ONE acquire for the wave -- a fence per
-  // candidate position had the wave invalidating its CU's L1 (the tower
-  // tiles' weight fragments too) up to 16 times -- then the keys in order
-  uint32_t cm = 0;
-  bool stop = false;
-#pragma unroll
-  for (int k = 0; k < kCacheBucket; ++k) {
-    const uint32_t st = w[k];
-    if (stop) continue;
-    if (st == kCacheEmpty) stop = true;
-    else if ((st & 3u) == kCacheReady && (st >> 16) == fp) cm |= 1u << k;
+// After the descent: the terminal branch of MCTS.search (mcts.py:176-180) or
+// the eval queue + plays_inferences probe + per-simulation dedup.
+__device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c, int s, Edge* E,
+                          const int32_t* path, int depth, int status, const Board& b) {
+  wave_stat(t, kStatSims);
+  wave_stat(t, kStatPathEdges, (unsigned)depth);
+  AZ_SEL_STAMP(s, 3);
+  if (depth > 0 && status != kOngoing) {
+    // get_result(keep_same_player=True): 1 for the player who just moved, 0 draw
+    backup(E, path, depth, status == kWin ? 1.0 : 0.0);
+    wave_stat(t, kStatTerminal);
+    return;
   }
-  if (cm) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    for (; cm; cm &= cm - 1) {
-      const int k = __builtin_ctz(cm);
-      if (same_board(c.keys[base + k], b)) {
-        hit = k;
+  const int q = wave_claim(t.eval_count);
+  t.eval_slot[q] = s;
+  t.eval_board[q] = b;
+  t.path_len[s] = depth;
+  AZ_SEL_STAMP(s, 4);
+  if (!c.enabled) {
+    t.eval_src[q] = -(q + 1);
+    wave_stat(t, kStatNNEvals);
+    return;
+  }
+  // repr(board) in plays_inferences (mcts.py:123).  Entries may be published
+  // concurrently by another lane's insert kernel: the acquire load pairs with
+  // its release exchange, so a Ready entry's key and payload are complete
+  // (a Claimed one reads as absent: the leaf is evaluated here, same result).
+  // Every Ready entry is live (LRU eviction, az_tree.h).
+  const uint64_t h = board_hash(b);
+  {
+    // the board's bucket: kCacheBucket state words (one 64-B segment) read
+    // at once with relaxed loads, scanned in registers; a candidate's key is
+    // read after an acquire fence (pairs with the insert's release)
+    const uint32_t gen =
+        (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t fp = cache_fp(h);
+    const uint32_t base = cache_bucket(c, h);
+    uint32_t w[kCacheBucket];
 #pragma unroll
-        for (int kk = 0; kk < kCacheBucket; ++kk)
-          if (kk == k) hst = w[kk];  // (constant indices: w stays in VGPRs)
-        break;
+    for (int k = 0; k < kCacheBucket; ++k)
+      w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int hit = -1;
+    uint32_t hst = 0;
+    // the fingerprint matches (inserts fill a bucket in slot order: nothing
+    // past an empty slot), then ONE acquire for the wave -- a fence per
+    // candidate position had the wave invalidating its CU's L1 (the tower
+    // tiles' weight fragments too) up to 16 times -- then the keys in order
+    uint32_t cm = 0;
+    bool stop = false;
+#pragma unroll
+    for (int k = 0; k < kCacheBucket; ++k) {
+      const uint32_t st = w[k];
+      if (stop) continue;
+      if (st == kCacheEmpty) stop = true;
+      else if ((st & 3u) == kCacheReady && (st >> 16) == fp) cm |= 1u << k;
+    }
+    if (cm) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (; cm; cm &= cm - 1) {
+        const int k = __builtin_ctz(cm);
+        if (same_board(c.keys[base + k], b)) {
+          hit = k;
+#pragma unroll
+          for (int kk = 0; kk < kCacheBucket; ++kk)
+            if (kk == k) hst = w[kk];  // (constant indices: w stays in VGPRs)
+          break;
+        }
       }
     }
-  }
-  if (hit < 0) return -1;
-  if (cache_age(hst, gen) != 0) {
-    // a hit on an older generation moves the entry into the current one
-    // (its last use: inserts evict the least recently used), at most one CAS
-    // per entry per generation.  The CAS must win -- or find the entry
-    // already moved by another reader and still this board -- else an insert
-    // may be overwriting the slot and the board counts as a miss (az_tree.h)
-    const uint32_t want = cache_word(fp, gen, kCacheReady);
-    const uint32_t prev = atomicCAS(c.state + base + hit, hst, want);
-    if (prev != hst) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (!(prev == want && same_board(c.keys[base + hit], b))) return -1;
+    bool use = hit >= 0;
+    if (use && cache_age(hst, gen) != 0) {
+      // a hit on an older generation moves the entry into the current one
+      // (its last use: inserts evict the least recently used), at most one CAS
+      // per entry per generation.  The CAS must win -- or find the entry
+      // already moved by another reader and still this board -- else an insert
+      // may be overwriting the slot and the board counts as a miss (az_tree.h)
+      const uint32_t want = cache_word(fp, gen, kCacheReady);
+      const uint32_t prev = atomicCAS(c.state + base + hit, hst, want);
+      if (prev != hst) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        use = prev == want && same_board(c.keys[base + hit], b);
+      }
+    }
+    if (use) {
+      const uint32_t idx = base + hit;
+      t.eval_src[q] = (int32_t)idx;
+      AZ_SEL_STAMP(s, 5);
+      AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
+      wave_stat(t, kStatCacheHits);
+      return;
     }
   }
-  return (int)(base + hit);
-}
-
-// A miss: one evaluator row per distinct board in this simulation.  Tag =
-// (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
-// empty, so the table needs no clearing.  A tag match is only a candidate:
-// the launch's last block (dedup_tail) compares the full boards.
-__device__ __forceinline__ void queue_miss(const TreeDev& t, int q, const Board& b, uint64_t h) {
+  AZ_SEL_STAMP(s, 5);
+  AZ_SEL_VALUE(s, 7, depth | (2 << 16) | ((uint64_t)s << 32));
+  // miss: one evaluator row per distinct board in this simulation.  Tag =
+  // (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
+  // empty, so the table needs no clearing.  A tag match is only a candidate:
+  // the launch's last block (dedup_tail) compares the full boards.
   wave_count(t.miss_count);
   const uint64_t tag = ((uint64_t)t.epoch << 32) | (uint32_t)(h >> 32);
   uint32_t slot = (uint32_t)h & t.step_mask;
@@ -282,42 +314,6 @@ __device__ __forceinline__ void queue_miss(const TreeDev& t, int q, const Board&
     }
     slot = (slot + 1) & t.step_mask;
   }
-}
-
-// After the descent: the terminal branch of MCTS.search (mcts.py:176-180) or
-// the eval queue + plays_inferences probe + per-simulation dedup.
-__device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c, int s, Edge* E,
-                          const int32_t* path, int depth, int status, const Board& b) {
-  wave_stat(t, kStatSims);
-  wave_stat(t, kStatPathEdges, (unsigned)depth);
-  AZ_SEL_STAMP(s, 3);
-  if (depth > 0 && status != kOngoing) {
-    // get_result(keep_same_player=True): 1 for the player who just moved, 0 draw
-    backup(E, path, depth, status == kWin ? 1.0 : 0.0);
-    wave_stat(t, kStatTerminal);
-    return;
-  }
-  const int q = wave_claim(t.eval_count);
-  t.eval_slot[q] = s;
-  t.eval_board[q] = b;
-  t.path_len[s] = depth;
-  AZ_SEL_STAMP(s, 4);
-  if (!c.enabled) {
-    t.eval_src[q] = -(q + 1);
-    wave_stat(t, kStatNNEvals);
-    return;
-  }
-  const uint64_t h = board_hash(b);
-  const int idx = cache_lookup(c, b, h);
-  AZ_SEL_STAMP(s, 5);
-  if (idx >= 0) {
-    t.eval_src[q] = (int32_t)idx;
-    AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
-    wave_stat(t, kStatCacheHits);
-    return;
-  }
-  AZ_SEL_VALUE(s, 7, depth | (2 << 16) | ((uint64_t)s << 32));
-  queue_miss(t, q, b, h);
 }
 
 // ---------------------------------------------------- Dirichlet root noise
@@ -432,46 +428,7 @@ __device__ __forceinline__ void select_body(const GameCfg& g, const TreeDev& t, 
 // expressions as the serial loop, so the chosen edge is identical.
 // SHAPE 1: Connect-4 (6x7, n = 4, gravity) with the compile-time one-word
 // play (play_c64); 0: any shape through play_bb's runtime masks.
-// Run-ahead (RA, self-play with the cache on; g.runahead > 0): the slot's
-// simulations go on inside the launch while their leaves need no evaluator --
-// a terminal leaf's backup, or a cache hit expanded right here by the group's
-// first lane (expand_leaf, the same arithmetic as the expand launch) -- up to
-// g.runahead of them, until the move's g.sims are done (sim_done, tagged with
-// the move) or a leaf misses the cache and is queued for the network.  The
-// slot's simulations stay in their order and each sees the tree its
-// predecessor left, so every search is the one the lockstep form computes
-// (plays_inferences hits never change a result): only the number of launches a
-// move waits for changes.  The host still enqueues g.sims simulations per move;
-// a slot that has finished its move leaves the later launches at once.
-template <int MAXA, int SHAPE>
-__device__ __forceinline__ bool expand_leaf(const GameCfg& g, const TreeDev& t, int s, const Board& b,
-                                            const float* __restrict__ p, float v, int depth);
-template <int MAXA, int SHAPE>
-__device__ __forceinline__ int leaf_runahead(const GameCfg& g, const TreeDev& t, const CacheDev& c, int s,
-                                             Edge* E, const int32_t* path, int depth, int status, const Board& b) {
-  wave_stat(t, kStatSims);
-  wave_stat(t, kStatPathEdges, (unsigned)depth);
-  if (depth > 0 && status != kOngoing) {
-    backup(E, path, depth, status == kWin ? 1.0 : 0.0);
-    wave_stat(t, kStatTerminal);
-    return 1;
-  }
-  const uint64_t h = board_hash(b);
-  const int idx = cache_lookup(c, b, h);
-  if (idx >= 0) {
-    wave_stat(t, kStatCacheHits);
-    const float* pay = c.pay + (size_t)idx * (g.A + 1);
-    return expand_leaf<MAXA, SHAPE>(g, t, s, b, pay, pay[g.A], depth) ? 1 : -1;
-  }
-  const int q = wave_claim(t.eval_count);
-  t.eval_slot[q] = s;
-  t.eval_board[q] = b;
-  t.path_len[s] = depth;
-  queue_miss(t, q, b, h);
-  return 0;
-}
-
-template <int L, bool NOISE, int SHAPE, bool RA = false>
+template <int L, bool NOISE, int SHAPE>
 __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDev& t, const CacheDev& c) {
   if (blockIdx.x == 0 && threadIdx.x < 4) t.next_counts[threadIdx.x * kCountStride] = 0;  // next simulation's counts
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -498,15 +455,6 @@ __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDe
   const BoardMasks mk = board_masks(g);
   Edge* E = slot_edges(g, t, s);
   int32_t* path = t.path + (size_t)s * g.max_depth;
-  int done = 0;  // RA: the slot's simulations of this move so far
-  if constexpr (RA) {
-    if (j == 0) done = t.sim_tag[s] == t.move_no ? t.sim_done[s] : 0;
-    done = __shfl(done, 0, L);
-  }
-  for (int r = 0;; ++r) {  // RA: one simulation per pass; else one pass
-  if constexpr (RA) {
-    if (r >= g.runahead || done >= g.sims) break;  // group-uniform
-  }
   Board b = t.root_board[s];
   int first = t.root_first[s], cnt = t.root_n[s];
   int depth = 0, status = kOngoing;
@@ -631,33 +579,13 @@ __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDe
     first = child;
     cnt = child_n;
   }
-  if constexpr (!RA) {
-    if (j == 0) {
-      AZ_SEL_STAMP(s, 2);
-      AZ_SEL_VALUE(s, 8, ph_load);
-      AZ_SEL_VALUE(s, 9, ph_reduce);
-      AZ_SEL_VALUE(s, 10, ph_play);
-      leaf_tail(g, t, c, s, E, path, depth, status, b);
-      AZ_SEL_STAMP(s, 6);
-    }
-    return;
-  } else {
-    int code = 0;
-    if (j == 0) code = leaf_runahead<L, SHAPE>(g, t, c, s, E, path, depth, status, b);
-    code = __shfl(code, 0, L);
-    if (code < 0) return;   // arena overflow (flagged)
-    if (code == 0) break;   // queued: the expand launch completes this simulation
-    ++done;
-    // the first lane's edge and root stores, seen by the whole group's next
-    // descent (one wave: its stores complete before the next loads issue)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  }
-  }
-  if constexpr (RA) {
-    if (j == 0) {
-      t.sim_tag[s] = t.move_no;
-      t.sim_done[s] = done;
-    }
+  if (j == 0) {
+    AZ_SEL_STAMP(s, 2);
+    AZ_SEL_VALUE(s, 8, ph_load);
+    AZ_SEL_VALUE(s, 9, ph_reduce);
+    AZ_SEL_VALUE(s, 10, ph_play);
+    leaf_tail(g, t, c, s, E, path, depth, status, b);
+    AZ_SEL_STAMP(s, 6);
   }
 }
 
@@ -720,9 +648,9 @@ __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t
   select_body<NOISE>(g, t, c);
   dedup_tail(t, c);
 }
-template <int L, bool NOISE, int SHAPE = 0, bool RA = false>
+template <int L, bool NOISE, int SHAPE = 0>
 __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
-  select_group_body<L, NOISE, SHAPE, RA>(g, t, c);
+  select_group_body<L, NOISE, SHAPE>(g, t, c);
   dedup_tail(t, c);
 }
 
@@ -824,14 +752,29 @@ __global__ __launch_bounds__(256) void synth_eval_kernel(GameCfg g, const Board*
 // SHAPE 1 (Connect-4, 6x7, n = 4, gravity): the legal columns are the top
 // row's empty cells, in action order = moves order, and fewer than 8 of them,
 // so normalize's numpy sum is the plain left-to-right one -- no cell scans.
-// evaluate_and_expand's expansion (mcts.py:145-161) of slot s's leaf b at
-// `depth` on its path, from the evaluator's (or the cache's) probabilities p
-// and value v: mask + normalise the priors, allocate the edges, back up -v.
-// False: the arena overflowed (flagged).  Run by one thread per leaf: the
-// expand launch's, or a select group's first lane for a cache hit (run-ahead).
-template <int MAXA, int SHAPE>
-__device__ __forceinline__ bool expand_leaf(const GameCfg& g, const TreeDev& t, int s, const Board& b,
-                                            const float* __restrict__ p, float v, int depth) {
+template <int MAXA, bool INSERT, int SHAPE = 0>
+__global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
+                                                     const float* __restrict__ probs,
+                                                     const float* __restrict__ values, int exp_blocks) {
+  if (INSERT && (int)blockIdx.x >= exp_blocks) {  // block-uniform
+    cache_insert_row(g, t, c, probs, values, ((int)blockIdx.x - exp_blocks) * blockDim.x + threadIdx.x);
+    return;
+  }
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *t.eval_count) return;
+  const int s = t.eval_slot[i];
+  const Board b = t.eval_board[i];
+  const int src = t.eval_src[i];
+  const float* p;
+  float v;
+  if (src >= 0) {  // cache hit
+    p = c.pay + (size_t)src * (g.A + 1);
+    v = p[g.A];
+  } else {
+    const int row = -src - 1;
+    p = probs + (size_t)row * g.A;
+    v = values[row];
+  }
   float masked[MAXA];
   int moves[MAXA];
   int nl = 0, nm = 0;
@@ -871,7 +814,7 @@ __device__ __forceinline__ bool expand_leaf(const GameCfg& g, const TreeDev& t, 
       base = __shfl(base, leader) + (unsigned long long)rank * ch;
       if (base + ch > (unsigned long long)t.pool_cap) {
         flag_error(t, kErrArena);
-        return false;
+        return;
       }
       first = (int)base;
       end = first + ch;
@@ -880,7 +823,7 @@ __device__ __forceinline__ bool expand_leaf(const GameCfg& g, const TreeDev& t, 
     t.slot_live[s] += nm;
   } else if (first + nm > g.arena_cap) {
     flag_error(t, kErrArena);
-    return false;
+    return;
   }
   if constexpr (SHAPE == 1) {
     int k = 0;
@@ -914,6 +857,7 @@ __device__ __forceinline__ bool expand_leaf(const GameCfg& g, const TreeDev& t, 
     }
   }
   t.arena_top[s] = first + nm;
+  const int depth = t.path_len[s];
   const int32_t* path = t.path + (size_t)s * g.max_depth;
   if (depth == 0) {
     t.root_first[s] = first;
@@ -928,34 +872,6 @@ __device__ __forceinline__ bool expand_leaf(const GameCfg& g, const TreeDev& t, 
   backup(E, path, depth, -(double)v);
   t.slot_expansions[s] += 1;
   wave_stat(t, kStatExpansions);
-  return true;
-}
-
-template <int MAXA, bool INSERT, int SHAPE = 0>
-__global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t, CacheDev c,
-                                                     const float* __restrict__ probs,
-                                                     const float* __restrict__ values, int exp_blocks) {
-  if (INSERT && (int)blockIdx.x >= exp_blocks) {  // block-uniform
-    cache_insert_row(g, t, c, probs, values, ((int)blockIdx.x - exp_blocks) * blockDim.x + threadIdx.x);
-    return;
-  }
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *t.eval_count) return;
-  const int s = t.eval_slot[i];
-  const Board b = t.eval_board[i];
-  const int src = t.eval_src[i];
-  const float* p;
-  float v;
-  if (src >= 0) {  // cache hit
-    p = c.pay + (size_t)src * (g.A + 1);
-    v = p[g.A];
-  } else {
-    const int row = -src - 1;
-    p = probs + (size_t)row * g.A;
-    v = values[row];
-  }
-  if (!expand_leaf<MAXA, SHAPE>(g, t, s, b, p, v, t.path_len[s])) return;
-  if (g.runahead) t.sim_done[s] += 1;  // the miss's simulation (run-ahead select counts the rest)
 }
 
 // --------------------------------------------------------------------- play
@@ -1224,37 +1140,9 @@ void launch_select(const GameCfg& g, const TreeDev& t, const CacheDev& c, hipStr
   const int lanes = g.A <= 8 ? 8 : g.A <= 16 ? 16 : g.A <= 32 ? 32 : g.A <= 64 ? 64 : 1;
   const int blocks = (int)(((int64_t)g.slots * lanes + kGameBlock - 1) / kGameBlock);
   const bool c4 = g.H == 6 && g.W == 7 && g.n == 4 && g.gravity && lanes == 8;
-  // run-ahead needs the cache (its hits) and the group form (lanes <= 64)
-  const bool ra = g.runahead > 0 && c.enabled && lanes > 1;
   if (c4) {  // Connect-4: the compile-time one-word play (play_c64)
-    if (ra) {
-      if (g.noise) select_group_kernel<8, true, 1, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-      else select_group_kernel<8, false, 1, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-    } else {
-      if (g.noise) select_group_kernel<8, true, 1><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-      else select_group_kernel<8, false, 1><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-    }
-    return;
-  }
-  if (ra) {
-    switch (lanes) {
-      case 8:
-        if (g.noise) select_group_kernel<8, true, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        else select_group_kernel<8, false, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        break;
-      case 16:
-        if (g.noise) select_group_kernel<16, true, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        else select_group_kernel<16, false, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        break;
-      case 32:
-        if (g.noise) select_group_kernel<32, true, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        else select_group_kernel<32, false, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        break;
-      default:
-        if (g.noise) select_group_kernel<64, true, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        else select_group_kernel<64, false, 0, true><<<blocks, kGameBlock, 0, s>>>(g, t, c);
-        break;
-    }
+    if (g.noise) select_group_kernel<8, true, 1><<<blocks, kGameBlock, 0, s>>>(g, t, c);
+    else select_group_kernel<8, false, 1><<<blocks, kGameBlock, 0, s>>>(g, t, c);
     return;
   }
   if (g.noise) {  // the root-noise instantiations (the default path carries none of their code)
