@@ -670,11 +670,15 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
   // the alternative tile height of a dual launch: a slot plan and an LDS
   // staging of its own
   const bool alt = 16 * MBT != T.tile_rows && 16 * MBT == T.alt_rows;
-  // small weights into LDS, in the background of the stem
-  dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob, (alt ? T.alt_staged_floats : T.staged_floats) / 4, wave,
-                 lane);
   const bool wpd_lds = alt ? T.alt_wpd_lds : T.wpd_lds;
   const bool wv1_lds = alt ? T.alt_wv1_lds : T.wv1_lds;
+  // (the alternative tiles' staged value dense wv1 -- 43 KB at Connect-4 --
+  // arrives during the last conv2, as wv1_xt's does: at the kernel's start
+  // it would queue ahead of the slot plan's and the boards' loads)
+  const bool wv1_late = alt && wv1_lds;
+  // small weights into LDS, in the background of the stem
+  dma_to_lds<NT>(reinterpret_cast<uint4*>(blob), T.blob,
+                 (wv1_late ? T.off_wv1 : alt ? T.alt_staged_floats : T.staged_floats) / 4, wave, lane);
   for (int i = tid; i < kZeroRows * kPitch / 16; i += NT) act[zrow * kPitch / 16 + i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 2) sm.flag[tid] = 0;  // published by the barrier after the stem's MFMAs
 
@@ -927,13 +931,13 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
       // block streams the value dense's wv1 into X's tile behind the heads'
       // partials while the taps run (every wave a share).  The same sums in
       // the same order as the in-place form: bitwise the same outputs
-      const bool wv1x = wv1_xt && d + 1 == depth;  // read before the K loop's asm ("memory")
+      const bool wv1x = (wv1_xt || wv1_late) && d + 1 == depth;  // read before the K loop's asm ("memory")
       auto mid = [&]() {
         rescale();
         __syncthreads();
         if (wv1x)
-          dma_to_lds<NT>(reinterpret_cast<uint4*>(reinterpret_cast<float*>(bufX) + TR * 48), T.blob + T.off_wv1,
-                         HW * J / 4, wave, lane);
+          dma_to_lds<NT>(reinterpret_cast<uint4*>(wv1_xt ? reinterpret_cast<float*>(bufX) + TR * 48 : blob + T.off_wv1),
+                         T.blob + T.off_wv1, HW * J / 4, wave, lane);
       };
 #pragma unroll
       for (int mb = 0; mb < MBW; ++mb)
@@ -1041,7 +1045,7 @@ __device__ __forceinline__ void tower16_tile(const TowerNet* __restrict__ net, c
   T16_STAMP4(54);
   T16_STAMP(42);
   T16_STAMP4(43);
-  if (wv1_xt) __builtin_amdgcn_s_waitcnt(0);  // this wave's wv1 DMA pieces have landed ...
+  if (wv1_xt || wv1_late) __builtin_amdgcn_s_waitcnt(0);  // this wave's wv1 DMA pieces have landed ...
   __syncthreads();  // ... the partials are complete; no activation row is read any more
   T16_STAMP(18);
   if constexpr (ROWS) {

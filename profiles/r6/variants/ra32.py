@@ -1,0 +1,5 @@
+# run-ahead depth 32 (az_engine.hip kRunAhead; product: 8)
+s = open("az_engine.hip").read()
+assert "constexpr int kRunAhead = 8;" in s
+s = s.replace("constexpr int kRunAhead = 8;", "constexpr int kRunAhead = 32;")
+open("az_engine.hip", "w").write(s)
