@@ -33,10 +33,10 @@ def main():
             float(r["AverageNs"]), float(r["Percentage"])
         print(f"| `{n}` | {c} | {tot / 1e6:.1f} | {avg / 1e3:.1f} | {pct:.2f} |")
     for r in rows:
-        if "tower16_kernel" in r["Name"]:
+        if "tower16_kernel" in r["Name"] or "tower16_dual_kernel" in r["Name"]:
             conv_calls += int(r["Calls"])
             conv_ns += float(r["TotalDurationNs"])
-    print(f"\ntower16_kernel (the whole forward): {conv_calls} launches, rocprof average "
+    print(f"\ntower16_kernel / tower16_dual_kernel (the whole forward): {conv_calls} launches, rocprof average "
           f"{conv_ns / max(conv_calls, 1) / 1e3:.1f} us per launch (whole trace, preroll included)")
     try:
         b = json.loads(open(f"{d}/bench_trace.json").read().strip().splitlines()[-1])
