@@ -111,16 +111,41 @@ __device__ void mt_seed(const TreeDev& t, int slots, int g, uint32_t seed) {
   t.mt[(size_t)kMtN * slots + g] = kMtN;  // force a twist on first use
 }
 
+// One twist of a slot's state in place (m: its word 0, words `slots` apart),
+// the serial loop's arithmetic in its order: word i takes words i, i+1 as
+// they were and word i+397 (as it was below i = 227, already new from there
+// on; word 0 is new when i = 623 reads it as i+1).  A batch of kTwistB words
+// loads every operand before its first store -- none of a batch's loads reads
+// a word that batch writes before that word's own update, and the words from
+// earlier batches are stored ahead of them in program order -- so a twist is
+// 39 memory round trips instead of 624 dependent load-store chains (a game's
+// reset twists once: slot_reset).
+__device__ void mt_twist(uint32_t* m, size_t slots) {
+  constexpr int kTwistB = 16;
+  static_assert(kMtN % kTwistB == 0 && 227 >= kTwistB, "batches never read their own stores");
+  uint32_t cur = m[0];
+  for (int i0 = 0; i0 < kMtN; i0 += kTwistB) {
+    uint32_t nx[kTwistB], far[kTwistB];
+#pragma unroll
+    for (int k = 0; k < kTwistB; ++k) {
+      const int i = i0 + k;
+      nx[k] = m[(size_t)(i + 1 < kMtN ? i + 1 : 0) * slots];
+      far[k] = m[(size_t)(i + 397 < kMtN ? i + 397 : i - 227) * slots];
+    }
+#pragma unroll
+    for (int k = 0; k < kTwistB; ++k) {
+      const uint32_t y = (cur & 0x80000000u) | (nx[k] & 0x7fffffffu);
+      m[(size_t)(i0 + k) * slots] = far[k] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      cur = nx[k];
+    }
+  }
+}
+
 __device__ uint32_t mt_next(const TreeDev& t, int slots, int g) {
   uint32_t* m = t.mt;
   uint32_t pos = m[(size_t)kMtN * slots + g];
   if (pos >= (uint32_t)kMtN) {
-    for (int i = 0; i < kMtN; ++i) {
-      const uint32_t y = (m[(size_t)i * slots + g] & 0x80000000u) |
-                         (m[(size_t)((i + 1) % kMtN) * slots + g] & 0x7fffffffu);
-      m[(size_t)i * slots + g] =
-          m[(size_t)((i + 397) % kMtN) * slots + g] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    }
+    mt_twist(m + g, (size_t)slots);
     pos = 0;
   }
   const uint32_t y = m[(size_t)pos * slots + g];
@@ -156,8 +181,24 @@ __device__ void slot_reset(const GameCfg& g, const TreeDev& t, int s, int64_t gi
   t.last_status[s] = kOngoing;
   mt_seed(t, t.mt_stride, s, seed);
   // the reference's play_game draws np.random.rand(1, H, W, 4) building its
-  // model between the seed and the game (az_config.rng_skip)
-  for (int k = 0; k < g.rng_skip; ++k) (void)mt_next(t, t.mt_stride, s);
+  // model between the seed and the game (az_config.rng_skip): the words are
+  // skipped, not drawn -- a twist whenever the index runs out, then the index
+  // (the state mt_next would leave, without 2 dependent round trips per word)
+  if (g.rng_skip > 0) {
+    uint32_t* m = t.mt + s;
+    const size_t slots = (size_t)t.mt_stride;
+    uint32_t pos = kMtN;  // mt_seed's
+    for (int n = g.rng_skip; n > 0;) {
+      if (pos >= (uint32_t)kMtN) {
+        mt_twist(m, slots);
+        pos = 0;
+      }
+      const int k = min(n, kMtN - (int)pos);
+      pos += (uint32_t)k;
+      n -= k;
+    }
+    m[(size_t)kMtN * slots] = pos;
+  }
 }
 
 // ------------------------------------------------------------------- select
