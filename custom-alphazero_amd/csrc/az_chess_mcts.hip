@@ -699,11 +699,19 @@ __device__ __forceinline__ void select_slot(const CCfg& g, const CTree& t, const
   Pos q = load_pos(t.root[s]);
   int first = t.root_first[s], cnt = t.root_n[s];
   int depth = 0;
+  // below the root an expanded node's children's visits sum to its edge's
+  // N - 1 (the first visit expanded it, every later one went on to a child),
+  // so sqrt(sum) is read alongside the children's edges instead of after a
+  // wave reduction over them: one dependent round trip per level, not two
+  int sum_next = -1;
   while (cnt > 0) {
-    int sum = 0;
-    for (int j = lane; j < cnt; j += 64) sum += E[first + j].N;
+    int sum = sum_next;
+    if (sum < 0) {  // the root: its children's visits, summed (wave-uniform)
+      sum = 0;
+      for (int j = lane; j < cnt; j += 64) sum += E[first + j].N;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+      for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    }
     if (sum >= g.pow_len) {
       if (lane == 0) flag(t, az::kErrPow);
       return;
@@ -740,6 +748,7 @@ __device__ __forceinline__ void select_slot(const CCfg& g, const CTree& t, const
     play(q, (uint16_t)e.action, true);  // Board.play(keep_same_player=True)
     first = e.child;
     cnt = e.child < 0 ? 0 : e.child_n;
+    sum_next = e.N - 1;
   }
   if (lane == 0) {
     store_pos(q, t.leaf[s]);
