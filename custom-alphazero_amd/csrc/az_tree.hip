@@ -242,6 +242,19 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
     wave_stat(t, kStatTerminal);
     return;
   }
+  // the cache bucket's state words are requested before the queue claim's
+  // atomic, so the two round trips overlap
+  const uint64_t h = board_hash(b);
+  uint32_t gen = 0, fp = 0, base = 0;
+  uint32_t w[kCacheBucket];
+  if (c.enabled) {
+    gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fp = cache_fp(h);
+    base = cache_bucket(c, h);
+#pragma unroll
+    for (int k = 0; k < kCacheBucket; ++k)
+      w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int q = wave_claim(t.eval_count);
   t.eval_slot[q] = s;
   t.eval_board[q] = b;
@@ -257,19 +270,10 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   // its release exchange, so a Ready entry's key and payload are complete
   // (a Claimed one reads as absent: the leaf is evaluated here, same result).
   // Every Ready entry is live (LRU eviction, az_tree.h).
-  const uint64_t h = board_hash(b);
   {
     // the board's bucket: kCacheBucket state words (one 64-B segment) read
-    // at once with relaxed loads, scanned in registers; a candidate's key is
-    // read after an acquire fence (pairs with the insert's release)
-    const uint32_t gen =
-        (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t fp = cache_fp(h);
-    const uint32_t base = cache_bucket(c, h);
-    uint32_t w[kCacheBucket];
-#pragma unroll
-    for (int k = 0; k < kCacheBucket; ++k)
-      w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // at once with relaxed loads (above), scanned in registers; a candidate's
+    // key is read after an acquire fence (pairs with the insert's release)
     int hit = -1;
     uint32_t hst = 0;
     // the fingerprint matches (inserts fill a bucket in slot order: nothing
@@ -491,13 +495,16 @@ __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDe
 #else
 #define AZ_SEL_PHASE(acc) ((void)0)
 #endif
-  if (s >= g.slots || t.game_id[s] < 0) return;  // whole groups leave together
+  if (s >= g.slots) return;  // whole groups leave together
+  // the slot's game id and root read together (an idle slot's root is stale, unused)
+  const int64_t game = t.game_id[s];
+  Board b = t.root_board[s];
+  int first = t.root_first[s], cnt = t.root_n[s];
+  if (game < 0) return;
   if (j == 0) AZ_SEL_STAMP(s, 1);
   const BoardMasks mk = board_masks(g);
   Edge* E = slot_edges(g, t, s);
   int32_t* path = t.path + (size_t)s * g.max_depth;
-  Board b = t.root_board[s];
-  int first = t.root_first[s], cnt = t.root_n[s];
   int depth = 0, status = kOngoing;
   // below the root, the children's visits sum to the parent edge's N - 1 (the
   // first visit expanded the node), so sqrt(sum) is fetched before the
@@ -802,10 +809,26 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     return;
   }
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *t.eval_count) return;
+  if (i >= g.slots) return;
+  // round trip 1: the queue entry, read beside the queue's count (entries past
+  // it are stale and unused); 2: the slot's arena, path and the leaf's
+  // outputs; 3: the path's edges -- every load of a trip issued together
+  const int n_eval = *t.eval_count;
   const int s = t.eval_slot[i];
   const Board b = t.eval_board[i];
   const int src = t.eval_src[i];
+  if (i >= n_eval) return;
+  Edge* E = slot_edges(g, t, s);
+  const int top0 = t.arena_top[s];
+  const int end0 = g.halves > 1 ? t.arena_end[s] : 0;
+  const int live0 = g.halves > 1 ? t.slot_live[s] : 0;
+  const int depth = t.path_len[s];
+  const int exps = t.slot_expansions[s];
+  const int32_t* path = t.path + (size_t)s * g.max_depth;
+  constexpr int K = 8;  // path levels read ahead (deeper ones after, one batch at a time)
+  int pv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) pv[k] = k < g.max_depth ? path[k] : 0;
   const float* p;
   float v;
   if (src >= 0) {  // cache hit
@@ -816,6 +839,14 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     p = probs + (size_t)row * g.A;
     v = values[row];
   }
+  int pn[K];
+  double pw[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k < depth) {
+      pn[k] = E[pv[k]].N;
+      pw[k] = E[pv[k]].W;
+    }
   float masked[MAXA];
   int moves[MAXA];
   int nl = 0, nm = 0;
@@ -839,12 +870,11 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     nm = moves_order(g, b, moves);
     sum = pairwise_sum_f32(masked, nl);
   }
-  Edge* E = slot_edges(g, t, s);
-  int first = t.arena_top[s];
+  int first = top0;
   if (g.halves > 1) {
     // pooled arena: the run goes into the slot's current chunk, or a new one
     // of kPoolChunkA * A edges bumped off the lane's half (one atomic per wave)
-    int end = t.arena_end[s];
+    int end = end0;
     if (first + nm > end) {
       const int ch = kPoolChunkA * g.A;
       const unsigned long long m = __ballot(1);
@@ -861,7 +891,7 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
       end = first + ch;
       t.arena_end[s] = end;
     }
-    t.slot_live[s] += nm;
+    t.slot_live[s] = live0 + nm;
   } else if (first + nm > g.arena_cap) {
     flag_error(t, kErrArena);
     return;
@@ -898,20 +928,33 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     }
   }
   t.arena_top[s] = first + nm;
-  const int depth = t.path_len[s];
-  const int32_t* path = t.path + (size_t)s * g.max_depth;
   if (depth == 0) {
     t.root_first[s] = first;
     t.root_n[s] = nm;
     t.root_value[s] = v;
   } else {
-    Edge& pe = E[path[depth - 1]];
+    int pe_id = 0;  // the leaf's edge: path[depth - 1]
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k == depth - 1) pe_id = pv[k];
+    if (depth > K) pe_id = path[depth - 1];
+    Edge& pe = E[pe_id];
     pe.child = first;
     pe.child_n = (int16_t)nm;
     pe.child_value = v;
   }
-  backup(E, path, depth, -(double)v);
-  t.slot_expansions[s] += 1;
+  // backup(-value) (mcts.py:175, 163-168): the edge at level d gets the
+  // leaf's -value negated depth - 1 - d times -- each edge once, so the
+  // levels' order does not change a bit
+  const double vb = -(double)v;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k < depth) {
+      E[pv[k]].N = pn[k] + 1;
+      E[pv[k]].W = pw[k] + (((depth - 1 - k) & 1) ? -vb : vb);
+    }
+  if (depth > K) backup(E, path + K, depth - K, vb);  // levels K.. (rare): the leaf's edge gets vb
+  t.slot_expansions[s] = exps + 1;
   wave_stat(t, kStatExpansions);
 }
 
