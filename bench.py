@@ -750,7 +750,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.timer(True)
+    eng.timer(os.environ.get("AZ_BENCH_WINDOW_EVENTS", "1") != "0")  # A/B of the events' own cost
     st0 = eng.stats()
     t0 = time.perf_counter()
     drained = 0

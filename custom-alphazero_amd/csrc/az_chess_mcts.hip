@@ -465,91 +465,115 @@ struct ExpandSmem {
   int first_s;
 };
 
-// b: the slot's network row, or kQHit (its cached priors and value in leaf_pay)
+// b: the slot's network row, or kQHit (its cached priors and value in leaf_pay).
+// Round trips, each one's loads issued together: 1. the slot's counts, arena
+// half and path (one level per lane), the leaf's value, first 64 moves and a
+// hit's first 64 priors; 2. the path's edges and the moves' action indices;
+// 3. the network row's priors -- where one load after another took eight.
 __device__ void expand_body(const CCfg& g, const CTree& t, const ChessCache& c, const float* __restrict__ probs,
                             const float* __restrict__ values, int b, int s, int lane, ExpandSmem& sm) {
   int* act = sm.act;
   float* sorted = sm.sorted;
-  {
-    const int n = t.leaf_n[s];
-    const uint16_t* mv = t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES;
-    const bool hit = b == kQHit;
-    __syncthreads();
-    if (hit) {  // plays_inferences[repr(board)] (mcts.py:123-128): the masked priors as stored
-      const float* lp = t.leaf_pay + (size_t)s * kPayFloats;
-      for (int j = lane; j < n; j += 64) sorted[j] = lp[j];
-    } else {
-      const float* pr = probs + (size_t)b * AZ_CHESS_ACTIONS;
-      for (int j = lane; j < n; j += 64) {
-        const int a = action_of(t.lut, mv[j]);
-        act[j] = a;
-        if (a < 0) flag(t, az::kErrIllegal);
-      }
-      __syncthreads();
-      // probabilities[legal_moves_mask]: the legal actions in action order
-      for (int j = lane; j < n; j += 64) {
-        const int a = act[j];
-        int r = 0;
-        for (int i = 0; i < n; ++i) r += act[i] < a;
-        sorted[r] = a >= 0 ? pr[a] : 0.f;
-      }
-    }
-    __syncthreads();
-    const float value = hit ? t.leaf_pay[(size_t)s * kPayFloats + AZ_CHESS_MAX_MOVES] : values[b];
-    // the network row's owner publishes it (duplicates of this simulation share the row)
-    const bool owner = !hit && t.eval_slot[b] == s;
-    if (owner && c.enabled) cache_insert_wave(t, c, s, lane, sorted, n, value);
-    if (lane == 0) {
-      // normalize_probabilities (mcts/utils.py:4-16): the sum in numpy's
-      // pairwise order here, the quotients per lane below
-      sm.sum = pairwise(sorted, n);
-      const int first = t.top[s];
-      if (first + n > g.half_cap) {
-        flag(t, az::kErrArena);
-        sm.first_s = -1;
-      } else {
-        t.top[s] = first + n;
-        sm.first_s = first;
-      }
-    }
-    __syncthreads();
-    const int first = sm.first_s;
-    const float sum = sm.sum;
-    if (first < 0) return;
-    Edge* E = arena(g, t, s, t.half[s]);
-    // zip(probabilities, node.board.moves): positional, python-chess move order
+  const bool hit = b == kQHit;
+  const int n = t.leaf_n[s];
+  const int top = t.top[s];
+  const int half = t.half[s];
+  const int depth = t.path_len[s];
+  const int32_t* path = t.path + (size_t)s * g.max_depth;
+  const int pth = lane < g.max_depth ? path[lane] : 0;  // path level `lane` (past depth: stale, unused)
+  const float* lp = t.leaf_pay + (size_t)s * kPayFloats;
+  const float value = hit ? lp[AZ_CHESS_MAX_MOVES] : values[b];
+  const int row_owner = hit ? -1 : t.eval_slot[b];
+  const uint16_t* mv = t.leaf_moves + (size_t)s * AZ_CHESS_MAX_MOVES;
+  const uint16_t m0 = mv[lane];  // moves 0..63 (64 < AZ_CHESS_MAX_MOVES)
+  const float lp0 = hit ? lp[lane] : 0.f;
+  Edge* E = arena(g, t, s, half);
+  int en = 0;
+  double ew = 0.0;
+  if (lane < depth) {  // backup's loads now, its stores at the end (a path's edges are distinct)
+    en = E[pth].N;
+    ew = E[pth].W;
+  }
+  __syncthreads();
+  if (hit) {  // plays_inferences[repr(board)] (mcts.py:123-128): the masked priors as stored
+    for (int j = lane; j < n; j += 64) sorted[j] = j < 64 ? lp0 : lp[j];
+  } else {
+    const float* pr = probs + (size_t)b * AZ_CHESS_ACTIONS;
     for (int j = lane; j < n; j += 64) {
-      Edge e;
-      e.W = 0.0;
-      e.prior = sum == 0.0f ? 1.0 / (double)n : (double)(float)(sorted[j] / sum);
-      e.N = 0;
-      e.child = az::kNoChild;
-      e.child_n = 0;
-      e.action = (int16_t)mv[j];
-      e.child_value = 0.f;
-      E[first + j] = e;
+      const int a = action_of(t.lut, j < 64 ? m0 : mv[j]);
+      act[j] = a;
+      if (a < 0) flag(t, az::kErrIllegal);
     }
-    const int depth = t.path_len[s];
-    const int32_t* path = t.path + (size_t)s * g.max_depth;
-    if (lane == 0) {
-      if (depth == 0) {
-        t.root_first[s] = first;
-        t.root_n[s] = n;
-        t.root_value[s] = value;
-      } else {
-        Edge& pe = E[path[depth - 1]];
-        pe.child = first;
-        pe.child_n = (int16_t)n;
-        pe.child_value = value;
-      }
+    __syncthreads();
+    // probabilities[legal_moves_mask]: the legal actions in action order
+    for (int j = lane; j < n; j += 64) {
+      const int a = act[j];
+      int r = 0;
+      for (int i = 0; i < n; ++i) r += act[i] < a;
+      sorted[r] = a >= 0 ? pr[a] : 0.f;
     }
-    backup_wave(E, path, depth, -(double)value, lane);
-    if (lane == 0) {
-      t.slot_exp[s] += 1;
-      atomicAdd(t.stats + az::kStatExpansions, 1ull);
-      if (hit) atomicAdd(t.stats + az::kStatCacheHits, 1ull);
-      else if (owner) atomicAdd(t.stats + az::kStatNNEvals, 1ull);
+  }
+  __syncthreads();
+  // the network row's owner publishes it (duplicates of this simulation share the row)
+  const bool owner = !hit && row_owner == s;
+  if (owner && c.enabled) cache_insert_wave(t, c, s, lane, sorted, n, value);
+  if (lane == 0) {
+    // normalize_probabilities (mcts/utils.py:4-16): the sum in numpy's
+    // pairwise order here, the quotients per lane below
+    sm.sum = pairwise(sorted, n);
+    if (top + n > g.half_cap) {
+      flag(t, az::kErrArena);
+      sm.first_s = -1;
+    } else {
+      t.top[s] = top + n;
+      sm.first_s = top;
     }
+  }
+  __syncthreads();
+  const int first = sm.first_s;
+  const float sum = sm.sum;
+  if (first < 0) return;
+  // zip(probabilities, node.board.moves): positional, python-chess move order
+  for (int j = lane; j < n; j += 64) {
+    Edge e;
+    e.W = 0.0;
+    e.prior = sum == 0.0f ? 1.0 / (double)n : (double)(float)(sorted[j] / sum);
+    e.N = 0;
+    e.child = az::kNoChild;
+    e.child_n = 0;
+    e.action = (int16_t)(j < 64 ? m0 : mv[j]);
+    e.child_value = 0.f;
+    E[first + j] = e;
+  }
+  const int leaf_edge = depth > 64 ? path[depth - 1] : __shfl(pth, depth > 0 ? depth - 1 : 0, 64);
+  if (lane == 0) {
+    if (depth == 0) {
+      t.root_first[s] = first;
+      t.root_n[s] = n;
+      t.root_value[s] = value;
+    } else {
+      Edge& pe = E[leaf_edge];
+      pe.child = first;
+      pe.child_n = (int16_t)n;
+      pe.child_value = value;
+    }
+  }
+  // backup(-value) (mcts.py:175, 163-168): level d gets it negated depth - 1 - d times
+  const double v = -(double)value;
+  if (lane < depth) {
+    E[pth].N = en + 1;
+    E[pth].W = ew + (((depth - 1 - lane) & 1) ? -v : v);
+  }
+  for (int d = lane + 64; d < depth; d += 64) {  // levels past 64 (a long game's deep tree)
+    Edge& e = E[path[d]];
+    e.N += 1;
+    e.W += ((depth - 1 - d) & 1) ? -v : v;
+  }
+  if (lane == 0) {
+    t.slot_exp[s] += 1;
+    atomicAdd(t.stats + az::kStatExpansions, 1ull);
+    if (hit) atomicAdd(t.stats + az::kStatCacheHits, 1ull);
+    else if (owner) atomicAdd(t.stats + az::kStatNNEvals, 1ull);
   }
 }
 

@@ -111,6 +111,7 @@ struct az_engine {
   hipEvent_t timer_ref = nullptr;  // common origin of every ConvTimer's intervals
   int64_t sp_first = 0, sp_n = 0;
   int64_t moves_issued = 0;        // self-play moves enqueued (lane drift bound, az_tree.h)
+  uint32_t leaf_epoch = 0;         // simulations enqueued, every lane's (TreeDev::leaf_epoch)
   int64_t drained = 0;             // finished games az_selfplay_drain has returned
   uint8_t* drain_dev = nullptr;    // packed records (device) and their pinned host copy
   uint8_t* drain_host = nullptr;
@@ -184,7 +185,6 @@ void set_counts(az::TreeDev& t, int32_t* base, int p) {
   t.eval_count = base + 4 * K * p;
   t.miss_count = t.eval_count + K;
   t.nn_count = t.eval_count + 2 * K;
-  t.dup_count = t.eval_count + 3 * K;
   t.next_counts = base + 4 * K * (p ^ 1);
 }
 
@@ -221,8 +221,9 @@ int host_evaluate(az_engine* e, Lane& L, const az::Board* rows, const int32_t* n
 // mcts.py:171-180), enqueued on the lane's stream
 int simulate(az_engine* e, Lane& L) {
   hipStream_t s = L.stream;
-  L.t.epoch += 1;  // fresh per-simulation dedup table (tags of older epochs read as empty)
-  // eval_count, miss_count, nn_count, dup_count: the epoch parity's block of
+  L.t.epoch += 1;
+  L.t.leaf_epoch = ++e->leaf_epoch;  // leaf records of any other simulation read as absent
+  // eval_count, miss_count, nn_count: the epoch parity's block of
   // four (zeroed by the previous simulation's select kernel, or at creation)
   set_counts(L.t, L.counts, L.t.epoch & 1);
   if (L.tree_timer.enabled) L.tree_timer.begin(s);
@@ -408,27 +409,19 @@ int make_lane(az_engine* e, Lane* L, int first, int n, bool own_queue) {
   t.path_len += f;
   t.slot_expansions += f;
   t.mt += f;  // word-major: stride stays the whole engine's slot count
-  t.eval_slot += f;
+  t.leaf_src += f;
+  t.leaf_board += f;
   t.eval_board += f;
-  t.eval_src += f;
-  t.miss_q += f;
+
   t.nn_board += f;
-  t.dup_q += f;
   t.last_move += f;
   t.last_status += f;
   t.last_policy += f * g.A;
   if (own_queue) {
     int rc;
-    size_t cap = 1024;
-    while (cap < 4 * (size_t)n) cap <<= 1;
-    if ((rc = e->alloc(&t.eval_count, az::kCountWords)) || (rc = e->alloc(&t.step_tag, cap)) ||
-        (rc = e->alloc(&t.step_row, cap)) || (rc = e->alloc(&t.sel_done, 1)))
-      return rc;
-    AZ_HIP(hipMemset(t.sel_done, 0, sizeof(uint32_t)));
-    AZ_HIP(hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)));
+    if ((rc = e->alloc(&t.eval_count, az::kCountWords))) return rc;
     AZ_HIP(hipMemset(t.eval_count, 0, az::kCountWords * sizeof(int32_t)));
     set_counts(t, t.eval_count, 0);
-    t.step_mask = (uint32_t)(cap - 1);
     t.epoch = 0;
   }
   L->counts = t.eval_count;
@@ -864,11 +857,9 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
       (rc = e->alloc(&t.ply, S)) || (rc = e->alloc(&t.game_id, S)) ||
       (rc = e->alloc(&t.path, S * g.max_depth)) || (rc = e->alloc(&t.path_len, S)) ||
       (rc = e->alloc(&t.slot_expansions, S)) || (rc = e->alloc(&t.mt, S * (az::kMtN + 1))) ||
-      (rc = e->alloc(&t.eval_slot, S)) || (rc = e->alloc(&t.eval_board, S)) ||
-      (rc = e->alloc(&t.eval_src, S)) || (rc = e->alloc(&t.miss_q, S)) ||
-      (rc = e->alloc(&t.nn_board, S)) ||
+      (rc = e->alloc(&t.leaf_src, S)) || (rc = e->alloc(&t.leaf_board, S)) ||
+      (rc = e->alloc(&t.eval_board, S)) || (rc = e->alloc(&t.nn_board, S)) ||
       (rc = e->alloc(&t.eval_count, az::kCountWords)) || (rc = e->alloc(&t.stats, az::kStatCount)) ||
-      (rc = e->alloc(&t.sel_done, 1)) ||
       (rc = e->alloc(&t.last_move, S)) || (rc = e->alloc(&t.last_status, S)) ||
       (rc = e->alloc(&t.last_policy, S * A)))
     return cleanup(rc);
@@ -883,17 +874,10 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   t.powtab = powtab;
   t.mt_stride = g.slots;
   set_counts(t, t.eval_count, 0);
-  {
-    size_t cap = 1024;
-    while (cap < 4 * S) cap <<= 1;  // load factor <= 25%
-    if ((rc = e->alloc(&t.step_tag, cap)) || (rc = e->alloc(&t.step_row, cap) ) ||
-        (rc = e->alloc(&t.dup_q, S)))
-      return cleanup(rc);
-    if (hipMemset(t.step_tag, 0, cap * sizeof(uint64_t)) != hipSuccess)
-      return cleanup(fail(AZ_E_HIP, "memset failed"));
-    t.step_mask = (uint32_t)(cap - 1);
-    t.epoch = 0;
-  }
+  t.epoch = 0;
+  // leaf records start untagged (leaf_epoch counts from 1)
+  if (hipMemset(t.leaf_src, 0, S * sizeof(uint64_t)) != hipSuccess)
+    return cleanup(fail(AZ_E_HIP, "memset failed"));
   if (c.cache_log2 < 0 || c.cache_log2 > 30 || (c.cache_log2 > 0 && c.cache_log2 < 4))
     return cleanup(fail(AZ_E_INVALID, "cache_log2 must be 0 (no cache) or 4..30"));
   if (c.cache_log2 > 0) {
@@ -919,7 +903,7 @@ int az_engine_create(int device, const az_config* cfg, az_engine** out) {
   }
   if (hipMemset(t.stats, 0, az::kStatCount * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(t.eval_count, 0, az::kCountWords * sizeof(int32_t)) != hipSuccess ||
-      hipMemset(t.sel_done, 0, sizeof(uint32_t)) != hipSuccess ||
+
       hipMemset(t.game_id, 0xff, S * sizeof(int64_t)) != hipSuccess)
     return cleanup(fail(AZ_E_HIP, "memset failed"));
   // evaluator buffers (batch = slots)

@@ -85,25 +85,22 @@ struct TreeDev {
   int32_t* slot_expansions;    // [slots], this game's expansions so far
   uint32_t* mt;                // [625][mt_stride], word-major MT19937 state (+ index)
   int32_t mt_stride;           // slots of the whole engine (a lane view offsets mt)
-  int32_t* eval_slot;          // [slots] compacted eval queue (leaves to expand)
-  Board* eval_board;           // [slots]
-  int32_t* eval_src;           // [slots] >= 0: cache entry; < 0: -(evaluator row + 1)
+  // the slot's leaf of this simulation, read by the expand launch (one
+  // thread per slot): (leaf_epoch << 32) | src, src >= 0 a cache entry, < 0
+  // -(evaluator row + 1); another simulation's tag: no leaf (idle, terminal)
+  uint64_t* leaf_src;          // [slots]
+  Board* leaf_board;           // [slots]
+  uint32_t leaf_epoch;         // this simulation's tag, unique over the engine's lanes
+  Board* eval_board;           // [slots] evaluator rows with the cache off (every leaf)
   int32_t* eval_count;         // [1]
-  int32_t* miss_q;             // [slots] eval-queue indices that missed the cache
   int32_t* miss_count;         // [1]
-  Board* nn_board;             // [slots] unique boards the evaluator computes (cache on)
+  Board* nn_board;             // [slots] evaluator rows with the cache on (the misses)
   int32_t* nn_count;           // [1]
-  int32_t* dup_q;              // [slots] misses whose board tag matched another miss
-  int32_t* dup_count;          // [1]
-  // eval/miss/nn/dup counts are one block of 4; two blocks alternate by
-  // simulation (epoch parity): the select kernel zeroes the other block, the
-  // next simulation's, so no memset launch sits between simulations
+  // eval/miss/nn counts (and a spare word) are one block of 4; two blocks
+  // alternate by simulation (epoch parity): the select kernel zeroes the
+  // other block, the next simulation's, so no memset launch sits between
   int32_t* next_counts;        // [4 * kCountStride] the block the next simulation uses
-  uint32_t* sel_done;          // [1] select blocks finished (the last one resolves the dedup, 0 after)
-  uint64_t* step_tag;          // [step_cap] per-simulation dedup table: (epoch << 32) | fp32
-  int32_t* step_row;           // [step_cap] evaluator row of the tag's owner
-  uint32_t step_mask;          // step_cap - 1
-  uint32_t epoch;              // simulation counter (tags of older epochs read as empty)
+  uint32_t epoch;              // the lane's simulation counter (its parity picks the block)
   unsigned long long* stats;   // [kStatCount]
   const double* powtab;        // [pow_len]: libm pow(n, 0.5), host-built
   // per-move outputs (MCTS API play())

@@ -119,7 +119,8 @@ __device__ void mt_seed(const TreeDev& t, int slots, int g, uint32_t seed) {
 // a word that batch writes before that word's own update, and the words from
 // earlier batches are stored ahead of them in program order -- so a twist is
 // 39 memory round trips instead of 624 dependent load-store chains (a game's
-// reset twists once: slot_reset).
+// reset twists once: slot_reset).  Batches of 48 words (13 round trips)
+// cost 3% of games/s (profiles/r6/ab_exp5.txt).
 __device__ void mt_twist(uint32_t* m, size_t slots) {
   constexpr int kTwistB = 16;
   static_assert(kMtN % kTwistB == 0 && 227 >= kTwistB, "batches never read their own stores");
@@ -213,11 +214,6 @@ __device__ unsigned long long g_sel_stamps[16384][12];
 extern "C" int az_diag_sel_stamps(unsigned long long* out, int n_slots) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_stamps), (size_t)std::min(n_slots, 16384) * 96) == hipSuccess ? 0 : -1;
 }
-// the last select launch's dedup tail: entry and end stamps, duplicates resolved
-__device__ unsigned long long g_sel_tail[3];
-extern "C" int az_diag_sel_tail(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_tail), sizeof(g_sel_tail)) == hipSuccess ? 0 : -1;
-}
 #else
 #define AZ_SEL_STAMP(s, k) ((void)0)
 #define AZ_SEL_VALUE(s, k, v) ((void)0)
@@ -230,7 +226,9 @@ __device__ __forceinline__ bool same_board(const Board& a, const Board& b) {
 }
 
 // After the descent: the terminal branch of MCTS.search (mcts.py:176-180) or
-// the eval queue + plays_inferences probe + per-simulation dedup.
+// the plays_inferences probe and, on a miss, an evaluator row.  The slot's
+// leaf record (leaf_src: this simulation's tag and where its outputs are;
+// leaf_board) is what the expand launch reads, one thread per slot.
 __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c, int s, Edge* E,
                           const int32_t* path, int depth, int status, const Board& b) {
   wave_stat(t, kStatSims);
@@ -247,6 +245,9 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   const uint64_t h = board_hash(b);
   uint32_t gen = 0, fp = 0, base = 0;
   uint32_t w[kCacheBucket];
+  const uint64_t tag = (uint64_t)t.leaf_epoch << 32;
+  t.leaf_board[s] = b;
+  t.path_len[s] = depth;
   if (c.enabled) {
     gen = (uint32_t)__hip_atomic_load(c.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     fp = cache_fp(h);
@@ -255,13 +256,11 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
     for (int k = 0; k < kCacheBucket; ++k)
       w[k] = __hip_atomic_load(c.state + base + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  const int q = wave_claim(t.eval_count);
-  t.eval_slot[q] = s;
-  t.eval_board[q] = b;
-  t.path_len[s] = depth;
   AZ_SEL_STAMP(s, 4);
-  if (!c.enabled) {
-    t.eval_src[q] = -(q + 1);
+  if (!c.enabled) {  // every leaf evaluated: its queue position is its row
+    const int q = wave_claim(t.eval_count);
+    t.eval_board[q] = b;
+    t.leaf_src[s] = tag | (uint32_t)(-(q + 1));
     wave_stat(t, kStatNNEvals);
     return;
   }
@@ -318,7 +317,7 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
     }
     if (use) {
       const uint32_t idx = base + hit;
-      t.eval_src[q] = (int32_t)idx;
+      t.leaf_src[s] = tag | idx;
       AZ_SEL_STAMP(s, 5);
       AZ_SEL_VALUE(s, 7, depth | (1 << 16) | ((uint64_t)s << 32));
       wave_stat(t, kStatCacheHits);
@@ -327,38 +326,17 @@ __device__ void leaf_tail(const GameCfg& g, const TreeDev& t, const CacheDev& c,
   }
   AZ_SEL_STAMP(s, 5);
   AZ_SEL_VALUE(s, 7, depth | (2 << 16) | ((uint64_t)s << 32));
-  // miss: one evaluator row per distinct board in this simulation.  Tag =
-  // (epoch << 32) | 32-bit board fingerprint; tags of older epochs count as
-  // empty, so the table needs no clearing.  A tag match is only a candidate:
-  // the launch's last block (dedup_tail) compares the full boards.
+  // miss: an evaluator row of its own.  (Rounds 2-6 shared one row between
+  // the slots of a simulation that reached the same board -- a dedup table
+  // and a last-block pass over its candidates; without them a board two
+  // slots meet in one simulation is evaluated twice, the same outputs, so the
+  // same searches; with the expand's per-slot leaf records +2.2%,
+  // profiles/r6/ab_exp5.txt.)
   wave_count(t.miss_count);
-  const uint64_t tag = ((uint64_t)t.epoch << 32) | (uint32_t)(h >> 32);
-  uint32_t slot = (uint32_t)h & t.step_mask;
-  for (uint32_t p = 0; p <= t.step_mask; ++p) {
-    const uint64_t cur = __hip_atomic_load(t.step_tag + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((uint32_t)(cur >> 32) != t.epoch) {  // empty in this epoch: try to own it
-      const uint64_t prev = atomicCAS((unsigned long long*)(t.step_tag + slot), cur, tag);
-      if (prev == cur) {
-        const int row = wave_claim(t.nn_count);
-        t.nn_board[row] = b;
-        t.step_row[slot] = row;
-        t.eval_src[q] = -(row + 1);
-        return;
-      }
-      if (prev == tag) {  // lost the race to the same tag
-        t.eval_src[q] = (int32_t)(0x80000000u | slot);
-        t.dup_q[wave_claim(t.dup_count)] = q;
-        return;
-      }
-      continue;  // someone else took this slot with another tag: re-read it
-    }
-    if (cur == tag) {
-      t.eval_src[q] = (int32_t)(0x80000000u | slot);
-      t.dup_q[wave_claim(t.dup_count)] = q;
-      return;
-    }
-    slot = (slot + 1) & t.step_mask;
-  }
+  const int row = wave_claim(t.nn_count);
+  t.nn_board[row] = b;
+  t.leaf_src[s] = tag | (uint32_t)(-(row + 1));
+  wave_stat(t, kStatNNEvals);
 }
 
 // ---------------------------------------------------- Dirichlet root noise
@@ -637,69 +615,13 @@ __device__ __forceinline__ void select_group_body(const GameCfg& g, const TreeDe
   }
 }
 
-// ----------------------------------------------------------- dedup resolve
-// Misses whose step tag matched an owner's: same board -> share the owner's
-// evaluator row; a fingerprint collision (different board) -> its own row.
-// Run by the select launch's last block to finish (every block fences its
-// writes, then counts itself done; the block that completes the count sees
-// all of them): no launch of its own between select and the network (round
-// 4: a separate kernel, 24,000 launches, 4.3% of the kernel time).
-__device__ __forceinline__ void dedup_tail(const TreeDev& t, const CacheDev& c) {
-  if (!c.enabled) return;  // uniform
-  __shared__ int last;
-  // every wave's eval_src / nn_board / step_row / dup_q stores drained, then
-  // ONE release per block before its count (not a full fence per wave); the
-  // block completing the count acquires (MI355X_MICROARCH.md, valid forms)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = atomicAdd(t.sel_done, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;  // block-uniform
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int n = __hip_atomic_load(t.dup_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef AZ_SEL_STAMPS
-  if (threadIdx.x == 0) {
-    g_sel_tail[0] = wall_clock64();
-    g_sel_tail[2] = (unsigned long long)n;
-  }
-#endif
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int q = t.dup_q[i];
-    const uint32_t slot = (uint32_t)t.eval_src[q] & 0x7fffffffu;
-    const int row = t.step_row[slot];
-    const Board b = t.eval_board[q];
-    if (same_board(t.nn_board[row], b)) {
-      t.eval_src[q] = -(row + 1);
-    } else {
-      const int r2 = atomicAdd(t.nn_count, 1);
-      t.nn_board[r2] = b;
-      t.eval_src[q] = -(r2 + 1);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#ifdef AZ_SEL_STAMPS
-    g_sel_tail[1] = wall_clock64();
-#endif
-    atomicAdd(t.stats + kStatNNEvals, (unsigned long long)*t.nn_count);
-    *t.sel_done = 0;  // the lane's next select launch counts from zero
-  }
-}
-
 template <bool NOISE>
 __global__ __launch_bounds__(kGameBlock) void select_kernel(GameCfg g, TreeDev t, CacheDev c) {
   select_body<NOISE>(g, t, c);
-  dedup_tail(t, c);
 }
 template <int L, bool NOISE, int SHAPE = 0>
 __global__ __launch_bounds__(kGameBlock) void select_group_kernel(GameCfg g, TreeDev t, CacheDev c) {
   select_group_body<L, NOISE, SHAPE>(g, t, c);
-  dedup_tail(t, c);
 }
 
 // ------------------------------------------------------------ cache insert
@@ -808,16 +730,14 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
     cache_insert_row(g, t, c, probs, values, ((int)blockIdx.x - exp_blocks) * blockDim.x + threadIdx.x);
     return;
   }
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.slots) return;
-  // round trip 1: the queue entry, read beside the queue's count (entries past
-  // it are stale and unused); 2: the slot's arena, path and the leaf's
-  // outputs; 3: the path's edges -- every load of a trip issued together
-  const int n_eval = *t.eval_count;
-  const int s = t.eval_slot[i];
-  const Board b = t.eval_board[i];
-  const int src = t.eval_src[i];
-  if (i >= n_eval) return;
+  // one thread per slot, two round trips: 1. the slot's leaf record (this
+  // simulation's tag: else no leaf to expand -- idle, terminal), arena and
+  // path row; 2. the leaf's outputs and the path's edges -- each trip's loads
+  // issued together (leaf records by slot, not a queue: one trip fewer)
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= g.slots) return;
+  const uint64_t leaf = t.leaf_src[s];
+  const Board b = t.leaf_board[s];
   Edge* E = slot_edges(g, t, s);
   const int top0 = t.arena_top[s];
   const int end0 = g.halves > 1 ? t.arena_end[s] : 0;
@@ -829,6 +749,8 @@ __global__ __launch_bounds__(kGameBlock) void expand_kernel(GameCfg g, TreeDev t
   int pv[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) pv[k] = k < g.max_depth ? path[k] : 0;
+  if ((uint32_t)(leaf >> 32) != t.leaf_epoch) return;
+  const int src = (int32_t)(uint32_t)leaf;
   const float* p;
   float v;
   if (src >= 0) {  // cache hit
