@@ -62,6 +62,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16/fp16 MFMA (no 2:1 sparsity)
 MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
 MAX_PREROLL = 4000
+WINDOW_EVENT_STRIDE = 4         # the timed window's tower events: every 4th launch of each lane
 CACHE_TURNOVER = 1.5            # cache inserts / capacity before the window (full table turned over: stationary)
 CACHE_FULL = 0.98               # ... and the table this full
 
@@ -750,7 +751,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.timer(os.environ.get("AZ_BENCH_WINDOW_EVENTS", "1") != "0")  # A/B of the events' own cost
+    # the tower timed by HIP events on every WINDOW_EVENT_STRIDE-th launch of
+    # each lane (an event pair on every launch cost 1.2% of games/s,
+    # profiles/r6/ab_exp5.txt); AZ_BENCH_WINDOW_EVENTS=0 / 1: none / every launch
+    ev_stride = int(os.environ.get("AZ_BENCH_WINDOW_EVENTS", str(WINDOW_EVENT_STRIDE)))
+    eng.timer(ev_stride != 0, every=ev_stride if ev_stride != 0 else 1)
     st0 = eng.stats()
     t0 = time.perf_counter()
     drained = 0
@@ -865,7 +870,11 @@ def main():
     issued = 3 * direct_flop if args.conv_algo != 1 else direct_flop
     per_forward = 1 if args.conv_algo == 0 else 2 * args.depth
     conv_avg_ms = conv_ms / max(conv_launches, 1)
-    boards_per_launch = local_evals / max(conv_launches / per_forward, 1)
+    # every lane launches one forward per simulation (timed or not)
+    all_launches = args.steps * args.sims * eng.lanes * per_forward
+    boards_per_launch = local_evals / max(all_launches / per_forward, 1)
+    if ev_stride >= 3:  # the union of the sampled intervals, scaled to every launch
+        busy_ms *= ev_stride
     if args.conv_algo == 0 and st1.get("issued_flop_per_board", 0) > 0:
         # the tower reports what it issues: its tiles' pad rows and stem in,
         # the slot plan's skipped border taps (exact zeros) out; the dual
@@ -881,6 +890,13 @@ def main():
         pmc_key += f"_{args.height}x{args.width}"
     roof = conv_roofline(args, args.conv_algo, per_forward, boards_per_launch, conv_avg_ms, busy_ms, local_evals,
                          conv_launches, direct_flop, issued, pmc, pmc_key)
+    if ev_stride >= 3:
+        roof["event_sampling"] = {
+            "every": ev_stride, "launches_all": all_launches,
+            "basis": (f"HIP events bracket every {ev_stride}th tower launch of each lane in the timed region "
+                      f"(avg_launch_ms over those {conv_launches}); boards_per_launch over all {all_launches} "
+                      f"launches (one per lane per simulation); busy_union from the timed launches' union x "
+                      f"{ev_stride}")}
 
     # the same kernels alone on one stream at the live per-lane batch (what a
     # launch costs without the other lane's kernels sharing the CUs)

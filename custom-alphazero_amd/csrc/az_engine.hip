@@ -1194,7 +1194,8 @@ int az_timer_enable(az_engine* e, int on) {
   AZ_HIP(hipEventRecord(e->timer_ref, e->stream));
   AZ_HIP(hipStreamSynchronize(e->stream));
   // on: 1 = conv launches, 2 = conv + select/expand launches (more events per
-  // simulation: bench.py times the tree kernels in a window of their own)
+  // simulation: bench.py times the tree kernels in a window of their own),
+  // k >= 3 = every k-th conv launch of each lane (sampled)
   std::vector<az::ConvTimer*> timers = {&e->timer, &e->whole.timer}, ttimers = {&e->whole.tree_timer};
   for (Lane* L : e->lanes)
     if (L != &e->whole) {
@@ -1206,6 +1207,7 @@ int az_timer_enable(az_engine* e, int on) {
     tm->reset();
     tm->ref = &e->timer_ref;
     tm->enabled = on != 0;
+    tm->stride = on >= 3 ? on : 1;
   }
   for (az::ConvTimer* tm : ttimers) {
     tm->flush();

@@ -153,6 +153,13 @@ struct NetDev {
 // can be taken next to the summed durations.
 struct ConvTimer {
   bool enabled = false;
+  // every stride-th launch timed (1: all): each event pair is a marker packet
+  // on the lane's stream between the kernels it brackets, on the simulation
+  // chain (bench.py's window: 1.2% of games/s with every launch timed,
+  // profiles/r6/ab_exp5.txt)
+  int stride = 1;
+  long long seq = 0;
+  bool cur = false;
   hipEvent_t* ref = nullptr;
   std::vector<hipEvent_t> pool;
   size_t used = 0;
@@ -161,6 +168,8 @@ struct ConvTimer {
   std::vector<std::pair<double, double>> intervals;  // [start, end) ms after *ref
   void begin(hipStream_t s) {
     if (!enabled) return;
+    cur = seq++ % stride == 0;
+    if (!cur) return;
     if (used + 2 > pool.size()) {
       for (int i = 0; i < 256; ++i) {
         hipEvent_t e;
@@ -173,7 +182,7 @@ struct ConvTimer {
     (void)hipEventRecord(pool[used++], s);
   }
   void end(hipStream_t s, int n_launches) {
-    if (!enabled) return;
+    if (!enabled || !cur) return;
     (void)hipEventRecord(pool[used++], s);
     launches += n_launches;
   }
@@ -193,6 +202,7 @@ struct ConvTimer {
     used = 0;
     total_ms = 0.0;
     launches = 0;
+    seq = 0;
     intervals.clear();
   }
   ~ConvTimer() {

@@ -483,8 +483,13 @@ class Engine:
     def cache_enable(self, on=True):
         _check(self._L.az_cache_enable(self._h, int(bool(on))))
 
-    def timer(self, on, tree=False):
-        _check(self._L.az_timer_enable(self._h, (2 if tree else 1) if on else 0))
+    def timer(self, on, tree=False, every=1):
+        """HIP-event timing of the network launches (az_stats conv_*); tree:
+        the select and expand launches too; every >= 3: every `every`-th
+        network launch of each lane only (conv_launches counts those)."""
+        if every not in (1,) and every < 3:
+            raise ValueError("every: 1 or >= 3")
+        _check(self._L.az_timer_enable(self._h, (every if every >= 3 else 2 if tree else 1) if on else 0))
 
     def pow_table(self, n):
         out = np.zeros(int(n), np.float64)

@@ -276,7 +276,8 @@ int az_cache_clear(az_engine* eng);
 /* Bypass (0) or use (1) an allocated cache; results are identical either way. */
 int az_cache_enable(az_engine* eng, int on);
 /* HIP-event timing for bench.py: on = 1 the conv launches, 2 also the
- * select and expand launches (az_stats conv_* / tree_*), 0 off. */
+ * select and expand launches (az_stats conv_* / tree_*), k >= 3 every k-th
+ * conv launch of each lane (conv_launches counts the timed ones), 0 off. */
 int az_timer_enable(az_engine* eng, int on);
 /* The host-built libm pow(k, 0.5) table the kernels use (tests). */
 int az_pow_table(az_engine* eng, double* out, int64_t n);
