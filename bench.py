@@ -62,7 +62,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16/fp16 MFMA (no 2:1 sparsity)
 MIN_PREROLL = 24                # untimed moves at least (game-completion rate stationary, ~1 game length)
 MAX_PREROLL = 4000
-WINDOW_EVENT_STRIDE = 4         # the timed window's tower events: every 4th launch of each lane
+WINDOW_EVENT_STRIDE = 1         # the timed window's tower events: every launch of each lane
 CACHE_TURNOVER = 1.5            # cache inserts / capacity before the window (full table turned over: stationary)
 CACHE_FULL = 0.98               # ... and the table this full
 
@@ -751,11 +751,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # the tower timed by HIP events on every WINDOW_EVENT_STRIDE-th launch of
-    # each lane (an event pair on every launch cost 1.2% of games/s,
-    # profiles/r6/ab_exp5.txt); AZ_BENCH_WINDOW_EVENTS=0 / 1: none / every launch
-    ev_stride = int(os.environ.get("AZ_BENCH_WINDOW_EVENTS", str(WINDOW_EVENT_STRIDE)))
-    eng.timer(ev_stride != 0, every=ev_stride if ev_stride != 0 else 1)
+    # the tower timed by HIP events on every launch of each lane
+    # (AZ_BENCH_WINDOW_EVENTS=k >= 3: every k-th; 0: none -- on one box every
+    # 4th ran 5% SLOWER than every launch, profiles/r6/final/ab_events.txt)
+    ev_env = os.environ.get("AZ_BENCH_WINDOW_EVENTS", str(WINDOW_EVENT_STRIDE))
+    ev_stride = 1 if ev_env == "tree" else int(ev_env)  # "tree": the select and expand launches too
+    eng.timer(ev_stride != 0, tree=ev_env == "tree", every=ev_stride if ev_stride != 0 else 1)
     st0 = eng.stats()
     t0 = time.perf_counter()
     drained = 0
