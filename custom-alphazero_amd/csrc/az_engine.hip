@@ -217,12 +217,22 @@ int host_evaluate(az_engine* e, Lane& L, const az::Board* rows, const int32_t* n
   return 0;
 }
 
+int sync_all(az_engine* e);
+
 // one simulation for every active slot of a lane (MCTS.search body,
 // mcts.py:171-180), enqueued on the lane's stream
 int simulate(az_engine* e, Lane& L) {
   hipStream_t s = L.stream;
   L.t.epoch += 1;
-  L.t.leaf_epoch = ++e->leaf_epoch;  // leaf records of any other simulation read as absent
+  // leaf records of any other simulation read as absent: the tag is unique
+  // over the engine's lanes; when it wraps (2^32 simulations) the records are
+  // cleared first, so none written 2^32 simulations ago can match
+  if (++e->leaf_epoch == 0) {
+    if (int rc = sync_all(e)) return rc;
+    AZ_HIP(hipMemset(e->t.leaf_src, 0, (size_t)e->g.slots * sizeof(uint64_t)));
+    e->leaf_epoch = 1;
+  }
+  L.t.leaf_epoch = e->leaf_epoch;
   // eval_count, miss_count, nn_count: the epoch parity's block of
   // four (zeroed by the previous simulation's select kernel, or at creation)
   set_counts(L.t, L.counts, L.t.epoch & 1);
